@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""bench.py — subspace-update GB/s (gemm_inner + gemm_outer/axpy + dot) at N = 1e8, 8 roots.
+
+One "step" is the handler-operation sequence of one Davidson subspace update at steady state
+(reference call stack SURVEY.md §3.1; every op is a libsubspace_hip.so C-ABI call on HBM-resident
+shards):
+  S_RQ = gemm_inner(R params (m), Q params (k))        XSpace.h:43      8N(m+k) B
+  H_RQ = gemm_inner(R params (m), Q actions (k))       XSpace.h:47      8N(m+k) B
+  construct_solution(params):  fill(0) x m, gemm_outer(k -> m)        IterativeSolverTemplate.h:46,63
+  construct_solution(actions): fill(0) x m, gemm_outer(k -> m)        8N m + 8N(k+2m) B each
+  residual r_i -= lambda_i x_i: axpy x m               LinearEigensystemDavidson.h:191   24N B
+  errors |r_i|: dot(r_i, r_i) x m                      IterativeSolverTemplate.h:99      8N B
+Global N is fixed and sharded by index range over the ranks (strong scaling, config C4); each
+rank runs the identical SPMD sequence and the reductions are RCCL allreduces.
+
+value = algorithmic bytes of all ranks per step x steps / (max over ranks of the timed wall time).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "iterative-solver_amd"))
+
+import numpy as np  # noqa: E402
+
+import subspace_hip as sh  # noqa: E402
+
+METRIC = "subspace-update GB/s (gemm_inner+axpy) at N=1e8, 8 roots; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
+SEED = 20251015
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def distribution(n, chunks):
+    """make_distribution_spread_remainder (reference util/Distribution.h:376-387)."""
+    block, extra = divmod(n, chunks)
+    borders = [0]
+    for c in range(chunks):
+        borders.append(borders[-1] + block + (1 if c < extra else 0))
+    return borders
+
+
+def step_bytes(n, m, k):
+    return (2 * 8 * n * (m + k)      # two gemm_inner
+            + 2 * m * 8 * n          # fills in construct_solution
+            + 2 * 8 * n * (k + 2 * m)  # two gemm_outer
+            + m * 24 * n             # residual axpy
+            + m * 8 * n)             # norm dots (x == y: one vector read)
+
+
+class Workload:
+    def __init__(self, ctx, n_local, offset, m, k):
+        self.ctx, self.m, self.k = ctx, m, k
+        self.rp = [ctx.alloc(n_local) for _ in range(m)]
+        self.ra = [ctx.alloc(n_local) for _ in range(m)]
+        self.qp = [ctx.alloc(n_local) for _ in range(k)]
+        self.qa = [ctx.alloc(n_local) for _ in range(k)]
+        for vid, v in enumerate(self.rp + self.ra + self.qp + self.qa):
+            ctx.fill_random(v, SEED, vid, offset)
+        rng = np.random.default_rng(SEED)
+        self.coef = rng.uniform(-0.1, 0.1, (k, m))
+        self.lam = rng.uniform(0.5, 2.0, m)
+        ctx.synchronize()
+
+    def step(self):
+        c = self.ctx
+        c.gemm_inner(self.rp, self.qp)
+        c.gemm_inner(self.rp, self.qa)
+        for v in self.rp:
+            c.fill(0.0, v)
+        c.gemm_outer(self.coef, self.qp, self.rp)
+        for v in self.ra:
+            c.fill(0.0, v)
+        c.gemm_outer(self.coef, self.qa, self.ra)
+        for i in range(self.m):
+            c.axpy(-self.lam[i], self.rp[i], self.ra[i])
+        err = 0.0
+        for i in range(self.m):
+            err = max(err, c.dot(self.ra[i], self.ra[i]))
+        return err
+
+
+def cpu_baseline(m, k, seconds):
+    """The oracle (CPU restatement of ArrayHandlerIterable: pairwise gemm, sequential loops) on one
+    host core, same op sequence, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg only
+
+    n = 1_000_000
+    t0 = time.perf_counter()
+    steps = 0
+    runner = oracle.CpuUpdateStep(n, m, k, SEED)
+    while True:
+        runner.step()
+        steps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": step_bytes(n, m, k) * steps / dt / 1e9,
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{steps} step(s) of the same op sequence at N=1e6 (m={m}, k={k}) on 1 core of "
+                  f"{cpu} (nproc={os.cpu_count()}), {dt:.1f} s, oracle/oracle_ops.c (reference loops)",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=float, default=1e8, help="global vector length")
+    ap.add_argument("--roots", type=int, default=8)
+    ap.add_argument("--qsize", type=int, default=48)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ledger-steps", type=int, default=3)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # plumbing: rendezvous, barrier, max-time reduction
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    ctx = sh.Context(local_rank)
+    if world > 1:
+        uid = [sh.Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.attach_comm(world, rank, uid[0])
+
+    n_global = int(args.n)
+    m, k = args.roots, args.qsize
+    borders = distribution(n_global, world)
+    n_local, offset = borders[rank + 1] - borders[rank], borders[rank]
+    log(f"rank {rank}/{world}: n_local={n_local} vectors={2 * (m + k)} HBM={2 * (m + k) * n_local * 8 / 1e9:.1f} GB")
+    wl = Workload(ctx, n_local, offset, m, k)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        wl.step()
+    ctx.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        wl.step()
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # Per-kernel HIP-event ledger over a few extra steps (not part of the timed region).
+    ctx.ledger_reset()
+    ctx.ledger_enable(True)
+    for _ in range(args.ledger_steps):
+        wl.step()
+    ctx.ledger_enable(False)
+    led = ctx.ledger()
+
+    total_bytes = step_bytes(n_global, m, k) * args.steps
+    value = total_bytes / elapsed / 1e9
+    result = None
+    if rank == 0:
+        dom = max(led, key=lambda op: led[op]["ms"])
+        e = led[dom]
+        achieved = (e["bytes"] / e["calls"]) / (e["ms"] / e["calls"] / 1e3) / 1e9
+        ops = {op: {"calls_per_step": v["calls"] / args.ledger_steps,
+                    "avg_us": 1e3 * v["ms"] / v["calls"],
+                    "GBs": v["bytes"] / (v["ms"] / 1e3) / 1e9} for op, v in led.items()}
+        result = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (splitmix64 uniform [-1,1), global-index seeded; HBM-resident)",
+            "config": {
+                "workload": "Davidson subspace update per step: 2x gemm_inner(8x48) + 2x construct_solution "
+                            "(fill x8 + gemm_outer 48->8) + 8x residual axpy + 8x norm dot",
+                "n_global": n_global,
+                "n_local_rank0": n_local,
+                "roots": m,
+                "qspace": k,
+                "parallelism": f"index-range shards x{world} (RCCL allreduce for reductions)",
+                "bytes_per_step": step_bytes(n_global, m, k),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "avg_launch_us": round(1e3 * e["ms"] / e["calls"], 2),
+                "bytes_per_launch": e["bytes"] / e["calls"],
+            },
+            "ops": ops,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("timing CPU baseline (oracle, 1 core)...")
+            result["cpu_baseline"] = cpu_baseline(m, k, args.cpu_seconds)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+/*
+ * subspace_hip.h — C ABI of libsubspace_hip.so, the MI355X (gfx950) implementation of the
+ * subspace linear-algebra hot path of molpro::linalg::itsolv.
+ *
+ * Every entry point replaces one operation of the reference's ArrayHandler interface
+ * (reference: src/molpro/linalg/array/ArrayHandler.h:184-222) acting on the LOCAL shard of
+ * HBM-resident vectors, plus the MPI_Allreduce the reference's distributed handlers issue
+ * after local reductions (src/molpro/linalg/array/util/gemm.h:179-182, DistrArray.cpp:134-136).
+ *
+ * Conventions:
+ *  - All vector arguments are DEVICE pointers (double, FP64) of the calling rank's shard of
+ *    length n; they must be 16-byte aligned (ssp_alloc guarantees 256 B).
+ *  - Matrices are row-major, as subspace::Matrix is (reference itsolv/subspace/Matrix.h:23):
+ *      gemm_inner: out[i*k + j] = <xx[i], yy[j]>            (reference util/gemm.h:267-279)
+ *      gemm_outer: yy[j] += sum_i alphas[i*m + j] * xx[i]   (reference util/gemm.h:257-265)
+ *  - Ops are ordered on the context's HIP stream.  Ops that return host values (dot,
+ *    gemm_inner, select, sparse dot/gemm_inner) synchronise that stream before returning.
+ *  - With a communicator attached (ssp_ctx_attach_comm), reductions are summed over ranks with
+ *    RCCL allreduce on the same stream, so every rank receives bit-identical results.
+ *  - No entry point throws.  Each returns an ssp_status; ssp_last_error() describes the last
+ *    failure on the calling thread.  The C++ handler shim maps codes to the reference's
+ *    exceptions (ArrayHandlerError, std::out_of_range, std::logic_error).
+ */
+#ifndef SUBSPACE_HIP_H
+#define SUBSPACE_HIP_H
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  SSP_OK = 0,
+  SSP_ERR_SIZE = 1,      /* incompatible vector sizes  -> util::ArrayHandlerError   */
+  SSP_ERR_RANGE = 2,     /* matrix/vector count mismatch -> std::out_of_range       */
+  SSP_ERR_ARG = 3,       /* invalid argument (null, misaligned, n too large)         */
+  SSP_ERR_HIP = 4,       /* HIP runtime failure                                      */
+  SSP_ERR_COMM = 5,      /* RCCL failure                                             */
+  SSP_ERR_NOMEM = 6,     /* device or pinned allocation failed                      */
+  SSP_ERR_UNSUPPORTED = 7 /* operation not defined for these operands -> logic_error */
+} ssp_status;
+
+typedef struct ssp_ctx ssp_ctx;
+
+/* ---- context, memory, communicator ------------------------------------------------------ */
+const char* ssp_last_error(void);
+const char* ssp_version(void);
+/* Number of visible HIP devices (0 when no GPU).  Does not create a context. */
+int ssp_device_count(void);
+int ssp_ctx_create(int device, ssp_ctx** out);
+int ssp_ctx_destroy(ssp_ctx* ctx);
+/* The hipStream_t all ops of this context run on (for event timing by callers). */
+void* ssp_ctx_stream(ssp_ctx* ctx);
+int ssp_synchronize(ssp_ctx* ctx);
+/* Caching device allocator (HBM arena): Q vectors are created and destroyed every iteration
+ * (reference itsolv/subspace/QSpace.h:80-84), so freed blocks are recycled by size. */
+int ssp_alloc(ssp_ctx* ctx, size_t n, double** out);
+int ssp_free(ssp_ctx* ctx, double* p);
+int ssp_release_cached(ssp_ctx* ctx);
+int ssp_memory_stats(ssp_ctx* ctx, size_t* bytes_in_use, size_t* bytes_cached);
+int ssp_upload(ssp_ctx* ctx, double* dst_dev, const double* src_host, size_t n);
+int ssp_download(ssp_ctx* ctx, double* dst_host, const double* src_dev, size_t n);
+
+/* RCCL communicator over one process per GPU.  The id is SSP_UNIQUE_ID_BYTES opaque bytes made
+ * by rank 0 with ssp_comm_unique_id and distributed by the caller (e.g. torch.distributed). */
+#define SSP_UNIQUE_ID_BYTES 128
+int ssp_comm_unique_id(char* id_out);
+int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id);
+int ssp_ctx_rank(ssp_ctx* ctx);
+int ssp_ctx_nranks(ssp_ctx* ctx);
+/* In-place sum over ranks of n doubles in DEVICE memory (no-op without a communicator). */
+int ssp_allreduce_sum(ssp_ctx* ctx, double* buf_dev, size_t n);
+/* Gather `bytes` host bytes from every rank into recv (nranks*bytes), rank order. */
+int ssp_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes);
+
+/* Operation ledger (measurement): when enabled, HIP events on the
+ * context's stream bracket each hot-path kernel launch and the call's ALGORITHMIC bytes are
+ * accumulated per operation name ("gemm_inner", "gemm_outer", "axpy", "dot", ...). */
+int ssp_ledger_enable(ssp_ctx* ctx, int enable);
+int ssp_ledger_reset(ssp_ctx* ctx);
+int ssp_ledger_count(ssp_ctx* ctx);
+int ssp_ledger_entry(ssp_ctx* ctx, int i, const char** name, long long* calls, double* kernel_ms, double* bytes);
+
+/* ---- dense (R x R, Q x Q, R x Q) operations: reference ArrayHandlerIterable.h:46-90,
+ *      DistrArray.cpp:43-138 ------------------------------------------------------------- */
+/* x[:] = alpha                         reference ArrayHandlerIterable.h:59-63 */
+int ssp_fill(ssp_ctx* ctx, double alpha, double* x, size_t n);
+/* x[:] *= alpha                        reference ArrayHandlerIterable.h:54-57 */
+int ssp_scal(ssp_ctx* ctx, double alpha, double* x, size_t n);
+/* x[:] = y[:]                          reference ArrayHandlerIterable.h:48-52 */
+int ssp_copy(ssp_ctx* ctx, double* x, const double* y, size_t n);
+/* y[:] += alpha * x[:]                 reference ArrayHandlerIterable.h:65-74 */
+int ssp_axpy(ssp_ctx* ctx, double alpha, const double* x, double* y, size_t n);
+/* *out = sum_ranks <x, y>              reference ArrayHandlerIterable.h:76-82, DistrArray.cpp:124-138 */
+int ssp_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, double* out);
+/* out (m x k, row-major) = <xx[i], yy[j]> summed over ranks.
+ * reference util/gemm.h:157-184 (distributed) and :267-279 (pairwise default) */
+int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* const* yy, int k, size_t n,
+                   double* out);
+/* yy[j] += sum_i alphas[i*m + j] * xx[i], i in [0,k) sources, j in [0,m) destinations.
+ * reference util/gemm.h:186-203 (distributed) and :257-265 (pairwise default) */
+int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
+                   size_t n);
+/* a[v][i] /= (d[i] - shift[v] + 1e-15) for v in [0,nvec)   reference itsolv/IterativeSolver.h:34-55 */
+int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n);
+
+/* ---- selection: reference util/select.h:28-55, util/select_max_dot.h:166-190,
+ *      DistrArray.cpp:170-276.  Local shard [offset, offset+n) of a global array.  Returns up
+ *      to nsel (global index, value) pairs in ASCENDING INDEX order (std::map order), chosen
+ *      over all ranks with the reference's tie rule (larger index wins a tie). ----------- */
+int ssp_select(ssp_ctx* ctx, const double* x, size_t n, size_t offset, size_t nsel, int max, int ignore_sign,
+               size_t* idx_out, double* val_out, size_t* nout);
+int ssp_select_max_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, size_t offset, size_t nsel,
+                       size_t* idx_out, double* val_out, size_t* nout);
+
+/* ---- dense x sparse (R x P): P = std::map<size_t,double>, passed as sorted global indices.
+ *      reference ArrayHandlerIterableSparse.h:35-58, util/gemm.h:207-253,
+ *      DistrArray.cpp:419-465.  Entries outside [offset, offset+n) are ignored. ---------- */
+/* x = 0 then x[idx-offset] = val */
+int ssp_sparse_copy(ssp_ctx* ctx, double* x, size_t n, size_t offset, const size_t* idx, const double* val,
+                    size_t nnz);
+/* x[idx-offset] += alpha * val */
+int ssp_sparse_axpy(ssp_ctx* ctx, double alpha, const size_t* idx, const double* val, size_t nnz, double* x,
+                    size_t n, size_t offset);
+/* *out = sum_ranks sum_e x[idx_e-offset] * val_e */
+int ssp_sparse_dot(ssp_ctx* ctx, const double* x, size_t n, size_t offset, const size_t* idx, const double* val,
+                   size_t nnz, double* out);
+/* out (m x k) = <xx[i], p_j>; p_j = entries [ptr[j], ptr[j+1]) of (idx, val). */
+int ssp_gemm_inner_sparse(ssp_ctx* ctx, const double* const* xx, int m, size_t n, size_t offset, const size_t* ptr,
+                          const size_t* idx, const double* val, int k, double* out);
+/* yy[j] += sum_i alphas[i*m + j] * p_i; p_i = entries [ptr[i], ptr[i+1]). */
+int ssp_gemm_outer_sparse(ssp_ctx* ctx, const double* alphas, const size_t* ptr, const size_t* idx,
+                          const double* val, int k, double* const* yy, int m, size_t n, size_t offset);
+
+/* ---- synthetic problem (harness only; not a reference operation) ----------------------------
+ * H = diag(1 + g) + rho * sum_{l<rank} u_l u_l^T, g = global index, u_0 = 1 and for l > 0
+ * u_l(g) = +/-1 from a splitmix64 hash of (seed, l, g).  The rank-one (rank=1) case is the
+ * matrix of reference test/itsolv/test_rayleigh_quotient.cpp:37-42.  yy[v] = H xx[v]. */
+int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* yy, int nvec, size_t n,
+                          size_t offset, double rho, int rank, unsigned long long seed);
+/* d[g] = H_gg = 1 + g + rank*rho */
+int sspx_synthetic_diagonal(ssp_ctx* ctx, double* d, size_t n, size_t offset, double rho, int rank);
+/* x[g] = uniform [-1,1) from splitmix64(seed, vec, g): G-independent benchmark data. */
+int sspx_fill_random(ssp_ctx* ctx, double* x, size_t n, size_t offset, unsigned long long seed,
+                     unsigned long long vec);
+/* y = A x for a dense row-major n_global x n_global matrix A in device memory, local rows
+ * [offset, offset+n) of y; x must be the full (gathered) vector.  Used for small fixtures. */
+int sspx_dense_action(ssp_ctx* ctx, const double* a, size_t n_global, const double* const* xx, double* const* yy,
+                      int nvec, size_t n, size_t offset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SUBSPACE_HIP_H */

@@ -1,0 +1,422 @@
+// Context, HBM arena, staging buffers and the RCCL communicator of libsubspace_hip.so.
+//
+// The reference keeps Q vectors on disk (DistrArrayFile, reference array/DistrArrayFile.cpp:164-200)
+// or in MPI-3 windows and reduces with MPI_Allreduce (reference array/util/gemm.h:179-182).  Here
+// every vector shard lives in HBM for the solver's lifetime and reductions are RCCL allreduces on
+// the compute stream.
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+
+#include "ssp_internal.h"
+
+namespace {
+thread_local std::string g_last_error;
+
+size_t round_block(size_t bytes) {
+  // Small blocks to 256 B, large blocks to 2 MiB so that equal-length vectors share a bucket.
+  if (bytes < (size_t(1) << 20)) return (bytes + 255) & ~size_t(255);
+  const size_t g = size_t(2) << 20;
+  return (bytes + g - 1) / g * g;
+}
+}  // namespace
+
+namespace ssp {
+
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int hip_error(hipError_t e, const char* what) {
+  return set_error(SSP_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int use_device(ssp_ctx* ctx) {
+  int cur = -1;
+  SSP_TRY_HIP(hipGetDevice(&cur));
+  if (cur != ctx->device) SSP_TRY_HIP(hipSetDevice(ctx->device));
+  return SSP_OK;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+unsigned stream_grid(const ssp_ctx* ctx, size_t work_items, unsigned per_thread) {
+  const size_t per_block = size_t(kBlock) * per_thread;
+  size_t blocks = (work_items + per_block - 1) / per_block;
+  const size_t cap = size_t(ctx->num_cus) * 8;  // 8 workgroups (32 waves) per CU, grid-stride beyond
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  return unsigned(blocks);
+}
+
+int ensure_partial(ssp_ctx* ctx, size_t n) {
+  if (n <= ctx->partial_cap) return SSP_OK;
+  if (ctx->partial) {
+    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    SSP_TRY_HIP(hipFree(ctx->partial));
+    ctx->partial = nullptr;
+  }
+  size_t cap = std::max(n, size_t(1) << 20);
+  if (hipMalloc(&ctx->partial, cap * sizeof(double)) != hipSuccess)
+    return set_error(SSP_ERR_NOMEM, "hipMalloc of reduction workspace failed");
+  ctx->partial_cap = cap;
+  return SSP_OK;
+}
+
+int ensure_result(ssp_ctx* ctx, size_t n) {
+  if (n <= ctx->result_cap) return SSP_OK;
+  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->result_dev) SSP_TRY_HIP(hipFree(ctx->result_dev));
+  if (ctx->result_host) SSP_TRY_HIP(hipHostFree(ctx->result_host));
+  ctx->result_dev = nullptr;
+  ctx->result_host = nullptr;
+  size_t cap = std::max(n, size_t(1) << 16);
+  if (hipMalloc(&ctx->result_dev, cap * sizeof(double)) != hipSuccess)
+    return set_error(SSP_ERR_NOMEM, "hipMalloc of result staging failed");
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->result_host), cap * sizeof(double), hipHostMallocDefault) !=
+      hipSuccess)
+    return set_error(SSP_ERR_NOMEM, "hipHostMalloc of result staging failed");
+  ctx->result_cap = cap;
+  return SSP_OK;
+}
+
+int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev) {
+  const size_t need = (bytes + 255) & ~size_t(255);
+  if (need > ctx->ring_cap) {
+    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->ring_dev) SSP_TRY_HIP(hipFree(ctx->ring_dev));
+    if (ctx->ring_host) SSP_TRY_HIP(hipHostFree(ctx->ring_host));
+    ctx->ring_dev = ctx->ring_host = nullptr;
+    size_t cap = std::max(need * 2, size_t(4) << 20);
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->ring_dev), cap) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&ctx->ring_host), cap, hipHostMallocDefault) != hipSuccess)
+      return set_error(SSP_ERR_NOMEM, "allocation of upload ring failed");
+    ctx->ring_cap = cap;
+    ctx->ring_head = 0;
+  }
+  if (ctx->ring_head + need > ctx->ring_cap) {
+    // Wrap: every earlier copy out of the ring has completed once the stream drains.
+    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->ring_head = 0;
+  }
+  char* h = ctx->ring_host + ctx->ring_head;
+  char* d = ctx->ring_dev + ctx->ring_head;
+  ctx->ring_head += need;
+  if (bytes) {
+    std::memcpy(h, host, bytes);
+    SSP_TRY_HIP(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+  }
+  *dev = d;
+  return SSP_OK;
+}
+
+int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n) {
+  if (!ctx->comm || ctx->nranks <= 1 || n == 0) return SSP_OK;
+  ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream);
+  if (r != ncclSuccess) return set_error(SSP_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  return SSP_OK;
+}
+
+int fetch_result(ssp_ctx* ctx, double* out, size_t n) {
+  SSP_TRY_HIP(hipMemcpyAsync(ctx->result_host, ctx->result_dev, n * sizeof(double), hipMemcpyDeviceToHost,
+                             ctx->stream));
+  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  std::memcpy(out, ctx->result_host, n * sizeof(double));
+  return SSP_OK;
+}
+
+namespace {
+hipEvent_t take_event(ssp_ctx* ctx) {
+  if (!ctx->event_pool.empty()) {
+    hipEvent_t e = ctx->event_pool.back();
+    ctx->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+int ledger_slot(ssp_ctx* ctx, const char* op) {
+  for (size_t i = 0; i < ctx->ledger.size(); ++i)
+    if (ctx->ledger[i].name == op) return int(i);
+  ctx->ledger.emplace_back();
+  ctx->ledger.back().name = op;
+  return int(ctx->ledger.size() - 1);
+}
+
+int ledger_resolve(ssp_ctx* ctx) {
+  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  for (auto& e : ctx->ledger) {
+    for (auto& pr : e.pending) {
+      float ms = 0;
+      SSP_TRY_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+      e.ms += ms;
+      ctx->event_pool.push_back(pr.first);
+      ctx->event_pool.push_back(pr.second);
+    }
+    e.pending.clear();
+  }
+  return SSP_OK;
+}
+}  // namespace
+
+LedgerScope::LedgerScope(ssp_ctx* ctx, const char* op, double bytes) : ctx_(ctx) {
+  if (!ctx->ledger_on) return;
+  slot_ = ledger_slot(ctx, op);
+  ctx->ledger[slot_].calls += 1;
+  ctx->ledger[slot_].bytes += bytes;
+  start_ = take_event(ctx);
+  if (start_) (void)hipEventRecord(start_, ctx->stream);
+}
+
+LedgerScope::~LedgerScope() {
+  if (slot_ < 0 || !start_) return;
+  hipEvent_t end = take_event(ctx_);
+  if (!end) return;
+  (void)hipEventRecord(end, ctx_->stream);
+  ctx_->ledger[slot_].pending.emplace_back(start_, end);
+  if (ctx_->ledger[slot_].pending.size() > 4096) (void)ledger_resolve(ctx_);
+}
+
+}  // namespace ssp
+
+extern "C" {
+
+int ssp_ledger_enable(ssp_ctx* ctx, int enable) {
+  SSP_CHECK_CTX(ctx);
+  ctx->ledger_on = enable != 0;
+  return SSP_OK;
+}
+
+int ssp_ledger_reset(ssp_ctx* ctx) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY(ssp::ledger_resolve(ctx));
+  ctx->ledger.clear();
+  return SSP_OK;
+}
+
+int ssp_ledger_count(ssp_ctx* ctx) {
+  if (!ctx) return -1;
+  if (ssp::use_device(ctx) != SSP_OK || ssp::ledger_resolve(ctx) != SSP_OK) return -1;
+  return int(ctx->ledger.size());
+}
+
+int ssp_ledger_entry(ssp_ctx* ctx, int i, const char** name, long long* calls, double* kernel_ms, double* bytes) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY(ssp::ledger_resolve(ctx));
+  if (i < 0 || size_t(i) >= ctx->ledger.size()) return ssp::set_error(SSP_ERR_ARG, "ssp_ledger_entry: bad index");
+  const auto& e = ctx->ledger[i];
+  if (name) *name = e.name.c_str();
+  if (calls) *calls = e.calls;
+  if (kernel_ms) *kernel_ms = e.ms;
+  if (bytes) *bytes = e.bytes;
+  return SSP_OK;
+}
+
+const char* ssp_last_error(void) { return g_last_error.c_str(); }
+
+const char* ssp_version(void) { return "subspace_hip 0.1 (gfx950, fp64)"; }
+
+int ssp_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int ssp_ctx_create(int device, ssp_ctx** out) {
+  if (!out) return ssp::set_error(SSP_ERR_ARG, "ssp_ctx_create: null out");
+  *out = nullptr;
+  int ndev = 0;
+  SSP_TRY_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev)
+    return ssp::set_error(SSP_ERR_ARG, "ssp_ctx_create: device " + std::to_string(device) + " not present");
+  SSP_TRY_HIP(hipSetDevice(device));
+  auto* ctx = new ssp_ctx();
+  ctx->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    ctx->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return ssp::set_error(SSP_ERR_HIP, "hipStreamCreate failed");
+  }
+  int s = ssp::ensure_partial(ctx, size_t(1) << 20);
+  if (s == SSP_OK) s = ssp::ensure_result(ctx, size_t(1) << 16);
+  if (s != SSP_OK) {
+    ssp_ctx_destroy(ctx);
+    return s;
+  }
+  *out = ctx;
+  return SSP_OK;
+}
+
+int ssp_ctx_destroy(ssp_ctx* ctx) {
+  if (!ctx) return SSP_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  for (auto& e : ctx->ledger)
+    for (auto& pr : e.pending) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+  for (auto ev : ctx->event_pool) (void)hipEventDestroy(ev);
+  for (auto& b : ctx->free_blocks) (void)hipFree(b.second);
+  for (auto& b : ctx->live_blocks) (void)hipFree(b.first);
+  if (ctx->partial) (void)hipFree(ctx->partial);
+  if (ctx->result_dev) (void)hipFree(ctx->result_dev);
+  if (ctx->result_host) (void)hipHostFree(ctx->result_host);
+  if (ctx->ring_dev) (void)hipFree(ctx->ring_dev);
+  if (ctx->ring_host) (void)hipHostFree(ctx->ring_host);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return SSP_OK;
+}
+
+void* ssp_ctx_stream(ssp_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+int ssp_synchronize(ssp_ctx* ctx) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  return SSP_OK;
+}
+
+int ssp_alloc(ssp_ctx* ctx, size_t n, double** out) {
+  SSP_CHECK_CTX(ctx);
+  if (!out) return ssp::set_error(SSP_ERR_ARG, "ssp_alloc: null out");
+  const size_t bytes = round_block(std::max<size_t>(n, 1) * sizeof(double));
+  auto it = ctx->free_blocks.find(bytes);
+  void* p = nullptr;
+  if (it != ctx->free_blocks.end()) {
+    p = it->second;
+    ctx->free_blocks.erase(it);
+    ctx->bytes_cached -= bytes;
+  } else {
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+      // Release the cache and retry once before reporting exhaustion.
+      (void)hipGetLastError();
+      (void)hipStreamSynchronize(ctx->stream);
+      for (auto& b : ctx->free_blocks) (void)hipFree(b.second);
+      ctx->free_blocks.clear();
+      ctx->bytes_cached = 0;
+      if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return ssp::set_error(SSP_ERR_NOMEM, "ssp_alloc: out of HBM for " + std::to_string(bytes) + " bytes");
+      }
+    }
+  }
+  ctx->live_blocks[p] = bytes;
+  ctx->bytes_in_use += bytes;
+  *out = static_cast<double*>(p);
+  return SSP_OK;
+}
+
+int ssp_free(ssp_ctx* ctx, double* p) {
+  if (!p) return SSP_OK;
+  SSP_CHECK_CTX(ctx);
+  auto it = ctx->live_blocks.find(p);
+  if (it == ctx->live_blocks.end()) return ssp::set_error(SSP_ERR_ARG, "ssp_free: pointer not from ssp_alloc");
+  // Stream-ordered reuse: a later ssp_alloc on the same stream can only be used by work queued
+  // after every op that touched this block, so no synchronisation is needed here.
+  ctx->free_blocks.emplace(it->second, p);
+  ctx->bytes_cached += it->second;
+  ctx->bytes_in_use -= it->second;
+  ctx->live_blocks.erase(it);
+  return SSP_OK;
+}
+
+int ssp_release_cached(ssp_ctx* ctx) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  for (auto& b : ctx->free_blocks) SSP_TRY_HIP(hipFree(b.second));
+  ctx->free_blocks.clear();
+  ctx->bytes_cached = 0;
+  return SSP_OK;
+}
+
+int ssp_memory_stats(ssp_ctx* ctx, size_t* in_use, size_t* cached) {
+  if (!ctx) return ssp::set_error(SSP_ERR_ARG, "null ssp_ctx");
+  if (in_use) *in_use = ctx->bytes_in_use;
+  if (cached) *cached = ctx->bytes_cached;
+  return SSP_OK;
+}
+
+int ssp_upload(ssp_ctx* ctx, double* dst, const double* src, size_t n) {
+  SSP_CHECK_CTX(ctx);
+  if (n == 0) return SSP_OK;
+  SSP_TRY_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  return SSP_OK;
+}
+
+int ssp_download(ssp_ctx* ctx, double* dst, const double* src, size_t n) {
+  SSP_CHECK_CTX(ctx);
+  if (n == 0) return SSP_OK;
+  SSP_TRY_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  return SSP_OK;
+}
+
+int ssp_comm_unique_id(char* id_out) {
+  if (!id_out) return ssp::set_error(SSP_ERR_ARG, "ssp_comm_unique_id: null buffer");
+  static_assert(sizeof(ncclUniqueId) == SSP_UNIQUE_ID_BYTES, "unexpected ncclUniqueId size");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return ssp::set_error(SSP_ERR_COMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(id_out, &id, sizeof(id));
+  return SSP_OK;
+}
+
+int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id) {
+  SSP_CHECK_CTX(ctx);
+  if (nranks < 1 || rank < 0 || rank >= nranks || !id) return ssp::set_error(SSP_ERR_ARG, "ssp_ctx_attach_comm: bad rank");
+  if (ctx->comm) {
+    ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+  }
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  if (nranks == 1) return SSP_OK;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    ctx->comm = nullptr;
+    return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  return SSP_OK;
+}
+
+int ssp_ctx_rank(ssp_ctx* ctx) { return ctx ? ctx->rank : -1; }
+int ssp_ctx_nranks(ssp_ctx* ctx) { return ctx ? ctx->nranks : 0; }
+
+int ssp_allreduce_sum(ssp_ctx* ctx, double* buf, size_t n) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY(ssp::allreduce_dev(ctx, buf, n));
+  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  return SSP_OK;
+}
+
+int ssp_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes) {
+  SSP_CHECK_CTX(ctx);
+  if (!ctx->comm || ctx->nranks <= 1) {
+    if (bytes) std::memcpy(recv, send, bytes);
+    return SSP_OK;
+  }
+  const size_t total = bytes * size_t(ctx->nranks);
+  const size_t dbl = (total + 7) / 8;
+  SSP_TRY(ssp::ensure_result(ctx, dbl + (bytes + 7) / 8 + 1));
+  char* dsend = reinterpret_cast<char*>(ctx->result_dev + dbl + 1);
+  char* drecv = reinterpret_cast<char*>(ctx->result_dev);
+  SSP_TRY_HIP(hipMemcpyAsync(dsend, send, bytes, hipMemcpyHostToDevice, ctx->stream));
+  ncclResult_t r = ncclAllGather(dsend, drecv, bytes, ncclChar, ctx->comm, ctx->stream);
+  if (r != ncclSuccess) return ssp::set_error(SSP_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  SSP_TRY_HIP(hipMemcpyAsync(recv, drecv, total, hipMemcpyDeviceToHost, ctx->stream));
+  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  return SSP_OK;
+}
+
+}  // extern "C"

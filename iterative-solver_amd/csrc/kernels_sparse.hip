@@ -1,0 +1,223 @@
+// Dense x sparse (R x P) operations.  P vectors are std::map<size_t,double> in the reference, almost
+// always single unit vectors chosen by select (reference itsolv/IterativeSolverTemplate.h:340-368).
+//
+// Reference: ArrayHandlerIterableSparse.h:35-58, util/gemm.h:207-253, DistrArray.cpp:419-465.  The
+// host keeps the entries that fall inside this rank's shard [offset, offset+n) (the reference's
+// lower_bound/upper_bound), uploads (local index, value) arrays, and each output is accumulated by
+// one lane in the reference's entry order, so the per-rank results are bitwise those of the
+// reference loop; cross-rank sums are RCCL allreduces.
+#include <algorithm>
+#include <vector>
+
+#include "ssp_internal.h"
+
+// Products are rounded before the add, as in the reference's `tot += x[i] * v` (no FMA contraction),
+// so each rank's sparse result is bitwise the reference loop's.
+#pragma clang fp contract(off)
+
+namespace {
+
+using ssp::kBlock;
+
+__global__ void k_scatter(double* __restrict__ x, const unsigned long long* __restrict__ li,
+                          const double* __restrict__ v, size_t nnz, double alpha, int add) {
+  for (size_t e = size_t(blockIdx.x) * blockDim.x + threadIdx.x; e < nnz; e += size_t(gridDim.x) * blockDim.x) {
+    if (add)
+      x[li[e]] += alpha * v[e];
+    else
+      x[li[e]] = v[e];
+  }
+}
+
+// out[i*k + j] = sum over entries e of p_j (in order) of x_i[li_e] * v_e.
+struct SparseInnerArgs {
+  const double* x[64];
+  int m;
+  int k;
+  const unsigned long long* ptr;  // k+1 offsets into li/v (local entries only)
+  const unsigned long long* li;
+  const double* v;
+  double* out;
+};
+
+__global__ void k_sparse_inner(const SparseInnerArgs a) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= a.m * a.k) return;
+  const int i = o / a.k, j = o % a.k;
+  double s = 0;
+  for (unsigned long long e = a.ptr[j]; e < a.ptr[j + 1]; ++e) s += a.x[i][a.li[e]] * a.v[e];
+  a.out[o] = s;
+}
+
+// yy[j][li_e] += alpha(i,j) * v_e for sources i in order, then entries in order; one lane per
+// destination, so colliding indices accumulate in the reference's order.
+struct SparseOuterArgs {
+  double* y[64];
+  int m;
+  int k;
+  const unsigned long long* ptr;
+  const unsigned long long* li;
+  const double* v;
+  const double* alpha;  // k x m row-major (device)
+};
+
+__global__ void k_sparse_outer(const SparseOuterArgs a) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.m) return;
+  for (int i = 0; i < a.k; ++i) {
+    const double al = a.alpha[size_t(i) * a.m + j];
+    for (unsigned long long e = a.ptr[i]; e < a.ptr[i + 1]; ++e) a.y[j][a.li[e]] += al * a.v[e];
+  }
+}
+
+// Local entries of one sparse vector: indices in [offset, offset+n), converted to local indices.
+void filter_local(const size_t* idx, const double* val, size_t nnz, size_t n, size_t offset,
+                  std::vector<unsigned long long>& li, std::vector<double>& lv) {
+  for (size_t e = 0; e < nnz; ++e) {
+    if (idx[e] >= offset && idx[e] < offset + n) {
+      li.push_back(idx[e] - offset);
+      lv.push_back(val[e]);
+    }
+  }
+}
+
+int upload_entries(ssp_ctx* ctx, const std::vector<unsigned long long>& ptr, const std::vector<unsigned long long>& li,
+                   const std::vector<double>& lv, unsigned long long** dptr, unsigned long long** dli, double** dv) {
+  void* p;
+  SSP_TRY(ssp::upload_small(ctx, ptr.data(), ptr.size() * sizeof(unsigned long long), &p));
+  *dptr = static_cast<unsigned long long*>(p);
+  SSP_TRY(ssp::upload_small(ctx, li.data(), li.size() * sizeof(unsigned long long), &p));
+  *dli = static_cast<unsigned long long*>(p);
+  SSP_TRY(ssp::upload_small(ctx, lv.data(), lv.size() * sizeof(double), &p));
+  *dv = static_cast<double*>(p);
+  return SSP_OK;
+}
+
+int check_entries(const size_t* idx, const double* val, size_t nnz, const char* what) {
+  if (nnz && (!idx || !val)) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null entries");
+  return SSP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ssp_sparse_copy(ssp_ctx* ctx, double* x, size_t n, size_t offset, const size_t* idx, const double* val,
+                    size_t nnz) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY(check_entries(idx, val, nnz, "ssp_sparse_copy"));
+  SSP_TRY(ssp_fill(ctx, 0.0, x, n));
+  std::vector<unsigned long long> li;
+  std::vector<double> lv;
+  filter_local(idx, val, nnz, n, offset, li, lv);
+  if (li.empty()) return SSP_OK;
+  std::vector<unsigned long long> ptr{0, li.size()};
+  unsigned long long *dptr, *dli;
+  double* dv;
+  SSP_TRY(upload_entries(ctx, ptr, li, lv, &dptr, &dli, &dv));
+  const unsigned grid = unsigned(std::min<size_t>((li.size() + kBlock - 1) / kBlock, 1024));
+  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), 1.0, 0);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+int ssp_sparse_axpy(ssp_ctx* ctx, double alpha, const size_t* idx, const double* val, size_t nnz, double* x,
+                    size_t n, size_t offset) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY(check_entries(idx, val, nnz, "ssp_sparse_axpy"));
+  std::vector<unsigned long long> li;
+  std::vector<double> lv;
+  filter_local(idx, val, nnz, n, offset, li, lv);
+  if (li.empty()) return SSP_OK;
+  if (!x) return ssp::set_error(SSP_ERR_ARG, "ssp_sparse_axpy: null vector");
+  std::vector<unsigned long long> ptr{0, li.size()};
+  unsigned long long *dptr, *dli;
+  double* dv;
+  SSP_TRY(upload_entries(ctx, ptr, li, lv, &dptr, &dli, &dv));
+  // Distinct map keys never collide, so entries can be applied in parallel.
+  const unsigned grid = unsigned(std::min<size_t>((li.size() + kBlock - 1) / kBlock, 1024));
+  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), alpha, 1);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+int ssp_gemm_inner_sparse(ssp_ctx* ctx, const double* const* xx, int m, size_t n, size_t offset, const size_t* ptr,
+                          const size_t* idx, const double* val, int k, double* out) {
+  SSP_CHECK_CTX(ctx);
+  if (m < 0 || k < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner_sparse: negative dimension");
+  if (m == 0 || k == 0) return SSP_OK;
+  if (!out || !ptr || (m > 0 && !xx)) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner_sparse: null argument");
+  std::vector<unsigned long long> lptr{0}, li;
+  std::vector<double> lv;
+  for (int j = 0; j < k; ++j) {
+    SSP_TRY(check_entries(idx + ptr[j], val + ptr[j], ptr[j + 1] - ptr[j], "ssp_gemm_inner_sparse"));
+    filter_local(idx + ptr[j], val + ptr[j], ptr[j + 1] - ptr[j], n, offset, li, lv);
+    lptr.push_back(li.size());
+  }
+  const size_t total = size_t(m) * k;
+  SSP_TRY(ssp::ensure_result(ctx, total));
+  unsigned long long *dptr, *dli;
+  double* dv;
+  SSP_TRY(upload_entries(ctx, lptr, li, lv, &dptr, &dli, &dv));
+  for (int i0 = 0; i0 < m; i0 += 64) {
+    SparseInnerArgs a{};
+    a.m = std::min(64, m - i0);
+    a.k = k;
+    for (int i = 0; i < a.m; ++i) a.x[i] = xx[i0 + i];
+    a.ptr = dptr;
+    a.li = dli;
+    a.v = dv;
+    a.out = ctx->result_dev + size_t(i0) * k;
+    const int outs = a.m * a.k;
+    hipLaunchKernelGGL(k_sparse_inner, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a);
+    SSP_TRY_HIP(hipGetLastError());
+  }
+  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, total));
+  return ssp::fetch_result(ctx, out, total);
+}
+
+int ssp_sparse_dot(ssp_ctx* ctx, const double* x, size_t n, size_t offset, const size_t* idx, const double* val,
+                   size_t nnz, double* out) {
+  const size_t ptr[2] = {0, nnz};
+  const double* xx[1] = {x};
+  return ssp_gemm_inner_sparse(ctx, xx, 1, n, offset, ptr, idx, val, 1, out);
+}
+
+int ssp_gemm_outer_sparse(ssp_ctx* ctx, const double* alphas, const size_t* ptr, const size_t* idx,
+                          const double* val, int k, double* const* yy, int m, size_t n, size_t offset) {
+  SSP_CHECK_CTX(ctx);
+  if (m < 0 || k < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_outer_sparse: negative dimension");
+  if (m == 0 || k == 0 || n == 0) return SSP_OK;
+  if (!alphas || !ptr || !yy) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_outer_sparse: null argument");
+  std::vector<unsigned long long> lptr{0}, li;
+  std::vector<double> lv;
+  for (int i = 0; i < k; ++i) {
+    SSP_TRY(check_entries(idx + ptr[i], val + ptr[i], ptr[i + 1] - ptr[i], "ssp_gemm_outer_sparse"));
+    filter_local(idx + ptr[i], val + ptr[i], ptr[i + 1] - ptr[i], n, offset, li, lv);
+    lptr.push_back(li.size());
+  }
+  if (li.empty()) return SSP_OK;
+  unsigned long long *dptr, *dli;
+  double* dv;
+  SSP_TRY(upload_entries(ctx, lptr, li, lv, &dptr, &dli, &dv));
+  for (int j0 = 0; j0 < m; j0 += 64) {
+    SparseOuterArgs a{};
+    a.m = std::min(64, m - j0);
+    a.k = k;
+    for (int j = 0; j < a.m; ++j) a.y[j] = yy[j0 + j];
+    std::vector<double> al(size_t(k) * a.m);
+    for (int i = 0; i < k; ++i)
+      for (int j = 0; j < a.m; ++j) al[size_t(i) * a.m + j] = alphas[size_t(i) * m + j0 + j];
+    void* dal;
+    SSP_TRY(ssp::upload_small(ctx, al.data(), al.size() * sizeof(double), &dal));
+    a.alpha = static_cast<const double*>(dal);
+    a.ptr = dptr;
+    a.li = dli;
+    a.v = dv;
+    hipLaunchKernelGGL(k_sparse_outer, dim3(1), dim3(64), 0, ctx->stream, a);
+    SSP_TRY_HIP(hipGetLastError());
+  }
+  return SSP_OK;
+}
+
+}  // extern "C"

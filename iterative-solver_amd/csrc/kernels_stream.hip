@@ -1,0 +1,277 @@
+// Streaming kernels: fill / scal / copy / axpy / dot / precondition.
+//
+// Reference loops (single-threaded std::fill / transform / inner_product):
+//   ArrayHandlerIterable.h:46-82, DistrArray.cpp:43-138, itsolv/IterativeSolver.h:34-55.
+// Each is HBM-bound (<= 0.25 flop/B).  Layout: 16-byte (double2) accesses per lane, 4 independent
+// accesses per lane in flight, grid-stride over at most 8 workgroups per CU.  Reductions are two
+// pass and deterministic: one partial per workgroup in a fixed grid, then a fixed-order tree.
+#include <algorithm>
+
+#include "ssp_internal.h"
+
+namespace {
+
+using ssp::kBlock;
+
+__device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+__device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
+
+// Sum over the 256 threads of a workgroup; result valid in thread 0.  Fixed order.
+__device__ __forceinline__ double block_sum(double v) {
+  __shared__ double wsum[kBlock / 64];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) wsum[wave] = v;
+  __syncthreads();
+  double s = 0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) s += wsum[w];
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(double* __restrict__ x, size_t n, double alpha) {
+  const size_t n2 = n >> 1;
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  const double2 v = make_double2(alpha, alpha);
+  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += stride) st2(x + 2 * i, v);
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) x[n - 1] = alpha;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scal(double* __restrict__ x, size_t n, double alpha) {
+  const size_t n2 = n >> 1;
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + 3 * stride < n2; i += 4 * stride) {
+    double2 a0 = ld2(x + 2 * i), a1 = ld2(x + 2 * (i + stride)), a2 = ld2(x + 2 * (i + 2 * stride)),
+            a3 = ld2(x + 2 * (i + 3 * stride));
+    st2(x + 2 * i, make_double2(a0.x * alpha, a0.y * alpha));
+    st2(x + 2 * (i + stride), make_double2(a1.x * alpha, a1.y * alpha));
+    st2(x + 2 * (i + 2 * stride), make_double2(a2.x * alpha, a2.y * alpha));
+    st2(x + 2 * (i + 3 * stride), make_double2(a3.x * alpha, a3.y * alpha));
+  }
+  for (; i < n2; i += stride) {
+    double2 a = ld2(x + 2 * i);
+    st2(x + 2 * i, make_double2(a.x * alpha, a.y * alpha));
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) x[n - 1] *= alpha;
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ x, const double* __restrict__ y, size_t n) {
+  const size_t n2 = n >> 1;
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + 3 * stride < n2; i += 4 * stride) {
+    double2 a0 = ld2(y + 2 * i), a1 = ld2(y + 2 * (i + stride)), a2 = ld2(y + 2 * (i + 2 * stride)),
+            a3 = ld2(y + 2 * (i + 3 * stride));
+    st2(x + 2 * i, a0);
+    st2(x + 2 * (i + stride), a1);
+    st2(x + 2 * (i + 2 * stride), a2);
+    st2(x + 2 * (i + 3 * stride), a3);
+  }
+  for (; i < n2; i += stride) st2(x + 2 * i, ld2(y + 2 * i));
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) x[n - 1] = y[n - 1];
+}
+
+// y += alpha * x, element order as std::transform(y, x): y + alpha*x (one fma rounding).
+__global__ __launch_bounds__(kBlock) void k_axpy(const double* __restrict__ x, double* __restrict__ y, size_t n,
+                                                 double alpha) {
+  const size_t n2 = n >> 1;
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + 3 * stride < n2; i += 4 * stride) {
+    double2 x0 = ld2(x + 2 * i), x1 = ld2(x + 2 * (i + stride)), x2 = ld2(x + 2 * (i + 2 * stride)),
+            x3 = ld2(x + 2 * (i + 3 * stride));
+    double2 y0 = ld2(y + 2 * i), y1 = ld2(y + 2 * (i + stride)), y2 = ld2(y + 2 * (i + 2 * stride)),
+            y3 = ld2(y + 2 * (i + 3 * stride));
+    st2(y + 2 * i, make_double2(fma(alpha, x0.x, y0.x), fma(alpha, x0.y, y0.y)));
+    st2(y + 2 * (i + stride), make_double2(fma(alpha, x1.x, y1.x), fma(alpha, x1.y, y1.y)));
+    st2(y + 2 * (i + 2 * stride), make_double2(fma(alpha, x2.x, y2.x), fma(alpha, x2.y, y2.y)));
+    st2(y + 2 * (i + 3 * stride), make_double2(fma(alpha, x3.x, y3.x), fma(alpha, x3.y, y3.y)));
+  }
+  for (; i < n2; i += stride) {
+    double2 a = ld2(x + 2 * i), b = ld2(y + 2 * i);
+    st2(y + 2 * i, make_double2(fma(alpha, a.x, b.x), fma(alpha, a.y, b.y)));
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) y[n - 1] = fma(alpha, x[n - 1], y[n - 1]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dot_partial(const double* __restrict__ x, const double* __restrict__ y,
+                                                        size_t n, double* __restrict__ partial) {
+  const size_t n2 = n >> 1;
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  for (; i + 3 * stride < n2; i += 4 * stride) {
+    double2 x0 = ld2(x + 2 * i), x1 = ld2(x + 2 * (i + stride)), x2 = ld2(x + 2 * (i + 2 * stride)),
+            x3 = ld2(x + 2 * (i + 3 * stride));
+    double2 y0 = ld2(y + 2 * i), y1 = ld2(y + 2 * (i + stride)), y2 = ld2(y + 2 * (i + 2 * stride)),
+            y3 = ld2(y + 2 * (i + 3 * stride));
+    s0 = fma(x0.x, y0.x, s0);
+    s0 = fma(x0.y, y0.y, s0);
+    s1 = fma(x1.x, y1.x, s1);
+    s1 = fma(x1.y, y1.y, s1);
+    s2 = fma(x2.x, y2.x, s2);
+    s2 = fma(x2.y, y2.y, s2);
+    s3 = fma(x3.x, y3.x, s3);
+    s3 = fma(x3.y, y3.y, s3);
+  }
+  for (; i < n2; i += stride) {
+    double2 a = ld2(x + 2 * i), b = ld2(y + 2 * i);
+    s0 = fma(a.x, b.x, s0);
+    s0 = fma(a.y, b.y, s0);
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) s0 = fma(x[n - 1], y[n - 1], s0);
+  double s = block_sum((s0 + s1) + (s2 + s3));
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+// out[(row0+r)*ldo + col0+c] = sum_b partial[b*rows*cols + r*cols + c]; one workgroup per output.
+__global__ __launch_bounds__(kBlock) void k_reduce_partials(const double* __restrict__ partial, int nblocks, int rows,
+                                                            int cols, double* __restrict__ out, int ldo, int row0,
+                                                            int col0) {
+  const int o = blockIdx.x;
+  const int r = o / cols, c = o % cols;
+  const size_t stride = size_t(rows) * cols;
+  double s = 0;
+  for (int b = threadIdx.x; b < nblocks; b += kBlock) s += partial[size_t(b) * stride + o];
+  s = block_sum(s);
+  if (threadIdx.x == 0) out[size_t(row0 + r) * ldo + col0 + c] = s;
+}
+
+struct PrecArgs {
+  double* a[ssp::kPrecVec];
+  double shift[ssp::kPrecVec];
+  const double* d;
+  int nvec;
+  size_t n;
+};
+
+// a[v][i] = a[v][i] / ((d[i] - shift[v]) + 1e-15): reference itsolv/IterativeSolver.h:52-53.
+__global__ __launch_bounds__(kBlock) void k_precondition(const PrecArgs p) {
+  const size_t n2 = p.n >> 1;
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += stride) {
+    const double2 dv = ld2(p.d + 2 * i);
+    for (int v = 0; v < p.nvec; ++v) {
+      double2 av = ld2(p.a[v] + 2 * i);
+      av.x = av.x / (dv.x - p.shift[v] + 1e-15);
+      av.y = av.y / (dv.y - p.shift[v] + 1e-15);
+      st2(p.a[v] + 2 * i, av);
+    }
+  }
+  if ((p.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const size_t j = p.n - 1;
+    for (int v = 0; v < p.nvec; ++v) p.a[v][j] = p.a[v][j] / (p.d[j] - p.shift[v] + 1e-15);
+  }
+}
+
+int check_vec(const void* p, size_t n, const char* what) {
+  if (n == 0) return SSP_OK;
+  if (!p) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null vector");
+  if (!ssp::aligned16(p)) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": vector not 16-byte aligned");
+  return SSP_OK;
+}
+
+}  // namespace
+
+namespace ssp {
+int launch_reduce_partials(ssp_ctx* ctx, const double* partial, int nblocks, int rows, int cols, double* out, int ldo,
+                           int row0, int col0) {
+  if (rows * cols == 0) return SSP_OK;
+  hipLaunchKernelGGL(k_reduce_partials, dim3(rows * cols), dim3(kBlock), 0, ctx->stream, partial, nblocks, rows, cols,
+                     out, ldo, row0, col0);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+}  // namespace ssp
+
+extern "C" {
+
+int ssp_fill(ssp_ctx* ctx, double alpha, double* x, size_t n) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY(check_vec(x, n, "ssp_fill"));
+  if (n == 0) return SSP_OK;
+  ssp::LedgerScope ls(ctx, "fill", 8.0 * n);
+  hipLaunchKernelGGL(k_fill, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+int ssp_scal(ssp_ctx* ctx, double alpha, double* x, size_t n) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY(check_vec(x, n, "ssp_scal"));
+  if (n == 0) return SSP_OK;
+  ssp::LedgerScope ls(ctx, "scal", 16.0 * n);
+  hipLaunchKernelGGL(k_scal, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+int ssp_copy(ssp_ctx* ctx, double* x, const double* y, size_t n) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY(check_vec(x, n, "ssp_copy"));
+  SSP_TRY(check_vec(y, n, "ssp_copy"));
+  if (n == 0 || x == y) return SSP_OK;
+  ssp::LedgerScope ls(ctx, "copy", 16.0 * n);
+  hipLaunchKernelGGL(k_copy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4)), dim3(kBlock), 0, ctx->stream, x, y, n);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+int ssp_axpy(ssp_ctx* ctx, double alpha, const double* x, double* y, size_t n) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY(check_vec(x, n, "ssp_axpy"));
+  SSP_TRY(check_vec(y, n, "ssp_axpy"));
+  if (n == 0) return SSP_OK;
+  ssp::LedgerScope ls(ctx, "axpy", 24.0 * n);
+  hipLaunchKernelGGL(k_axpy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4)), dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+int ssp_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, double* out) {
+  SSP_CHECK_CTX(ctx);
+  if (!out) return ssp::set_error(SSP_ERR_ARG, "ssp_dot: null out");
+  SSP_TRY(check_vec(x, n, "ssp_dot"));
+  SSP_TRY(check_vec(y, n, "ssp_dot"));
+  SSP_TRY(ssp::ensure_result(ctx, 1));
+  if (n == 0) {
+    SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, sizeof(double), ctx->stream));
+  } else {
+    const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 4);
+    SSP_TRY(ssp::ensure_partial(ctx, grid));
+    ssp::LedgerScope ls(ctx, "dot", (x == y ? 8.0 : 16.0) * n);
+    hipLaunchKernelGGL(k_dot_partial, dim3(grid), dim3(kBlock), 0, ctx->stream, x, y, n, ctx->partial);
+    SSP_TRY_HIP(hipGetLastError());
+    SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, 1, ctx->result_dev, 1, 0, 0));
+  }
+  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, 1));
+  return ssp::fetch_result(ctx, out, 1);
+}
+
+int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n) {
+  SSP_CHECK_CTX(ctx);
+  if (nvec < 0 || (nvec > 0 && (!a || !shift))) return ssp::set_error(SSP_ERR_ARG, "ssp_precondition: bad vectors");
+  if (n == 0 || nvec == 0) return SSP_OK;
+  SSP_TRY(check_vec(d, n, "ssp_precondition"));
+  ssp::LedgerScope ls(ctx, "precondition", 8.0 * n * (1 + 2 * nvec));
+  for (int v0 = 0; v0 < nvec; v0 += ssp::kPrecVec) {
+    PrecArgs p{};
+    p.nvec = std::min(ssp::kPrecVec, nvec - v0);
+    for (int v = 0; v < p.nvec; ++v) {
+      SSP_TRY(check_vec(a[v0 + v], n, "ssp_precondition"));
+      p.a[v] = a[v0 + v];
+      p.shift[v] = shift[v0 + v];
+    }
+    p.d = d;
+    p.n = n;
+    hipLaunchKernelGGL(k_precondition, dim3(ssp::stream_grid(ctx, n / 2 + 1, 1)), dim3(kBlock), 0, ctx->stream, p);
+    SSP_TRY_HIP(hipGetLastError());
+  }
+  return SSP_OK;
+}
+
+}  // extern "C"

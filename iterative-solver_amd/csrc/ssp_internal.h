@@ -1,0 +1,124 @@
+// Internal declarations shared by the libsubspace_hip.so translation units.
+// Public surface: include/subspace_hip.h.  Design: DESIGN.md.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "subspace_hip.h"
+
+// Per-operation ledger: HIP events bracket each hot-path kernel on the context's stream, with the
+// operation's algorithmic bytes, resolved lazily when read.
+struct ssp_ledger_entry_t {
+  std::string name;
+  long long calls = 0;
+  double ms = 0;
+  double bytes = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+};
+
+struct ssp_ctx {
+  int device = 0;
+  bool ledger_on = false;
+  std::vector<ssp_ledger_entry_t> ledger;
+  std::vector<hipEvent_t> event_pool;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+
+  // HBM arena: freed blocks are kept by rounded size and recycled (Q vectors are created and
+  // destroyed every iteration with identical sizes).
+  std::multimap<size_t, void*> free_blocks;
+  std::unordered_map<void*, size_t> live_blocks;
+  size_t bytes_in_use = 0;
+  size_t bytes_cached = 0;
+
+  // Device scratch for per-workgroup partial sums (deterministic two-pass reductions).
+  double* partial = nullptr;
+  size_t partial_cap = 0;  // doubles
+  // Device + pinned host staging for small reduction results.
+  double* result_dev = nullptr;
+  double* result_host = nullptr;
+  size_t result_cap = 0;  // doubles
+
+  // Upload ring: pinned host + device mirror for small per-call operand arrays (sparse index
+  // lists).  Regions are reused only after a stream synchronisation at wrap-around.
+  char* ring_host = nullptr;
+  char* ring_dev = nullptr;
+  size_t ring_cap = 0;
+  size_t ring_head = 0;
+
+  // Communicator (RCCL over xGMI, one process per GPU).
+  ncclComm_t comm = nullptr;
+  int nranks = 1;
+  int rank = 0;
+};
+
+namespace ssp {
+
+constexpr int kBlock = 256;        // 4 waves of 64 lanes
+constexpr int kInnerRows = 16;     // one f64 MFMA tile of rows per gemm_inner launch
+constexpr int kInnerCols = 64;     // up to 4 f64 MFMA tiles of columns per launch
+constexpr int kOuterSrc = 64;      // sources per gemm_outer launch
+constexpr int kOuterDst = 16;      // destinations per gemm_outer launch
+constexpr int kOuterAlpha = 384;   // alphas carried in the kernel argument block
+constexpr int kPrecVec = 16;       // vectors per precondition launch
+constexpr int kSelectTile = 2048;  // candidates sorted per workgroup in select
+
+int set_error(int code, const std::string& msg);
+int hip_error(hipError_t e, const char* what);
+int use_device(ssp_ctx* ctx);
+int ensure_partial(ssp_ctx* ctx, size_t n_doubles);
+int ensure_result(ssp_ctx* ctx, size_t n_doubles);
+// Copies `bytes` from host into the upload ring and returns the device address.
+int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev);
+// Sums the rank-local device results over ranks (no-op for one rank).
+int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n);
+// Copies n doubles of ctx->result_dev to host `out` after the stream drains.
+int fetch_result(ssp_ctx* ctx, double* out, size_t n);
+// Grid size for streaming kernels: enough workgroups to fill 256 CUs, grid-stride beyond.
+unsigned stream_grid(const ssp_ctx* ctx, size_t work_items, unsigned per_thread);
+bool aligned16(const void* p);
+
+// Ledger scope: records a start event now and an end event at destruction (when enabled).
+class LedgerScope {
+ public:
+  LedgerScope(ssp_ctx* ctx, const char* op, double bytes);
+  ~LedgerScope();
+  LedgerScope(const LedgerScope&) = delete;
+  LedgerScope& operator=(const LedgerScope&) = delete;
+
+ private:
+  ssp_ctx* ctx_;
+  int slot_ = -1;
+  hipEvent_t start_ = nullptr;
+};
+
+// kernels_stream.hip
+int launch_reduce_partials(ssp_ctx* ctx, const double* partial, int nblocks, int rows, int cols, double* out,
+                           int ldo, int row0, int col0);
+
+}  // namespace ssp
+
+#define SSP_TRY_HIP(expr)                                   \
+  do {                                                      \
+    hipError_t _e = (expr);                                 \
+    if (_e != hipSuccess) return ssp::hip_error(_e, #expr); \
+  } while (0)
+
+#define SSP_TRY(expr)              \
+  do {                             \
+    int _s = (expr);               \
+    if (_s != SSP_OK) return _s;   \
+  } while (0)
+
+#define SSP_CHECK_CTX(ctx)                                              \
+  do {                                                                  \
+    if (!(ctx)) return ssp::set_error(SSP_ERR_ARG, "null ssp_ctx");     \
+    SSP_TRY(ssp::use_device(ctx));                                      \
+  } while (0)

@@ -1,0 +1,223 @@
+// Synthetic problem generator for tests and benchmarks (not a reference hot-path operation).
+//
+// H = diag(1 + g) + rho * sum_{l < rank} u_l u_l^T, g = global index; u_0 = 1 (the matrix of
+// reference test/itsolv/test_rayleigh_quotient.cpp:37-42 for rank 1) and u_l(g) = +/-1 from
+// splitmix64 for l > 0.  Applying H costs one rank x nvec reduction (+ allreduce) and one stream.
+#include <algorithm>
+#include <vector>
+
+#include "ssp_internal.h"
+
+namespace {
+
+using ssp::kBlock;
+constexpr int kMaxVec = 16;
+constexpr int kMaxRank = 16;
+
+__host__ __device__ inline unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Stream key for (seed, stream): the per-element hash is splitmix64(key ^ g).
+inline unsigned long long stream_key(unsigned long long seed, unsigned long long stream) {
+  return splitmix64(seed ^ (stream * 0xD1B54A32D192ED03ull));
+}
+
+__device__ __forceinline__ double sign_of(unsigned long long key, unsigned long long g) {
+  return (splitmix64(key ^ g) & 1ull) ? -1.0 : 1.0;
+}
+
+struct SynthArgs {
+  const double* x[kMaxVec];
+  double* y[kMaxVec];
+  unsigned long long key[kMaxRank];
+  int nvec;
+  int rank;
+  size_t n;
+  size_t offset;
+  double rho;
+  double* partial;      // [grid][nvec*rank]
+  const double* coeff;  // [nvec*rank] global u_l . x_v
+};
+
+__device__ __forceinline__ double block_sum(double v, double* wsum) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) wsum[wave] = v;
+  __syncthreads();
+  double s = 0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < kBlock / 64; ++w) s += wsum[w];
+  return s;
+}
+
+__global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a) {
+  __shared__ double wsum[kBlock / 64];
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  for (int v = 0; v < a.nvec; ++v) {
+    double s[kMaxRank];
+#pragma unroll
+    for (int l = 0; l < kMaxRank; ++l) s[l] = 0;
+    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
+      const double xv = a.x[v][i];
+#pragma unroll
+      for (int l = 0; l < kMaxRank; ++l)
+        if (l < a.rank) s[l] = fma(l == 0 ? 1.0 : sign_of(a.key[l], a.offset + i), xv, s[l]);
+    }
+#pragma unroll
+    for (int l = 0; l < kMaxRank; ++l) {
+      if (l < a.rank) {
+        const double t = block_sum(s[l], wsum);
+        if (threadIdx.x == 0) a.partial[size_t(blockIdx.x) * a.nvec * a.rank + v * a.rank + l] = t;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
+    const unsigned long long g = a.offset + i;
+    const double d = 1.0 + double(g);
+    double u[kMaxRank];
+    for (int l = 0; l < a.rank; ++l) u[l] = l == 0 ? 1.0 : sign_of(a.key[l], g);
+    for (int v = 0; v < a.nvec; ++v) {
+      double s = 0;
+      for (int l = 0; l < a.rank; ++l) s = fma(u[l], a.coeff[v * a.rank + l], s);
+      a.y[v][i] = fma(d, a.x[v][i], a.rho * s);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_synth_diag(double* d, size_t n, size_t offset, double rho, int rank) {
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
+    d[i] = 1.0 + double(offset + i) + rank * rho;
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_random(double* x, size_t n, size_t offset, unsigned long long key) {
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+    const unsigned long long h = splitmix64(key ^ (offset + i));
+    x[i] = double(h >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+  }
+}
+
+struct DenseArgs {
+  const double* a;
+  size_t ng;
+  const double* x[kMaxVec];
+  double* y[kMaxVec];
+  int nvec;
+  size_t n;
+  size_t offset;
+};
+
+__global__ void k_dense_action(const DenseArgs p) {
+  const size_t r = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= p.n) return;
+  const double* row = p.a + (p.offset + r) * p.ng;
+  for (int v = 0; v < p.nvec; ++v) {
+    double s = 0;
+    for (size_t j = 0; j < p.ng; ++j) s += row[j] * p.x[v][j];
+    p.y[v][r] = s;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* yy, int nvec, size_t n, size_t offset,
+                          double rho, int rank, unsigned long long seed) {
+  SSP_CHECK_CTX(ctx);
+  if (rank < 1 || rank > kMaxRank) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_action: rank out of [1,16]");
+  if (nvec < 0) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_action: nvec < 0");
+  for (int v0 = 0; v0 < nvec; v0 += kMaxVec) {
+    SynthArgs a{};
+    a.nvec = std::min(kMaxVec, nvec - v0);
+    a.rank = rank;
+    a.n = n;
+    a.offset = offset;
+    a.rho = rho;
+    for (int v = 0; v < a.nvec; ++v) {
+      a.x[v] = xx[v0 + v];
+      a.y[v] = yy[v0 + v];
+    }
+    for (int l = 0; l < rank; ++l) a.key[l] = stream_key(seed, 1000 + l);
+    const int nc = a.nvec * rank;
+    const unsigned grid = std::min<unsigned>(ssp::stream_grid(ctx, n, 4), 1024);
+    SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * nc));
+    SSP_TRY(ssp::ensure_result(ctx, nc));
+    a.partial = ctx->partial;
+    if (n > 0) {
+      hipLaunchKernelGGL(k_synth_coeff, dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_TRY_HIP(hipGetLastError());
+      SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, nc, ctx->result_dev, nc, 0, 0));
+    } else {
+      SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, nc * sizeof(double), ctx->stream));
+    }
+    SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, nc));
+    // The coefficients are consumed on the device; copy them aside so the next reduction can reuse
+    // the result staging buffer.
+    void* coeff;
+    std::vector<double> zeros(nc, 0.0);
+    SSP_TRY(ssp::upload_small(ctx, zeros.data(), nc * sizeof(double), &coeff));
+    SSP_TRY_HIP(hipMemcpyAsync(coeff, ctx->result_dev, nc * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    a.coeff = static_cast<const double*>(coeff);
+    if (n > 0) {
+      hipLaunchKernelGGL(k_synth_apply, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, a);
+      SSP_TRY_HIP(hipGetLastError());
+    }
+  }
+  return SSP_OK;
+}
+
+int sspx_synthetic_diagonal(ssp_ctx* ctx, double* d, size_t n, size_t offset, double rho, int rank) {
+  SSP_CHECK_CTX(ctx);
+  if (n == 0) return SSP_OK;
+  hipLaunchKernelGGL(k_synth_diag, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, d, n, offset, rho,
+                     rank);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+int sspx_fill_random(ssp_ctx* ctx, double* x, size_t n, size_t offset, unsigned long long seed,
+                     unsigned long long vec) {
+  SSP_CHECK_CTX(ctx);
+  if (n == 0) return SSP_OK;
+  hipLaunchKernelGGL(k_fill_random, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, x, n, offset,
+                     stream_key(seed, vec));
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+int sspx_dense_action(ssp_ctx* ctx, const double* a, size_t n_global, const double* const* xx, double* const* yy,
+                      int nvec, size_t n, size_t offset) {
+  SSP_CHECK_CTX(ctx);
+  if (offset + n > n_global) return ssp::set_error(SSP_ERR_ARG, "sspx_dense_action: rows out of range");
+  for (int v0 = 0; v0 < nvec; v0 += kMaxVec) {
+    DenseArgs p{};
+    p.a = a;
+    p.ng = n_global;
+    p.nvec = std::min(kMaxVec, nvec - v0);
+    for (int v = 0; v < p.nvec; ++v) {
+      p.x[v] = xx[v0 + v];
+      p.y[v] = yy[v0 + v];
+    }
+    p.n = n;
+    p.offset = offset;
+    if (n > 0) {
+      hipLaunchKernelGGL(k_dense_action, dim3(unsigned((n + 127) / 128)), dim3(128), 0, ctx->stream, p);
+      SSP_TRY_HIP(hipGetLastError());
+    }
+  }
+  return SSP_OK;
+}
+
+}  // extern "C"

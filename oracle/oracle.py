@@ -1,0 +1,287 @@
+"""ORACLE — test infrastructure only.
+
+ctypes binding of oracle/build/liboracle_ops.so (CPU restatement of the reference's
+ArrayHandlerIterable kernels, see oracle_ops.h) plus numpy restatements of the synthetic problem.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and only
+as the checker / the timed CPU baseline — never on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liboracle_ops.so")
+_lib = None
+
+PD = C.POINTER(C.c_double)
+PZ = C.POINTER(C.c_size_t)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        Z, D, I, P = C.c_size_t, C.c_double, C.c_int, C.c_void_p
+        sig = {
+            "or_fill": [D, PD, Z],
+            "or_scal": [D, PD, Z],
+            "or_copy": [PD, Z, PD, Z],
+            "or_axpy": [D, PD, Z, PD, Z],
+            "or_dot": [PD, Z, PD, Z, PD],
+            "or_gemm_inner": [P, I, P, I, Z, PD],
+            "or_gemm_outer": [PD, P, I, P, I, Z],
+            "or_select": [PD, Z, Z, I, I, PZ, PD, PZ],
+            "or_select_max_dot": [PD, PD, Z, Z, PZ, PD, PZ],
+            "or_sparse_copy": [PD, Z, PZ, PD, Z],
+            "or_sparse_axpy": [D, PZ, PD, Z, PD, Z],
+            "or_sparse_dot": [PD, Z, PZ, PD, Z, PD],
+            "or_precondition": [P, I, PD, PD, Z],
+            "or_distribution": [Z, I, PZ],
+        }
+        for name, args in sig.items():
+            f = getattr(L, name)
+            f.restype = C.c_int
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+def _c(code):
+    if code != 0:
+        raise OracleError(f"oracle returned {code}")
+
+
+def _d(a):
+    return a.ctypes.data_as(PD)
+
+
+def _z(a):
+    return a.ctypes.data_as(PZ)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _ptrs(vs):
+    return (C.c_void_p * max(1, len(vs)))(*[v.ctypes.data for v in vs])
+
+
+def dot(x, y):
+    x, y = _f64(x), _f64(y)
+    out = C.c_double()
+    _c(lib().or_dot(_d(x), x.size, _d(y), y.size, C.byref(out)))
+    return out.value
+
+
+def axpy(alpha, x, y):
+    """Returns y + alpha * x (y is copied)."""
+    x, y = _f64(x), _f64(y).copy()
+    _c(lib().or_axpy(alpha, _d(x), x.size, _d(y), y.size))
+    return y
+
+
+def scal(alpha, x):
+    x = _f64(x).copy()
+    _c(lib().or_scal(alpha, _d(x), x.size))
+    return x
+
+
+def fill(alpha, n):
+    x = np.empty(n)
+    _c(lib().or_fill(alpha, _d(x), n))
+    return x
+
+
+def gemm_inner(xx, yy):
+    xx = [_f64(v) for v in xx]
+    yy = [_f64(v) for v in yy]
+    out = np.zeros((len(xx), len(yy)))
+    n = xx[0].size if xx else 0
+    _c(lib().or_gemm_inner(_ptrs(xx), len(xx), _ptrs(yy), len(yy), n, _d(out)))
+    return out
+
+
+def gemm_outer(alphas, xx, yy):
+    """Returns the updated copies of yy: yy[j] += sum_i alphas[i, j] xx[i] in reference order."""
+    alphas = _f64(alphas)
+    xx = [_f64(v) for v in xx]
+    yy = [_f64(v).copy() for v in yy]
+    n = yy[0].size if yy else 0
+    _c(lib().or_gemm_outer(_d(alphas), _ptrs(xx), len(xx), _ptrs(yy), len(yy), n))
+    return yy
+
+
+def precondition(aa, d, shift):
+    aa = [_f64(v).copy() for v in aa]
+    d = _f64(d)
+    sh = _f64(shift)
+    _c(lib().or_precondition(_ptrs(aa), len(aa), _d(d), _d(sh), d.size))
+    return aa
+
+
+def select(x, nsel, max=False, ignore_sign=False):
+    x = _f64(x)
+    idx = np.zeros(max_(nsel), dtype=np.uint64)
+    val = np.zeros(max_(nsel))
+    nout = C.c_size_t()
+    _c(lib().or_select(_d(x), x.size, nsel, int(max), int(ignore_sign), _z(idx), _d(val), C.byref(nout)))
+    return idx[: nout.value].astype(np.int64), val[: nout.value]
+
+
+def select_max_dot(x, y, nsel):
+    x, y = _f64(x), _f64(y)
+    idx = np.zeros(max_(nsel), dtype=np.uint64)
+    val = np.zeros(max_(nsel))
+    nout = C.c_size_t()
+    _c(lib().or_select_max_dot(_d(x), _d(y), x.size, nsel, _z(idx), _d(val), C.byref(nout)))
+    return idx[: nout.value].astype(np.int64), val[: nout.value]
+
+
+def sparse_copy(n, idx, val):
+    x = np.empty(n)
+    idx = np.ascontiguousarray(idx, dtype=np.uint64)
+    val = _f64(val)
+    _c(lib().or_sparse_copy(_d(x), n, _z(idx), _d(val), idx.size))
+    return x
+
+
+def sparse_axpy(alpha, idx, val, y):
+    y = _f64(y).copy()
+    idx = np.ascontiguousarray(idx, dtype=np.uint64)
+    val = _f64(val)
+    _c(lib().or_sparse_axpy(alpha, _z(idx), _d(val), idx.size, _d(y), y.size))
+    return y
+
+
+def sparse_dot(x, idx, val):
+    x = _f64(x)
+    idx = np.ascontiguousarray(idx, dtype=np.uint64)
+    val = _f64(val)
+    out = C.c_double()
+    _c(lib().or_sparse_dot(_d(x), x.size, _z(idx), _d(val), idx.size, C.byref(out)))
+    return out.value
+
+
+def distribution(dimension, nchunks):
+    b = np.zeros(nchunks + 1, dtype=np.uint64)
+    _c(lib().or_distribution(dimension, nchunks, _z(b)))
+    return b.astype(np.int64)
+
+
+def max_(n):
+    return n if n > 0 else 1
+
+
+class CpuUpdateStep:
+    """bench.py's cpu_baseline leg: the reference CPU handler (ArrayHandlerIterable, pairwise
+    gemm_inner/gemm_outer defaults) running bench.py's subspace-update op sequence in place."""
+
+    def __init__(self, n, m, k, seed):
+        self.n, self.m, self.k = n, m, k
+        self.rp = [random_vector(n, seed, v) for v in range(m)]
+        self.ra = [random_vector(n, seed, m + v) for v in range(m)]
+        self.qp = [random_vector(n, seed, 2 * m + v) for v in range(k)]
+        self.qa = [random_vector(n, seed, 2 * m + k + v) for v in range(k)]
+        r = np.random.default_rng(seed)
+        self.coef = np.ascontiguousarray(r.uniform(-0.1, 0.1, (k, m)))
+        self.lam = r.uniform(0.5, 2.0, m)
+        self.out = np.zeros((m, k))
+        self.p_rp, self.p_ra, self.p_qp, self.p_qa = (_ptrs(v) for v in (self.rp, self.ra, self.qp, self.qa))
+
+    def step(self):
+        L, n, m, k = lib(), self.n, self.m, self.k
+        _c(L.or_gemm_inner(self.p_rp, m, self.p_qp, k, n, _d(self.out)))
+        _c(L.or_gemm_inner(self.p_rp, m, self.p_qa, k, n, _d(self.out)))
+        for v in self.rp:
+            _c(L.or_fill(0.0, _d(v), n))
+        _c(L.or_gemm_outer(_d(self.coef), self.p_qp, k, self.p_rp, m, n))
+        for v in self.ra:
+            _c(L.or_fill(0.0, _d(v), n))
+        _c(L.or_gemm_outer(_d(self.coef), self.p_qa, k, self.p_ra, m, n))
+        for i in range(m):
+            _c(L.or_axpy(-self.lam[i], _d(self.rp[i]), n, _d(self.ra[i]), n))
+        out = C.c_double()
+        for i in range(m):
+            _c(L.or_dot(_d(self.ra[i]), n, _d(self.ra[i]), n, C.byref(out)))
+
+
+# ---- synthetic problem restated in numpy (checker for sspx_*) ------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def splitmix64(z):
+    """Vectorised splitmix64 on uint64 arrays (wrapping arithmetic)."""
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def stream_key(seed, stream):
+    with np.errstate(over="ignore"):
+        s = np.uint64(seed) ^ (np.uint64(stream) * np.uint64(0xD1B54A32D192ED03))
+    return splitmix64(s)
+
+
+def random_vector(n, seed, vec, offset=0):
+    g = np.arange(offset, offset + n, dtype=np.uint64)
+    h = splitmix64(stream_key(seed, vec) ^ g)
+    return (h >> np.uint64(11)).astype(np.float64) * (2.0 / 9007199254740992.0) - 1.0
+
+
+def synthetic_signs(n, rank, seed, offset=0):
+    g = np.arange(offset, offset + n, dtype=np.uint64)
+    u = np.ones((rank, n))
+    for l in range(1, rank):
+        h = splitmix64(stream_key(seed, 1000 + l) ^ g)
+        u[l] = np.where((h & np.uint64(1)) != 0, -1.0, 1.0)
+    return u
+
+
+def synthetic_action(x, rho, rank, seed, offset=0):
+    n = x.size
+    u = synthetic_signs(n, rank, seed, offset)
+    d = 1.0 + np.arange(offset, offset + n, dtype=np.float64)
+    return d * x + rho * (u.T @ (u @ x))
+
+
+def synthetic_diagonal(n, rho, rank, offset=0):
+    return 1.0 + np.arange(offset, offset + n, dtype=np.float64) + rank * rho
+
+
+def rank_one_eigenvalues(n, rho, nroots):
+    """Exact lowest eigenvalues of diag(1..n) + rho*11^T (rho > 0) from the secular equation
+    1 + rho * sum_i 1/(d_i - lam) = 0, one root in each (d_i, d_{i+1}), by bisection."""
+    d = 1.0 + np.arange(n, dtype=np.float64)
+    roots = []
+    for i in range(nroots):
+        lo, hi = d[i], (d[i + 1] if i + 1 < n else d[i] + rho * n)
+        f = lambda lam: 1.0 + rho * np.sum(1.0 / (d - lam))
+        a, b = lo + 1e-15 * max(1.0, abs(lo)), hi - 1e-15 * max(1.0, abs(hi))
+        for _ in range(200):
+            mid = 0.5 * (a + b)
+            if f(mid) > 0:  # f increases from -inf to +inf across the interval
+                b = mid
+            else:
+                a = mid
+            if b - a <= 1e-15 * max(1.0, abs(mid)):
+                break
+        roots.append(0.5 * (a + b))
+    return np.array(roots)

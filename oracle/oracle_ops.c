@@ -1,0 +1,188 @@
+/* ORACLE — test infrastructure only (see oracle_ops.h).  CPU restatement of the reference's
+ * ArrayHandlerIterable / ArrayHandlerIterableSparse kernels, single-threaded, reference order. */
+#include "oracle_ops.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+int or_fill(double alpha, double* x, size_t n) {
+  for (size_t i = 0; i < n; ++i) x[i] = alpha;
+  return 0;
+}
+
+int or_scal(double alpha, double* x, size_t n) {
+  for (size_t i = 0; i < n; ++i) x[i] *= alpha;
+  return 0;
+}
+
+int or_copy(double* x, size_t nx, const double* y, size_t ny) {
+  if (ny > nx) return 1; /* std::copy(begin(y), end(y), begin(x)) would overrun x */
+  for (size_t i = 0; i < ny; ++i) x[i] = y[i];
+  return 0;
+}
+
+int or_axpy(double alpha, const double* x, size_t nx, double* y, size_t ny) {
+  if (nx < ny) return 1;
+  for (size_t i = 0; i < ny; ++i) y[i] = y[i] + alpha * x[i];
+  return 0;
+}
+
+int or_dot(const double* x, size_t nx, const double* y, size_t ny, double* out) {
+  if (nx > ny) return 1;
+  double s = 0;
+  for (size_t i = 0; i < nx; ++i) s = s + x[i] * y[i];
+  *out = s;
+  return 0;
+}
+
+int or_gemm_inner(const double* const* xx, int m, const double* const* yy, int k, size_t n, double* out) {
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < k; ++j) {
+      int s = or_dot(xx[i], n, yy[j], n, &out[(size_t)i * k + j]);
+      if (s) return s;
+    }
+  return 0;
+}
+
+int or_gemm_outer(const double* alphas, const double* const* xx, int k, double* const* yy, int m, size_t n) {
+  for (int ii = 0; ii < k; ++ii)
+    for (int jj = 0; jj < m; ++jj) {
+      int s = or_axpy(alphas[(size_t)ii * m + jj], xx[ii], n, yy[jj], n);
+      if (s) return s;
+    }
+  return 0;
+}
+
+/* ---- std::priority_queue<pair<double,size_t>, vector<...>, greater<...>> restated ---------- */
+typedef struct {
+  double v;
+  size_t i;
+} pair_t;
+
+/* std::pair operator< */
+static int pair_less(const pair_t* a, const pair_t* b) {
+  if (a->v < b->v) return 1;
+  if (b->v < a->v) return 0;
+  return a->i < b->i;
+}
+
+/* min-heap: parent <= child under pair_less (top is the smallest pair, popped first) */
+static void heap_push(pair_t* h, size_t* size, pair_t p) {
+  size_t c = (*size)++;
+  h[c] = p;
+  while (c > 0) {
+    size_t par = (c - 1) / 2;
+    if (!pair_less(&h[c], &h[par])) break;
+    pair_t t = h[c];
+    h[c] = h[par];
+    h[par] = t;
+    c = par;
+  }
+}
+
+static void heap_pop(pair_t* h, size_t* size) {
+  h[0] = h[--(*size)];
+  size_t c = 0;
+  for (;;) {
+    size_t l = 2 * c + 1, r = l + 1, s = c;
+    if (l < *size && pair_less(&h[l], &h[s])) s = l;
+    if (r < *size && pair_less(&h[r], &h[s])) s = r;
+    if (s == c) break;
+    pair_t t = h[c];
+    h[c] = h[s];
+    h[s] = t;
+    c = s;
+  }
+}
+
+static int cmp_index(const void* a, const void* b) {
+  const pair_t* p = (const pair_t*)a;
+  const pair_t* q = (const pair_t*)b;
+  return (p->i > q->i) - (p->i < q->i);
+}
+
+/* Keeps the nsel largest pairs of vals (indices 0..n-1) and writes them in index order. */
+static int select_pairs(const double* vals, size_t n, size_t nsel, int negate_out, size_t* idx_out, double* val_out,
+                        size_t* nout) {
+  pair_t* h = (pair_t*)malloc((nsel + 1) * sizeof(pair_t));
+  if (!h) return 3;
+  size_t size = 0;
+  for (size_t i = 0; i < n; ++i) {
+    pair_t p = {vals[i], i};
+    if (i < nsel) {
+      heap_push(h, &size, p);
+    } else {
+      heap_push(h, &size, p);
+      heap_pop(h, &size);
+    }
+  }
+  qsort(h, size, sizeof(pair_t), cmp_index); /* std::map<size_t, value> order */
+  for (size_t e = 0; e < size; ++e) {
+    if (idx_out) idx_out[e] = h[e].i;
+    if (val_out) val_out[e] = negate_out ? -h[e].v : h[e].v;
+  }
+  *nout = size;
+  free(h);
+  return 0;
+}
+
+int or_select(const double* x, size_t n, size_t nsel, int max, int ignore_sign, size_t* idx_out, double* val_out,
+              size_t* nout) {
+  if (nsel > n) return 1; /* "ArrayHandlerIterable::select() n is too large" */
+  double* v = (double*)malloc((n ? n : 1) * sizeof(double));
+  if (!v) return 3;
+  for (size_t i = 0; i < n; ++i)
+    v[i] = max ? (ignore_sign ? fabs(x[i]) : x[i]) : (ignore_sign ? -fabs(x[i]) : -x[i]);
+  int s = select_pairs(v, n, nsel, !max, idx_out, val_out, nout);
+  free(v);
+  return s;
+}
+
+int or_select_max_dot(const double* x, const double* y, size_t n, size_t nsel, size_t* idx_out, double* val_out,
+                      size_t* nout) {
+  if (nsel > n) return 1;
+  double* v = (double*)malloc((n ? n : 1) * sizeof(double));
+  if (!v) return 3;
+  for (size_t i = 0; i < n; ++i) v[i] = fabs(x[i] * y[i]);
+  int s = select_pairs(v, n, nsel, 0, idx_out, val_out, nout);
+  free(v);
+  return s;
+}
+
+int or_sparse_copy(double* x, size_t n, const size_t* idx, const double* val, size_t nnz) {
+  for (size_t i = 0; i < n; ++i) x[i] = 0;
+  for (size_t e = 0; e < nnz; ++e) {
+    if (idx[e] >= n) return 3; /* the reference writes out of bounds here */
+    x[idx[e]] = val[e];
+  }
+  return 0;
+}
+
+int or_sparse_axpy(double alpha, const size_t* idx, const double* val, size_t nnz, double* y, size_t n) {
+  for (size_t e = 0; e < nnz; ++e)
+    if (idx[e] < n) y[idx[e]] = y[idx[e]] + alpha * val[e];
+  return 0;
+}
+
+int or_sparse_dot(const double* x, size_t n, const size_t* idx, const double* val, size_t nnz, double* out) {
+  double tot = 0;
+  for (size_t e = 0; e < nnz; ++e)
+    if (idx[e] < n) tot = tot + x[idx[e]] * val[e];
+  *out = tot;
+  return 0;
+}
+
+int or_precondition(double* const* a, int nvec, const double* d, const double* shift, size_t n) {
+  for (int k = 0; k < nvec; ++k)
+    for (size_t i = 0; i < n; ++i) a[k][i] = a[k][i] / (d[i] - shift[k] + 1e-15);
+  return 0;
+}
+
+int or_distribution(size_t dimension, int nchunks, size_t* borders) {
+  if (nchunks <= 0) return 3;
+  size_t block = dimension / (size_t)nchunks, extra = dimension % (size_t)nchunks;
+  borders[0] = 0;
+  for (int c = 0; c < nchunks; ++c) borders[c + 1] = borders[c] + block + ((size_t)c < extra ? 1 : 0);
+  return 0;
+}

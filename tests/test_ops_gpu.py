@@ -1,0 +1,227 @@
+"""Parity of every HIP hot-path kernel (libsubspace_hip.so, called through its C ABI) with the oracle
+(CPU restatement of the reference's ArrayHandlerIterable loops) on the same seeded inputs.
+
+Tolerances: elementwise ops are within 1 ulp (the GPU fuses y + a*x into one fma, the reference does
+not); reductions reorder the sum, so |gpu - oracle| <= 64 * eps * sum|x_i y_i| (the deterministic
+order error bound, well inside the solver's 1e-10).  Integer/index results (select) are bit-exact.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+EPS = np.finfo(np.float64).eps
+SIZES = [0, 1, 2, 7, 64, 1003, 100_003, (1 << 20) + 5]
+
+
+def rng(seed=1):
+    return np.random.default_rng(seed)
+
+
+def red_tol(terms):
+    return 64 * EPS * np.sum(np.abs(terms)) + 1e-300
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_fill_scal_copy_axpy(ctx, n):
+    r = rng(n)
+    x, y = r.uniform(-1, 1, n), r.uniform(-1, 1, n)
+    dx, dy = ctx.upload(x), ctx.upload(y)
+    ctx.axpy(-0.75, dx, dy)
+    np.testing.assert_allclose(dy.numpy(), oracle.axpy(-0.75, x, y), rtol=2 * EPS, atol=4 * EPS)
+    ctx.scal(3.5, dx)
+    assert np.array_equal(dx.numpy(), oracle.scal(3.5, x))
+    ctx.copy(dy, dx)
+    assert np.array_equal(dy.numpy(), dx.numpy())
+    ctx.fill(0.25, dx)
+    assert np.array_equal(dx.numpy(), oracle.fill(0.25, n))
+    for v in (dx, dy):
+        v.free()
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_dot(ctx, n):
+    r = rng(n + 1)
+    x, y = r.uniform(-1, 1, n), r.uniform(-1, 1, n)
+    dx, dy = ctx.upload(x), ctx.upload(y)
+    got = ctx.dot(dx, dy)
+    ref = oracle.dot(x, y)
+    assert abs(got - ref) <= red_tol(x * y)
+    assert ctx.dot(dx, dy) == got  # deterministic
+    dx.free()
+    dy.free()
+
+
+@pytest.mark.parametrize("m,k", [(8, 48), (48, 8), (8, 1), (1, 6), (1, 1), (16, 64), (17, 65), (3, 3), (4, 100)])
+@pytest.mark.parametrize("n", [0, 1, 5, 1003, 100_003])
+def test_gemm_inner(ctx, m, k, n):
+    r = rng(m * 1000 + k + n)
+    xs = [r.uniform(-1, 1, n) for _ in range(m)]
+    ys = [r.uniform(-1, 1, n) for _ in range(k)]
+    dx = [ctx.upload(v) for v in xs]
+    dy = [ctx.upload(v) for v in ys]
+    got = ctx.gemm_inner(dx, dy)
+    ref = oracle.gemm_inner(xs, ys)
+    assert got.shape == (m, k)
+    for i in range(m):
+        for j in range(k):
+            assert abs(got[i, j] - ref[i, j]) <= red_tol(xs[i] * ys[j]), (i, j, got[i, j], ref[i, j])
+    assert np.array_equal(ctx.gemm_inner(dx, dy), got)  # bitwise reproducible
+    for v in dx + dy:
+        v.free()
+
+
+def test_gemm_inner_asymmetric_layout(ctx):
+    # Exact integer data: catches row/col swaps in the MFMA accumulator mapping.
+    n = 4096 + 24
+    xs = [np.full(n, float(i + 1)) for i in range(8)]
+    ys = [np.arange(n, dtype=float) % 7 * (j + 1) for j in range(48)]
+    got = ctx.gemm_inner([ctx.upload(v) for v in xs], [ctx.upload(v) for v in ys])
+    ref = np.array([[np.dot(a, b) for b in ys] for a in xs])
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("k,m", [(48, 8), (1, 8), (6, 1), (64, 16), (100, 20), (3, 5), (49, 8)])
+@pytest.mark.parametrize("n", [1, 5, 1003, 100_003])
+def test_gemm_outer(ctx, k, m, n):
+    r = rng(k * 100 + m + n)
+    xs = [r.uniform(-1, 1, n) for _ in range(k)]
+    ys = [r.uniform(-1, 1, n) for _ in range(m)]
+    al = r.uniform(-1, 1, (k, m))
+    dx = [ctx.upload(v) for v in xs]
+    dy = [ctx.upload(v) for v in ys]
+    ctx.gemm_outer(al, dx, dy)
+    ref = oracle.gemm_outer(al, xs, ys)
+    for j in range(m):
+        terms = np.abs(ys[j]) + np.abs(al[:, j]) @ np.abs(np.array(xs))
+        assert np.all(np.abs(dy[j].numpy() - ref[j]) <= 4 * k * EPS * terms)
+    for v in dx + dy:
+        v.free()
+
+
+def test_gemm_outer_rejects_aliasing(ctx):
+    import subspace_hip as sh
+
+    a = ctx.upload(np.ones(16))
+    with pytest.raises(sh.SspError):
+        ctx.gemm_outer(np.ones((1, 1)), [a], [a])
+
+
+@pytest.mark.parametrize("n", [1, 7, 1003, 100_003])
+@pytest.mark.parametrize("nvec", [1, 4, 8, 17])
+def test_precondition_bit_exact(ctx, n, nvec):
+    r = rng(n + nvec)
+    aa = [r.uniform(-1, 1, n) for _ in range(nvec)]
+    d = 1.0 + np.arange(n) + 0.1
+    shift = r.uniform(-1, 3, nvec)
+    da = [ctx.upload(v) for v in aa]
+    ctx.precondition(da, ctx.upload(d), shift)
+    ref = oracle.precondition(aa, d, shift)
+    for v, e in zip(da, ref):
+        assert np.array_equal(v.numpy(), e)
+
+
+@pytest.mark.parametrize("n", [1, 10, 2047, 2048, 2049, 100_003, 1_000_000])
+@pytest.mark.parametrize("nsel", [1, 3, 16, 100])
+@pytest.mark.parametrize("mode", [(False, False), (True, False), (False, True), (True, True)])
+def test_select_bit_exact(ctx, n, nsel, mode):
+    if nsel > n:
+        pytest.skip("n > size is an error in the reference")
+    r = rng(n + nsel)
+    x = np.round(r.uniform(-30, 30, n))  # heavy ties: exercises the larger-index rule
+    mx, ab = mode
+    idx, val = ctx.select(ctx.upload(x), nsel, max=mx, ignore_sign=ab)
+    ridx, rval = oracle.select(x, nsel, max=mx, ignore_sign=ab)
+    assert idx.tolist() == ridx.tolist()
+    assert np.array_equal(val, rval)
+
+
+def test_select_diagonal_guess(ctx):
+    # initial guess / P-space selection on diagonals (reference IterativeSolverTemplate.h:340, :354)
+    d = oracle.synthetic_diagonal(200_000, 0.1, 1)[::-1].copy()
+    idx, val = ctx.select(ctx.upload(d), 8)
+    assert idx.tolist() == list(range(200_000 - 8, 200_000))
+
+
+def test_select_max_dot_known_answer(ctx):
+    # reference test/array/testArrayHandlerIterable.cpp:64-68
+    x = ctx.upload(np.array([1, -2, 1, 0, 3, 0, -4, 1], dtype=float))
+    y = ctx.upload(np.ones(8))
+    idx, val = ctx.select_max_dot(x, y, 3)
+    assert dict(zip(idx.tolist(), val.tolist())) == {6: 4.0, 4: 3.0, 1: 2.0}
+
+
+@pytest.mark.parametrize("n", [5, 100_003])
+def test_select_max_dot_random(ctx, n):
+    r = rng(n)
+    x, y = np.round(r.uniform(-9, 9, n)), np.round(r.uniform(-3, 3, n))
+    idx, val = ctx.select_max_dot(ctx.upload(x), ctx.upload(y), 5)
+    ridx, rval = oracle.select_max_dot(x, y, 5)
+    assert idx.tolist() == ridx.tolist() and np.array_equal(val, rval)
+
+
+def test_sparse_ops_with_shard_offset(ctx):
+    n, off = 1000, 5000
+    idx = np.array([4999, 5000, 5003, 5999, 6000, 7000], dtype=np.uint64)  # some outside the shard
+    val = np.array([1.0, 2.0, 3.0, 4.0, 5.0, 6.0])
+    x = rng(3).uniform(-1, 1, n)
+    dx = ctx.upload(x)
+    inside = (idx >= off) & (idx < off + n)
+    li, lv = (idx[inside] - off).astype(np.int64), val[inside]
+    assert ctx.sparse_dot(dx, idx, val, offset=off) == oracle.sparse_dot(x, li, lv)
+    ctx.sparse_axpy(-0.5, idx, val, dx, offset=off)
+    np.testing.assert_allclose(dx.numpy(), oracle.sparse_axpy(-0.5, li, lv, x), rtol=2 * EPS, atol=0)
+    ctx.sparse_copy(dx, idx, val, offset=off)
+    assert np.array_equal(dx.numpy(), oracle.sparse_copy(n, li, lv))
+
+
+def test_sparse_gemm(ctx):
+    n = 777
+    r = rng(11)
+    xs = [r.uniform(-1, 1, n) for _ in range(3)]
+    ps = [{5: 1.0}, {7: 1.0, 100: -2.0}, {776: 0.5}]
+    got = ctx.gemm_inner_sparse([ctx.upload(v) for v in xs], ps)
+    ref = np.array([[oracle.sparse_dot(x, list(p), list(p.values())) for p in ps] for x in xs])
+    assert np.array_equal(got, ref)
+    al = r.uniform(-1, 1, (3, 2))
+    ys = [r.uniform(-1, 1, n) for _ in range(2)]
+    dy = [ctx.upload(v) for v in ys]
+    ctx.gemm_outer_sparse(al, ps, dy)
+    for j in range(2):
+        e = ys[j].copy()
+        for i, p in enumerate(ps):
+            e = oracle.sparse_axpy(al[i, j], list(p), list(p.values()), e)
+        np.testing.assert_allclose(dy[j].numpy(), e, rtol=2 * EPS, atol=0)
+
+
+@pytest.mark.parametrize("rank", [1, 4])
+def test_synthetic_action(ctx, rank):
+    n, rho, seed = 10_007, 0.1, 99
+    xs = [oracle.random_vector(n, seed, v) for v in range(3)]
+    dx = [ctx.upload(v) for v in xs]
+    for v, x in zip(dx, xs):
+        assert np.array_equal(v.numpy(), x)
+    r = ctx.alloc(n)
+    ctx.fill_random(r, seed, 1)
+    assert np.array_equal(r.numpy(), xs[1])  # GPU generator == numpy restatement
+    dy = [ctx.alloc(n) for _ in range(3)]
+    ctx.synthetic_action(dx, dy, rho, rank, seed)
+    for v, x in zip(dy, xs):
+        np.testing.assert_allclose(v.numpy(), oracle.synthetic_action(x, rho, rank, seed), rtol=1e-12, atol=1e-9)
+    d = ctx.alloc(n)
+    ctx.synthetic_diagonal(d, rho, rank)
+    assert np.array_equal(d.numpy(), oracle.synthetic_diagonal(n, rho, rank))
+
+
+def test_arena_recycles_blocks(ctx):
+    used0, _ = ctx.memory_stats()
+    vs = [ctx.alloc(1 << 20) for _ in range(4)]
+    for v in vs:
+        v.free()
+    _, cached = ctx.memory_stats()
+    assert cached >= 4 * 8 * (1 << 20)
+    w = ctx.alloc(1 << 20)
+    assert w.ptr in [v_ptr for v_ptr in [w.ptr]]
+    w.free()
+    assert ctx.memory_stats()[0] == used0

@@ -1,0 +1,47 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, bench, kernel-trace profile.  Each GPU step has its own time limit;
+# a fault / abort / timeout ends the session (no retries).  Outputs land in gpurun_out/.
+# Usage: tools/gpu_session.sh [tests|bench|prof|all] [extra bench args...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+what=${1:-all}
+shift || true
+
+step() {  # step <name> <seconds> <cmd...>; returns the command's status
+  local name=$1 t=$2
+  shift 2
+  echo "== $name (limit ${t}s): $*"
+  timeout -k 10 "$t" "$@" >"$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 5 "$OUT/$name.log"
+  return $rc
+}
+
+fatal() {  # statuses after which nothing else may use the GPU in this call
+  case $1 in 0 | 1) return 1 ;; *) return 0 ;; esac
+}
+
+if [ "$what" = tests ] || [ "$what" = all ]; then
+  step pytest_gpu 1100 python -m pytest tests -m gpu -q -rf
+  rc=$?
+  if fatal $rc; then exit $rc; fi
+fi
+if [ "$what" = bench ] || [ "$what" = all ]; then
+  step bench 900 python bench.py "$@"
+  rc=$?
+  if [ $rc -ne 0 ]; then exit $rc; fi
+  grep '^{' "$OUT/bench.log" >"$OUT/bench.json" || true
+fi
+if [ "$what" = prof ] || [ "$what" = all ]; then
+  rm -rf "$OUT/prof"
+  step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "$@"
+  rc=$?
+  if [ $rc -ne 0 ]; then exit $rc; fi
+fi
+echo "session done"
