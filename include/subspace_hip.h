@@ -138,6 +138,9 @@ int ssp_gemm_outer_sparse(ssp_ctx* ctx, const double* alphas, const size_t* ptr,
  * matrix of reference test/itsolv/test_rayleigh_quotient.cpp:37-42.  yy[v] = H xx[v]. */
 int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* yy, int nvec, size_t n,
                           size_t offset, double rho, int rank, unsigned long long seed);
+/* yy[v] += rho * sum_l w[v*rank + l] u_l  (the low-rank part of H applied to P-space vectors) */
+int sspx_synthetic_add_lowrank(ssp_ctx* ctx, double* const* yy, int nvec, size_t n, size_t offset, double rho,
+                               int rank, unsigned long long seed, const double* w);
 /* d[g] = H_gg = 1 + g + rank*rho */
 int sspx_synthetic_diagonal(ssp_ctx* ctx, double* d, size_t n, size_t offset, double rho, int rank);
 /* x[g] = uniform [-1,1) from splitmix64(seed, vec, g): G-independent benchmark data. */

@@ -94,6 +94,19 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
   }
 }
 
+// y[v][i] += rho * sum_l u_l(g) coeff[v*rank + l]
+__global__ __launch_bounds__(kBlock) void k_synth_add(const SynthArgs a) {
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
+    const unsigned long long g = a.offset + i;
+    for (int v = 0; v < a.nvec; ++v) {
+      double s = 0;
+      for (int l = 0; l < a.rank; ++l) s = fma(l == 0 ? 1.0 : sign_of(a.key[l], g), a.coeff[v * a.rank + l], s);
+      a.y[v][i] = fma(a.rho, s, a.y[v][i]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_synth_diag(double* d, size_t n, size_t offset, double rho, int rank) {
   const size_t stride = size_t(gridDim.x) * kBlock;
   for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
@@ -174,6 +187,29 @@ int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* 
       hipLaunchKernelGGL(k_synth_apply, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
     }
+  }
+  return SSP_OK;
+}
+
+int sspx_synthetic_add_lowrank(ssp_ctx* ctx, double* const* yy, int nvec, size_t n, size_t offset, double rho,
+                               int rank, unsigned long long seed, const double* w) {
+  SSP_CHECK_CTX(ctx);
+  if (rank < 1 || rank > kMaxRank) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_add_lowrank: rank out of [1,16]");
+  if (n == 0 || nvec <= 0) return SSP_OK;
+  for (int v0 = 0; v0 < nvec; v0 += kMaxVec) {
+    SynthArgs a{};
+    a.nvec = std::min(kMaxVec, nvec - v0);
+    a.rank = rank;
+    a.n = n;
+    a.offset = offset;
+    a.rho = rho;
+    for (int v = 0; v < a.nvec; ++v) a.y[v] = yy[v0 + v];
+    for (int l = 0; l < rank; ++l) a.key[l] = stream_key(seed, 1000 + l);
+    void* coeff;
+    SSP_TRY(ssp::upload_small(ctx, w + size_t(v0) * rank, size_t(a.nvec) * rank * sizeof(double), &coeff));
+    a.coeff = static_cast<const double*>(coeff);
+    hipLaunchKernelGGL(k_synth_add, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, a);
+    SSP_TRY_HIP(hipGetLastError());
   }
   return SSP_OK;
 }

@@ -1,0 +1,294 @@
+// libitsolv_hbm.so: the restated solvers (include/itsolv_hbm/solvers.h) over HBM vectors and the
+// HIP handlers, behind the C ABI of include/itsolv_hbm.h.  Problem actions run on the device
+// (sspx_* kernels), so R, Q and the diagonals never leave HBM during a solve.
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "itsolv_hbm.h"
+#include "itsolv_hbm/hbm_handlers.h"
+#include "itsolv_hbm/problems.h"
+
+using molpro::linalg::hbm::check;
+using molpro::linalg::hbm::Device;
+using molpro::linalg::hbm::SparseP;
+using molpro::linalg::hbm::Vec;
+using molpro::linalg::itsolv::CVecRef;
+using molpro::linalg::itsolv::Problem;
+using molpro::linalg::itsolv::VecRef;
+namespace pr = molpro::linalg::itsolv::problems;
+
+namespace {
+
+thread_local std::string g_error;
+
+std::shared_ptr<Device> borrow(ssp_ctx* ctx) {
+  // The caller owns the context; the Device must not destroy it.
+  return std::make_shared<Device>(ctx, true);
+}
+
+Vec zero_vec(const std::shared_ptr<Device>& dev, size_t n) {
+  Vec v(dev, n);
+  check(ssp_fill(dev->ctx(), 0.0, v.data(), v.local_size()), "ssp_fill");
+  return v;
+}
+
+std::vector<double*> ptrs(const VecRef<Vec>& v) {
+  std::vector<double*> p;
+  for (auto& x : v) p.push_back(x.get().data());
+  return p;
+}
+std::vector<const double*> cptrs(const CVecRef<Vec>& v) {
+  std::vector<const double*> p;
+  for (auto& x : v) p.push_back(x.get().data());
+  return p;
+}
+
+// H = diag(1+g) + rho sum_l u_l u_l^T, applied on the device.
+class SyntheticProblem : public Problem<Vec, SparseP> {
+ public:
+  SyntheticProblem(std::shared_ptr<Device> dev, const pr::SyntheticSpec& s) : m_dev(std::move(dev)), m_s(s) {}
+
+  bool diagonals(Vec& d) const override {
+    check(sspx_synthetic_diagonal(ctx(), d.data(), d.local_size(), d.offset(), m_s.rho, m_s.rank),
+          "sspx_synthetic_diagonal");
+    return true;
+  }
+  void action(const CVecRef<Vec>& params, const VecRef<Vec>& actions) const override {
+    if (params.empty()) return;
+    auto x = cptrs(params);
+    auto y = ptrs(actions);
+    const auto& v0 = params.front().get();
+    check(sspx_synthetic_action(ctx(), x.data(), y.data(), int(params.size()), v0.local_size(), v0.offset(), m_s.rho,
+                                m_s.rank, m_s.seed),
+          "sspx_synthetic_action");
+  }
+  // r = H (x - 1); value = 0 (unused by DIIS)
+  double residual(const Vec& x, Vec& r) const override {
+    Vec t(x);
+    Vec ones(m_dev, x.size());
+    check(ssp_fill(ctx(), 1.0, ones.data(), ones.local_size()), "ssp_fill");
+    check(ssp_axpy(ctx(), -1.0, ones.data(), t.data(), t.local_size()), "ssp_axpy");
+    const double* xp[1] = {t.data()};
+    double* yp[1] = {r.data()};
+    check(sspx_synthetic_action(ctx(), xp, yp, 1, t.local_size(), t.offset(), m_s.rho, m_s.rank, m_s.seed),
+          "sspx_synthetic_action");
+    return 0;
+  }
+  std::vector<double> pp_action_matrix(const std::vector<SparseP>& pp) const override {
+    std::vector<size_t> idx;
+    for (auto& p : pp) idx.push_back(p.begin()->first);
+    std::vector<double> m;
+    for (size_t i : idx)
+      for (size_t j : idx) m.push_back(m_s.h(i, j));
+    return m;
+  }
+  // actions[k] += sum_p c[k][p] H e_{i_p}: diagonal part as a sparse axpy, low-rank part on the device.
+  void p_action(const std::vector<std::vector<double>>& c, const CVecRef<SparseP>& pp,
+                const VecRef<Vec>& actions) const override {
+    for (size_t k = 0; k < c.size(); ++k) {
+      auto& a = actions[k].get();
+      std::vector<size_t> idx;
+      std::vector<double> val;
+      std::vector<double> w(size_t(m_s.rank), 0.0);
+      for (size_t p = 0; p < pp.size(); ++p) {
+        for (auto& [i, coef] : pp[p].get()) {
+          idx.push_back(i);
+          val.push_back((1.0 + double(i)) * coef * c[k][p]);
+          for (int l = 0; l < m_s.rank; ++l) w[size_t(l)] += c[k][p] * coef * m_s.u(l, i);
+        }
+      }
+      check(ssp_sparse_axpy(ctx(), 1.0, idx.data(), val.data(), idx.size(), a.data(), a.local_size(), a.offset()),
+            "ssp_sparse_axpy");
+      double* yp[1] = {a.data()};
+      check(sspx_synthetic_add_lowrank(ctx(), yp, 1, a.local_size(), a.offset(), m_s.rho, m_s.rank, m_s.seed, w.data()),
+            "sspx_synthetic_add_lowrank");
+    }
+  }
+
+ private:
+  ssp_ctx* ctx() const { return m_dev->ctx(); }
+  std::shared_ptr<Device> m_dev;
+  pr::SyntheticSpec m_s;
+};
+
+// Dense row-major H, single rank: H resident in HBM, action by a row-per-lane kernel.
+class DenseProblem : public Problem<Vec, SparseP> {
+ public:
+  DenseProblem(std::shared_ptr<Device> dev, const double* h, size_t n) : m_dev(std::move(dev)), m_h(h, h + n * n), m_n(n) {
+    if (m_dev->nranks() != 1) throw std::invalid_argument("dense fixture problems run on a single rank");
+    check(ssp_alloc(ctx(), n * n, &m_dh), "ssp_alloc");
+    check(ssp_upload(ctx(), m_dh, h, n * n), "ssp_upload");
+  }
+  ~DenseProblem() override { ssp_free(ctx(), m_dh); }
+  bool diagonals(Vec& d) const override {
+    std::vector<double> v(m_n);
+    for (size_t i = 0; i < m_n; ++i) v[i] = m_h[i * m_n + i];
+    d.set_local_values(v);
+    return true;
+  }
+  void action(const CVecRef<Vec>& params, const VecRef<Vec>& actions) const override {
+    if (params.empty()) return;
+    auto x = cptrs(params);
+    auto y = ptrs(actions);
+    check(sspx_dense_action(ctx(), m_dh, m_n, x.data(), y.data(), int(params.size()), m_n, 0), "sspx_dense_action");
+  }
+  double residual(const Vec& x, Vec& r) const override {
+    Vec t(x);
+    Vec ones(m_dev, x.size());
+    check(ssp_fill(ctx(), 1.0, ones.data(), m_n), "ssp_fill");
+    check(ssp_axpy(ctx(), -1.0, ones.data(), t.data(), m_n), "ssp_axpy");
+    const double* xp[1] = {t.data()};
+    double* yp[1] = {r.data()};
+    check(sspx_dense_action(ctx(), m_dh, m_n, xp, yp, 1, m_n, 0), "sspx_dense_action");
+    return 0;
+  }
+  std::vector<double> pp_action_matrix(const std::vector<SparseP>& pp) const override {
+    std::vector<double> m;
+    for (auto& a : pp)
+      for (auto& b : pp) m.push_back(m_h[a.begin()->first * m_n + b.begin()->first]);
+    return m;
+  }
+  void p_action(const std::vector<std::vector<double>>& c, const CVecRef<SparseP>& pp,
+                const VecRef<Vec>& actions) const override {
+    for (size_t k = 0; k < c.size(); ++k) {
+      std::vector<double> add(m_n, 0.0);
+      for (size_t p = 0; p < pp.size(); ++p)
+        for (auto& [i, coef] : pp[p].get())
+          for (size_t j = 0; j < m_n; ++j) add[j] += m_h[j * m_n + i] * coef * c[k][p];
+      Vec t(m_dev, m_n);
+      t.set_local_values(add);
+      auto& a = actions[k].get();
+      check(ssp_axpy(ctx(), 1.0, t.data(), a.data(), m_n), "ssp_axpy");
+    }
+  }
+
+ private:
+  ssp_ctx* ctx() const { return m_dev->ctx(); }
+  std::shared_ptr<Device> m_dev;
+  std::vector<double> m_h;
+  size_t m_n;
+  double* m_dh = nullptr;
+};
+
+template <class P>
+double residual_norm(const P& problem, const std::shared_ptr<Device>& dev, const Vec& x, double e) {
+  Vec ax(dev, x.size());
+  problem.action(CVecRef<Vec>{std::cref(x)}, VecRef<Vec>{std::ref(ax)});
+  check(ssp_axpy(dev->ctx(), -e, x.data(), ax.data(), ax.local_size()), "ssp_axpy");
+  double rr = 0, xx = 0;
+  check(ssp_dot(dev->ctx(), ax.data(), ax.data(), ax.local_size(), &rr), "ssp_dot");
+  check(ssp_dot(dev->ctx(), x.data(), x.data(), x.local_size(), &xx), "ssp_dot");
+  return std::sqrt(std::abs(rr) / std::abs(xx));
+}
+
+template <class F>
+int guarded(F f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_error = e.what();
+    return 1;
+  }
+}
+
+itsolv_options opts_or_default(const itsolv_options* o) {
+  itsolv_options d;
+  pr::default_options(&d);
+  return o ? *o : d;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* itsolv_last_error(void) { return g_error.c_str(); }
+
+void itsolv_default_options(itsolv_options* opt) { pr::default_options(opt); }
+
+int itsolv_davidson_synthetic(ssp_ctx* ctx, size_t n, double rho, int rank, unsigned long long seed,
+                              const itsolv_options* opt, itsolv_result* out, double* solutions_out) {
+  return guarded([&] {
+    auto dev = borrow(ctx);
+    const auto o = opts_or_default(opt);
+    SyntheticProblem problem(dev, pr::SyntheticSpec(n, rho, rank, seed));
+    std::memset(out, 0, sizeof(*out));
+    pr::run_davidson<Vec, Vec, SparseP>(
+        molpro::linalg::hbm::make_handlers(), problem, [&] { return zero_vec(dev, n); },
+        [&](const Vec& x, double e) { return residual_norm(problem, dev, x, e); }, o, *out,
+        [&](size_t r, const Vec& x) {
+          if (!solutions_out) return;
+          auto v = x.local_values();
+          std::memcpy(solutions_out + r * v.size(), v.data(), v.size() * sizeof(double));
+        });
+  });
+}
+
+int itsolv_davidson_dense(ssp_ctx* ctx, const double* h, size_t n, const itsolv_options* opt, itsolv_result* out,
+                          double* solutions_out) {
+  return guarded([&] {
+    auto dev = borrow(ctx);
+    const auto o = opts_or_default(opt);
+    DenseProblem problem(dev, h, n);
+    std::memset(out, 0, sizeof(*out));
+    pr::run_davidson<Vec, Vec, SparseP>(
+        molpro::linalg::hbm::make_handlers(), problem, [&] { return zero_vec(dev, n); },
+        [&](const Vec& x, double e) { return residual_norm(problem, dev, x, e); }, o, *out,
+        [&](size_t r, const Vec& x) {
+          if (!solutions_out) return;
+          auto v = x.local_values();
+          std::memcpy(solutions_out + r * n, v.data(), n * sizeof(double));
+        });
+  });
+}
+
+int itsolv_diis_synthetic(ssp_ctx* ctx, size_t n, double rho, int rank, unsigned long long seed,
+                          const itsolv_options* opt, itsolv_result* out, double* x_out) {
+  return guarded([&] {
+    auto dev = borrow(ctx);
+    const auto o = opts_or_default(opt);
+    SyntheticProblem problem(dev, pr::SyntheticSpec(n, rho, rank, seed));
+    std::memset(out, 0, sizeof(*out));
+    pr::run_diis<Vec, Vec, SparseP>(
+        molpro::linalg::hbm::make_handlers(), problem, [&] { return zero_vec(dev, n); },
+        [&](Vec& x) {
+          const size_t i0 = 0;
+          const double one = 1.0;
+          check(ssp_sparse_copy(x.ctx(), x.data(), x.local_size(), x.offset(), &i0, &one, 1), "ssp_sparse_copy");
+        },
+        o, *out,
+        [&](const Vec& x) {
+          if (!x_out) return;
+          auto v = x.local_values();
+          std::memcpy(x_out, v.data(), v.size() * sizeof(double));
+        });
+  });
+}
+
+int itsolv_diis_dense(ssp_ctx* ctx, const double* h, size_t n, const itsolv_options* opt, itsolv_result* out,
+                      double* x_out) {
+  return guarded([&] {
+    auto dev = borrow(ctx);
+    const auto o = opts_or_default(opt);
+    DenseProblem problem(dev, h, n);
+    std::memset(out, 0, sizeof(*out));
+    pr::run_diis<Vec, Vec, SparseP>(
+        molpro::linalg::hbm::make_handlers(), problem, [&] { return zero_vec(dev, n); },
+        [&](Vec& x) {
+          const size_t i0 = 0;
+          const double one = 1.0;
+          check(ssp_sparse_copy(x.ctx(), x.data(), x.local_size(), x.offset(), &i0, &one, 1), "ssp_sparse_copy");
+        },
+        o, *out,
+        [&](const Vec& x) {
+          if (!x_out) return;
+          auto v = x.local_values();
+          std::memcpy(x_out, v.data(), v.size() * sizeof(double));
+        });
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,501 @@
+// Small dense linear algebra of the subspace problem (host, matrices of at most a few hundred rows).
+//
+// The reference delegates these to LAPACKE dsyev and Eigen 3.3.7 (reference
+// itsolv/helper-implementation.h).  Neither is available here, so they are restated on top of one
+// cyclic-Jacobi symmetric eigensolver (accurate to a few ulps for the symmetric / well-conditioned
+// matrices the solvers build), reproducing the reference's conventions:
+//   * eigensolver_lapacke_dsyev: eigenvalues ascending, eigenvector i in column i   (:122-158)
+//   * svd_system(hermitian): eigenpairs listed largest first, value <= threshold kept (:184-192, :263-296)
+//   * get_rank: count of eigenvalues >= threshold * max                              (:221-231)
+//   * eigenproblem: Hbar = S^-1/2 U^T H U S^-1/2 on the first `rank` eigenpairs of S in ascending
+//     order, eigenvalues ascending, back-transform, sign fixed so that the largest-|.| component is
+//     positive                                                                        (:318-543)
+//   * solve_DIIS: augmented [B -1; -1 0] system solved by a pseudo-inverse (SVD threshold 0) (:619-669)
+// The non-hermitian branch (JacobiSVD of S + general real EigenSolver) uses a one-sided Jacobi SVD and
+// a Hessenberg-QR eigensolver; those paths are only exercised by the non-hermitian tests.
+#pragma once
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <limits>
+#include <list>
+#include <numeric>
+#include <stdexcept>
+#include <vector>
+
+namespace molpro::linalg::itsolv {
+
+template <typename T>
+struct SVD {
+  using value_type = T;
+  value_type value;
+  std::vector<value_type> u;
+  std::vector<value_type> v;
+};
+
+namespace dense {
+
+// Symmetric eigen-decomposition of the n x n matrix a (either storage order: only the symmetric
+// part is used).  On return evals is ascending and column i of evecs (evecs[j + n*i]) is the
+// unit eigenvector of evals[i].
+inline void sym_eigen(size_t n, const std::vector<double>& a, std::vector<double>& evals, std::vector<double>& evecs) {
+  std::vector<double> A(n * n);
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j) A[i * n + j] = 0.5 * (a[i * n + j] + a[j * n + i]);
+  std::vector<double> V(n * n, 0.0);
+  for (size_t i = 0; i < n; ++i) V[i * n + i] = 1.0;  // V[row*n + col], column = eigenvector
+  for (int sweep = 0; sweep < 100; ++sweep) {
+    double off = 0, diag = 0;
+    for (size_t i = 0; i < n; ++i) {
+      diag += A[i * n + i] * A[i * n + i];
+      for (size_t j = i + 1; j < n; ++j) off += A[i * n + j] * A[i * n + j];
+    }
+    if (off == 0 || off <= 1e-34 * diag) break;
+    for (size_t p = 0; p + 1 < n; ++p) {
+      for (size_t q = p + 1; q < n; ++q) {
+        const double apq = A[p * n + q];
+        if (apq == 0) continue;
+        const double app = A[p * n + p], aqq = A[q * n + q];
+        const double theta = (aqq - app) / (2 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (std::abs(theta) + std::sqrt(theta * theta + 1));
+        const double c = 1 / std::sqrt(t * t + 1), s = t * c;
+        for (size_t k = 0; k < n; ++k) {
+          const double akp = A[k * n + p], akq = A[k * n + q];
+          A[k * n + p] = c * akp - s * akq;
+          A[k * n + q] = s * akp + c * akq;
+        }
+        for (size_t k = 0; k < n; ++k) {
+          const double apk = A[p * n + k], aqk = A[q * n + k];
+          A[p * n + k] = c * apk - s * aqk;
+          A[q * n + k] = s * apk + c * aqk;
+        }
+        A[p * n + q] = A[q * n + p] = 0;
+        for (size_t k = 0; k < n; ++k) {
+          const double vkp = V[k * n + p], vkq = V[k * n + q];
+          V[k * n + p] = c * vkp - s * vkq;
+          V[k * n + q] = s * vkp + c * vkq;
+        }
+      }
+    }
+  }
+  std::vector<size_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return A[x * n + x] < A[y * n + y]; });
+  evals.resize(n);
+  evecs.assign(n * n, 0.0);
+  for (size_t i = 0; i < n; ++i) {
+    evals[i] = A[order[i] * n + order[i]];
+    for (size_t j = 0; j < n; ++j) evecs[j + n * i] = V[j * n + order[i]];
+  }
+}
+
+// One-sided Jacobi SVD of the nrows x ncols column-major matrix m (nrows >= ncols assumed padded):
+// singular values descending, thin U (nrows x ncols) and V (ncols x ncols), column-major.
+inline void jacobi_svd(size_t nrows, size_t ncols, const std::vector<double>& m, std::vector<double>& sv,
+                       std::vector<double>& U, std::vector<double>& V) {
+  const size_t n = ncols, r = std::max(nrows, ncols);
+  std::vector<double> W(r * n, 0.0);  // column-major r x n
+  for (size_t j = 0; j < n; ++j)
+    for (size_t i = 0; i < nrows; ++i) W[i + r * j] = m[i + nrows * j];
+  std::vector<double> Vm(n * n, 0.0);
+  for (size_t i = 0; i < n; ++i) Vm[i + n * i] = 1;
+  for (int sweep = 0; sweep < 100; ++sweep) {
+    bool rotated = false;
+    for (size_t p = 0; p + 1 < n; ++p)
+      for (size_t q = p + 1; q < n; ++q) {
+        double alpha = 0, beta = 0, gamma = 0;
+        for (size_t i = 0; i < r; ++i) {
+          alpha += W[i + r * p] * W[i + r * p];
+          beta += W[i + r * q] * W[i + r * q];
+          gamma += W[i + r * p] * W[i + r * q];
+        }
+        if (gamma == 0 || std::abs(gamma) <= 1e-16 * std::sqrt(alpha * beta)) continue;
+        rotated = true;
+        const double zeta = (beta - alpha) / (2 * gamma);
+        const double t = (zeta >= 0 ? 1.0 : -1.0) / (std::abs(zeta) + std::sqrt(1 + zeta * zeta));
+        const double c = 1 / std::sqrt(1 + t * t), s = c * t;
+        for (size_t i = 0; i < r; ++i) {
+          const double wp = W[i + r * p], wq = W[i + r * q];
+          W[i + r * p] = c * wp - s * wq;
+          W[i + r * q] = s * wp + c * wq;
+        }
+        for (size_t i = 0; i < n; ++i) {
+          const double vp = Vm[i + n * p], vq = Vm[i + n * q];
+          Vm[i + n * p] = c * vp - s * vq;
+          Vm[i + n * q] = s * vp + c * vq;
+        }
+      }
+    if (!rotated) break;
+  }
+  std::vector<double> norms(n);
+  for (size_t j = 0; j < n; ++j) {
+    double s = 0;
+    for (size_t i = 0; i < r; ++i) s += W[i + r * j] * W[i + r * j];
+    norms[j] = std::sqrt(s);
+  }
+  std::vector<size_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return norms[x] > norms[y]; });
+  sv.resize(n);
+  U.assign(nrows * n, 0.0);
+  V.assign(n * n, 0.0);
+  for (size_t k = 0; k < n; ++k) {
+    const size_t j = order[k];
+    sv[k] = norms[j];
+    for (size_t i = 0; i < nrows; ++i) U[i + nrows * k] = norms[j] > 0 ? W[i + r * j] / norms[j] : 0.0;
+    for (size_t i = 0; i < n; ++i) V[i + n * k] = Vm[i + n * j];
+  }
+}
+
+// Eigenvalues / eigenvectors of a general real n x n matrix (column-major), via Hessenberg reduction
+// and the shifted QR algorithm on the complex Schur form (small n only).
+inline void general_eigen(size_t n, const std::vector<double>& a, std::vector<std::complex<double>>& evals,
+                          std::vector<std::complex<double>>& evecs) {
+  using cd = std::complex<double>;
+  // Complex Schur via unshifted-then-Wilkinson-shifted QR on the complex matrix (n is tiny).
+  std::vector<cd> T(n * n), Q(n * n, cd(0));
+  for (size_t i = 0; i < n; ++i) {
+    Q[i + n * i] = 1;
+    for (size_t j = 0; j < n; ++j) T[i + n * j] = a[i + n * j];
+  }
+  auto givens = [&](size_t k, cd x, cd y, cd& c, cd& s) {
+    double r = std::sqrt(std::norm(x) + std::norm(y));
+    if (r == 0) {
+      c = 1;
+      s = 0;
+      return;
+    }
+    c = x / r;
+    s = y / r;
+  };
+  for (size_t hi = n; hi > 1;) {
+    int iter = 0;
+    for (;;) {
+      const double sub = std::abs(T[(hi - 1) + n * (hi - 2)]);
+      const double scale = std::abs(T[(hi - 1) + n * (hi - 1)]) + std::abs(T[(hi - 2) + n * (hi - 2)]);
+      if (sub <= 1e-15 * (scale > 0 ? scale : 1) || iter > 300) {
+        T[(hi - 1) + n * (hi - 2)] = 0;
+        --hi;
+        break;
+      }
+      ++iter;
+      // Wilkinson shift from the trailing 2x2 block.
+      cd a11 = T[(hi - 2) + n * (hi - 2)], a12 = T[(hi - 2) + n * (hi - 1)], a21 = T[(hi - 1) + n * (hi - 2)],
+         a22 = T[(hi - 1) + n * (hi - 1)];
+      cd tr = a11 + a22, det = a11 * a22 - a12 * a21;
+      cd disc = std::sqrt(tr * tr / 4.0 - det);
+      cd mu1 = tr / 2.0 + disc, mu2 = tr / 2.0 - disc;
+      cd mu = std::abs(mu1 - a22) < std::abs(mu2 - a22) ? mu1 : mu2;
+      if (iter % 11 == 0) mu += cd(std::abs(a21), 0);  // exceptional shift
+      for (size_t i = 0; i < hi; ++i) T[i + n * i] -= mu;
+      std::vector<cd> cs(hi), sn(hi);
+      for (size_t k = 0; k + 1 < hi; ++k) {
+        cd c, s;
+        givens(k, T[k + n * k], T[(k + 1) + n * k], c, s);
+        cs[k] = c;
+        sn[k] = s;
+        for (size_t j = 0; j < n; ++j) {
+          cd x = T[k + n * j], y = T[(k + 1) + n * j];
+          T[k + n * j] = std::conj(c) * x + std::conj(s) * y;
+          T[(k + 1) + n * j] = -s * x + c * y;
+        }
+      }
+      for (size_t k = 0; k + 1 < hi; ++k) {
+        cd c = cs[k], s = sn[k];
+        for (size_t i = 0; i < n; ++i) {
+          cd x = T[i + n * k], y = T[i + n * (k + 1)];
+          T[i + n * k] = x * c + y * s;
+          T[i + n * (k + 1)] = -x * std::conj(s) + y * std::conj(c);
+          cd qx = Q[i + n * k], qy = Q[i + n * (k + 1)];
+          Q[i + n * k] = qx * c + qy * s;
+          Q[i + n * (k + 1)] = -qx * std::conj(s) + qy * std::conj(c);
+        }
+      }
+      for (size_t i = 0; i < hi; ++i) T[i + n * i] += mu;
+    }
+  }
+  evals.resize(n);
+  for (size_t i = 0; i < n; ++i) evals[i] = T[i + n * i];
+  // Eigenvectors of the triangular T by back substitution, then rotate by Q; unit 2-norm.
+  evecs.assign(n * n, cd(0));
+  for (size_t k = 0; k < n; ++k) {
+    std::vector<cd> y(n, cd(0));
+    y[k] = 1;
+    for (size_t i = k; i-- > 0;) {
+      cd s = 0;
+      for (size_t j = i + 1; j <= k; ++j) s += T[i + n * j] * y[j];
+      cd d = T[i + n * i] - T[k + n * k];
+      if (std::abs(d) < 1e-300) d = 1e-300;
+      y[i] = -s / d;
+    }
+    double nrm = 0;
+    std::vector<cd> x(n, cd(0));
+    for (size_t i = 0; i < n; ++i) {
+      for (size_t j = 0; j <= k; ++j) x[i] += Q[i + n * j] * y[j];
+      nrm += std::norm(x[i]);
+    }
+    nrm = std::sqrt(nrm);
+    // Remove the arbitrary complex phase: the largest component becomes real positive, so the
+    // eigenvector of a real eigenvalue is real (as Eigen::EigenSolver returns it).
+    size_t big = 0;
+    for (size_t i = 0; i < n; ++i)
+      if (std::abs(x[i]) > std::abs(x[big])) big = i;
+    const cd phase = std::abs(x[big]) > 0 ? x[big] / std::abs(x[big]) : cd(1);
+    for (size_t i = 0; i < n; ++i) evecs[i + n * k] = x[i] / (nrm * phase);
+  }
+}
+
+}  // namespace dense
+
+// ---- reference helper conventions -----------------------------------------------------------------
+
+// LAPACK dsyev role: eigenvalues ascending, eigenvectors column-major.  Returns 0.
+inline int eigensolver_lapacke_dsyev(const std::vector<double>& matrix, std::vector<double>& eigenvectors,
+                                     std::vector<double>& eigenvalues, const size_t dimension) {
+  if (eigenvectors.size() != matrix.size())
+    throw std::runtime_error("Matrix of eigenvectors and input matrix are not the same size!");
+  if (eigenvectors.size() != dimension * dimension || eigenvalues.size() != dimension)
+    throw std::runtime_error("Size of eigenvectors/eigenvlaues do not match dimension!");
+  dense::sym_eigen(dimension, matrix, eigenvalues, eigenvectors);
+  return 0;
+}
+
+// Eigenpairs of a symmetric matrix as a list, largest eigenvalue first (reference :167-195).
+inline std::list<SVD<double>> eigensolver_lapacke_dsyev(size_t dimension, const std::vector<double>& matrix) {
+  std::vector<double> vecs(dimension * dimension), vals(dimension);
+  eigensolver_lapacke_dsyev(matrix, vecs, vals, dimension);
+  std::list<SVD<double>> out;
+  for (size_t i = dimension; i-- > 0;) {
+    SVD<double> s;
+    s.value = vals[i];
+    s.v.assign(vecs.begin() + dimension * i, vecs.begin() + dimension * (i + 1));
+    out.push_back(std::move(s));
+  }
+  return out;
+}
+
+template <typename value_type>
+size_t get_rank(const std::vector<value_type>& eigenvalues, value_type threshold) {
+  if (eigenvalues.empty()) return 0;
+  const value_type thr = threshold * *std::max_element(eigenvalues.begin(), eigenvalues.end());
+  return size_t(std::count_if(eigenvalues.begin(), eigenvalues.end(), [&](value_type v) { return v >= thr; }));
+}
+
+template <typename value_type>
+size_t get_rank(const std::list<SVD<value_type>>& svds, value_type threshold) {
+  value_type mx = 0;
+  for (auto& s : svds) mx = std::max(mx, s.value);
+  size_t r = 0;
+  for (auto& s : svds)
+    if (s.value > threshold * mx) ++r;
+  return r;
+}
+
+// Singular (eigen, when hermitian) pairs with value below `threshold` (reference :263-296).
+// m is row-major nrows x ncols.
+inline std::list<SVD<double>> svd_system(size_t nrows, size_t ncols, const std::vector<double>& m, double threshold,
+                                         bool hermitian = false, bool reduce_to_rank = false) {
+  std::list<SVD<double>> svds;
+  if (m.empty()) return svds;
+  if (hermitian) {
+    svds = eigensolver_lapacke_dsyev(nrows, m);
+    for (auto s = svds.begin(); s != svds.end();)
+      if (s->value > threshold)
+        s = svds.erase(s);
+      else
+        ++s;
+  } else {
+    // Eigen::Map<Matrix> of the row-major buffer reads it column-major: the SVD is of m^T viewed
+    // as nrows x ncols column-major, exactly as the reference's svd_eigen_jacobi does.
+    std::vector<double> sv, U, V;
+    dense::jacobi_svd(nrows, ncols, m, sv, U, V);
+    for (size_t i = ncols; i-- > 0;) {
+      if (std::abs(sv[i]) < threshold) {
+        SVD<double> t;
+        t.value = sv[i];
+        for (size_t j = 0; j < ncols; ++j) t.v.push_back(V[j + ncols * i]);
+        svds.push_back(std::move(t));
+      }
+    }
+  }
+  if (reduce_to_rank) {
+    const size_t rank = get_rank(svds, threshold);
+    for (size_t i = ncols; i > rank && !svds.empty(); --i) svds.pop_back();
+  }
+  return svds;
+}
+
+// Generalised eigenproblem H c = e S c of the subspace (reference :318-543).  matrix (H) is
+// row-major, metric (S) is read column-major as the reference's Eigen::Map does (S is symmetric in
+// the hermitian case).  eigenvectors: column-major dimension x nsol (column k = root k).
+inline void eigenproblem(std::vector<double>& eigenvectors, std::vector<double>& eigenvalues,
+                         const std::vector<double>& matrix, const std::vector<double>& metric, size_t dimension,
+                         bool hermitian, double svdThreshold, int verbosity, bool condone_complex) {
+  using cd = std::complex<double>;
+  const size_t n = dimension;
+  std::vector<double> H(n * n);  // column-major copy of the row-major input
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j) H[i + n * j] = matrix[i * n + j];
+  std::vector<double> sing, U, V;  // U, V column-major n x n
+  size_t rank = 0;
+  if (hermitian) {
+    std::vector<double> vecs(n * n), vals(n);
+    if (eigensolver_lapacke_dsyev(metric, vecs, vals, n) != 0) throw std::runtime_error("Eigensolver did not converge");
+    sing = vals;
+    U = V = vecs;
+    rank = get_rank(vals, svdThreshold);
+  } else {
+    dense::jacobi_svd(n, n, metric, sing, U, V);
+    // Eigen's JacobiSVD::rank(): singular values above max * max(n,n) * machine epsilon.
+    const double thr = (sing.empty() ? 0 : sing[0]) * double(n) * std::numeric_limits<double>::epsilon();
+    rank = size_t(std::count_if(sing.begin(), sing.end(), [&](double s) { return s > thr; }));
+  }
+  std::vector<double> svmh(rank);
+  for (size_t k = 0; k < rank; ++k) svmh[k] = sing[k] > 1e-14 ? 1 / std::sqrt(sing[k]) : 0;
+  // Hbar = diag(svmh) U_r^T H V_r diag(svmh)  (rank x rank, column-major)
+  std::vector<double> HV(n * rank, 0.0);
+  for (size_t j = 0; j < rank; ++j)
+    for (size_t i = 0; i < n; ++i) {
+      double s = 0;
+      for (size_t l = 0; l < n; ++l) s += H[i + n * l] * V[l + n * j];
+      HV[i + n * j] = s;
+    }
+  std::vector<double> Hbar(rank * rank, 0.0);
+  for (size_t j = 0; j < rank; ++j)
+    for (size_t i = 0; i < rank; ++i) {
+      double s = 0;
+      for (size_t l = 0; l < n; ++l) s += U[l + n * i] * HV[l + n * j];
+      Hbar[i + rank * j] = svmh[i] * s * svmh[j];
+    }
+  std::vector<cd> evals_c(rank), y(rank * rank);
+  if (hermitian) {
+    std::vector<double> ev, vec;
+    dense::sym_eigen(rank, Hbar, ev, vec);
+    for (size_t i = 0; i < rank; ++i) evals_c[i] = ev[i];
+    for (size_t i = 0; i < rank * rank; ++i) y[i] = vec[i];
+  } else {
+    dense::general_eigen(rank, Hbar, evals_c, y);
+    double imag_norm = 0;
+    for (auto& e : evals_c) imag_norm += e.imag() * e.imag();
+    if (std::sqrt(imag_norm) < 1e-10) {
+      for (auto& e : evals_c) e = e.real();
+      for (size_t i = 0; i < rank; ++i) {
+        double in = 0;
+        for (size_t l = 0; l < rank; ++l) in += std::norm(y[l + rank * i].imag());
+        if (std::sqrt(in) > 1e-10 && i + 1 < rank && std::abs(evals_c[i] - evals_c[i + 1]) < 1e-10) {
+          double rn = 0, imn = 0;
+          for (size_t l = 0; l < rank; ++l) {
+            rn += std::pow(y[l + rank * i].real(), 2);
+            imn += std::pow(y[l + rank * i].imag(), 2);
+          }
+          for (size_t l = 0; l < rank; ++l) {
+            const cd v = y[l + rank * i];
+            y[l + rank * (i + 1)] = v.imag() / std::sqrt(imn);
+            y[l + rank * i] = v.real() / std::sqrt(rn);
+          }
+        }
+      }
+    }
+  }
+  // Back-transform: X = V_r diag(svmh) Y  (n x rank)
+  std::vector<cd> X(n * rank, cd(0));
+  for (size_t k = 0; k < rank; ++k)
+    for (size_t i = 0; i < n; ++i) {
+      cd s = 0;
+      for (size_t l = 0; l < rank; ++l) s += V[i + n * l] * svmh[l] * y[l + rank * k];
+      X[i + n * k] = s;
+    }
+  // Selection sort ascending by real part (first minimum wins), sign fix on the largest component.
+  std::vector<size_t> used;
+  std::vector<cd> sv(rank), sX(n * rank);
+  for (size_t k = 0; k < rank; ++k) {
+    size_t ll = 0;
+    while (std::count(used.begin(), used.end(), ll)) ++ll;
+    for (size_t l = 0; l < rank; ++l)
+      if (!std::count(used.begin(), used.end(), l) && evals_c[l].real() < evals_c[ll].real()) ll = l;
+    used.push_back(ll);
+    sv[k] = evals_c[ll];
+    for (size_t i = 0; i < n; ++i) sX[i + n * k] = X[i + n * ll];
+    // (the reference scans the first `rank` components for the largest)
+    size_t mc = 0;
+    for (size_t l = 0; l < rank && l < n; ++l)
+      if (std::abs(sX[l + n * k].real()) > std::abs(sX[mc + n * k].real())) mc = l;
+    if (sX[mc + n * k].real() < 0)
+      for (size_t i = 0; i < n; ++i) sX[i + n * k] = -sX[i + n * k];
+  }
+  if (!hermitian) {
+    // Normalise each eigenvector in the S metric and fix its phase (reference :451-506).
+    std::vector<double> Sc(n * n);
+    for (size_t i = 0; i < n * n; ++i) Sc[i] = metric[i];
+    for (int repeat = 0; repeat < 3; ++repeat)
+      for (size_t k = 0; k < rank; ++k) {
+        if (std::abs(sv[k]) < 1e-12) {
+          for (size_t i = 0; i < n; ++i) sX[i + n * k] = cd(sX[i + n * k].real() + 0.3256897 * sX[i + n * k].imag(), 0);
+        }
+        cd ovl = 0;
+        for (size_t i = 0; i < n; ++i) {
+          cd t = 0;
+          for (size_t j = 0; j < n; ++j) t += Sc[i + n * j] * sX[j + n * k];
+          ovl += std::conj(sX[i + n * k]) * t;
+        }
+        for (size_t i = 0; i < n; ++i) sX[i + n * k] /= std::sqrt(ovl.real());
+        size_t lmax = 0;
+        for (size_t l = 0; l < n; ++l)
+          if (std::abs(sX[l + n * k]) > std::abs(sX[lmax + n * k])) lmax = l;
+        if (sX[lmax + n * k].real() < 0)
+          for (size_t i = 0; i < n; ++i) sX[i + n * k] = -sX[i + n * k];
+      }
+  }
+  if (condone_complex) {
+    for (size_t root = 0; root < rank; ++root) {
+      if (sv[root].imag() != 0 && root + 1 < rank) {
+        sv[root] = sv[root + 1] = sv[root].real();
+        for (size_t i = 0; i < n; ++i) {
+          const cd a = sX[i + n * root], b = sX[i + n * (root + 1)];
+          sX[i + n * root] = a.real();
+          sX[i + n * (root + 1)] = b.imag();
+        }
+        ++root;
+      }
+    }
+  }
+  double imag = 0;
+  for (auto& x : sX) imag += x.imag() * x.imag();
+  for (auto& e : sv) imag += e.imag() * e.imag();
+  if (std::sqrt(imag) > 1e-10) throw std::runtime_error("unexpected complex solution found");
+  eigenvectors.resize(n * rank);
+  eigenvalues.resize(rank);
+  for (size_t i = 0; i < n * rank; ++i) eigenvectors[i] = sX[i].real();
+  for (size_t k = 0; k < rank; ++k) eigenvalues[k] = sv[k].real();
+  (void)verbosity;
+}
+
+// DIIS extrapolation coefficients (reference :619-669).  matrix: column-major dimension^2.
+inline void solve_DIIS(std::vector<double>& solution, const std::vector<double>& matrix, const size_t dimension,
+                       double svdThreshold, int verbosity = 0) {
+  const size_t na = dimension + 1;
+  std::vector<double> B(na * na, 0.0), rhs(na, 0.0);
+  for (size_t i = 0; i < dimension; ++i)
+    for (size_t j = 0; j < dimension; ++j) B[i + na * j] = matrix[i + dimension * j];
+  for (size_t i = 0; i < dimension; ++i) B[dimension + na * i] = B[i + na * dimension] = -1;
+  rhs[dimension] = -1;
+  // SVD solve with threshold 0 (reference :650): pseudo-inverse over the non-zero singular values.
+  std::vector<double> sv, U, V;
+  dense::jacobi_svd(na, na, B, sv, U, V);
+  std::vector<double> coeff(na, 0.0);
+  for (size_t k = 0; k < na; ++k) {
+    if (!(sv[k] > 0)) continue;
+    double ub = 0;
+    for (size_t i = 0; i < na; ++i) ub += U[i + na * k] * rhs[i];
+    for (size_t i = 0; i < na; ++i) coeff[i] += V[i + na * k] * ub / sv[k];
+  }
+  solution.resize(dimension);
+  for (size_t k = 0; k < dimension; ++k) {
+    if (std::isnan(std::abs(coeff[k]))) throw std::overflow_error("NaN detected in DIIS submatrix solution");
+    solution[k] = coeff[k];
+  }
+  (void)svdThreshold;
+  (void)verbosity;
+}
+
+}  // namespace molpro::linalg::itsolv

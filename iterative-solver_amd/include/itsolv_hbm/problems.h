@@ -1,0 +1,149 @@
+// Problem definitions shared by the device solver entry points (host/itsolv_capi.cpp) and the CPU
+// oracle (oracle/itsolv_oracle.cpp), and the generic solve drivers both run.
+//
+// Synthetic H = diag(1 + g) + rho * sum_{l<rank} u_l u_l^T with u_0 = 1 and u_l(g) = +/-1 from
+// splitmix64 (the rank-one case is reference test/itsolv/test_rayleigh_quotient.cpp:37-42).  The
+// hash is the same function the HIP kernels (csrc/synthetic.hip) and oracle/oracle.py evaluate.
+#pragma once
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <functional>
+#include <vector>
+
+#include "itsolv_hbm.h"
+#include "solvers.h"
+
+namespace molpro::linalg::itsolv::problems {
+
+inline uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+inline uint64_t stream_key(uint64_t seed, uint64_t stream) { return splitmix64(seed ^ (stream * 0xD1B54A32D192ED03ull)); }
+
+struct SyntheticSpec {
+  size_t n;
+  double rho;
+  int rank;
+  uint64_t seed;
+  std::vector<uint64_t> keys;  // per low-rank vector
+  SyntheticSpec(size_t n_, double rho_, int rank_, uint64_t seed_) : n(n_), rho(rho_), rank(rank_), seed(seed_) {
+    for (int l = 0; l < rank; ++l) keys.push_back(stream_key(seed, 1000 + uint64_t(l)));
+  }
+  double u(int l, size_t g) const { return l == 0 ? 1.0 : ((splitmix64(keys[l] ^ uint64_t(g)) & 1ull) ? -1.0 : 1.0); }
+  double h(size_t i, size_t j) const {
+    double s = 0;
+    for (int l = 0; l < rank; ++l) s += u(l, i) * u(l, j);
+    return (i == j ? 1.0 + double(i) : 0.0) + rho * s;
+  }
+  double diagonal(size_t g) const { return 1.0 + double(g) + rank * rho; }
+};
+
+inline void apply_options(const itsolv_options& o, Options& base) {
+  base.n_roots = o.nroots;
+  base.convergence_threshold = o.convergence_threshold;
+  if (o.max_iter > 0) base.max_iter = o.max_iter;
+  base.max_p = o.max_p;
+  if (o.p_threshold > 0) base.p_threshold = o.p_threshold;
+  base.verbosity = Verbosity(o.verbosity);
+}
+
+// Runs LinearEigensystemDavidson::solve and fills `out`.  make_vec() creates a zeroed R vector;
+// residual_norm(x, e) returns |H x - e x| (computed by the caller's action).
+template <class R, class Q, class P>
+void run_davidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R, P>& problem,
+                  const std::function<R()>& make_vec, const std::function<double(const R&, double)>& residual_norm,
+                  const itsolv_options& o, itsolv_result& out, const std::function<void(size_t, const R&)>& emit) {
+  LinearEigensystemDavidson<R, Q, P> solver(handlers);
+  LinearEigensystemDavidsonOptions opt;
+  apply_options(o, opt);
+  if (o.max_size_qspace > 0) opt.max_size_qspace = o.max_size_qspace;
+  if (o.reset_D > 0) opt.reset_D = o.reset_D;
+  if (o.reset_D_max_Q_size > 0) opt.reset_D_max_Q_size = o.reset_D_max_Q_size;
+  opt.hermiticity = o.hermitian != 0;
+  solver.set_options(opt);
+  const size_t nwork = size_t(o.nwork > 0 ? o.nwork : o.nroots);
+  std::vector<R> params, actions;
+  for (size_t i = 0; i < nwork; ++i) {
+    params.push_back(make_vec());
+    actions.push_back(make_vec());
+  }
+  out.n_eig_trace = 0;
+  solver.iteration_hook = [&] {
+    const auto ev = solver.eigenvalues();
+    if (!ev.empty() && out.n_eig_trace < 256) out.eig_trace[out.n_eig_trace++] = ev.front();
+  };
+  const auto t0 = std::chrono::steady_clock::now();
+  out.converged = solver.solve(params, actions, problem, o.generate_initial_guess != 0);
+  out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const auto& st = solver.statistics();
+  out.iterations = st.iterations;
+  out.r_creations = st.r_creations;
+  out.q_creations = st.q_creations;
+  const auto ev = solver.eigenvalues();
+  out.nroots = int(std::min<size_t>(ev.size(), ITSOLV_MAX_ROOTS));
+  for (int i = 0; i < out.nroots; ++i) {
+    out.eigenvalues[i] = ev[i];
+    out.errors[i] = i < int(solver.errors().size()) ? solver.errors()[i] : 0.0;
+  }
+  // Solutions root by root (only nwork buffers), residuals recomputed from the problem's action.
+  for (int r = 0; r < out.nroots; ++r) {
+    std::vector<R> x, g;
+    x.push_back(make_vec());
+    g.push_back(make_vec());
+    solver.solution(std::vector<int>{r}, x, g);
+    out.residual_norms[r] = residual_norm(x[0], ev[r]);
+    if (emit) emit(size_t(r), x[0]);
+  }
+}
+
+// Runs NonLinearEquationsDIIS::solve from x0 (set by init) and fills `out`.
+template <class R, class Q, class P>
+void run_diis(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R, P>& problem,
+              const std::function<R()>& make_vec, const std::function<void(R&)>& init,
+              const itsolv_options& o, itsolv_result& out, const std::function<void(const R&)>& emit) {
+  NonLinearEquationsDIIS<R, Q, P> solver(handlers);
+  NonLinearEquationsDIISOptions opt;
+  apply_options(o, opt);
+  opt.n_roots = 1;
+  if (o.max_size_qspace > 0) opt.max_size_qspace = o.max_size_qspace;
+  solver.set_options(opt);
+  R x = make_vec(), g = make_vec();
+  init(x);
+  const auto t0 = std::chrono::steady_clock::now();
+  out.converged = solver.solve(x, g, problem);
+  out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const auto& st = solver.statistics();
+  out.iterations = st.iterations;
+  out.r_creations = st.r_creations;
+  out.q_creations = st.q_creations;
+  out.nroots = 1;
+  out.errors[0] = solver.errors().empty() ? 0.0 : solver.errors().front();
+  out.eigenvalues[0] = 0;
+  out.n_eig_trace = 0;
+  R xs = make_vec(), gs = make_vec();
+  solver.solution(xs, gs);
+  problem.residual(xs, gs);
+  out.residual_norms[0] = std::sqrt(std::abs(handlers->rr().dot(gs, gs)));
+  if (emit) emit(xs);
+}
+
+inline void default_options(itsolv_options* o) {
+  o->nroots = 1;
+  o->nwork = 0;
+  o->max_iter = 100;
+  o->max_size_qspace = 0;
+  o->reset_D = 0;
+  o->reset_D_max_Q_size = 0;
+  o->max_p = 0;
+  o->p_threshold = 0;
+  o->convergence_threshold = 1e-8;
+  o->hermitian = 1;
+  o->generate_initial_guess = 1;
+  o->verbosity = 0;
+}
+
+}  // namespace molpro::linalg::itsolv::problems

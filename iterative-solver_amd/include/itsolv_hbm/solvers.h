@@ -1,0 +1,703 @@
+// Iterative solvers over the ArrayHandlers boundary: LinearEigensystemDavidson and
+// NonLinearEquationsDIIS, with the reverse-communication interface (add_vector / end_iteration /
+// solution) and the one-call solve(parameters, actions, problem).
+//
+// Restated from the reference:
+//   Problem                         itsolv/IterativeSolver.h:76-172, precondition_default :34-63
+//   detail::construct_solution etc. itsolv/IterativeSolverTemplate.h:19-117
+//   IterativeSolverTemplate          :126-600 (add_vector :140-166, add_p :176-187, solution :191-215,
+//                                    solve :322-408, solve_and_generate_working_set :518-563)
+//   SubspaceSolverLinEig             itsolv/subspace/SubspaceSolverLinEig.h:23-124
+//   SubspaceSolverDIIS               itsolv/subspace/SubspaceSolverDIIS.h:19-96
+//   LinearEigensystemDavidson        itsolv/LinearEigensystemDavidson.h:27-199
+//   NonLinearEquationsDIIS           itsolv/NonLinearEquationsDIIS.h:28-185
+// All vector work goes through the handlers; these classes only move small matrices around, so
+// with HBM handlers the same code is the GPU solver and with the oracle's CPU handlers it is the
+// reference CPU path.
+#pragma once
+#include <algorithm>
+#include <cmath>
+#include <functional>
+#include <limits>
+#include <map>
+#include <memory>
+#include <numeric>
+#include <stdexcept>
+#include <vector>
+
+#include "rspace.h"
+
+namespace molpro::linalg::itsolv {
+
+using subspace::EqnData;
+using subspace::Matrix;
+
+// Generic preconditioner for iterable containers (reference IterativeSolver.h:46-55).  Device vector
+// types supply their own overload.
+template <class T, typename = typename T::iterator>
+void precondition_default(const VecRef<T>& action, const std::vector<double>& shift, const T& diagonals) {
+  for (size_t k = 0; k < action.size(); ++k) {
+    auto& a = action[k].get();
+    auto d = diagonals.begin();
+    for (auto it = a.begin(); it != a.end(); ++it, ++d) *it = *it / (*d - shift[k] + 1e-15);
+  }
+}
+
+template <typename R, typename P = std::map<size_t, typename R::value_type>>
+class Problem {
+ public:
+  using container_t = R;
+  using value_t = typename R::value_type;
+  virtual ~Problem() = default;
+  virtual value_t residual(const R& parameters, R& residual) const { return 0; }
+  virtual void action(const CVecRef<R>& parameters, const VecRef<R>& action) const {}
+  virtual bool diagonals(container_t& d) const { return false; }
+  virtual void precondition(const VecRef<R>& residual, const std::vector<value_t>& shift) const {}
+  virtual void precondition(const VecRef<R>& residual, const std::vector<value_t>& shift, const R& diagonals) const {
+    precondition_default(residual, shift, diagonals);
+  }
+  virtual std::vector<double> pp_action_matrix(const std::vector<P>& pparams) const {
+    if (!pparams.empty()) throw std::logic_error("P-space unavailable: unimplemented pp_action_matrix() in Problem class");
+    return {};
+  }
+  virtual void p_action(const std::vector<std::vector<value_t>>& p_coefficients, const CVecRef<P>& pparams,
+                        const VecRef<container_t>& actions) const {
+    if (!pparams.empty()) throw std::logic_error("P-space unavailable: unimplemented p_action() in Problem class");
+  }
+};
+
+namespace detail {
+
+inline std::vector<std::pair<size_t, size_t>> parameter_batches(size_t nsol, size_t nparam) {
+  std::vector<std::pair<size_t, size_t>> b;
+  if (nparam && nsol)
+    for (size_t s = 0; s < nsol; s += nparam) b.emplace_back(s, std::min(s + nparam, nsol));
+  return b;
+}
+
+// params[i] = sum over P, Q, D of solutions(roots[i], .) (reference IterativeSolverTemplate.h:33-65):
+// fill(0) then one gemm_outer per space.
+template <class R, class Q, class P>
+void construct_solution(const VecRef<R>& params, const std::vector<int>& roots, const Matrix<double>& sol,
+                        const CVecRef<P>& pp, const CVecRef<Q>& qp, const CVecRef<Q>& dp, size_t oP, size_t oQ,
+                        size_t oD, ArrayHandlers<R, Q, P>& h) {
+  if (roots.empty()) return;
+  for (size_t i = 0; i < roots.size(); ++i) h.rr().fill(0, params.at(i));
+  Matrix<double> cp({pp.size(), roots.size()}), cq({qp.size(), roots.size()}), cd({dp.size(), roots.size()});
+  for (size_t i = 0; i < roots.size(); ++i) {
+    for (size_t j = 0; j < pp.size(); ++j) cp(j, i) = sol(roots[i], oP + j);
+    for (size_t j = 0; j < qp.size(); ++j) cq(j, i) = sol(roots[i], oQ + j);
+    for (size_t j = 0; j < dp.size(); ++j) cd(j, i) = sol(roots[i], oD + j);
+  }
+  h.rp().gemm_outer(cp, pp, params);
+  h.rq().gemm_outer(cq, qp, params);
+  h.rq().gemm_outer(cd, dp, params);
+}
+
+inline std::vector<std::vector<double>> construct_vectorP(const std::vector<int>& roots, const Matrix<double>& sol,
+                                                          size_t oP, size_t nP) {
+  std::vector<std::vector<double>> v;
+  for (auto r : roots) {
+    v.emplace_back();
+    for (size_t j = 0; j < nP; ++j) v.back().push_back(sol(r, oP + j));
+  }
+  return v;
+}
+
+template <class R>
+void normalise_pairs(size_t n, const VecRef<R>& params, const VecRef<R>& actions, array::ArrayHandler<R, R>& h,
+                     Logger& log) {
+  for (size_t i = 0; i < n; ++i) {
+    const double d = std::sqrt(std::abs(h.dot(params.at(i), params.at(i))));
+    if (d > 1.0e-14) {
+      h.scal(1. / d, params.at(i));
+      h.scal(1. / d, actions.at(i));
+    } else {
+      log.msg("solution parameter's length is too small, dot = " + Logger::scientific(d), Logger::Warn);
+    }
+  }
+}
+
+template <class R>
+void update_errors(std::vector<double>& errors, const CVecRef<R>& residual, array::ArrayHandler<R, R>& h) {
+  for (size_t i = 0; i < errors.size(); ++i) errors[i] = std::sqrt(std::abs(h.dot(residual[i], residual[i])));
+}
+
+// The nw roots with the largest errors above threshold, in ascending root order (reference :104-117).
+inline std::vector<int> select_working_set(size_t nw, const std::vector<double>& errors, double thr,
+                                           const std::vector<double>& value_errors, double value_thr) {
+  std::multimap<double, size_t, std::greater<double>> ordered;
+  for (size_t i = 0; i < errors.size(); ++i)
+    if (errors[i] > thr || (i < value_errors.size() && value_errors[i] > value_thr)) ordered.emplace(errors[i], i);
+  std::vector<int> ws;
+  for (auto it = ordered.begin(); it != ordered.end() && ws.size() < nw; ++it) ws.push_back(int(it->second));
+  std::sort(ws.begin(), ws.end());
+  return ws;
+}
+
+}  // namespace detail
+
+// ---- subspace problem solvers -------------------------------------------------------------------
+
+class SubspaceSolver {
+ public:
+  virtual ~SubspaceSolver() = default;
+  virtual void solve(const subspace::SubspaceData& data, size_t nroots_max) = 0;
+  void set_error(int root, double e) { m_errors.at(root) = e; }
+  void set_error(const std::vector<int>& roots, const std::vector<double>& e) {
+    for (size_t i = 0; i < roots.size(); ++i) set_error(roots[i], e[i]);
+  }
+  const Matrix<double>& solutions() const { return m_solutions; }
+  virtual const std::vector<double>& eigenvalues() const { return m_eigenvalues; }
+  const std::vector<double>& errors() const { return m_errors; }
+  size_t size() const { return m_solutions.rows(); }
+
+ protected:
+  Matrix<double> m_solutions;  // one row per root
+  std::vector<double> m_eigenvalues;
+  std::vector<double> m_errors;
+};
+
+// Dense eigenproblem (or linear equations when rhs is present) in the subspace.
+class SubspaceSolverLinEig : public SubspaceSolver {
+ public:
+  explicit SubspaceSolverLinEig(std::shared_ptr<Logger> log) : m_logger(std::move(log)) {}
+  void solve(const subspace::SubspaceData& data, size_t nroots_max) override {
+    const auto& h = data.at(EqnData::H);
+    const auto& s = data.at(EqnData::S);
+    const size_t dim = h.rows();
+    std::vector<double> evec;
+    eigenproblem(evec, m_eigenvalues, h.data(), s.data(), dim, m_hermitian, m_svd_solver_threshold, 0, true);
+    const size_t nsol = dim ? evec.size() / dim : 0;
+    const size_t nroots = std::min(nroots_max, nsol);
+    m_eigenvalues.resize(nroots);
+    m_solutions = Matrix<double>({nroots, dim});
+    for (size_t k = 0; k < nroots; ++k)
+      for (size_t j = 0; j < dim; ++j) m_solutions(k, j) = evec[j + dim * k];
+    m_errors.assign(nroots, std::numeric_limits<double>::max());
+    if (m_logger->data_dump) m_logger->msg("eigenvectors = " + as_string(m_solutions), Logger::Info);
+  }
+  void set_hermiticity(bool h) { m_hermitian = h; }
+  bool get_hermiticity() const { return m_hermitian; }
+  double m_svd_solver_threshold = 1.0e-14;
+
+ private:
+  std::shared_ptr<Logger> m_logger;
+  bool m_hermitian = false;
+};
+
+class SubspaceSolverDIIS : public SubspaceSolver {
+ public:
+  SubspaceSolverDIIS(std::shared_ptr<Logger> log, const bool& converged) : m_converged(converged), m_logger(std::move(log)) {}
+  void solve(const subspace::SubspaceData& data, size_t) override {
+    const auto& kH = data.at(EqnData::H);
+    const size_t dim = kH.rows();
+    m_solutions = Matrix<double>({1, dim});
+    if (m_converged) {
+      m_solutions.fill(0);
+      if (dim) m_solutions(0, 0) = 1;
+      return;
+    }
+    std::vector<double> matrix;
+    matrix.reserve(dim * dim);
+    for (size_t i = 0; i < dim; ++i)
+      for (size_t j = 0; j < dim; ++j) matrix.push_back(kH(j, i));
+    std::vector<double> sol(dim);
+    solve_DIIS(sol, matrix, dim, 1e-10, 1);
+    for (size_t i = 0; i < dim; ++i) m_solutions(0, i) = sol[i];
+    m_errors.assign(1, dim ? kH(0, 0) : 0.0);
+  }
+  const std::vector<double>& eigenvalues() const override {
+    throw std::logic_error("eigenvalues() not available in non-linear method");
+  }
+
+ private:
+  const bool& m_converged;
+  std::shared_ptr<Logger> m_logger;
+};
+
+// ---- the solver template ------------------------------------------------------------------------
+
+template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>
+class IterativeSolverTemplate {
+ public:
+  using value_type = typename R::value_type;
+  using scalar_type = double;
+  using VectorP = std::vector<value_type>;
+  using fapply_on_p_type = std::function<void(const std::vector<VectorP>&, const CVecRef<P>&, const VecRef<R>&)>;
+
+  virtual ~IterativeSolverTemplate() = default;
+  IterativeSolverTemplate(const IterativeSolverTemplate&) = delete;
+
+  virtual bool nonlinear() const = 0;
+
+  // Adds the working-set parameters and their actions (residuals for non-linear solvers) to the
+  // subspace, solves it and returns the new working set in parameters / actions.
+  virtual int add_vector(const VecRef<R>& parameters, const VecRef<R>& actions) {
+    if (m_xspace->dimensions().nP != 0 && !m_apply_p)
+      throw std::runtime_error("Solver contains P space but no valid apply_p function. Make sure add_p was called correctly.");
+    const size_t nW = std::min(m_working_set.size(), parameters.size());
+    auto cp = cwrap(parameters.begin(), parameters.begin() + nW);
+    auto ca = cwrap(actions.begin(), actions.begin() + nW);
+    m_stats->r_creations += int(nW);
+    m_xspace->update_qspace(cp, ca);
+    m_stats->q_creations += int(2 * nW);
+    auto ws = solve_and_generate_working_set(parameters, actions);
+    read_handler_counts(*m_stats, *m_handlers);
+    m_end_iteration_needed = true;
+    return int(ws);
+  }
+  int add_vector(std::vector<R>& parameters, std::vector<R>& actions) { return add_vector(wrap(parameters), wrap(actions)); }
+  virtual int add_vector(R& parameters, R& actions, value_type value = 0) {
+    return add_vector(wrap_arg(parameters), wrap_arg(actions));
+  }
+
+  size_t add_p(const CVecRef<P>& pparams, const std::vector<double>& pp_action_matrix, const VecRef<R>& parameters,
+               const VecRef<R>& actions, fapply_on_p_type apply_p) {
+    if (!pparams.empty() && pparams.size() < n_roots())
+      throw std::runtime_error("P space must be empty or at least as large as number of roots sought");
+    if (apply_p) m_apply_p = std::move(apply_p);
+    m_xspace->update_pspace(pparams, pp_action_matrix);
+    auto ws = solve_and_generate_working_set(parameters, actions);
+    read_handler_counts(*m_stats, *m_handlers);
+    return ws;
+  }
+
+  void solution(const std::vector<int>& roots, const VecRef<R>& parameters, const VecRef<R>& residual) {
+    check_roots(roots, parameters.size());
+    const auto& d = m_xspace->dimensions();
+    detail::construct_solution(parameters, roots, m_subspace_solver->solutions(), m_xspace->cparamsp(),
+                               m_xspace->cparamsq(), m_xspace->cparamsd(), d.oP, d.oQ, d.oD, *m_handlers);
+    detail::construct_solution(residual, roots, m_subspace_solver->solutions(), CVecRef<P>{}, m_xspace->cactionsq(),
+                               m_xspace->cactionsd(), d.oP, d.oQ, d.oD, *m_handlers);
+    auto pvec = detail::construct_vectorP(roots, m_subspace_solver->solutions(), d.oP, d.nP);
+    if (m_normalise_solution) detail::normalise_pairs(roots.size(), parameters, residual, m_handlers->rr(), *m_logger);
+    if (m_apply_p) m_apply_p(pvec, m_xspace->cparamsp(), residual);
+    construct_residual(roots, cwrap(parameters), residual);
+    read_handler_counts(*m_stats, *m_handlers);
+  }
+  void solution(const std::vector<int>& roots, std::vector<R>& parameters, std::vector<R>& residual) {
+    solution(roots, wrap(parameters), wrap(residual));
+  }
+  void solution(R& parameters, R& residual) { solution(std::vector<int>(1, 0), wrap_arg(parameters), wrap_arg(residual)); }
+
+  void solution_params(const std::vector<int>& roots, const VecRef<R>& parameters) {
+    check_roots(roots, parameters.size());
+    const auto& d = m_xspace->dimensions();
+    detail::construct_solution(parameters, roots, m_subspace_solver->solutions(), m_xspace->cparamsp(),
+                               m_xspace->cparamsq(), m_xspace->cparamsd(), d.oP, d.oQ, d.oD, *m_handlers);
+  }
+
+  virtual size_t end_iteration(const VecRef<R>& parameters, const VecRef<R>& actions) = 0;
+  size_t end_iteration(std::vector<R>& parameters, std::vector<R>& actions) {
+    return end_iteration(wrap(parameters), wrap(actions));
+  }
+  size_t end_iteration(R& parameters, R& actions) { return end_iteration(wrap_arg(parameters), wrap_arg(actions)); }
+  bool end_iteration_needed() const { return m_end_iteration_needed; }
+
+  const std::vector<int>& working_set() const { return m_working_set; }
+  virtual std::vector<double> working_set_eigenvalues() const { return std::vector<double>(m_working_set.size(), 0); }
+  size_t n_roots() const { return m_nroots; }
+  void set_n_roots(size_t n) {
+    m_nroots = n;
+    m_working_set.resize(n);
+    std::iota(m_working_set.begin(), m_working_set.end(), 0);
+  }
+  const std::vector<double>& errors() const { return m_errors; }
+  const Statistics& statistics() const { return *m_stats; }
+  const subspace::Dimensions& dimensions() const { return m_xspace->dimensions(); }
+  void set_convergence_threshold(double t) { m_convergence_threshold = t; }
+  double convergence_threshold() const { return m_convergence_threshold; }
+  void set_convergence_threshold_value(double t) { m_convergence_threshold_value = t; }
+  void set_verbosity(Verbosity v) { m_verbosity = v; }
+  Verbosity get_verbosity() const { return m_verbosity; }
+  void set_max_iter(int n) { m_max_iter = n; }
+  int get_max_iter() const { return m_max_iter; }
+  void set_max_p(int n) { m_max_p = size_t(n); }
+  int get_max_p() const { return int(m_max_p); }
+  void set_p_threshold(double t) { m_p_threshold = t; }
+  double get_p_threshold() const { return m_p_threshold; }
+  std::shared_ptr<Logger> logger() const { return m_logger; }
+  subspace::XSpace<R, Q, P>& xspace() { return *m_xspace; }
+
+  virtual void set_options(const Options& o) {
+    if (o.n_roots) set_n_roots(size_t(*o.n_roots));
+    if (o.convergence_threshold) set_convergence_threshold(*o.convergence_threshold);
+    if (o.verbosity) set_verbosity(*o.verbosity);
+    if (o.max_iter) set_max_iter(*o.max_iter);
+    if (o.max_p) set_max_p(int(*o.max_p));
+    if (o.p_threshold) set_p_threshold(*o.p_threshold);
+  }
+
+  // One-call driver (reference IterativeSolverTemplate.h:322-408).
+  bool solve(const VecRef<R>& parameters, const VecRef<R>& actions, const Problem<R, P>& problem,
+             bool generate_initial_guess = false) {
+    if (parameters.empty()) throw std::runtime_error("Empty container passed to IterativeSolver::solve()");
+    if (parameters.size() != actions.size()) throw std::runtime_error("Inconsistent container sizes in IterativeSolver::solve()");
+    const bool use_diagonals = problem.diagonals(actions.at(0));
+    std::unique_ptr<Q> diagonals;
+    if (use_diagonals) diagonals = std::make_unique<Q>(m_handlers->qr().copy(actions.at(0)));
+    if (generate_initial_guess) {
+      if (!use_diagonals) throw std::runtime_error("Default initial guess requested, but diagonal elements are not available");
+      auto guess = m_handlers->qq().select(parameters.size(), *diagonals);
+      size_t root = 0;
+      for (const auto& g : guess) m_handlers->rp().copy(parameters[root++], P{{g.first, 1}});
+    }
+    int nwork = int(parameters.size());
+    std::vector<P> pspace;
+    if (use_diagonals && m_max_p > 0) {
+      auto selectp = m_handlers->qq().select(m_max_p, *diagonals);
+      for (auto s = selectp.begin(); s != selectp.end(); ++s)
+        if (s->second > selectp.begin()->second + m_p_threshold) {
+          selectp.erase(s, selectp.end());
+          break;
+        }
+      for (const auto& s : selectp) pspace.push_back(P{{s.first, 1}});
+      fapply_on_p_type apply = [&problem](const std::vector<VectorP>& c, const CVecRef<P>& pp, const VecRef<R>& a) {
+        problem.p_action(c, pp, a);
+      };
+      auto ppm = problem.pp_action_matrix(pspace);
+      nwork = int(add_p(cwrap(pspace), ppm, parameters, actions, apply));
+    }
+    for (int iter = 0; iter < m_max_iter && nwork > 0; ++iter) {
+      if (nonlinear()) {
+        const auto value = problem.residual(parameters.front(), actions.front());
+        nwork = add_vector(parameters.front().get(), actions.front().get(), value);
+      } else if (iter > 0 || pspace.empty()) {
+        problem.action(cwrap(parameters.begin(), parameters.begin() + nwork), wrap(actions.begin(), actions.begin() + nwork));
+        nwork = add_vector(parameters, actions);
+      }
+      while (end_iteration_needed()) {
+        if (nwork > 0) {
+          if (use_diagonals) {
+            m_handlers->rq().copy(parameters.at(0), *diagonals);
+            problem.precondition(wrap(actions.begin(), actions.begin() + nwork), working_set_eigenvalues(),
+                                 parameters.at(0));
+          } else {
+            problem.precondition(wrap(actions.begin(), actions.begin() + nwork), working_set_eigenvalues());
+          }
+        }
+        nwork = int(end_iteration(parameters, actions));
+      }
+      if (iteration_hook) iteration_hook();
+      if (m_verbosity >= Verbosity::Iteration) report();
+    }
+    const double emax = m_errors.empty() ? 0 : *std::max_element(m_errors.begin(), m_errors.end());
+    return nwork == 0 && emax <= m_convergence_threshold;
+  }
+  bool solve(std::vector<R>& parameters, std::vector<R>& actions, const Problem<R, P>& problem,
+             bool generate_initial_guess = false) {
+    return solve(wrap(parameters), wrap(actions), problem, generate_initial_guess);
+  }
+  bool solve(R& parameters, R& actions, const Problem<R, P>& problem, bool generate_initial_guess = false) {
+    return solve(wrap_arg(parameters), wrap_arg(actions), problem, generate_initial_guess);
+  }
+
+  //! Called after every iteration of solve() (measurement / tracing; not part of the reference API).
+  std::function<void()> iteration_hook;
+
+  virtual void report(std::ostream& o = std::cout) const {
+    o << "iteration " << m_stats->iterations;
+    if (!m_errors.empty()) {
+      auto it = std::max_element(m_errors.begin(), m_errors.end());
+      o << (n_roots() > 1 ? ", |residual[" + std::to_string(it - m_errors.begin()) + "]| = " : ", |residual| = ")
+        << std::scientific << *it << std::defaultfloat;
+    }
+    o << std::endl;
+  }
+
+ protected:
+  IterativeSolverTemplate(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, std::shared_ptr<SubspaceSolver> ss,
+                          std::shared_ptr<Logger> logger)
+      : m_handlers(std::move(handlers)),
+        m_xspace(std::make_shared<subspace::XSpace<R, Q, P>>(m_handlers, logger)),
+        m_subspace_solver(std::move(ss)),
+        m_stats(std::make_shared<Statistics>()),
+        m_logger(std::move(logger)) {
+    set_n_roots(1);
+  }
+
+  virtual void set_value_errors() {}
+  virtual void construct_residual(const std::vector<int>& roots, const CVecRef<R>& params, const VecRef<R>& actions) = 0;
+
+  // reference IterativeSolverTemplate.h:518-563
+  size_t solve_and_generate_working_set(const VecRef<R>& parameters, const VecRef<R>& action) {
+    m_subspace_solver->solve(m_xspace->data, n_roots());
+    const size_t nsol = m_subspace_solver->size();
+    std::vector<std::pair<Q, Q>> temp;
+    const auto batches = detail::parameter_batches(nsol, parameters.size());
+    for (const auto& [s0, s1] : batches) {
+      std::vector<int> roots(s1 - s0);
+      std::iota(roots.begin(), roots.end(), int(s0));
+      solution(roots, parameters, action);
+      std::vector<double> errors(roots.size(), 0);
+      detail::update_errors(errors, cwrap(action), m_handlers->rr());
+      if (batches.size() > 1) {
+        for (size_t i = 0; i < roots.size(); ++i)
+          temp.emplace_back(m_handlers->qr().copy(parameters[i]), m_handlers->qr().copy(action[i]));
+        m_stats->q_creations += int(2 * roots.size());
+      }
+      m_subspace_solver->set_error(roots, errors);
+    }
+    set_value_errors();
+    m_errors = m_subspace_solver->errors();
+    m_working_set = detail::select_working_set(parameters.size(), m_errors, m_convergence_threshold, m_value_errors,
+                                               m_convergence_threshold_value);
+    for (size_t i = 0; i < m_working_set.size(); ++i) {
+      const size_t root = size_t(m_working_set[i]);
+      if (batches.size() > 1) {
+        m_handlers->rq().copy(parameters[i], temp.at(root).first);
+        m_handlers->rq().copy(action[i], temp.at(root).second);
+      } else {
+        if (root < i) throw std::logic_error("incorrect ordering of roots");
+        if (root > i) {
+          m_handlers->rr().copy(parameters[i], parameters[root]);
+          m_handlers->rr().copy(action[i], action[root]);
+        }
+      }
+    }
+    return m_working_set.size();
+  }
+
+  void check_roots(const std::vector<int>& roots, size_t nparams) const {
+    if (roots.size() > nparams) throw std::runtime_error("asking for more roots than parameters");
+    if (!roots.empty() && size_t(*std::max_element(roots.begin(), roots.end())) >= m_subspace_solver->solutions().rows())
+      throw std::runtime_error("asking for more roots than there are solutions");
+  }
+
+  std::shared_ptr<ArrayHandlers<R, Q, P>> m_handlers;
+  std::shared_ptr<subspace::XSpace<R, Q, P>> m_xspace;
+  std::shared_ptr<SubspaceSolver> m_subspace_solver;
+  std::shared_ptr<Statistics> m_stats;
+  std::shared_ptr<Logger> m_logger;
+  std::vector<double> m_errors, m_value_errors;
+  std::vector<int> m_working_set;
+  size_t m_nroots = 0;
+  double m_convergence_threshold = 1.0e-8;
+  double m_convergence_threshold_value = std::numeric_limits<double>::max();
+  bool m_normalise_solution = false;
+  fapply_on_p_type m_apply_p{};
+  Verbosity m_verbosity = Verbosity::Iteration;
+  int m_max_iter = 100;
+  size_t m_max_p = 0;
+  double m_p_threshold = std::numeric_limits<double>::max();
+  bool m_end_iteration_needed = true;
+};
+
+// ---- Davidson ----------------------------------------------------------------------------------
+
+template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>
+class LinearEigensystemDavidson : public IterativeSolverTemplate<R, Q, P> {
+  using Base = IterativeSolverTemplate<R, Q, P>;
+
+ public:
+  explicit LinearEigensystemDavidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers,
+                                     std::shared_ptr<Logger> logger = std::make_shared<Logger>())
+      : Base(std::move(handlers), std::make_shared<SubspaceSolverLinEig>(logger), logger) {
+    set_hermiticity(m_hermiticity);
+    this->m_normalise_solution = false;
+  }
+
+  bool nonlinear() const override { return false; }
+
+  // reference LinearEigensystemDavidson.h:63-83
+  size_t end_iteration(const VecRef<R>& parameters, const VecRef<R>& action) override {
+    if (m_resetter.do_reset(size_t(this->m_stats->iterations), this->m_xspace->dimensions())) {
+      m_resetting = true;
+      this->m_working_set = m_resetter.run(parameters, *this->m_xspace, this->m_subspace_solver->solutions(),
+                                           norm_thresh, svd_thresh, *this->m_handlers, *this->m_logger);
+    } else {
+      m_resetting = false;
+      this->m_working_set = propose_rspace(parameters, action);
+    }
+    this->m_stats->iterations++;
+    read_handler_counts(*this->m_stats, *this->m_handlers);
+    this->m_end_iteration_needed = false;
+    return this->m_working_set.size();
+  }
+  using Base::end_iteration;
+
+  std::vector<double> eigenvalues() const { return this->m_subspace_solver->eigenvalues(); }
+  std::vector<double> working_set_eigenvalues() const override {
+    std::vector<double> e;
+    for (auto i : this->working_set()) e.push_back(this->m_subspace_solver->eigenvalues().at(i));
+    return e;
+  }
+
+  void set_reset_D(size_t n) { m_resetter.set_nreset(n); }
+  int get_reset_D() const { return m_resetter.get_nreset(); }
+  void set_reset_D_maxQ_size(size_t n) { m_resetter.set_max_Qsize(n); }
+  int get_reset_D_maxQ_size() const { return m_resetter.get_max_Qsize(); }
+  int get_max_size_qspace() const { return m_max_size_qspace; }
+  void set_max_size_qspace(int n) {
+    m_max_size_qspace = n;
+    if (m_resetter.get_max_Qsize() > m_max_size_qspace) m_resetter.set_max_Qsize(size_t(m_max_size_qspace));
+  }
+  void set_hermiticity(bool h) {
+    m_hermiticity = h;
+    this->m_xspace->set_hermiticity(h);
+    std::static_pointer_cast<SubspaceSolverLinEig>(this->m_subspace_solver)->set_hermiticity(h);
+  }
+  bool get_hermiticity() const { return m_hermiticity; }
+
+  void set_options(const Options& o) override {
+    Base::set_options(o);
+    if (auto* d = dynamic_cast<const LinearEigensystemDavidsonOptions*>(&o)) {
+      if (d->reset_D) set_reset_D(size_t(*d->reset_D));
+      if (d->reset_D_max_Q_size) set_reset_D_maxQ_size(size_t(*d->reset_D_max_Q_size));
+      if (d->max_size_qspace) set_max_size_qspace(*d->max_size_qspace);
+      if (d->norm_thresh) norm_thresh = *d->norm_thresh;
+      if (d->svd_thresh) svd_thresh = *d->svd_thresh;
+      if (d->hermiticity) set_hermiticity(*d->hermiticity);
+    }
+  }
+
+  double norm_thresh = 1e-10;  // propose_rspace_norm_thresh
+  double svd_thresh = 1e-12;   // propose_rspace_svd_thresh
+
+ protected:
+  void set_value_errors() override {
+    const auto cur = this->m_subspace_solver->eigenvalues();
+    this->m_value_errors.assign(cur.size(), std::numeric_limits<double>::max());
+    for (size_t i = 0; i < std::min(m_last_values.size(), cur.size()); ++i)
+      this->m_value_errors[i] = std::abs(cur[i] - m_last_values[i]);
+    if (!m_resetting) m_last_values = cur;
+  }
+
+  // r_i -= lambda_i x_i (reference LinearEigensystemDavidson.h:186-192)
+  void construct_residual(const std::vector<int>& roots, const CVecRef<R>& params, const VecRef<R>& actions) override {
+    const auto& ev = eigenvalues();
+    for (size_t i = 0; i < roots.size(); ++i) this->m_handlers->rr().axpy(-ev.at(roots[i]), params.at(i), actions.at(i));
+  }
+
+  // reference propose_rspace.h:553-624
+  std::vector<int> propose_rspace(const VecRef<R>& parameters, const VecRef<R>& residuals) {
+    auto& xs = *this->m_xspace;
+    auto& ss = *this->m_subspace_solver;
+    auto& h = *this->m_handlers;
+    auto& log = *this->m_logger;
+    const auto solutions = ss.solutions();
+    auto q_delete = detail::limit_qspace_size(xs.dimensions(), size_t(m_max_size_qspace), solutions, log);
+    if (!q_delete.empty()) {
+      auto [dp, da] = detail::construct_dspace(solutions, xs, q_delete, norm_thresh, svd_thresh, h.qq(), log);
+      std::sort(q_delete.begin(), q_delete.end(), std::greater<int>());
+      for (int iq : q_delete) xs.eraseq(size_t(iq));
+      auto wdp = wrap(dp);
+      auto wda = wrap(da);
+      xs.update_dspace(wdp, wda);
+      ss.solve(xs.data, solutions.rows());
+    }
+    auto wres = wrap(residuals.begin(), residuals.begin() + this->working_set().size());
+    detail::normalise(wres, h.rr(), log);
+    const auto full = detail::append_overlap_with_r(xs.data.at(EqnData::S), cwrap(wres), xs.cparamsp(), xs.cparamsq(),
+                                                    xs.cparamsd(), h);
+    auto redundant = detail::redundant_parameters(full, xs.dimensions().nX, wres.size(), svd_thresh, log);
+    detail::delete_parameters(redundant, wres);
+    auto null_params = detail::modified_gram_schmidt(wres, xs.data.at(EqnData::S), xs.dimensions(), xs.cparamsp(),
+                                                     xs.cparamsq(), xs.cparamsd(), norm_thresh, h);
+    detail::delete_parameters(null_params, wres);
+    detail::normalise(wres, h.rr(), log);
+    for (size_t i = 0; i < wres.size(); ++i) h.rr().copy(parameters.at(i), wres.at(i));
+    return detail::get_new_working_set(this->working_set(), cwrap(residuals), cwrap(wres));
+  }
+
+  int m_max_size_qspace = std::numeric_limits<int>::max();
+  detail::DSpaceResetter<Q> m_resetter;
+  bool m_hermiticity = false;
+  std::vector<double> m_last_values;
+  bool m_resetting = false;
+};
+
+// ---- DIIS --------------------------------------------------------------------------------------
+
+template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>
+class NonLinearEquationsDIIS : public IterativeSolverTemplate<R, Q, P> {
+  using Base = IterativeSolverTemplate<R, Q, P>;
+
+ public:
+  using typename Base::value_type;
+  explicit NonLinearEquationsDIIS(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers,
+                                  std::shared_ptr<Logger> logger = std::make_shared<Logger>())
+      : Base(std::move(handlers), std::make_shared<SubspaceSolverDIIS>(logger, m_converged), logger) {
+    this->m_xspace->set_hermiticity(true);
+    this->m_xspace->set_action_action();
+  }
+
+  bool nonlinear() const override { return true; }
+
+  // reference NonLinearEquationsDIIS.h:285-304
+  int add_vector(R& parameters, R& residual, value_type value = 0) override {
+    const double error = std::sqrt(this->m_handlers->rr().dot(residual, residual));
+    m_converged = error < this->m_convergence_threshold;
+    auto& xs = *this->m_xspace;
+    for (auto del = least_important_vector(xs.data[EqnData::H]);
+         xs.size() >= size_t(m_max_size_qspace) || del.second < m_svd_thresh;
+         del = least_important_vector(xs.data[EqnData::H]))
+      xs.eraseq(del.first);
+    const int nwork = Base::add_vector(wrap_arg(parameters), wrap_arg(residual));
+    this->m_errors.front() = error;
+    return nwork;
+  }
+  using Base::add_vector;
+
+  // reference NonLinearEquationsDIIS.h:305-321
+  size_t end_iteration(const VecRef<R>& parameters, const VecRef<R>& action) override {
+    this->solution_params(this->m_working_set, parameters);
+    this->m_end_iteration_needed = false;
+    if (this->m_errors.front() < this->m_convergence_threshold) {
+      this->m_working_set.clear();
+      return 0;
+    }
+    this->m_working_set.assign(1, 0);
+    this->m_handlers->rr().axpy(-1, action.front(), parameters.front());
+    this->m_stats->iterations++;
+    return 1;
+  }
+  using Base::end_iteration;
+
+  void set_norm_thresh(double t) { m_norm_thresh = t; }
+  void set_svd_thresh(double t) { m_svd_thresh = t; }
+  void set_max_size_qspace(int n) { m_max_size_qspace = n; }
+  int get_max_size_qspace() const { return m_max_size_qspace; }
+
+  void set_options(const Options& o) override {
+    Base::set_options(o);
+    if (auto* d = dynamic_cast<const NonLinearEquationsDIISOptions*>(&o)) {
+      if (d->max_size_qspace) set_max_size_qspace(*d->max_size_qspace);
+      if (d->norm_thresh) set_norm_thresh(*d->norm_thresh);
+      if (d->svd_thresh) set_svd_thresh(*d->svd_thresh);
+    }
+  }
+
+ protected:
+  void construct_residual(const std::vector<int>&, const CVecRef<R>&, const VecRef<R>&) override {}
+
+  // reference NonLinearEquationsDIIS.h:254-282
+  std::pair<size_t, double> least_important_vector(const Matrix<double>& H) const {
+    std::pair<size_t, double> result{0, std::numeric_limits<double>::max()};
+    const size_t n = H.cols();
+    if (n < 2) return result;
+    std::vector<double> ev, vec;
+    dense::sym_eigen(n, H.data(), ev, vec);
+    double evmax = 0;
+    for (size_t i = 0; i < n; ++i) {
+      evmax = std::max(evmax, ev[i]);
+      if (ev[i] < result.second) {
+        result.second = ev[i];
+        result.first = 1;
+        for (size_t j = 1; j < n; ++j)
+          if (std::abs(vec[j + n * i]) > std::abs(vec[result.first + n * i])) result.first = j;
+      }
+    }
+    result.second /= evmax;
+    if (result.second > m_svd_thresh) result = {n - 1, std::numeric_limits<double>::max()};
+    return result;
+  }
+
+  bool m_converged = false;
+  double m_norm_thresh = 1e-10;
+  double m_svd_thresh = 1e-12;
+  int m_max_size_qspace = std::numeric_limits<int>::max();
+};
+
+}  // namespace molpro::linalg::itsolv

@@ -1,0 +1,151 @@
+"""ctypes binding of libitsolv_hbm.so (C ABI: include/itsolv_hbm.h): the restated Davidson / DIIS
+solvers running over the HBM handlers.  The options / result structures are shared with the
+oracle's CPU twin (oracle/itsolv_oracle.cpp)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+import subspace_hip as sh
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libitsolv_hbm.so")
+MAX_ROOTS = 64
+
+EXPORTS = [
+    "itsolv_last_error", "itsolv_default_options", "itsolv_davidson_synthetic", "itsolv_davidson_dense",
+    "itsolv_diis_synthetic", "itsolv_diis_dense",
+]
+
+
+class Options(C.Structure):
+    _fields_ = [
+        ("nroots", C.c_int),
+        ("nwork", C.c_int),
+        ("max_iter", C.c_int),
+        ("max_size_qspace", C.c_int),
+        ("reset_D", C.c_int),
+        ("reset_D_max_Q_size", C.c_int),
+        ("max_p", C.c_int),
+        ("p_threshold", C.c_double),
+        ("convergence_threshold", C.c_double),
+        ("hermitian", C.c_int),
+        ("generate_initial_guess", C.c_int),
+        ("verbosity", C.c_int),
+    ]
+
+
+class Result(C.Structure):
+    _fields_ = [
+        ("converged", C.c_int),
+        ("iterations", C.c_int),
+        ("r_creations", C.c_int),
+        ("q_creations", C.c_int),
+        ("nroots", C.c_int),
+        ("eigenvalues", C.c_double * MAX_ROOTS),
+        ("errors", C.c_double * MAX_ROOTS),
+        ("residual_norms", C.c_double * MAX_ROOTS),
+        ("seconds", C.c_double),
+        ("n_eig_trace", C.c_int),
+        ("eig_trace", C.c_double * 256),
+    ]
+
+    def as_dict(self):
+        k = self.nroots
+        return {
+            "converged": bool(self.converged),
+            "iterations": self.iterations,
+            "r_creations": self.r_creations,
+            "q_creations": self.q_creations,
+            "eigenvalues": np.array(self.eigenvalues[:k]),
+            "errors": np.array(self.errors[:k]),
+            "residual_norms": np.array(self.residual_norms[:k]),
+            "seconds": self.seconds,
+            "eig_trace": np.array(self.eig_trace[: self.n_eig_trace]),
+        }
+
+
+def make_options(**kw) -> Options:
+    o = Options(nroots=1, nwork=0, max_iter=100, max_size_qspace=0, reset_D=0, reset_D_max_Q_size=0, max_p=0,
+                p_threshold=0.0, convergence_threshold=1e-8, hermitian=1, generate_initial_guess=1, verbosity=0)
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise KeyError(k)
+        setattr(o, k, v)
+    return o
+
+
+_lib = None
+
+
+def load_library():
+    global _lib
+    if _lib is None:
+        sh.load_library()  # libsubspace_hip.so first (dependency, RTLD_GLOBAL)
+        if not os.path.exists(LIB_PATH):
+            raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C iterative-solver_amd`")
+        L = C.CDLL(LIB_PATH)
+        P, Z, D, I, U = C.c_void_p, C.c_size_t, C.c_double, C.c_int, C.c_ulonglong
+        PO, PR, PD = C.POINTER(Options), C.POINTER(Result), C.POINTER(C.c_double)
+        sig = {
+            "itsolv_last_error": (C.c_char_p, []),
+            "itsolv_default_options": (None, [PO]),
+            "itsolv_davidson_synthetic": (I, [P, Z, D, I, U, PO, PR, PD]),
+            "itsolv_davidson_dense": (I, [P, PD, Z, PO, PR, PD]),
+            "itsolv_diis_synthetic": (I, [P, Z, D, I, U, PO, PR, PD]),
+            "itsolv_diis_dense": (I, [P, PD, Z, PO, PR, PD]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _call(fn, args, nout):
+    res = Result()
+    out = np.zeros(max(1, nout))
+    code = fn(*args, C.byref(res), out.ctypes.data_as(C.POINTER(C.c_double)))
+    if code != 0:
+        raise RuntimeError(f"{fn.__name__}: {load_library().itsolv_last_error().decode()}")
+    return res.as_dict(), out
+
+
+def davidson_synthetic(ctx: sh.Context, n: int, rho: float, rank: int, seed: int, n_local: int | None = None, **opts):
+    o = make_options(**opts)
+    nl = n if n_local is None else n_local
+    r, sol = _call(load_library().itsolv_davidson_synthetic, (ctx.handle, n, rho, rank, seed, C.byref(o)),
+                   o.nroots * nl)
+    r["solutions"] = sol[: o.nroots * nl].reshape(o.nroots, nl)
+    return r
+
+
+def davidson_dense(ctx: sh.Context, h: np.ndarray, **opts):
+    h = np.ascontiguousarray(h, dtype=np.float64)
+    n = h.shape[0]
+    o = make_options(**opts)
+    r, sol = _call(load_library().itsolv_davidson_dense,
+                   (ctx.handle, h.ctypes.data_as(C.POINTER(C.c_double)), n, C.byref(o)), o.nroots * n)
+    r["solutions"] = sol[: o.nroots * n].reshape(o.nroots, n)
+    return r
+
+
+def diis_synthetic(ctx: sh.Context, n: int, rho: float, rank: int, seed: int, n_local: int | None = None, **opts):
+    o = make_options(**opts)
+    nl = n if n_local is None else n_local
+    r, x = _call(load_library().itsolv_diis_synthetic, (ctx.handle, n, rho, rank, seed, C.byref(o)), nl)
+    r["x"] = x[:nl]
+    return r
+
+
+def diis_dense(ctx: sh.Context, h: np.ndarray, **opts):
+    h = np.ascontiguousarray(h, dtype=np.float64)
+    n = h.shape[0]
+    o = make_options(**opts)
+    r, x = _call(load_library().itsolv_diis_dense, (ctx.handle, h.ctypes.data_as(C.POINTER(C.c_double)), n,
+                                                    C.byref(o)), n)
+    r["x"] = x[:n]
+    return r

@@ -35,7 +35,7 @@ EXPORTS = [
     "ssp_ledger_entry", "ssp_fill", "ssp_scal", "ssp_copy", "ssp_axpy", "ssp_dot",
     "ssp_gemm_inner", "ssp_gemm_outer", "ssp_precondition", "ssp_select", "ssp_select_max_dot",
     "ssp_sparse_copy", "ssp_sparse_axpy", "ssp_sparse_dot", "ssp_gemm_inner_sparse", "ssp_gemm_outer_sparse",
-    "sspx_synthetic_action", "sspx_synthetic_diagonal", "sspx_fill_random", "sspx_dense_action",
+    "sspx_synthetic_action", "sspx_synthetic_add_lowrank", "sspx_synthetic_diagonal", "sspx_fill_random", "sspx_dense_action",
 ]
 
 
@@ -109,6 +109,7 @@ def _declare(lib):
         "ssp_gemm_inner_sparse": (I, [P, P, I, Z, Z, PZ, PZ, PD, I, PD]),
         "ssp_gemm_outer_sparse": (I, [P, PD, PZ, PZ, PD, I, P, I, Z, Z]),
         "sspx_synthetic_action": (I, [P, P, P, I, Z, Z, D, I, C.c_ulonglong]),
+        "sspx_synthetic_add_lowrank": (I, [P, P, I, Z, Z, D, I, C.c_ulonglong, PD]),
         "sspx_synthetic_diagonal": (I, [P, P, Z, Z, D, I]),
         "sspx_fill_random": (I, [P, P, Z, Z, C.c_ulonglong, C.c_ulonglong]),
         "sspx_dense_action": (I, [P, P, Z, P, P, I, Z, Z]),

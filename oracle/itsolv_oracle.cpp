@@ -1,0 +1,341 @@
+// ORACLE — test infrastructure only (see oracle_ops.h).
+//
+// The reference CPU path: the restated solvers (the same host templates the device library runs)
+// over CPU handlers that call the oracle's restatement of ArrayHandlerIterable /
+// ArrayHandlerIterableSparse (oracle_ops.c): sequential std::inner_product dots, element-order
+// axpys, pairwise gemm_inner_default / gemm_outer_default (reference util/gemm.h:257-279).
+// Exports oracle_* twins of the include/itsolv_hbm.h entry points; tests compare the two.
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "itsolv_hbm.h"
+#include "itsolv_hbm/problems.h"
+#include "itsolv_hbm/sparse_handler.h"
+#include "oracle_ops.h"
+
+using molpro::linalg::array::ArrayHandler;
+using molpro::linalg::hbm::ArrayHandlerSparse;
+using molpro::linalg::itsolv::ArrayHandlers;
+using molpro::linalg::itsolv::CVecRef;
+using molpro::linalg::itsolv::Problem;
+using molpro::linalg::itsolv::VecRef;
+using molpro::linalg::itsolv::subspace::Matrix;
+namespace pr = molpro::linalg::itsolv::problems;
+
+using V = std::vector<double>;
+using SP = std::map<size_t, double>;
+
+namespace {
+
+thread_local std::string g_error;
+
+void ok(int s, const char* what) {
+  if (s == 1) throw molpro::linalg::array::util::ArrayHandlerError(std::string(what) + ": incompatible sizes");
+  if (s != 0) throw std::runtime_error(std::string(what) + ": oracle error");
+}
+
+// reference ArrayHandlerIterable<std::vector<double>> (ArrayHandlerIterable.h:34-128)
+class IterableHandler : public ArrayHandler<V, V> {
+ public:
+  V copy(const V& s) override { return V(s); }
+  void copy(V& x, const V& y) override { ok(or_copy(x.data(), x.size(), y.data(), y.size()), "copy"); }
+  void scal(double a, V& x) override { or_scal(a, x.data(), x.size()); }
+  void fill(double a, V& x) override { or_fill(a, x.data(), x.size()); }
+  void axpy(double a, const V& x, V& y) override { ok(or_axpy(a, x.data(), x.size(), y.data(), y.size()), "axpy"); }
+  double dot(const V& x, const V& y) override {
+    double r = 0;
+    ok(or_dot(x.data(), x.size(), y.data(), y.size(), &r), "dot");
+    return r;
+  }
+  // gemm_outer_default / gemm_inner_default: pairwise axpy / dot
+  void gemm_outer(const Matrix<double> al, const CVecRef<V>& xx, const VecRef<V>& yy) override {
+    for (size_t i = 0; i < al.rows(); ++i)
+      for (size_t j = 0; j < al.cols(); ++j) axpy(al(i, j), xx.at(i).get(), yy[j].get());
+  }
+  Matrix<double> gemm_inner(const CVecRef<V>& xx, const CVecRef<V>& yy) override {
+    Matrix<double> m({xx.size(), yy.size()});
+    if (xx.empty() || yy.empty()) return m;
+    for (size_t i = 0; i < m.rows(); ++i)
+      for (size_t j = 0; j < m.cols(); ++j) m(i, j) = dot(xx.at(i).get(), yy.at(j).get());
+    return m;
+  }
+  std::map<size_t, double> select_max_dot(size_t n, const V& x, const V& y) override {
+    if (n > x.size() || n > y.size()) error("ArrayHandlerIterable::select_max_dot() n is too large");
+    return to_map(n, [&](size_t* i, double* v, size_t* c) {
+      return or_select_max_dot(x.data(), y.data(), std::min(x.size(), y.size()), n, i, v, c);
+    });
+  }
+  std::map<size_t, double> select(size_t n, const V& x, bool max = false, bool ignore_sign = false) override {
+    if (n > x.size()) error("ArrayHandlerIterable::select() n is too large");
+    return to_map(n, [&](size_t* i, double* v, size_t* c) { return or_select(x.data(), x.size(), n, max, ignore_sign, i, v, c); });
+  }
+  template <class F>
+  static std::map<size_t, double> to_map(size_t n, F f) {
+    std::vector<size_t> idx(std::max<size_t>(n, 1));
+    std::vector<double> val(std::max<size_t>(n, 1));
+    size_t c = 0;
+    ok(f(idx.data(), val.data(), &c), "select");
+    std::map<size_t, double> out;
+    for (size_t e = 0; e < c; ++e) out.emplace(idx[e], val[e]);
+    return out;
+  }
+};
+
+// reference ArrayHandlerIterableSparse<std::vector<double>, std::map<size_t,double>> (:151-217)
+class IterableSparseHandler : public ArrayHandler<V, SP> {
+ public:
+  V copy(const SP& s) override {
+    V r;
+    copy(r, s);
+    return r;
+  }
+  void copy(V& x, const SP& y) override {
+    std::fill(x.begin(), x.end(), 0.0);
+    for (auto& [i, v] : y) x.at(i) = v;
+  }
+  void scal(double, V&) override {}
+  void fill(double, V&) override {}
+  void axpy(double a, const SP& x, V& y) override {
+    for (auto& [i, v] : x)
+      if (i < y.size()) y[i] = y[i] + a * v;
+  }
+  double dot(const V& x, const SP& y) override {
+    double t = 0;
+    for (auto& [i, v] : y)
+      if (i < x.size()) t = t + x[i] * v;
+    return t;
+  }
+  void gemm_outer(const Matrix<double> al, const CVecRef<SP>& xx, const VecRef<V>& yy) override {
+    for (size_t i = 0; i < al.rows(); ++i)
+      for (size_t j = 0; j < al.cols(); ++j) axpy(al(i, j), xx.at(i).get(), yy[j].get());
+  }
+  Matrix<double> gemm_inner(const CVecRef<V>& xx, const CVecRef<SP>& yy) override {
+    Matrix<double> m({xx.size(), yy.size()});
+    for (size_t i = 0; i < m.rows(); ++i)
+      for (size_t j = 0; j < m.cols(); ++j) m(i, j) = dot(xx.at(i).get(), yy.at(j).get());
+    return m;
+  }
+  std::map<size_t, double> select_max_dot(size_t n, const V& x, const SP& y) override {
+    std::vector<double> prod;
+    std::vector<size_t> keys;
+    for (auto& [i, v] : y)
+      if (i < x.size()) {
+        keys.push_back(i);
+        prod.push_back(std::abs(x[i] * v));
+      }
+    auto sel = IterableHandler::to_map(std::min(n, prod.size()), [&](size_t* i, double* v, size_t* c) {
+      return or_select_max_dot(prod.data(), std::vector<double>(prod.size(), 1.0).data(), prod.size(),
+                               std::min(n, prod.size()), i, v, c);
+    });
+    std::map<size_t, double> out;
+    for (auto& [k, v] : sel) out.emplace(keys[k], v);
+    return out;
+  }
+  std::map<size_t, double> select(size_t n, const V& x, bool max = false, bool ignore_sign = false) override {
+    return IterableHandler::to_map(n, [&](size_t* i, double* v, size_t* c) { return or_select(x.data(), x.size(), n, max, ignore_sign, i, v, c); });
+  }
+};
+
+std::shared_ptr<ArrayHandlers<V, V, SP>> cpu_handlers() {
+  auto dense = [] { return std::make_shared<IterableHandler>(); };
+  auto sparse = [] { return std::make_shared<IterableSparseHandler>(); };
+  return ArrayHandlers<V, V, SP>::create()
+      .rr(dense())
+      .qq(dense())
+      .pp(std::make_shared<ArrayHandlerSparse>())
+      .rq(dense())
+      .rp(sparse())
+      .qr(dense())
+      .qp(sparse())
+      .build_shared();
+}
+
+class SyntheticCpu : public Problem<V, SP> {
+ public:
+  explicit SyntheticCpu(const pr::SyntheticSpec& s) : m_s(s) {
+    m_u.resize(size_t(s.rank));
+    for (int l = 0; l < s.rank; ++l) {
+      m_u[l].resize(s.n);
+      for (size_t g = 0; g < s.n; ++g) m_u[l][g] = s.u(l, g);
+    }
+  }
+  bool diagonals(V& d) const override {
+    for (size_t g = 0; g < d.size(); ++g) d[g] = m_s.diagonal(g);
+    return true;
+  }
+  void apply(const V& x, V& y) const {
+    std::vector<double> c(size_t(m_s.rank));
+    for (int l = 0; l < m_s.rank; ++l) or_dot(m_u[l].data(), x.size(), x.data(), x.size(), &c[l]);
+    for (size_t g = 0; g < x.size(); ++g) {
+      double s = 0;
+      for (int l = 0; l < m_s.rank; ++l) s += m_u[l][g] * c[l];
+      y[g] = (1.0 + double(g)) * x[g] + m_s.rho * s;
+    }
+  }
+  void action(const CVecRef<V>& p, const VecRef<V>& a) const override {
+    for (size_t k = 0; k < p.size(); ++k) apply(p[k].get(), a[k].get());
+  }
+  double residual(const V& x, V& r) const override {
+    V t(x);
+    for (auto& v : t) v -= 1.0;
+    apply(t, r);
+    return 0;
+  }
+  std::vector<double> pp_action_matrix(const std::vector<SP>& pp) const override {
+    std::vector<double> m;
+    for (auto& a : pp)
+      for (auto& b : pp) m.push_back(m_s.h(a.begin()->first, b.begin()->first));
+    return m;
+  }
+  void p_action(const std::vector<std::vector<double>>& c, const CVecRef<SP>& pp, const VecRef<V>& a) const override {
+    for (size_t k = 0; k < c.size(); ++k) {
+      auto& y = a[k].get();
+      std::vector<double> w(size_t(m_s.rank), 0.0);
+      for (size_t p = 0; p < pp.size(); ++p)
+        for (auto& [i, coef] : pp[p].get()) {
+          y[i] += (1.0 + double(i)) * coef * c[k][p];
+          for (int l = 0; l < m_s.rank; ++l) w[l] += c[k][p] * coef * m_s.u(l, i);
+        }
+      for (size_t g = 0; g < y.size(); ++g) {
+        double s = 0;
+        for (int l = 0; l < m_s.rank; ++l) s += m_u[l][g] * w[l];
+        y[g] += m_s.rho * s;
+      }
+    }
+  }
+
+ private:
+  pr::SyntheticSpec m_s;
+  std::vector<std::vector<double>> m_u;
+};
+
+class DenseCpu : public Problem<V, SP> {
+ public:
+  DenseCpu(const double* h, size_t n) : m_h(h, h + n * n), m_n(n) {}
+  bool diagonals(V& d) const override {
+    for (size_t i = 0; i < m_n; ++i) d[i] = m_h[i * m_n + i];
+    return true;
+  }
+  void apply(const V& x, V& y) const {
+    for (size_t i = 0; i < m_n; ++i) {
+      double s = 0;
+      for (size_t j = 0; j < m_n; ++j) s += m_h[i * m_n + j] * x[j];
+      y[i] = s;
+    }
+  }
+  void action(const CVecRef<V>& p, const VecRef<V>& a) const override {
+    for (size_t k = 0; k < p.size(); ++k) apply(p[k].get(), a[k].get());
+  }
+  double residual(const V& x, V& r) const override {
+    V t(x);
+    for (auto& v : t) v -= 1.0;
+    apply(t, r);
+    return 0;
+  }
+  std::vector<double> pp_action_matrix(const std::vector<SP>& pp) const override {
+    std::vector<double> m;
+    for (auto& a : pp)
+      for (auto& b : pp) m.push_back(m_h[a.begin()->first * m_n + b.begin()->first]);
+    return m;
+  }
+  void p_action(const std::vector<std::vector<double>>& c, const CVecRef<SP>& pp, const VecRef<V>& a) const override {
+    for (size_t k = 0; k < c.size(); ++k)
+      for (size_t p = 0; p < pp.size(); ++p)
+        for (auto& [i, coef] : pp[p].get())
+          for (size_t j = 0; j < m_n; ++j) a[k].get()[j] += m_h[j * m_n + i] * coef * c[k][p];
+  }
+
+ private:
+  std::vector<double> m_h;
+  size_t m_n;
+};
+
+template <class P>
+double residual_norm(const P& problem, const V& x, double e) {
+  V ax(x.size());
+  problem.apply(x, ax);
+  double rr = 0, xx = 0;
+  for (size_t i = 0; i < x.size(); ++i) {
+    const double r = ax[i] - e * x[i];
+    rr += r * r;
+    xx += x[i] * x[i];
+  }
+  return std::sqrt(rr / xx);
+}
+
+template <class F>
+int guarded(F f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_error = e.what();
+    return 1;
+  }
+}
+
+itsolv_options opts_or_default(const itsolv_options* o) {
+  itsolv_options d;
+  pr::default_options(&d);
+  return o ? *o : d;
+}
+
+template <class P>
+int davidson(const P& problem, size_t n, const itsolv_options* opt, itsolv_result* out, double* sol) {
+  return guarded([&] {
+    std::memset(out, 0, sizeof(*out));
+    pr::run_davidson<V, V, SP>(
+        cpu_handlers(), problem, [&] { return V(n, 0.0); },
+        [&](const V& x, double e) { return residual_norm(problem, x, e); }, opts_or_default(opt), *out,
+        [&](size_t r, const V& x) {
+          if (sol) std::memcpy(sol + r * n, x.data(), n * sizeof(double));
+        });
+  });
+}
+
+template <class P>
+int diis(const P& problem, size_t n, const itsolv_options* opt, itsolv_result* out, double* xo) {
+  return guarded([&] {
+    std::memset(out, 0, sizeof(*out));
+    pr::run_diis<V, V, SP>(
+        cpu_handlers(), problem, [&] { return V(n, 0.0); }, [](V& x) { x.at(0) = 1.0; }, opts_or_default(opt), *out,
+        [&](const V& x) {
+          if (xo) std::memcpy(xo, x.data(), n * sizeof(double));
+        });
+  });
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* oracle_itsolv_last_error(void) { return g_error.c_str(); }
+
+int oracle_davidson_synthetic(size_t n, double rho, int rank, unsigned long long seed, const itsolv_options* opt,
+                              itsolv_result* out, double* solutions_out) {
+  SyntheticCpu p(pr::SyntheticSpec(n, rho, rank, seed));
+  return davidson(p, n, opt, out, solutions_out);
+}
+
+int oracle_davidson_dense(const double* h, size_t n, const itsolv_options* opt, itsolv_result* out,
+                          double* solutions_out) {
+  DenseCpu p(h, n);
+  return davidson(p, n, opt, out, solutions_out);
+}
+
+int oracle_diis_synthetic(size_t n, double rho, int rank, unsigned long long seed, const itsolv_options* opt,
+                          itsolv_result* out, double* x_out) {
+  SyntheticCpu p(pr::SyntheticSpec(n, rho, rank, seed));
+  return diis(p, n, opt, out, x_out);
+}
+
+int oracle_diis_dense(const double* h, size_t n, const itsolv_options* opt, itsolv_result* out, double* x_out) {
+  DenseCpu p(h, n);
+  return diis(p, n, opt, out, x_out);
+}
+
+}  // extern "C"

@@ -187,6 +187,85 @@ def max_(n):
     return n if n > 0 else 1
 
 
+ITSOLV_PATH = os.path.join(_HERE, "build", "liboracle_itsolv.so")
+_itsolv = None
+
+
+def itsolv_lib():
+    """The reference CPU solver path (restated solvers + CPU handlers), oracle_* entry points."""
+    global _itsolv
+    if _itsolv is None:
+        if not os.path.exists(ITSOLV_PATH):
+            build()
+        from itsolv_hbm import Options, Result  # struct layouts shared with the device library
+
+        L = C.CDLL(ITSOLV_PATH)
+        Z, D, I, U = C.c_size_t, C.c_double, C.c_int, C.c_ulonglong
+        PO, PR, PDd = C.POINTER(Options), C.POINTER(Result), C.POINTER(C.c_double)
+        for name, args in {
+            "oracle_davidson_synthetic": [Z, D, I, U, PO, PR, PDd],
+            "oracle_davidson_dense": [PDd, Z, PO, PR, PDd],
+            "oracle_diis_synthetic": [Z, D, I, U, PO, PR, PDd],
+            "oracle_diis_dense": [PDd, Z, PO, PR, PDd],
+        }.items():
+            f = getattr(L, name)
+            f.restype = I
+            f.argtypes = args
+        L.oracle_itsolv_last_error.restype = C.c_char_p
+        _itsolv = L
+    return _itsolv
+
+
+def _solve(fn, args, nout):
+    from itsolv_hbm import Result
+
+    res = Result()
+    out = np.zeros(max(1, nout))
+    if fn(*args, C.byref(res), out.ctypes.data_as(PD)) != 0:
+        raise OracleError(itsolv_lib().oracle_itsolv_last_error().decode())
+    return res.as_dict(), out
+
+
+def davidson_synthetic(n, rho, rank, seed, **opts):
+    from itsolv_hbm import make_options
+
+    o = make_options(**opts)
+    r, sol = _solve(itsolv_lib().oracle_davidson_synthetic, (n, rho, rank, seed, C.byref(o)), o.nroots * n)
+    r["solutions"] = sol[: o.nroots * n].reshape(o.nroots, n)
+    return r
+
+
+def davidson_dense(h, **opts):
+    from itsolv_hbm import make_options
+
+    h = _f64(h)
+    n = h.shape[0]
+    o = make_options(**opts)
+    r, sol = _solve(itsolv_lib().oracle_davidson_dense, (_d(h), n, C.byref(o)), o.nroots * n)
+    r["solutions"] = sol[: o.nroots * n].reshape(o.nroots, n)
+    return r
+
+
+def diis_synthetic(n, rho, rank, seed, **opts):
+    from itsolv_hbm import make_options
+
+    o = make_options(**opts)
+    r, x = _solve(itsolv_lib().oracle_diis_synthetic, (n, rho, rank, seed, C.byref(o)), n)
+    r["x"] = x[:n]
+    return r
+
+
+def diis_dense(h, **opts):
+    from itsolv_hbm import make_options
+
+    h = _f64(h)
+    n = h.shape[0]
+    o = make_options(**opts)
+    r, x = _solve(itsolv_lib().oracle_diis_dense, (_d(h), n, C.byref(o)), n)
+    r["x"] = x[:n]
+    return r
+
+
 class CpuUpdateStep:
     """bench.py's cpu_baseline leg: the reference CPU handler (ArrayHandlerIterable, pairwise
     gemm_inner/gemm_outer defaults) running bench.py's subspace-update op sequence in place."""

@@ -1,0 +1,121 @@
+"""Solver-level parity: LinearEigensystemDavidson / NonLinearEquationsDIIS running on the HIP handlers
+(libitsolv_hbm.so -> libsubspace_hip.so, HBM-resident vectors) against the reference CPU path
+(oracle: the same host algorithm over the restated ArrayHandlerIterable) on identical problems.
+
+Bar (BASELINE.json north_star): eigenvalues within 1e-10 relative, identical iteration counts,
+residual norms below the convergence threshold.  At N = 1e7 / 1e8 (configs C2 / C3) the CPU path is
+too slow to run here, so the GPU result is checked against the exact eigenvalues of the rank-one
+matrix (secular equation, oracle.rank_one_eigenvalues) and its own recomputed residuals.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import itsolv_hbm as ih
+import oracle
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+G = json.load(open(os.path.join(GOLD, "eigen_golden.json")))
+
+
+def hamiltonian(name, split):
+    t = open(os.path.join(GOLD, name + ".hamiltonian")).read().split()
+    n = int(t[0])
+    return np.array(t[1 : 1 + n * n], dtype=float).reshape(n, n) + np.diag(split * np.arange(n))
+
+
+def assert_same_run(gpu, cpu, rel=1e-10):
+    assert gpu["converged"] and cpu["converged"]
+    assert gpu["iterations"] == cpu["iterations"]
+    assert gpu["r_creations"] == cpu["r_creations"]
+    scale = np.maximum(np.abs(cpu["eigenvalues"]), 1.0)
+    assert np.all(np.abs(gpu["eigenvalues"] - cpu["eigenvalues"]) <= rel * scale), (gpu["eigenvalues"], cpu["eigenvalues"])
+
+
+@pytest.mark.parametrize("name,split", [("he", 0.0), ("hf", 1e-8), ("bh", 1e-8)])
+@pytest.mark.parametrize("nroot,np_", [(1, 0), (2, 0), (3, 0), (1, 4), (3, 6)])
+def test_fixture_davidson_gpu_vs_cpu(ctx, name, split, nroot, np_):
+    if name == "he" and nroot > 1:
+        pytest.skip("degenerate pair in he")
+    h = hamiltonian(name, split)
+    kw = dict(nroots=nroot, max_p=np_, convergence_threshold=1e-8, max_size_qspace=6 * nroot, reset_D=8)
+    gpu = ih.davidson_dense(ctx, h, **kw)
+    cpu = oracle.davidson_dense(h, **kw)
+    assert_same_run(gpu, cpu)
+    assert np.all(gpu["errors"] <= 2e-8)
+    assert np.max(np.abs(gpu["eigenvalues"] - np.array(G[name]["eigenvalues"][:nroot]))) < 1e-10
+    for a, b in zip(gpu["solutions"], cpu["solutions"]):
+        assert abs(abs(np.dot(a, b)) / (np.linalg.norm(a) * np.linalg.norm(b)) - 1) < 1e-8
+
+
+def test_ones_100_gpu_vs_cpu(ctx):
+    n = 100
+    h = np.ones((n, n)) + np.diag(np.arange(n) - 1.0)
+    for nroot, np_ in ((1, 0), (3, 20), (10, 20)):
+        kw = dict(nroots=nroot, max_p=np_, convergence_threshold=1e-8, max_size_qspace=6 * nroot, reset_D=8)
+        assert_same_run(ih.davidson_dense(ctx, h, **kw), oracle.davidson_dense(h, **kw))
+
+
+@pytest.mark.parametrize("n", [2, 7, 20, 50])
+def test_diis_dense_gpu_vs_cpu(ctx, n):
+    h = np.ones((n, n)) + np.diag((np.arange(n) + 2) * 10.0)
+    kw = dict(convergence_threshold=1e-8, max_size_qspace=6)
+    gpu, cpu = ih.diis_dense(ctx, h, **kw), oracle.diis_dense(h, **kw)
+    assert gpu["converged"] and cpu["converged"] and gpu["iterations"] == cpu["iterations"]
+    np.testing.assert_allclose(gpu["x"], np.ones(n), atol=1e-8)
+    np.testing.assert_allclose(gpu["x"], cpu["x"], atol=1e-10)
+
+
+@pytest.mark.parametrize("rank", [1, 4])
+@pytest.mark.parametrize("nroot,np_", [(1, 0), (4, 0), (8, 0), (4, 8), (8, 16)])
+def test_synthetic_davidson_gpu_vs_cpu(ctx, rank, nroot, np_):
+    n, rho, seed = 100_003, 0.1, 20251015
+    kw = dict(nroots=nroot, max_p=np_, convergence_threshold=1e-8, max_size_qspace=6 * nroot, reset_D=8)
+    gpu = ih.davidson_synthetic(ctx, n, rho, rank, seed, **kw)
+    cpu = oracle.davidson_synthetic(n, rho, rank, seed, **kw)
+    assert_same_run(gpu, cpu)
+    assert np.all(gpu["residual_norms"] <= 1e-7)
+    if rank == 1:
+        np.testing.assert_allclose(gpu["eigenvalues"], oracle.rank_one_eigenvalues(n, rho, nroot), rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("n,rank", [(1000, 1), (1000, 3)])
+def test_diis_synthetic_converges_gpu_vs_cpu(ctx, n, rank):
+    kw = dict(convergence_threshold=1e-8, max_size_qspace=6)
+    gpu, cpu = ih.diis_synthetic(ctx, n, 0.1, rank, 3, **kw), oracle.diis_synthetic(n, 0.1, rank, 3, **kw)
+    assert gpu["converged"] and cpu["converged"]
+    assert gpu["iterations"] == cpu["iterations"]
+    np.testing.assert_allclose(gpu["x"], np.ones(n), atol=1e-8)
+
+
+def test_diis_synthetic_trajectory_gpu_vs_cpu(ctx):
+    # At large N the diag(1 + g) scaling stalls the reference DIIS above an absolute 1e-8 residual
+    # (both paths alike); parity is then checked on a fixed-length trajectory.
+    n, rho, rank, seed = 200_001, 0.1, 3, 3
+    kw = dict(convergence_threshold=1e-12, max_size_qspace=6, max_iter=20)
+    gpu, cpu = ih.diis_synthetic(ctx, n, rho, rank, seed, **kw), oracle.diis_synthetic(n, rho, rank, seed, **kw)
+    assert gpu["iterations"] == cpu["iterations"] == 20
+    assert abs(gpu["errors"][0] - cpu["errors"][0]) <= 1e-6 * abs(cpu["errors"][0]) + 1e-12
+    np.testing.assert_allclose(gpu["x"], cpu["x"], atol=1e-9)
+
+
+def test_config_c2_n1e7_four_roots(ctx):
+    # BASELINE config 2: Davidson, 4 roots, N = 1e7, Q in HBM on one MI355X.
+    n, rho = 10_000_000, 0.1
+    r = ih.davidson_synthetic(ctx, n, rho, 1, 1, nroots=4, convergence_threshold=1e-8, max_size_qspace=24, reset_D=8)
+    assert r["converged"]
+    np.testing.assert_allclose(r["eigenvalues"], oracle.rank_one_eigenvalues(n, rho, 4), rtol=1e-10, atol=0)
+    assert np.all(r["residual_norms"] <= 1e-7)
+
+
+def test_config_c3_n1e8_eight_roots_pspace(ctx):
+    # BASELINE config 3: Davidson, 8 roots + P space (sparse map), N = 1e8, one MI355X.
+    n, rho = 100_000_000, 0.1
+    r = ih.davidson_synthetic(ctx, n, rho, 1, 1, nroots=8, max_p=16, convergence_threshold=1e-8, max_size_qspace=48,
+                              reset_D=8)
+    assert r["converged"]
+    np.testing.assert_allclose(r["eigenvalues"], oracle.rank_one_eigenvalues(n, rho, 8), rtol=1e-10, atol=0)
+    assert np.all(r["residual_norms"] <= 1e-7)
