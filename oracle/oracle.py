@@ -348,11 +348,18 @@ def synthetic_diagonal(n, rho, rank, offset=0):
 def rank_one_eigenvalues(n, rho, nroots):
     """Exact lowest eigenvalues of diag(1..n) + rho*11^T (rho > 0) from the secular equation
     1 + rho * sum_i 1/(d_i - lam) = 0, one root in each (d_i, d_{i+1}), by bisection."""
-    d = 1.0 + np.arange(n, dtype=np.float64)
+    K = min(n, 4096)
+    d = 1.0 + np.arange(K, dtype=np.float64)
+    if n > K:
+        from scipy.special import digamma  # sum_{i=K}^{n-1} 1/(i+1-lam) = psi(n+1-lam) - psi(K+1-lam)
+
+        tail = lambda lam: digamma(n + 1.0 - lam) - digamma(K + 1.0 - lam)
+    else:
+        tail = lambda lam: 0.0
     roots = []
     for i in range(nroots):
         lo, hi = d[i], (d[i + 1] if i + 1 < n else d[i] + rho * n)
-        f = lambda lam: 1.0 + rho * np.sum(1.0 / (d - lam))
+        f = lambda lam: 1.0 + rho * (np.sum(1.0 / (d - lam)) + tail(lam))
         a, b = lo + 1e-15 * max(1.0, abs(lo)), hi - 1e-15 * max(1.0, abs(hi))
         for _ in range(200):
             mid = 0.5 * (a + b)
