@@ -5,15 +5,17 @@
 // every vector of the panel is read from HBM exactly once per call:
 //   gemm_inner  bytes = 8 N (m + k)       gemm_outer  bytes = 8 N (k + 2 m)
 //
-// gemm_inner runs on the f64 matrix cores (v_mfma_f64_16x16x4_f64).  The contraction index of the
-// MFMA is the vector index n, so one wave instruction consumes 4 (x 2 registers) elements of 16 x
-// vectors and 16 y vectors.  Lane l (c = l & 15, q = l >> 4) loads 16 B of vector c at element
-// base + 2q: for a fixed vector the four q-lanes read one contiguous 64 B segment.  The two doubles
-// of that load feed two MFMAs, so the contraction order within a 8-element chunk is permuted — the
-// result is the same sum in a different rounding order.  Accumulators: one 16x16 f64 tile (4
-// doubles per lane) per 16 columns.  Per-wave partial tiles are summed through LDS to one partial
-// per workgroup, then summed over workgroups in a fixed order (ssp::launch_reduce_partials), so the
-// result is bitwise reproducible run to run and identical on every rank after the RCCL allreduce.
+// gemm_inner runs on the f64 matrix cores with the 4-block v_mfma_f64_4x4x4_f64 (measured lane map,
+// tools/mfma_probe.hip):  lane l = 16k + 4b + i holds A_b[i][k] and B_b[k][i];  C_b[i][j] sits in
+// lane 16i + 4b + j.  Rows / columns are groups of 4 vectors; the contraction (MFMA k and block b)
+// runs over the vector index n.  The 16 lanes that hold one vector (same l & 3) load 16 B each at
+// position p = l >> 2, i.e. 256 contiguous bytes per vector per load instruction (4 vectors per
+// 1 KiB wave load), which streams at the HBM read rate (6.1 TB/s measured for 8 x 48 at N = 1e8,
+// against 3.7 TB/s for the 16x16x4 layout, whose 16 x 64 B segments per load halve the load-path
+// efficiency).  The two doubles of each 16 B load feed two MFMAs, so the summation order within a
+// 32-element chunk is a fixed permutation.  Block partials are folded with two lane shuffles, waves
+// through LDS, workgroups by a fixed-order second pass (ssp::launch_reduce_partials): bitwise
+// reproducible, and identical on every rank after the RCCL allreduce.
 #include <algorithm>
 #include <vector>
 
@@ -22,89 +24,96 @@
 namespace {
 
 using ssp::kBlock;
-typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
 __device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
 
 struct InnerArgs {
-  const double* x[ssp::kInnerRows];
-  const double* y[ssp::kInnerCols];
+  const double* x[ssp::kInnerRows];  // rows: MG groups of 4
+  const double* y[ssp::kInnerCols];  // columns: NG groups of 4
   int m;
   int k;
   size_t n;
   double* partial;  // [gridDim.x][m][k]
 };
 
-// NT: column tiles of 16 (k <= 16*NT); U: 8-element chunks per wave per iteration.
-template <int NT, int U>
+template <int MG, int NG>
 __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane & 15, q = lane >> 4;
-  const double* xp = c < a.m ? a.x[c] : nullptr;
-  const double* yp[NT];
+  const int r = lane & 3, p = lane >> 2;
+  const double* xp[MG];
+  const double* yp[NG];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) yp[t] = (16 * t + c < a.k) ? a.y[16 * t + c] : nullptr;
-
-  f64x4 acc[NT];
+  for (int g = 0; g < MG; ++g) xp[g] = (4 * g + r < a.m) ? a.x[4 * g + r] : nullptr;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f64x4{0, 0, 0, 0};
+  for (int h = 0; h < NG; ++h) yp[h] = (4 * h + r < a.k) ? a.y[4 * h + r] : nullptr;
+  double acc[MG][NG];
+#pragma unroll
+  for (int g = 0; g < MG; ++g)
+#pragma unroll
+    for (int h = 0; h < NG; ++h) acc[g][h] = 0;
 
   const size_t gw = size_t(blockIdx.x) * (kBlock / 64) + wave;
   const size_t nw = size_t(gridDim.x) * (kBlock / 64);
-  const size_t chunk = 8 * U;
-  const size_t nchunks = a.n / chunk;
+  const size_t nchunks = a.n / 32;
   const double2 z2 = make_double2(0, 0);
   for (size_t ch = gw; ch < nchunks; ch += nw) {
-    const size_t base = ch * chunk + 2 * q;
-    double2 xv[U];
-    double2 yv[U][NT];
+    const size_t e = ch * 32 + 2 * p;
+    double2 xv[MG], yv[NG];
 #pragma unroll
-    for (int u = 0; u < U; ++u) xv[u] = xp ? ld2(xp + base + 8 * u) : z2;
+    for (int g = 0; g < MG; ++g) xv[g] = xp[g] ? ld2(xp[g] + e) : z2;
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int h = 0; h < NG; ++h) yv[h] = yp[h] ? ld2(yp[h] + e) : z2;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) yv[u][t] = yp[t] ? ld2(yp[t] + base + 8 * u) : z2;
+    for (int g = 0; g < MG; ++g)
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[u].x, yv[u][t].x, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[u].y, yv[u][t].y, acc[t], 0, 0, 0);
+      for (int h = 0; h < NG; ++h) {
+        acc[g][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(xv[g].x, yv[h].x, acc[g][h], 0, 0, 0);
+        acc[g][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(xv[g].y, yv[h].y, acc[g][h], 0, 0, 0);
       }
   }
-  // Remainder [nchunks*chunk, n): 8-element sub-chunks spread over the waves, guarded loads.
-  for (size_t s = nchunks * chunk + gw * 8; s < a.n; s += nw * 8) {
-    const size_t i0 = s + 2 * q, i1 = i0 + 1;
-    const double x0 = (xp && i0 < a.n) ? xp[i0] : 0.0;
-    const double x1 = (xp && i1 < a.n) ? xp[i1] : 0.0;
+  // Remainder [32 * nchunks, n): 32-element chunks spread over the waves, guarded element loads.
+  for (size_t s = nchunks * 32 + gw * 32; s < a.n; s += nw * 32) {
+    const size_t i0 = s + 2 * p, i1 = i0 + 1;
+    double x0[MG], x1[MG];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const double y0 = (yp[t] && i0 < a.n) ? yp[t][i0] : 0.0;
-      const double y1 = (yp[t] && i1 < a.n) ? yp[t][i1] : 0.0;
-      acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, y0, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, y1, acc[t], 0, 0, 0);
+    for (int g = 0; g < MG; ++g) {
+      x0[g] = (xp[g] && i0 < a.n) ? xp[g][i0] : 0.0;
+      x1[g] = (xp[g] && i1 < a.n) ? xp[g][i1] : 0.0;
+    }
+#pragma unroll
+    for (int h = 0; h < NG; ++h) {
+      const double y0 = (yp[h] && i0 < a.n) ? yp[h][i0] : 0.0;
+      const double y1 = (yp[h] && i1 < a.n) ? yp[h][i1] : 0.0;
+#pragma unroll
+      for (int g = 0; g < MG; ++g) {
+        acc[g][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(x0[g], y0, acc[g][h], 0, 0, 0);
+        acc[g][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(x1[g], y1, acc[g][h], 0, 0, 0);
+      }
     }
   }
 
-  // Workgroup reduction of the 4 waves' tiles.  f64 16x16x4 C layout: register r of lane l holds
-  // C[row = (l >> 4) + 4 r][col = l & 15].
-  __shared__ double red[kBlock / 64][NT * 4][64];
+  // Fold the 4 blocks (lane bits 2-3), then the 4 waves through LDS.
+  __shared__ double red[kBlock / 64][MG * NG][16];
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+  for (int g = 0; g < MG; ++g)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[wave][t * 4 + r][lane] = acc[t][r];
+    for (int h = 0; h < NG; ++h) {
+      double v = acc[g][h];
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if ((lane & 12) == 0) red[wave][g * NG + h][(lane >> 4) * 4 + (lane & 3)] = v;
+    }
   __syncthreads();
   const size_t mk = size_t(a.m) * a.k;
   double* out = a.partial + size_t(blockIdx.x) * mk;
-  for (int s = threadIdx.x; s < NT * 4 * 64; s += kBlock) {
-    const int tr = s >> 6, ln = s & 63;
-    const int t = tr >> 2, r = tr & 3;
-    const int row = (ln >> 4) + 4 * r, col = 16 * t + (ln & 15);
+  for (int s = threadIdx.x; s < MG * NG * 16; s += kBlock) {
+    const int gh = s >> 4, e = s & 15;
+    const int row = 4 * (gh / NG) + (e >> 2), col = 4 * (gh % NG) + (e & 3);
     if (row < a.m && col < a.k) {
-      double v = red[0][tr][ln];
+      double v = red[0][gh][e];
 #pragma unroll
-      for (int w = 1; w < kBlock / 64; ++w) v += red[w][tr][ln];
+      for (int w = 1; w < kBlock / 64; ++w) v += red[w][gh][e];
       out[size_t(row) * a.k + col] = v;
     }
   }
@@ -185,30 +194,49 @@ int check_ptrs(const double* const* v, int count, size_t n, const char* what) {
   return SSP_OK;
 }
 
-// Number of workgroups for a gemm_inner launch: enough to give every CU 4 workgroups (16 waves)
-// when n allows, otherwise one wave per 8U-element chunk.
-unsigned inner_grid(const ssp_ctx* ctx, size_t n, int U) {
-  const size_t chunks = n / (8 * U) + 1;
-  size_t blocks = (chunks + 3) / 4;
+// Column groups per launch for MG row groups (accumulator registers: MG * NG doubles per lane).
+constexpr int ng_max(int mg) { return mg == 1 ? 16 : mg == 2 ? 12 : mg == 3 ? 8 : 6; }
+
+// Workgroups per gemm_inner launch: 4 per CU (16 waves) when n allows, else one wave per chunk.
+unsigned inner_grid(const ssp_ctx* ctx, size_t n) {
+  const size_t chunks = n / 32 + 1;
+  const size_t blocks = (chunks + 3) / 4;
   const size_t cap = size_t(ctx->num_cus) * 4;
   return unsigned(std::max<size_t>(1, std::min(blocks, cap)));
 }
 
-template <int NT>
-void launch_inner_nt(ssp_ctx* ctx, unsigned grid, const InnerArgs& a) {
-  constexpr int U = NT <= 2 ? 4 : 2;
-  hipLaunchKernelGGL((k_gemm_inner<NT, U>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+template <int MG, int NG>
+void launch_inner_t(ssp_ctx* ctx, unsigned grid, const InnerArgs& a) {
+  hipLaunchKernelGGL((k_gemm_inner<MG, NG>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
 }
 
-int launch_inner(ssp_ctx* ctx, const InnerArgs& a, unsigned grid, int nt) {
-  switch (nt) {
-    case 1: launch_inner_nt<1>(ctx, grid, a); break;
-    case 2: launch_inner_nt<2>(ctx, grid, a); break;
-    case 3: launch_inner_nt<3>(ctx, grid, a); break;
-    default: launch_inner_nt<4>(ctx, grid, a); break;
+// Smallest instantiated NG >= need (need <= ng_max(MG)).
+template <int MG>
+int launch_inner_mg(ssp_ctx* ctx, unsigned grid, const InnerArgs& a, int need) {
+  if (need <= 1) launch_inner_t<MG, 1>(ctx, grid, a);
+  else if (need <= 2) launch_inner_t<MG, 2>(ctx, grid, a);
+  else if (need <= 3) launch_inner_t<MG, 3>(ctx, grid, a);
+  else if (need <= 4) launch_inner_t<MG, 4>(ctx, grid, a);
+  else if (need <= 6) launch_inner_t<MG, 6>(ctx, grid, a);
+  else if constexpr (ng_max(MG) >= 8) {
+    if (need <= 8) launch_inner_t<MG, 8>(ctx, grid, a);
+    else if constexpr (ng_max(MG) >= 12) {
+      if (need <= 12) launch_inner_t<MG, 12>(ctx, grid, a);
+      else if constexpr (ng_max(MG) >= 16) launch_inner_t<MG, 16>(ctx, grid, a);
+    }
   }
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
+}
+
+int launch_inner(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
+  const int mg = (a.m + 3) / 4, need = (a.k + 3) / 4;
+  switch (mg) {
+    case 1: return launch_inner_mg<1>(ctx, grid, a, need);
+    case 2: return launch_inner_mg<2>(ctx, grid, a, need);
+    case 3: return launch_inner_mg<3>(ctx, grid, a, need);
+    default: return launch_inner_mg<4>(ctx, grid, a, need);
+  }
 }
 
 int launch_outer(ssp_ctx* ctx, const OuterArgs& a) {
@@ -239,7 +267,7 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
   if (m == 0 || k == 0) return SSP_OK;
   SSP_TRY(check_ptrs(xx, m, n, "ssp_gemm_inner"));
   SSP_TRY(check_ptrs(yy, k, n, "ssp_gemm_inner"));
-  // Put the shorter side on the MFMA rows (padded to 16), the longer on the columns.
+  // Put the shorter side on the MFMA rows (groups of 4, at most 16 per launch), the longer on the columns.
   const bool swap = m > k;
   const double* const* rows = swap ? yy : xx;
   const double* const* cols = swap ? xx : yy;
@@ -256,18 +284,19 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
     const double nvec = double(std::unique(distinct.begin(), distinct.end()) - distinct.begin());
     ssp::LedgerScope ls(ctx, "gemm_inner", 8.0 * n * nvec);
     for (int r0 = 0; r0 < R; r0 += ssp::kInnerRows) {
-      for (int c0 = 0; c0 < C; c0 += ssp::kInnerCols) {
+      const int mr = std::min(ssp::kInnerRows, R - r0);
+      const int cols_per_launch = 4 * ng_max((mr + 3) / 4);
+      for (int c0 = 0; c0 < C; c0 += cols_per_launch) {
         InnerArgs a{};
-        a.m = std::min(ssp::kInnerRows, R - r0);
-        a.k = std::min(ssp::kInnerCols, C - c0);
+        a.m = mr;
+        a.k = std::min(cols_per_launch, C - c0);
         a.n = n;
         for (int i = 0; i < a.m; ++i) a.x[i] = rows[r0 + i];
         for (int j = 0; j < a.k; ++j) a.y[j] = cols[c0 + j];
-        const int nt = (a.k + 15) / 16;
-        const unsigned grid = inner_grid(ctx, n, nt <= 2 ? 4 : 2);
+        const unsigned grid = inner_grid(ctx, n);
         SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * a.m * a.k));
         a.partial = ctx->partial;
-        SSP_TRY(launch_inner(ctx, a, grid, nt));
+        SSP_TRY(launch_inner(ctx, a, grid));
         SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), a.m, a.k, ctx->result_dev, C, r0, c0));
       }
     }

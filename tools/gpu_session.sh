@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: GPU tests, bench, kernel-trace profile.  Each GPU step has its own time limit;
 # a fault / abort / timeout ends the session (no retries).  Outputs land in gpurun_out/.
-# Usage: tools/gpu_session.sh [tests|bench|prof|all] [extra bench args...]
+# Usage: tools/gpu_session.sh [tests|bench|prof|pmc|all] [extra bench args...]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -43,5 +43,16 @@ if [ "$what" = prof ] || [ "$what" = all ]; then
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "$@"
   rc=$?
   if [ $rc -ne 0 ]; then exit $rc; fi
+fi
+if [ "$what" = pmc ] || [ "$what" = all ]; then
+  # HBM traffic counters, one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass);
+  # kernel trace only, no runtime/API tracing alongside --pmc.
+  for c in FETCH_SIZE WRITE_SIZE; do
+    rm -rf "$OUT/pmc_$c"
+    step "pmc_$c" 600 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- \
+      python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 --no-cpu-baseline "$@"
+    rc=$?
+    if [ $rc -ne 0 ]; then exit $rc; fi
+  done
 fi
 echo "session done"
