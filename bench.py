@@ -88,6 +88,28 @@ class Workload:
         return err
 
 
+OP_KERNELS = {"gemm_inner": ("k_gemm_inner",), "gemm_outer": ("k_gemm_outer",), "axpy": ("k_axpy",),
+              "fill": ("k_fill",), "dot": ("k_dot_partial",)}
+
+
+def pmc_traffic(path, op, n_global, m, k, world):
+    """HBM bytes per launch of `op`'s main kernel from a committed rocprofv3 --pmc summary
+    (tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE, gfx950 corrections) of THIS workload."""
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    w = d.get("workload") or {}
+    if (w.get("n_global"), w.get("roots"), w.get("qspace"), w.get("n_gpus")) != (n_global, m, k, world):
+        return None, None
+    prefixes = OP_KERNELS.get(op, ())
+    for name, v in d["kernels"].items():
+        base = name.split("<")[0]
+        if base in prefixes:
+            return v["hbm_bytes_per_dispatch"], os.path.relpath(path, ROOT) + ":" + name
+    return None, None
+
+
 def cpu_baseline(m, k, seconds):
     """The oracle (CPU restatement of ArrayHandlerIterable: pairwise gemm, sequential loops) on one
     host core, same op sequence, bounded sample."""
@@ -133,6 +155,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ledger-steps", type=int, default=3)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r1", "pmc_traffic_n1e8.json"),
+                    help="rocprofv3 --pmc summary of this workload (roofline.traffic)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -195,6 +219,7 @@ def main():
         dom = max(led, key=lambda op: led[op]["ms"])
         e = led[dom]
         achieved = (e["bytes"] / e["calls"]) / (e["ms"] / e["calls"] / 1e3) / 1e9
+        traffic, traffic_src = pmc_traffic(args.pmc_json, dom, n_global, m, k, world)
         ops = {op: {"calls_per_step": v["calls"] / args.ledger_steps,
                     "avg_us": 1e3 * v["ms"] / v["calls"],
                     "GBs": v["bytes"] / (v["ms"] / 1e3) / 1e9} for op, v in led.items()}
@@ -228,7 +253,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_launch_us": round(1e3 * e["ms"] / e["calls"], 2),
                 "bytes_per_launch": e["bytes"] / e["calls"],
             },

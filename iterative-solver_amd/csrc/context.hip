@@ -41,10 +41,10 @@ int use_device(ssp_ctx* ctx) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-unsigned stream_grid(const ssp_ctx* ctx, size_t work_items, unsigned per_thread) {
+unsigned stream_grid(const ssp_ctx* ctx, size_t work_items, unsigned per_thread, unsigned blocks_per_cu) {
   const size_t per_block = size_t(kBlock) * per_thread;
   size_t blocks = (work_items + per_block - 1) / per_block;
-  const size_t cap = size_t(ctx->num_cus) * 8;  // 8 workgroups (32 waves) per CU, grid-stride beyond
+  const size_t cap = size_t(ctx->num_cus) * blocks_per_cu;  // grid-stride beyond
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   return unsigned(blocks);

@@ -3,7 +3,9 @@
 // Reference loops (single-threaded std::fill / transform / inner_product):
 //   ArrayHandlerIterable.h:46-82, DistrArray.cpp:43-138, itsolv/IterativeSolver.h:34-55.
 // Each is HBM-bound (<= 0.25 flop/B).  Layout: 16-byte (double2) accesses per lane, 4 independent
-// accesses per lane in flight, grid-stride over at most 8 workgroups per CU.  Reductions are two
+// accesses per lane in flight, grid-stride.  Grid caps and nontemporal accesses follow the sweep in
+// tools/mb_stream.hip (profiles/r1/mb_stream*.txt): fill and axpy run best with one pass over a
+// large grid (64 workgroups per CU), dot with 8 per CU and nontemporal loads.  Reductions are two
 // pass and deterministic: one partial per workgroup in a fixed grid, then a fixed-order tree.
 #include <algorithm>
 
@@ -82,14 +84,16 @@ __global__ __launch_bounds__(kBlock) void k_axpy(const double* __restrict__ x, d
   const size_t stride = size_t(gridDim.x) * kBlock;
   size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   for (; i + 3 * stride < n2; i += 4 * stride) {
-    double2 x0 = ld2(x + 2 * i), x1 = ld2(x + 2 * (i + stride)), x2 = ld2(x + 2 * (i + 2 * stride)),
-            x3 = ld2(x + 2 * (i + 3 * stride));
-    double2 y0 = ld2(y + 2 * i), y1 = ld2(y + 2 * (i + stride)), y2 = ld2(y + 2 * (i + 2 * stride)),
-            y3 = ld2(y + 2 * (i + 3 * stride));
-    st2(y + 2 * i, make_double2(fma(alpha, x0.x, y0.x), fma(alpha, x0.y, y0.y)));
-    st2(y + 2 * (i + stride), make_double2(fma(alpha, x1.x, y1.x), fma(alpha, x1.y, y1.y)));
-    st2(y + 2 * (i + 2 * stride), make_double2(fma(alpha, x2.x, y2.x), fma(alpha, x2.y, y2.y)));
-    st2(y + 2 * (i + 3 * stride), make_double2(fma(alpha, x3.x, y3.x), fma(alpha, x3.y, y3.y)));
+    using ssp::ld2nt;
+    using ssp::st2nt;
+    double2 x0 = ld2nt(x + 2 * i), x1 = ld2nt(x + 2 * (i + stride)), x2 = ld2nt(x + 2 * (i + 2 * stride)),
+            x3 = ld2nt(x + 2 * (i + 3 * stride));
+    double2 y0 = ld2nt(y + 2 * i), y1 = ld2nt(y + 2 * (i + stride)), y2 = ld2nt(y + 2 * (i + 2 * stride)),
+            y3 = ld2nt(y + 2 * (i + 3 * stride));
+    st2nt(y + 2 * i, make_double2(fma(alpha, x0.x, y0.x), fma(alpha, x0.y, y0.y)));
+    st2nt(y + 2 * (i + stride), make_double2(fma(alpha, x1.x, y1.x), fma(alpha, x1.y, y1.y)));
+    st2nt(y + 2 * (i + 2 * stride), make_double2(fma(alpha, x2.x, y2.x), fma(alpha, x2.y, y2.y)));
+    st2nt(y + 2 * (i + 3 * stride), make_double2(fma(alpha, x3.x, y3.x), fma(alpha, x3.y, y3.y)));
   }
   for (; i < n2; i += stride) {
     double2 a = ld2(x + 2 * i), b = ld2(y + 2 * i);
@@ -98,6 +102,8 @@ __global__ __launch_bounds__(kBlock) void k_axpy(const double* __restrict__ x, d
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) y[n - 1] = fma(alpha, x[n - 1], y[n - 1]);
 }
 
+// SAME: x == y (norms), one load stream.
+template <bool SAME>
 __global__ __launch_bounds__(kBlock) void k_dot_partial(const double* __restrict__ x, const double* __restrict__ y,
                                                         size_t n, double* __restrict__ partial) {
   const size_t n2 = n >> 1;
@@ -105,10 +111,16 @@ __global__ __launch_bounds__(kBlock) void k_dot_partial(const double* __restrict
   size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
   for (; i + 3 * stride < n2; i += 4 * stride) {
-    double2 x0 = ld2(x + 2 * i), x1 = ld2(x + 2 * (i + stride)), x2 = ld2(x + 2 * (i + 2 * stride)),
-            x3 = ld2(x + 2 * (i + 3 * stride));
-    double2 y0 = ld2(y + 2 * i), y1 = ld2(y + 2 * (i + stride)), y2 = ld2(y + 2 * (i + 2 * stride)),
-            y3 = ld2(y + 2 * (i + 3 * stride));
+    using ssp::ld2nt;
+    double2 x0 = ld2nt(x + 2 * i), x1 = ld2nt(x + 2 * (i + stride)), x2 = ld2nt(x + 2 * (i + 2 * stride)),
+            x3 = ld2nt(x + 2 * (i + 3 * stride));
+    double2 y0 = x0, y1 = x1, y2 = x2, y3 = x3;
+    if (!SAME) {
+      y0 = ld2nt(y + 2 * i);
+      y1 = ld2nt(y + 2 * (i + stride));
+      y2 = ld2nt(y + 2 * (i + 2 * stride));
+      y3 = ld2nt(y + 2 * (i + 3 * stride));
+    }
     s0 = fma(x0.x, y0.x, s0);
     s0 = fma(x0.y, y0.y, s0);
     s1 = fma(x1.x, y1.x, s1);
@@ -195,7 +207,7 @@ int ssp_fill(ssp_ctx* ctx, double alpha, double* x, size_t n) {
   SSP_TRY(check_vec(x, n, "ssp_fill"));
   if (n == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "fill", 8.0 * n);
-  hipLaunchKernelGGL(k_fill, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
+  hipLaunchKernelGGL(k_fill, dim3(ssp::stream_grid(ctx, n / 2 + 1, 1, 64)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -227,7 +239,7 @@ int ssp_axpy(ssp_ctx* ctx, double alpha, const double* x, double* y, size_t n) {
   SSP_TRY(check_vec(y, n, "ssp_axpy"));
   if (n == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "axpy", 24.0 * n);
-  hipLaunchKernelGGL(k_axpy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4)), dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+  hipLaunchKernelGGL(k_axpy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -244,7 +256,10 @@ int ssp_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, double* ou
     const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 4);
     SSP_TRY(ssp::ensure_partial(ctx, grid));
     ssp::LedgerScope ls(ctx, "dot", (x == y ? 8.0 : 16.0) * n);
-    hipLaunchKernelGGL(k_dot_partial, dim3(grid), dim3(kBlock), 0, ctx->stream, x, y, n, ctx->partial);
+    if (x == y)
+      hipLaunchKernelGGL(k_dot_partial<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, x, y, n, ctx->partial);
+    else
+      hipLaunchKernelGGL(k_dot_partial<false>, dim3(grid), dim3(kBlock), 0, ctx->stream, x, y, n, ctx->partial);
     SSP_TRY_HIP(hipGetLastError());
     SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, 1, ctx->result_dev, 1, 0, 0));
   }

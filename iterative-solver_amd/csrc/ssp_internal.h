@@ -82,7 +82,21 @@ int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n);
 // Copies n doubles of ctx->result_dev to host `out` after the stream drains.
 int fetch_result(ssp_ctx* ctx, double* out, size_t n);
 // Grid size for streaming kernels: enough workgroups to fill 256 CUs, grid-stride beyond.
-unsigned stream_grid(const ssp_ctx* ctx, size_t work_items, unsigned per_thread);
+// Workgroups for a grid-stride streaming launch: enough for work_items / (kBlock * per_thread),
+// at most blocks_per_cu per CU.
+unsigned stream_grid(const ssp_ctx* ctx, size_t work_items, unsigned per_thread, unsigned blocks_per_cu = 8);
+
+// Nontemporal 16-byte accesses for vectors streamed exactly once per kernel (measured on gfx950,
+// tools/mb_stream.hip: +3-10 % on dot / axpy / gemm_outer against plain global loads/stores).
+typedef double nt_double2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 ld2nt(const double* p) {
+  const nt_double2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_double2*>(p));
+  return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ void st2nt(double* p, double2 v) {
+  const nt_double2 w = {v.x, v.y};
+  __builtin_nontemporal_store(w, reinterpret_cast<nt_double2*>(p));
+}
 bool aligned16(const void* p);
 
 // Ledger scope: records a start event now and an end event at destruction (when enabled).

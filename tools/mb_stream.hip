@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void k_o1(const OArgs a) {
 }
 
 // o2: U positions per thread per iteration (p, p + 64 within the wave's 2U KiB window).
-template <int M, int B, int U>
+template <int M, int B, int U, bool NTX = false, bool NTY = false>
 __global__ __launch_bounds__(256) void k_o2(const OArgs a) {
   const int lane = threadIdx.x & 63;
   const size_t gw = size_t(blockIdx.x) * 4 + (threadIdx.x >> 6), nw = size_t(gridDim.x) * 4;
@@ -115,7 +115,8 @@ __global__ __launch_bounds__(256) void k_o2(const OArgs a) {
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int b = 0; b < B; ++b)
-          xv[u][b] = (p0 + 64 * u < n2) ? ld2(a.x[i + b] + 2 * (p0 + 64 * u)) : make_double2(0, 0);
+          xv[u][b] = (p0 + 64 * u < n2) ? (NTX ? ld2nt(a.x[i + b] + 2 * (p0 + 64 * u)) : ld2(a.x[i + b] + 2 * (p0 + 64 * u)))
+                                        : make_double2(0, 0);
 #pragma unroll
       for (int b = 0; b < B; ++b)
 #pragma unroll
@@ -132,7 +133,10 @@ __global__ __launch_bounds__(256) void k_o2(const OArgs a) {
     for (int u = 0; u < U; ++u)
       if (p0 + 64 * u < n2)
 #pragma unroll
-        for (int j = 0; j < M; ++j) st2(a.y[j] + 2 * (p0 + 64 * u), acc[u][j]);
+        for (int j = 0; j < M; ++j) {
+          if (NTY) st2nt(a.y[j] + 2 * (p0 + 64 * u), acc[u][j]);
+          else st2(a.y[j] + 2 * (p0 + 64 * u), acc[u][j]);
+        }
   }
 }
 
@@ -232,24 +236,26 @@ int main(int argc, char** argv) {
   auto rep = [&](const char* name, int g, float ms, double bytes) {
     printf("%-26s g=%-6d %8.3f ms  %7.1f GB/s\n", name, g, ms, bytes / ms / 1e6);
   };
-  for (int g : {1024, 2048, 4096}) {
-    rep("outer o0", g, timeit([&] { hipLaunchKernelGGL((k_o0<8>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-    rep("outer o1 B8", g, timeit([&] { hipLaunchKernelGGL((k_o1<8, 8, false>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-    rep("outer o1 B16", g, timeit([&] { hipLaunchKernelGGL((k_o1<8, 16, false>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-    rep("outer o1 B8 nt", g, timeit([&] { hipLaunchKernelGGL((k_o1<8, 8, true>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-    rep("outer o2 B8 U2", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 8, 2>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-    rep("outer o2 B4 U4", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 4, 4>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
+  const int mode = argc > 2 ? atoi(argv[2]) : 0;
+  if (mode == 0) {
+    for (int g : {256, 512, 1024, 2048}) {
+      rep("outer o1 B8 nt", g, timeit([&] { hipLaunchKernelGGL((k_o1<8, 8, true>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
+      rep("outer o2 B4 U4", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 4, 4>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
+      rep("outer o2 B4 U4 ntx", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 4, 4, true, false>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
+      rep("outer o2 B4 U4 ntx nty", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 4, 4, true, true>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
+      rep("outer o2 B2 U8 ntx", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 2, 8, true, false>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
+      rep("outer o2 B4 U2 ntx", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 4, 2, true, false>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
+      rep("outer o2 B8 U4 ntx", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 8, 4, true, false>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
+    }
   }
-  for (int g : {1024, 2048, 4096, 8192}) {
-    rep("fill U4", g, timeit([&] { hipLaunchKernelGGL((k_fill<false, 4>), dim3(g), dim3(256), 0, 0, vec[0], n, 0.0); }, 10), vb);
-    rep("fill U4 nt", g, timeit([&] { hipLaunchKernelGGL((k_fill<true, 4>), dim3(g), dim3(256), 0, 0, vec[0], n, 0.0); }, 10), vb);
+  for (int g : {2048, 8192, 16384}) {
     rep("fill U1", g, timeit([&] { hipLaunchKernelGGL((k_fill<false, 1>), dim3(g), dim3(256), 0, 0, vec[0], n, 0.0); }, 10), vb);
-    rep("axpy U4", g, timeit([&] { hipLaunchKernelGGL((k_axpy<false, 4>), dim3(g), dim3(256), 0, 0, vec[1], vec[2], n, 0.5); }, 10), 3 * vb);
+    rep("fill U2", g, timeit([&] { hipLaunchKernelGGL((k_fill<false, 2>), dim3(g), dim3(256), 0, 0, vec[0], n, 0.0); }, 10), vb);
+    rep("axpy U1 nt", g, timeit([&] { hipLaunchKernelGGL((k_axpy<true, 1>), dim3(g), dim3(256), 0, 0, vec[1], vec[2], n, 0.5); }, 10), 3 * vb);
+    rep("axpy U2 nt", g, timeit([&] { hipLaunchKernelGGL((k_axpy<true, 2>), dim3(g), dim3(256), 0, 0, vec[1], vec[2], n, 0.5); }, 10), 3 * vb);
     rep("axpy U4 nt", g, timeit([&] { hipLaunchKernelGGL((k_axpy<true, 4>), dim3(g), dim3(256), 0, 0, vec[1], vec[2], n, 0.5); }, 10), 3 * vb);
-    rep("axpy U2", g, timeit([&] { hipLaunchKernelGGL((k_axpy<false, 2>), dim3(g), dim3(256), 0, 0, vec[1], vec[2], n, 0.5); }, 10), 3 * vb);
-    rep("dot U4", g, timeit([&] { hipLaunchKernelGGL((k_dot<false, 4>), dim3(g), dim3(256), 0, 0, vec[3], n, partial); }, 10), vb);
+    rep("dot U2 nt", g, timeit([&] { hipLaunchKernelGGL((k_dot<true, 2>), dim3(g), dim3(256), 0, 0, vec[3], n, partial); }, 10), vb);
     rep("dot U4 nt", g, timeit([&] { hipLaunchKernelGGL((k_dot<true, 4>), dim3(g), dim3(256), 0, 0, vec[3], n, partial); }, 10), vb);
-    rep("dot U8", g, timeit([&] { hipLaunchKernelGGL((k_dot<false, 8>), dim3(g), dim3(256), 0, 0, vec[3], n, partial); }, 10), vb);
   }
   return 0;
 }

@@ -9,7 +9,7 @@ Conventions (/opt/skills/guides/MI355X_MICROARCH.md, "HBM" section):
 Every kernel of this library streams with 16 B/lane loads and stores (double2), so both
 corrections apply.  The JSON written here is what bench.py reports as roofline.traffic.
 
-usage: tools/pmc_summary.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <out.json> [label]
+usage: tools/pmc_summary.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <out.json> [label] [n_global,m,k,gpus]
 """
 import csv
 import json
@@ -36,6 +36,10 @@ def short(name):
 def main():
     fdir, wdir, out = sys.argv[1:4]
     label = sys.argv[4] if len(sys.argv) > 4 else ""
+    workload = None
+    if len(sys.argv) > 5:
+        n, m, k, g = (int(float(v)) for v in sys.argv[5].split(","))
+        workload = {"n_global": n, "roots": m, "qspace": k, "n_gpus": g}
     fetch = per_kernel(f"{fdir}/run_counter_collection.csv", "FETCH_SIZE")
     write = per_kernel(f"{wdir}/run_counter_collection.csv", "WRITE_SIZE")
     res = {}
@@ -51,7 +55,7 @@ def main():
             "raw_fetch_kib_avg": sum(fv) / len(fv) if fv else None,
             "raw_write_kib_avg": sum(wv) / len(wv) if wv else None,
         }
-    json.dump({"label": label, "corrections": "read = 2 x FETCH_SIZE KiB x 1024; write = WRITE_SIZE KiB x 1024",
+    json.dump({"label": label, "workload": workload, "corrections": "read = 2 x FETCH_SIZE KiB x 1024; write = WRITE_SIZE KiB x 1024",
                "kernels": res}, open(out, "w"), indent=1)
     for k, v in res.items():
         print(f"{k:40s} n={v['dispatches']:4d} read={v['read_bytes_per_dispatch'] or 0:.4g} "
