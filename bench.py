@@ -20,7 +20,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import struct
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -40,12 +42,9 @@ def log(*a):
 
 
 def distribution(n, chunks):
-    """make_distribution_spread_remainder (reference util/Distribution.h:376-387)."""
-    block, extra = divmod(n, chunks)
-    borders = [0]
-    for c in range(chunks):
-        borders.append(borders[-1] + block + (1 if c < extra else 0))
-    return borders
+    """Shard borders from ssp_shard_range (make_distribution_spread_remainder, reference
+    util/Distribution.h:99-109)."""
+    return [sh.shard_range(n, chunks, r)[0] for r in range(chunks)] + [n]
 
 
 def step_bytes(n, m, k):
@@ -110,6 +109,28 @@ def pmc_traffic(path, op, n_global, m, k, world):
     return None, None
 
 
+def rendezvous_uid(rank, world, timeout=300.0):
+    """RCCL unique id from rank 0 to every rank of this node through a file keyed by the launcher
+    (MASTER_ADDR/PORT and the parent pid all local ranks share).  No torch in this process: it
+    would bring a second HIP runtime next to libsubspace_hip.so's."""
+    tag = "{}_{}_{}".format(os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"),
+                            os.getppid())
+    path = os.path.join(tempfile.gettempdir(), f"ssp_bench_uid_{tag}")
+    if rank == 0:
+        uid = sh.Context.unique_id()
+        with open(path + ".tmp", "wb") as f:
+            f.write(uid)
+        os.replace(path + ".tmp", path)
+        return uid, path
+    t0 = time.time()
+    while not os.path.exists(path):
+        if time.time() - t0 > timeout:
+            raise TimeoutError(f"rank {rank}: no RCCL id at {path}")
+        time.sleep(0.05)
+    with open(path, "rb") as f:
+        return f.read(), None
+
+
 def cpu_baseline(m, k, seconds):
     """The oracle (CPU restatement of ArrayHandlerIterable: pairwise gemm, sequential loops) on one
     host core, same op sequence, bounded sample."""
@@ -162,18 +183,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # plumbing: rendezvous, barrier, max-time reduction
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-
+    uid, uid_path = rendezvous_uid(rank, world) if world > 1 else (None, None)
     ctx = sh.Context(local_rank)
     if world > 1:
-        uid = [sh.Context.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx.attach_comm(world, rank, uid[0])
+        ctx.attach_comm(world, rank, uid)  # collective: returns once every rank has joined
+        if uid_path:
+            os.remove(uid_path)
 
     n_global = int(args.n)
     m, k = args.roots, args.qsize
@@ -183,8 +201,8 @@ def main():
     wl = Workload(ctx, n_local, offset, m, k)
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        if world > 1:
+            ctx.barrier()
 
     for _ in range(args.warmup):
         wl.step()
@@ -197,12 +215,8 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if world > 1:  # max over ranks
+        elapsed = max(struct.unpack("<d", b)[0] for b in ctx.allgather_bytes(struct.pack("<d", elapsed)))
 
     # Per-kernel HIP-event ledger over a few extra steps (not part of the timed region).
     ctx.ledger_reset()
@@ -266,9 +280,7 @@ def main():
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    barrier()
     ctx.close()
 
 

@@ -72,6 +72,16 @@ int ssp_ctx_nranks(ssp_ctx* ctx);
 int ssp_allreduce_sum(ssp_ctx* ctx, double* buf_dev, size_t n);
 /* Gather `bytes` host bytes from every rank into recv (nranks*bytes), rank order. */
 int ssp_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes);
+/* Host-callback communicator in place of RCCL: reductions are staged through host memory and
+ * handed to the callbacks (return 0 on success).  For transports without RCCL and for testing
+ * the sharded path with several ranks on one device.  Replaces any attached RCCL communicator. */
+typedef int (*ssp_host_allreduce_fn)(double* buf, size_t n, void* user);
+typedef int (*ssp_host_allgather_fn)(const void* send, void* recv, size_t bytes, void* user);
+int ssp_ctx_attach_host_comm(ssp_ctx* ctx, int nranks, int rank, ssp_host_allreduce_fn allreduce,
+                             ssp_host_allgather_fn allgather, void* user);
+/* Shard of a global length n owned by `rank` of `nranks` (host only, no context):
+ * make_distribution_spread_remainder, reference util/Distribution.h:99-109. */
+int ssp_shard_range(size_t n, int nranks, int rank, size_t* offset, size_t* length);
 
 /* Operation ledger (measurement): when enabled, HIP events on the
  * context's stream bracket each hot-path kernel launch and the call's ALGORITHMIC bytes are
@@ -110,6 +120,13 @@ int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, 
  *      over all ranks with the reference's tie rule (larger index wins a tie). ----------- */
 int ssp_select(ssp_ctx* ctx, const double* x, size_t n, size_t offset, size_t nsel, int max, int ignore_sign,
                size_t* idx_out, double* val_out, size_t* nout);
+/* Merge of per-rank selections (host only, no context): rank r's count[r] <= stride results are
+ * idx/val[r*stride ...] as ssp_select returns them (val = x, |x| or |x*y|).  Keeps the nsel
+ * largest (v', index) pairs, v' = max ? val : -val, ties to the larger index, and returns them
+ * ordered by index -- the reference heap's result (util/select.h:28-55).  ssp_select and
+ * ssp_select_max_dot (max = 1) merge their all-gathered candidates with this function. */
+int ssp_select_merge(int nranks, const size_t* counts, size_t stride, const size_t* idx, const double* val,
+                     size_t nsel, int max, size_t* idx_out, double* val_out, size_t* nout);
 int ssp_select_max_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, size_t offset, size_t nsel,
                        size_t* idx_out, double* val_out, size_t* nout);
 

@@ -112,7 +112,19 @@ int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev) {
 }
 
 int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n) {
-  if (!ctx->comm || ctx->nranks <= 1 || n == 0) return SSP_OK;
+  if (ctx->nranks <= 1 || n == 0) return SSP_OK;
+  if (ctx->host_allreduce) {
+    // Host-callback communicator: stage through the host (test / fallback transport only).
+    std::vector<double> h(n);
+    SSP_TRY_HIP(hipMemcpyAsync(h.data(), buf, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->host_allreduce(h.data(), n, ctx->host_user) != 0)
+      return set_error(SSP_ERR_COMM, "host allreduce callback failed");
+    SSP_TRY_HIP(hipMemcpyAsync(buf, h.data(), n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    return SSP_OK;
+  }
+  if (!ctx->comm) return SSP_OK;
   ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream);
   if (r != ncclSuccess) return set_error(SSP_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
   return SSP_OK;
@@ -377,6 +389,9 @@ int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id) {
     ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
   }
+  ctx->host_allreduce = nullptr;
+  ctx->host_allgather = nullptr;
+  ctx->host_user = nullptr;
   ctx->nranks = nranks;
   ctx->rank = rank;
   if (nranks == 1) return SSP_OK;
@@ -387,6 +402,35 @@ int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id) {
     ctx->comm = nullptr;
     return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
   }
+  return SSP_OK;
+}
+
+int ssp_ctx_attach_host_comm(ssp_ctx* ctx, int nranks, int rank, ssp_host_allreduce_fn allreduce,
+                             ssp_host_allgather_fn allgather, void* user) {
+  SSP_CHECK_CTX(ctx);
+  if (nranks < 1 || rank < 0 || rank >= nranks) return ssp::set_error(SSP_ERR_ARG, "ssp_ctx_attach_host_comm: bad rank");
+  if (nranks > 1 && (!allreduce || !allgather))
+    return ssp::set_error(SSP_ERR_ARG, "ssp_ctx_attach_host_comm: null callback");
+  if (ctx->comm) {
+    ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+  }
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  ctx->host_allreduce = allreduce;
+  ctx->host_allgather = allgather;
+  ctx->host_user = user;
+  return SSP_OK;
+}
+
+int ssp_shard_range(size_t n, int nranks, int rank, size_t* offset, size_t* length) {
+  if (nranks < 1 || rank < 0 || rank >= nranks || !offset || !length)
+    return ssp::set_error(SSP_ERR_ARG, "ssp_shard_range: bad arguments");
+  // make_distribution_spread_remainder (reference util/Distribution.h:99-109).
+  const size_t p = size_t(nranks), r = size_t(rank);
+  const size_t block = n / p, extra = n % p;
+  *offset = r * block + std::min(r, extra);
+  *length = block + (r < extra ? 1 : 0);
   return SSP_OK;
 }
 
@@ -402,6 +446,11 @@ int ssp_allreduce_sum(ssp_ctx* ctx, double* buf, size_t n) {
 
 int ssp_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes) {
   SSP_CHECK_CTX(ctx);
+  if (ctx->host_allgather && ctx->nranks > 1) {
+    if (ctx->host_allgather(send, recv, bytes, ctx->host_user) != 0)
+      return ssp::set_error(SSP_ERR_COMM, "host allgather callback failed");
+    return SSP_OK;
+  }
   if (!ctx->comm || ctx->nranks <= 1) {
     if (bytes) std::memcpy(recv, send, bytes);
     return SSP_OK;

@@ -158,39 +158,61 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
     const size_t real = std::min(n, nsel);
     local.resize(real);
   }
-  // Fixed-size exchange: nsel slots per rank, padded with key 0.
-  std::vector<Cand> send(nsel, Cand{0ull, 0ull});
-  std::copy(local.begin(), local.end(), send.begin());
-  std::vector<unsigned long long> counts_send{local.size()};
-  std::vector<Cand> all(nsel * size_t(ctx->nranks));
-  std::vector<unsigned long long> counts(ctx->nranks);
-  if (ctx->nranks > 1) {
-    SSP_TRY(ssp_allgather_host(ctx, counts_send.data(), counts.data(), sizeof(unsigned long long)));
-    if (nsel) SSP_TRY(ssp_allgather_host(ctx, send.data(), all.data(), sizeof(Cand) * nsel));
-  } else {
-    counts[0] = local.size();
-    all = send;
+  // This rank's best n as (global index, returned value), then the fixed-size exchange: nsel
+  // slots per rank plus the real count, and the same host merge on every rank.
+  std::vector<size_t> lidx(nsel, 0);
+  std::vector<double> lval(nsel, 0.0);
+  for (size_t e = 0; e < local.size(); ++e) {
+    const double v = key_value(local[e].key);
+    lidx[e] = size_t(local[e].idx);
+    lval[e] = (mode == 0 && !max) ? -v : v;
   }
-  std::vector<Cand> merged;
-  for (int r = 0; r < ctx->nranks; ++r)
-    for (size_t e = 0; e < counts[r]; ++e) merged.push_back(all[size_t(r) * nsel + e]);
-  std::sort(merged.begin(), merged.end(), [](const Cand& p, const Cand& q) {
-    return p.key > q.key || (p.key == q.key && p.idx > q.idx);
-  });
-  if (merged.size() > nsel) merged.resize(nsel);
-  std::sort(merged.begin(), merged.end(), [](const Cand& p, const Cand& q) { return p.idx < q.idx; });
-  for (size_t e = 0; e < merged.size(); ++e) {
-    const double v = key_value(merged[e].key);
-    if (idx_out) idx_out[e] = size_t(merged[e].idx);
-    if (val_out) val_out[e] = (mode == 0 && !max) ? -v : v;
+  const int nr = ctx->nranks;
+  std::vector<size_t> counts(nr), gidx(nsel * size_t(nr)), gval_bits(nsel * size_t(nr));
+  const size_t my_count = local.size();
+  SSP_TRY(ssp_allgather_host(ctx, &my_count, counts.data(), sizeof(size_t)));
+  if (nsel) {
+    SSP_TRY(ssp_allgather_host(ctx, lidx.data(), gidx.data(), sizeof(size_t) * nsel));
+    SSP_TRY(ssp_allgather_host(ctx, lval.data(), gval_bits.data(), sizeof(double) * nsel));
   }
-  *nout = merged.size();
-  return SSP_OK;
+  const double* gval = reinterpret_cast<const double*>(gval_bits.data());
+  return ssp_select_merge(nr, counts.data(), nsel, gidx.data(), gval, nsel, (mode == 1) ? 1 : max, idx_out, val_out,
+                          nout);
 }
 
 }  // namespace
 
 extern "C" {
+
+int ssp_select_merge(int nranks, const size_t* counts, size_t stride, const size_t* idx, const double* val,
+                     size_t nsel, int max, size_t* idx_out, double* val_out, size_t* nout) {
+  if (!nout || nranks < 1 || (nranks > 0 && !counts)) return ssp::set_error(SSP_ERR_ARG, "ssp_select_merge: bad args");
+  *nout = 0;
+  struct Item {
+    unsigned long long key;
+    size_t idx;
+    double val;
+  };
+  std::vector<Item> merged;
+  for (int r = 0; r < nranks; ++r) {
+    if (counts[r] > stride) return ssp::set_error(SSP_ERR_ARG, "ssp_select_merge: count exceeds stride");
+    for (size_t e = 0; e < counts[r]; ++e) {
+      const size_t s = size_t(r) * stride + e;
+      merged.push_back({order_key(max ? val[s] : -val[s]), idx[s], val[s]});
+    }
+  }
+  // The reference heap keeps the n largest (v', index) pairs: v' descending, larger index first.
+  std::sort(merged.begin(), merged.end(),
+            [](const Item& p, const Item& q) { return p.key > q.key || (p.key == q.key && p.idx > q.idx); });
+  if (merged.size() > nsel) merged.resize(nsel);
+  std::sort(merged.begin(), merged.end(), [](const Item& p, const Item& q) { return p.idx < q.idx; });
+  for (size_t e = 0; e < merged.size(); ++e) {
+    if (idx_out) idx_out[e] = merged[e].idx;
+    if (val_out) val_out[e] = merged[e].val;
+  }
+  *nout = merged.size();
+  return SSP_OK;
+}
 
 int ssp_select(ssp_ctx* ctx, const double* x, size_t n, size_t offset, size_t nsel, int max, int ignore_sign,
                size_t* idx_out, double* val_out, size_t* nout) {

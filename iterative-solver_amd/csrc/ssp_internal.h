@@ -55,6 +55,10 @@ struct ssp_ctx {
 
   // Communicator (RCCL over xGMI, one process per GPU).
   ncclComm_t comm = nullptr;
+  // Host-callback communicator (ssp_ctx_attach_host_comm), used instead of RCCL when set.
+  ssp_host_allreduce_fn host_allreduce = nullptr;
+  ssp_host_allgather_fn host_allgather = nullptr;
+  void* host_user = nullptr;
   int nranks = 1;
   int rank = 0;
 };

@@ -60,10 +60,9 @@ class Device {
   int nranks() const { return ssp_ctx_nranks(m_ctx); }
   // Shard of a global length n owned by this rank.
   std::pair<size_t, size_t> shard(size_t n) const {
-    const size_t r = size_t(rank()), p = size_t(nranks());
-    const size_t block = n / p, extra = n % p;
-    const size_t offset = r * block + std::min(r, extra);
-    return {offset, block + (r < extra ? 1 : 0)};
+    size_t offset = 0, length = 0;
+    check(ssp_shard_range(n, nranks(), rank(), &offset, &length), "ssp_shard_range");
+    return {offset, length};
   }
 
  private:

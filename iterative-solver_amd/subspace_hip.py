@@ -6,6 +6,7 @@ HIP runtime to load); creating a Context requires a visible MI355X and raises ot
 """
 from __future__ import annotations
 
+import builtins
 import ctypes as C
 import os
 from typing import Sequence
@@ -31,7 +32,8 @@ EXPORTS = [
     "ssp_last_error", "ssp_version", "ssp_device_count", "ssp_ctx_create", "ssp_ctx_destroy", "ssp_ctx_stream",
     "ssp_synchronize", "ssp_alloc", "ssp_free", "ssp_release_cached", "ssp_memory_stats", "ssp_upload",
     "ssp_download", "ssp_comm_unique_id", "ssp_ctx_attach_comm", "ssp_ctx_rank", "ssp_ctx_nranks",
-    "ssp_allreduce_sum", "ssp_allgather_host", "ssp_ledger_enable", "ssp_ledger_reset", "ssp_ledger_count",
+    "ssp_allreduce_sum", "ssp_allgather_host", "ssp_ctx_attach_host_comm", "ssp_shard_range", "ssp_select_merge",
+    "ssp_ledger_enable", "ssp_ledger_reset", "ssp_ledger_count",
     "ssp_ledger_entry", "ssp_fill", "ssp_scal", "ssp_copy", "ssp_axpy", "ssp_dot",
     "ssp_gemm_inner", "ssp_gemm_outer", "ssp_precondition", "ssp_select", "ssp_select_max_dot",
     "ssp_sparse_copy", "ssp_sparse_axpy", "ssp_sparse_dot", "ssp_gemm_inner_sparse", "ssp_gemm_outer_sparse",
@@ -66,6 +68,8 @@ Z = C.c_size_t
 I = C.c_int
 PD = C.POINTER(C.c_double)
 PZ = C.POINTER(C.c_size_t)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, PD, C.c_size_t, C.c_void_p)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 
 
 def _declare(lib):
@@ -89,6 +93,9 @@ def _declare(lib):
         "ssp_ctx_nranks": (I, [P]),
         "ssp_allreduce_sum": (I, [P, P, Z]),
         "ssp_allgather_host": (I, [P, P, P, Z]),
+        "ssp_ctx_attach_host_comm": (I, [P, I, I, ALLREDUCE_FN, ALLGATHER_FN, P]),
+        "ssp_shard_range": (I, [Z, I, I, PZ, PZ]),
+        "ssp_select_merge": (I, [I, PZ, Z, PZ, PD, Z, I, PZ, PD, PZ]),
         "ssp_ledger_enable": (I, [P, I]),
         "ssp_ledger_reset": (I, [P]),
         "ssp_ledger_count": (I, [P]),
@@ -118,6 +125,179 @@ def _declare(lib):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+
+
+def shard_range(n: int, nranks: int, rank: int):
+    """(offset, length) of rank's shard (ssp_shard_range: the reference's
+    make_distribution_spread_remainder).  Host only."""
+    off, ln = C.c_size_t(), C.c_size_t()
+    _check(load_library().ssp_shard_range(n, nranks, rank, C.byref(off), C.byref(ln)))
+    return off.value, ln.value
+
+
+def select_merge(parts, nsel: int, max: bool = False):
+    """ssp_select_merge over per-rank (idx, val) selections, as ssp_select merges its all-gathered
+    candidates.  Host only.  Returns (idx, val) ordered by index."""
+    nr = len(parts)
+    stride = max_(builtins.max((len(i) for i, _ in parts), default=0))
+    counts = np.array([len(i) for i, _ in parts], dtype=np.uint64)
+    idx = np.zeros(nr * stride, dtype=np.uint64)
+    val = np.zeros(nr * stride)
+    for r, (i, v) in enumerate(parts):
+        idx[r * stride:r * stride + len(i)] = i
+        val[r * stride:r * stride + len(v)] = v
+    oi, ov, cnt = np.zeros(max_(nsel), dtype=np.uint64), np.zeros(max_(nsel)), C.c_size_t()
+    _check(load_library().ssp_select_merge(nr, _zptr(counts), stride, _zptr(idx), _dptr(val), nsel, int(max),
+                                           _zptr(oi), _dptr(ov), C.byref(cnt)))
+    return oi[:cnt.value].astype(np.int64), ov[:cnt.value]
+
+
+class TorchHostComm:
+    """Host-side callbacks for ssp_ctx_attach_host_comm over a torch.distributed (gloo) group:
+    allreduce(sum) of doubles and allgather of raw bytes.  Plumbing for running the sharded
+    path with several ranks where RCCL is unavailable (several ranks on one device, CPU tests)."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.group = torch, dist, group
+        self.nranks = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.allreduce_cb = ALLREDUCE_FN(self._allreduce)
+        self.allgather_cb = ALLGATHER_FN(self._allgather)
+
+    def _allreduce(self, buf, n, _user):
+        try:
+            a = np.ctypeslib.as_array(buf, shape=(n,))
+            t = self.torch.from_numpy(a.copy())
+            self.dist.all_reduce(t, group=self.group)
+            a[:] = t.numpy()
+            return 0
+        except Exception:  # noqa: BLE001 - reported to the C side as a status
+            return 1
+
+    def _allgather(self, send, recv, nbytes, _user):
+        try:
+            src = np.frombuffer((C.c_char * nbytes).from_address(send), dtype=np.uint8).copy() if nbytes else \
+                np.zeros(0, dtype=np.uint8)
+            outs = [self.torch.zeros(nbytes, dtype=self.torch.uint8) for _ in range(self.nranks)]
+            self.dist.all_gather(outs, self.torch.from_numpy(src), group=self.group)
+            dst = (C.c_char * (nbytes * self.nranks)).from_address(recv)
+            for r, o in enumerate(outs):
+                dst[r * nbytes:(r + 1) * nbytes] = o.numpy().tobytes()
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+
+
+class HubComm:
+    """Host communicator over plain TCP sockets (stdlib only, no torch): rank 0 is the hub, every
+    collective gathers the ranks' buffers there in rank order and sends the result back, so all
+    ranks receive bit-identical sums.  Used to run the sharded path with several ranks on ONE
+    device (RCCL refuses duplicate devices) and in multi-process CPU tests."""
+
+    def __init__(self, rank: int, nranks: int, addr: str = "127.0.0.1", port: int = 0, timeout: float = 120.0):
+        import socket
+        import struct
+        import time
+
+        self.rank, self.nranks, self._struct = rank, nranks, struct
+        self.peers = {}
+        if nranks > 1:
+            if rank == 0:
+                srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+                srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+                srv.bind((addr, port))
+                srv.listen(nranks)
+                srv.settimeout(timeout)
+                for _ in range(nranks - 1):
+                    c, _a = srv.accept()
+                    c.settimeout(timeout)
+                    (r,) = struct.unpack("<i", self._recv(c, 4))
+                    self.peers[r] = c
+                srv.close()
+            else:
+                t0 = time.time()
+                while True:
+                    try:
+                        c = socket.create_connection((addr, port), timeout=timeout)
+                        break
+                    except OSError:
+                        if time.time() - t0 > timeout:
+                            raise
+                        time.sleep(0.05)
+                c.sendall(struct.pack("<i", rank))
+                self.peers[0] = c
+        self.allreduce_cb = ALLREDUCE_FN(self._allreduce_cb)
+        self.allgather_cb = ALLGATHER_FN(self._allgather_cb)
+
+    @staticmethod
+    def _recv(c, n):
+        out = bytearray()
+        while len(out) < n:
+            b = c.recv(n - len(out))
+            if not b:
+                raise ConnectionError("HubComm: peer closed")
+            out += b
+        return bytes(out)
+
+    def _send_msg(self, c, data: bytes):
+        c.sendall(self._struct.pack("<Q", len(data)) + data)
+
+    def _recv_msg(self, c):
+        (n,) = self._struct.unpack("<Q", self._recv(c, 8))
+        return self._recv(c, n)
+
+    def allgather(self, data: bytes) -> list:
+        if self.nranks == 1:
+            return [data]
+        if self.rank == 0:
+            parts = [data] + [self._recv_msg(self.peers[r]) for r in range(1, self.nranks)]
+            blob = b"".join(self._struct.pack("<Q", len(p)) + p for p in parts)
+            for r in range(1, self.nranks):
+                self._send_msg(self.peers[r], blob)
+        else:
+            self._send_msg(self.peers[0], data)
+            blob = self._recv_msg(self.peers[0])
+            parts, o = [], 0
+            while o < len(blob):
+                (n,) = self._struct.unpack_from("<Q", blob, o)
+                parts.append(blob[o + 8:o + 8 + n])
+                o += 8 + n
+        return parts
+
+    def allreduce(self, a: np.ndarray) -> np.ndarray:
+        parts = self.allgather(np.ascontiguousarray(a, dtype=np.float64).tobytes())
+        s = np.frombuffer(parts[0], dtype=np.float64).copy()
+        for p in parts[1:]:
+            s += np.frombuffer(p, dtype=np.float64)
+        return s
+
+    def barrier(self):
+        self.allgather(b"")
+
+    def close(self):
+        for c in self.peers.values():
+            c.close()
+        self.peers = {}
+
+    def _allreduce_cb(self, buf, n, _user):
+        try:
+            a = np.ctypeslib.as_array(buf, shape=(n,))
+            a[:] = self.allreduce(a)
+            return 0
+        except Exception:  # noqa: BLE001 - reported to the C side as a status
+            return 1
+
+    def _allgather_cb(self, send, recv, nbytes, _user):
+        try:
+            data = C.string_at(send, nbytes) if nbytes else b""
+            parts = self.allgather(data)
+            C.memmove(recv, b"".join(parts), nbytes * self.nranks)
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
 
 
 def _check(code: int):
@@ -225,7 +405,28 @@ class Context:
     def attach_comm(self, nranks: int, rank: int, uid: bytes):
         _check(self.lib.ssp_ctx_attach_comm(self.handle, nranks, rank, uid))
 
+    def allgather_bytes(self, data: bytes) -> list:
+        """Every rank's `data` (equal lengths), rank order, over the attached communicator."""
+        nr = self.lib.ssp_ctx_nranks(self.handle)
+        send = C.create_string_buffer(data, len(data))
+        recv = C.create_string_buffer(len(data) * nr)
+        _check(self.lib.ssp_allgather_host(self.handle, send, recv, len(data)))
+        return [recv.raw[r * len(data):(r + 1) * len(data)] for r in range(nr)]
+
+    def barrier(self):
+        """Device-ordered barrier: a one-element allreduce on the context stream, then a sync."""
+        if not hasattr(self, "_barrier_buf"):
+            self._barrier_buf = self.alloc(1)
+        _check(self.lib.ssp_allreduce_sum(self.handle, self._barrier_buf.ptr, 1))
+        self.synchronize()
+
     # -- ledger (HIP-event kernel times + algorithmic bytes per operation) --------------------------
+    def attach_host_comm(self, comm):
+        """Reductions over ranks through host callbacks (e.g. gloo) instead of RCCL."""
+        self._host_comm = comm  # keep the ctypes callbacks alive
+        _check(self.lib.ssp_ctx_attach_host_comm(self.handle, comm.nranks, comm.rank, comm.allreduce_cb,
+                                                  comm.allgather_cb, None))
+
     def ledger_enable(self, on: bool = True):
         _check(self.lib.ssp_ledger_enable(self.handle, int(on)))
 

@@ -1,0 +1,178 @@
+"""One rank of a multi-process check of the sharded path (launched by tests/test_distributed*.py).
+
+  --comm gloo : launched by `torch.distributed.run`; reductions go through a gloo process group
+                (subspace_hip.TorchHostComm).  torch is imported BEFORE the HIP library so the
+                process holds one HIP runtime.
+  --comm hub  : launched as plain subprocesses (RANK, WORLD_SIZE, SSP_HUB_PORT in the env);
+                reductions go through subspace_hip.HubComm (stdlib sockets, no torch).
+
+Cases:
+  reductions  (CPU) oracle shard pieces + the product's host exchange + ssp_select_merge
+  gpu_ops     (GPU) every reducing op of libsubspace_hip.so on shards, host communicator attached
+  gpu_solver  (GPU) Davidson / DIIS on sharded HBM vectors vs the single-rank CPU reference path
+
+Exit status 0 = every assertion held on this rank.
+"""
+import argparse
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, os.path.join(ROOT, "iterative-solver_amd"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+
+EPS = 2.220446049250313e-16
+
+
+def make_comm(kind):
+    if kind == "gloo":
+        import torch.distributed as dist  # first: one HIP runtime in this process
+
+        dist.init_process_group("gloo")
+        import subspace_hip as sh
+
+        return sh.TorchHostComm()
+    import subspace_hip as sh
+
+    return sh.HubComm(int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), "127.0.0.1",
+                      int(os.environ["SSP_HUB_PORT"]))
+
+
+def case_reductions(comm):
+    import numpy as np
+
+    import oracle
+    import subspace_hip as sh
+
+    rank, world = comm.rank, comm.nranks
+    for n in (1, 3, 1001, 20_000):
+        m, k, seed = 3, 5, 20251015
+        off, ln = sh.shard_range(n, world, rank)
+        full = [oracle.random_vector(n, seed, v) for v in range(m + k)]
+        xs = [v[off:off + ln] for v in full]
+        # gemm_inner: rank-local block summed over ranks through the allreduce callback.
+        buf = np.ascontiguousarray((oracle.gemm_inner(xs[:m], xs[m:]) if ln else np.zeros((m, k))).ravel())
+        assert comm.allreduce_cb(buf.ctypes.data_as(sh.PD), buf.size, None) == 0
+        terms = np.abs(np.stack(full[:m])) @ np.abs(np.stack(full[m:])).T
+        assert np.all(np.abs(buf.reshape(m, k) - oracle.gemm_inner(full[:m], full[m:])) <= 64 * EPS * terms + 1e-300)
+        # sparse dot: P entries filtered to the shard range (DistrArray.cpp:419-465), then summed.
+        pidx = np.unique(np.random.default_rng(seed).integers(0, n, 50))
+        pval = np.linspace(-1, 1, pidx.size)
+        sel = (pidx >= off) & (pidx < off + ln)
+        d = np.array([oracle.sparse_dot(xs[0], pidx[sel] - off, pval[sel]) if ln else 0.0])
+        assert comm.allreduce_cb(d.ctypes.data_as(sh.PD), 1, None) == 0
+        assert abs(d[0] - oracle.sparse_dot(full[0], pidx, pval)) <= 1e-13 * np.sum(np.abs(pval))
+        # select: per-rank best n all-gathered as raw bytes, merged identically on every rank.
+        nsel = min(9, n)
+        li, lv = oracle.select(xs[1], min(nsel, ln)) if ln else (np.zeros(0, np.int64), np.zeros(0))
+        li = li + off
+        cnts = np.zeros(world, dtype=np.uint64)
+        cnt = np.array([li.size], dtype=np.uint64)
+        assert comm.allgather_cb(cnt.ctypes.data, cnts.ctypes.data, 8, None) == 0
+        si, sv = np.zeros(nsel, np.uint64), np.zeros(nsel)
+        si[:li.size], sv[:lv.size] = li, lv
+        gi, gv = np.zeros(nsel * world, np.uint64), np.zeros(nsel * world)
+        assert comm.allgather_cb(si.ctypes.data, gi.ctypes.data, 8 * nsel, None) == 0
+        assert comm.allgather_cb(sv.ctypes.data, gv.ctypes.data, 8 * nsel, None) == 0
+        parts = [(gi[r * nsel:r * nsel + int(cnts[r])], gv[r * nsel:r * nsel + int(cnts[r])]) for r in range(world)]
+        mi, mv = sh.select_merge(parts, nsel)
+        ri, rv = oracle.select(full[1], nsel)
+        assert np.array_equal(mi, ri) and np.array_equal(mv, rv), (mi, ri, mv, rv)
+
+
+def case_gpu_ops(comm):
+    import numpy as np
+
+    import oracle
+    import subspace_hip as sh
+
+    rank, world = comm.rank, comm.nranks
+    ctx = sh.Context(0)
+    ctx.attach_host_comm(comm)
+    assert (ctx.lib.ssp_ctx_rank(ctx.handle), ctx.lib.ssp_ctx_nranks(ctx.handle)) == (rank, world)
+    for n in (5, 1003, 100_003):
+        off, ln = sh.shard_range(n, world, rank)
+        rng = np.random.default_rng(n)
+        X = rng.uniform(-1, 1, (6, n))
+        X[3] = rng.integers(-3, 4, n)  # ties for select
+        xs = [ctx.upload(np.ascontiguousarray(v[off:off + ln])) for v in X]
+        tol = lambda terms: 64 * EPS * terms + 1e-300  # noqa: E731
+        g = ctx.dot(xs[0], xs[1])
+        assert abs(g - oracle.dot(X[0], X[1])) <= tol(np.sum(np.abs(X[0] * X[1])))
+        M = ctx.gemm_inner(xs[:2], xs[2:])
+        terms = np.abs(X[:2]) @ np.abs(X[2:]).T
+        assert np.all(np.abs(M - oracle.gemm_inner(list(X[:2]), list(X[2:]))) <= tol(terms))
+        for mx, ig in ((False, False), (True, False), (False, True)):
+            nsel = min(7, n)
+            gi, gv = ctx.select(xs[3], nsel, max=mx, ignore_sign=ig, offset=off)
+            ri, rv = oracle.select(X[3], nsel, max=mx, ignore_sign=ig)
+            assert np.array_equal(gi, ri) and np.array_equal(gv, rv), (mx, ig, gi, ri)
+        gi, gv = ctx.select_max_dot(xs[3], xs[4], min(5, n), offset=off)
+        ri, rv = oracle.select_max_dot(X[3], X[4], min(5, n))
+        assert np.array_equal(gi, ri) and np.allclose(gv, rv, rtol=0, atol=0)
+        pidx = np.unique(rng.integers(0, n, 40))
+        pval = np.linspace(-2, 2, pidx.size)
+        sd = ctx.sparse_dot(xs[0], pidx, pval, offset=off)
+        assert abs(sd - oracle.sparse_dot(X[0], pidx, pval)) <= 1e-13 * np.sum(np.abs(pval))
+        # elementwise op with global indices: sparse axpy lands only in the owning shard
+        ctx.sparse_axpy(0.5, pidx, pval, xs[5], offset=off)
+        assert np.array_equal(ctx.download(xs[5]), oracle.sparse_axpy(0.5, pidx, pval, X[5])[off:off + ln])
+        # synthetic action: a rank x nvec reduction across shards
+        y = ctx.alloc(ln)
+        ctx.synthetic_action([xs[0]], [y], 0.1, 3, 11, offset=off)
+        ref = oracle.synthetic_action(X[0], 0.1, 3, 11)[off:off + ln]
+        assert np.allclose(ctx.download(y), ref, rtol=1e-12, atol=1e-9)
+    ctx.close()
+
+
+def case_gpu_solver(comm):
+    import numpy as np
+
+    import itsolv_hbm as ih
+    import oracle
+    import subspace_hip as sh
+
+    rank, world = comm.rank, comm.nranks
+    ctx = sh.Context(0)
+    ctx.attach_host_comm(comm)
+    n, rho, seed = 100_003, 0.1, 20251015
+    _, nl = sh.shard_range(n, world, rank)
+    for rk, nroot, np_ in ((1, 4, 0), (4, 4, 8)):
+        kw = dict(nroots=nroot, max_p=np_, convergence_threshold=1e-8, max_size_qspace=6 * nroot, reset_D=8)
+        g = ih.davidson_synthetic(ctx, n, rho, rk, seed, n_local=nl, **kw)
+        c = oracle.davidson_synthetic(n, rho, rk, seed, **kw)
+        assert g["converged"] and c["converged"]
+        assert g["iterations"] == c["iterations"], (g["iterations"], c["iterations"])
+        scale = np.maximum(np.abs(c["eigenvalues"]), 1.0)
+        assert np.all(np.abs(g["eigenvalues"] - c["eigenvalues"]) <= 1e-10 * scale)
+        # every rank holds the same subspace results
+        ev = comm.allreduce(np.asarray(g["eigenvalues"])) / world
+        assert np.array_equal(ev, np.asarray(g["eigenvalues"]))
+    kw = dict(convergence_threshold=1e-8, max_size_qspace=6)
+    g = ih.diis_synthetic(ctx, 3000, 0.01, 3, 3, n_local=sh.shard_range(3000, world, rank)[1], **kw)
+    c = oracle.diis_synthetic(3000, 0.01, 3, 3, **kw)
+    assert g["converged"] and c["converged"] and g["iterations"] == c["iterations"]
+    ctx.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--comm", choices=["gloo", "hub"], required=True)
+    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver"], required=True)
+    a = ap.parse_args()
+    comm = make_comm(a.comm)
+    {"reductions": case_reductions, "gpu_ops": case_gpu_ops, "gpu_solver": case_gpu_solver}[a.case](comm)
+    if a.comm == "gloo":
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        comm.barrier()
+        comm.close()
+    print(f"rank {comm.rank}/{comm.nranks} {a.case} OK", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,24 @@
+"""The sharded (N > 1) product path on a real MI355X: two ranks, each a separate process holding
+its index-range shard in HBM, reductions exchanged through the host communicator
+(ssp_ctx_attach_host_comm + subspace_hip.HubComm, since RCCL refuses two ranks on one device).
+
+Everything above the transport is the code the 8-GPU RCCL runs execute: the shard ranges, the
+local kernels, the reduce-then-exchange of dot / gemm_inner / sparse dots / synthetic actions,
+the select all-gather + ssp_select_merge, the global-index filtering of sparse ops, and the SPMD
+solver.  The bar is the unsharded reference: select bit-exact, reductions to rounding, and the
+sharded Davidson / DIIS runs take the same iterations as the CPU reference path with eigenvalues
+within 1e-10 (tests/dist_worker.py).
+"""
+import pytest
+
+from test_distributed import run_hub
+
+pytestmark = pytest.mark.gpu
+
+
+def test_world2_ops_on_shards():
+    run_hub("gpu_ops", timeout=600)
+
+
+def test_world2_davidson_and_diis_on_shards():
+    run_hub("gpu_solver", timeout=900)
