@@ -111,6 +111,11 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
  * reference util/gemm.h:186-203 (distributed) and :257-265 (pairwise default) */
 int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
                    size_t n);
+/* Fused modified-Gram-Schmidt step: yy[j] += c[j] * x, then out[j] = <yy[j], z> summed over ranks.
+ * Equals ssp_gemm_outer({x} -> yy) followed by ssp_gemm_inner(yy, {z}) with bit-identical yy; one
+ * pass over yy (reference propose_rspace.h:430-443 issues them as separate handler calls). */
+int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const* yy, int m, const double* z, size_t n,
+                   double* out);
 /* a[v][i] /= (d[i] - shift[v] + 1e-15) for v in [0,nvec)   reference itsolv/IterativeSolver.h:34-55 */
 int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n);
 

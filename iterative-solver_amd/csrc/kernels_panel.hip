@@ -209,6 +209,67 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
   }
 }
 
+// Fused MGS step: y_j += c_j x (the same fma as a one-source gemm_outer),
+// then the updated y_j dotted with z, in one pass: R is read and written once instead of being read
+// again by the next gemm_inner.  Bytes 8N(2 + 2m).
+struct AxpyInnerArgs {
+  const double* x;
+  const double* z;
+  double* y[ssp::kOuterDst];
+  double c[ssp::kOuterDst];
+  int m;
+  size_t n;
+  double* partial;  // [gridDim.x][m]
+};
+
+template <int M>
+__global__ __launch_bounds__(kBlock) void k_axpy_inner(const AxpyInnerArgs a) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  const size_t n2 = a.n >> 1, stride = size_t(gridDim.x) * kBlock;
+  double acc[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) acc[j] = 0;
+  for (size_t p = size_t(blockIdx.x) * kBlock + threadIdx.x; p < n2; p += stride) {
+    const double2 xv = ld2nt(a.x + 2 * p), zv = ld2nt(a.z + 2 * p);
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      if (j < a.m) {
+        double2 y = ld2nt(a.y[j] + 2 * p);
+        y.x = fma(a.c[j], xv.x, y.x);
+        y.y = fma(a.c[j], xv.y, y.y);
+        st2nt(a.y[j] + 2 * p, y);
+        acc[j] = fma(y.x, zv.x, acc[j]);
+        acc[j] = fma(y.y, zv.y, acc[j]);
+      }
+    }
+  }
+  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const size_t e = a.n - 1;
+    for (int j = 0; j < a.m; ++j) {
+      const double y = fma(a.c[j], a.x[e], a.y[j][e]);
+      a.y[j][e] = y;
+      acc[j] = fma(y, a.z[e], acc[j]);
+    }
+  }
+  __shared__ double red[kBlock / 64][M];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    double v = acc[j];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) red[wave][j] = v;
+  }
+  __syncthreads();
+  if (int(threadIdx.x) < a.m) {
+    double s = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+    a.partial[size_t(blockIdx.x) * a.m + threadIdx.x] = s;
+  }
+}
+
 int check_ptrs(const double* const* v, int count, size_t n, const char* what) {
   if (count > 0 && !v) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null vector list");
   if (n == 0) return SSP_OK;
@@ -365,6 +426,51 @@ int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, 
     }
   }
   return SSP_OK;
+}
+
+int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const* yy, int m, const double* z, size_t n,
+                   double* out) {
+  SSP_CHECK_CTX(ctx);
+  if (m < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_inner: negative dimension");
+  if (m == 0) return SSP_OK;
+  if (!c || !out) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_inner: null coefficients or out");
+  SSP_TRY(check_ptrs(&x, 1, n, "ssp_axpy_inner"));
+  SSP_TRY(check_ptrs(&z, 1, n, "ssp_axpy_inner"));
+  SSP_TRY(check_ptrs(const_cast<const double* const*>(yy), m, n, "ssp_axpy_inner"));
+  for (int j = 0; j < m; ++j)
+    if (yy[j] == x || yy[j] == z) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_inner: a destination aliases x or z");
+  SSP_TRY(ssp::ensure_result(ctx, size_t(m)));
+  if (n == 0) {
+    SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, size_t(m) * sizeof(double), ctx->stream));
+  } else {
+    ssp::LedgerScope ls(ctx, "axpy_inner", 8.0 * n * (2.0 + 2.0 * m));
+    const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 1);
+    for (int j0 = 0; j0 < m; j0 += ssp::kOuterDst) {
+      AxpyInnerArgs a{};
+      a.m = std::min(ssp::kOuterDst, m - j0);
+      a.n = n;
+      a.x = x;
+      a.z = z;
+      for (int j = 0; j < a.m; ++j) {
+        a.y[j] = yy[j0 + j];
+        a.c[j] = c[j0 + j];
+      }
+      SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * a.m));
+      a.partial = ctx->partial;
+      if (a.m <= 1)
+        hipLaunchKernelGGL((k_axpy_inner<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      else if (a.m <= 4)
+        hipLaunchKernelGGL((k_axpy_inner<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      else if (a.m <= 8)
+        hipLaunchKernelGGL((k_axpy_inner<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      else
+        hipLaunchKernelGGL((k_axpy_inner<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_TRY_HIP(hipGetLastError());
+      SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, a.m, ctx->result_dev, m, 0, j0));
+    }
+  }
+  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, size_t(m)));
+  return ssp::fetch_result(ctx, out, size_t(m));
 }
 
 }  // extern "C"

@@ -43,16 +43,18 @@ __global__ __launch_bounds__(kBlock) void k_fill(double* __restrict__ x, size_t 
 }
 
 __global__ __launch_bounds__(kBlock) void k_scal(double* __restrict__ x, size_t n, double alpha) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
   const size_t n2 = n >> 1;
   const size_t stride = size_t(gridDim.x) * kBlock;
   size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   for (; i + 3 * stride < n2; i += 4 * stride) {
-    double2 a0 = ld2(x + 2 * i), a1 = ld2(x + 2 * (i + stride)), a2 = ld2(x + 2 * (i + 2 * stride)),
-            a3 = ld2(x + 2 * (i + 3 * stride));
-    st2(x + 2 * i, make_double2(a0.x * alpha, a0.y * alpha));
-    st2(x + 2 * (i + stride), make_double2(a1.x * alpha, a1.y * alpha));
-    st2(x + 2 * (i + 2 * stride), make_double2(a2.x * alpha, a2.y * alpha));
-    st2(x + 2 * (i + 3 * stride), make_double2(a3.x * alpha, a3.y * alpha));
+    double2 a0 = ld2nt(x + 2 * i), a1 = ld2nt(x + 2 * (i + stride)), a2 = ld2nt(x + 2 * (i + 2 * stride)),
+            a3 = ld2nt(x + 2 * (i + 3 * stride));
+    st2nt(x + 2 * i, make_double2(a0.x * alpha, a0.y * alpha));
+    st2nt(x + 2 * (i + stride), make_double2(a1.x * alpha, a1.y * alpha));
+    st2nt(x + 2 * (i + 2 * stride), make_double2(a2.x * alpha, a2.y * alpha));
+    st2nt(x + 2 * (i + 3 * stride), make_double2(a3.x * alpha, a3.y * alpha));
   }
   for (; i < n2; i += stride) {
     double2 a = ld2(x + 2 * i);
@@ -62,16 +64,18 @@ __global__ __launch_bounds__(kBlock) void k_scal(double* __restrict__ x, size_t 
 }
 
 __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ x, const double* __restrict__ y, size_t n) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
   const size_t n2 = n >> 1;
   const size_t stride = size_t(gridDim.x) * kBlock;
   size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   for (; i + 3 * stride < n2; i += 4 * stride) {
-    double2 a0 = ld2(y + 2 * i), a1 = ld2(y + 2 * (i + stride)), a2 = ld2(y + 2 * (i + 2 * stride)),
-            a3 = ld2(y + 2 * (i + 3 * stride));
-    st2(x + 2 * i, a0);
-    st2(x + 2 * (i + stride), a1);
-    st2(x + 2 * (i + 2 * stride), a2);
-    st2(x + 2 * (i + 3 * stride), a3);
+    double2 a0 = ld2nt(y + 2 * i), a1 = ld2nt(y + 2 * (i + stride)), a2 = ld2nt(y + 2 * (i + 2 * stride)),
+            a3 = ld2nt(y + 2 * (i + 3 * stride));
+    st2nt(x + 2 * i, a0);
+    st2nt(x + 2 * (i + stride), a1);
+    st2nt(x + 2 * (i + 2 * stride), a2);
+    st2nt(x + 2 * (i + 3 * stride), a3);
   }
   for (; i < n2; i += stride) st2(x + 2 * i, ld2(y + 2 * i));
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) x[n - 1] = y[n - 1];
@@ -217,7 +221,7 @@ int ssp_scal(ssp_ctx* ctx, double alpha, double* x, size_t n) {
   SSP_TRY(check_vec(x, n, "ssp_scal"));
   if (n == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "scal", 16.0 * n);
-  hipLaunchKernelGGL(k_scal, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
+  hipLaunchKernelGGL(k_scal, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -228,7 +232,7 @@ int ssp_copy(ssp_ctx* ctx, double* x, const double* y, size_t n) {
   SSP_TRY(check_vec(y, n, "ssp_copy"));
   if (n == 0 || x == y) return SSP_OK;
   ssp::LedgerScope ls(ctx, "copy", 16.0 * n);
-  hipLaunchKernelGGL(k_copy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4)), dim3(kBlock), 0, ctx->stream, x, y, n);
+  hipLaunchKernelGGL(k_copy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, y, n);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }

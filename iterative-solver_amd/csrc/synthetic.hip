@@ -151,6 +151,8 @@ int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* 
   SSP_CHECK_CTX(ctx);
   if (rank < 1 || rank > kMaxRank) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_action: rank out of [1,16]");
   if (nvec < 0) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_action: nvec < 0");
+  // x read twice (coefficients, then apply) and y written: 24 N per vector.
+  ssp::LedgerScope ls(ctx, "action(synthetic)", 24.0 * n * nvec);
   for (int v0 = 0; v0 < nvec; v0 += kMaxVec) {
     SynthArgs a{};
     a.nvec = std::min(kMaxVec, nvec - v0);
@@ -196,6 +198,7 @@ int sspx_synthetic_add_lowrank(ssp_ctx* ctx, double* const* yy, int nvec, size_t
   SSP_CHECK_CTX(ctx);
   if (rank < 1 || rank > kMaxRank) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_add_lowrank: rank out of [1,16]");
   if (n == 0 || nvec <= 0) return SSP_OK;
+  ssp::LedgerScope ls(ctx, "p_action(synthetic)", 16.0 * n * nvec);
   for (int v0 = 0; v0 < nvec; v0 += kMaxVec) {
     SynthArgs a{};
     a.nvec = std::min(kMaxVec, nvec - v0);

@@ -164,4 +164,20 @@ class ArrayHandler {
   std::unique_ptr<Counter> m_counter;
 };
 
+// Capabilities of a vector type's handlers beyond the reference interface.
+// Both default to off, so the reference call sequence is kept for every other type (the CPU
+// oracle path in particular); the HBM handlers switch them on (hbm_handlers.h).
+//  * batched_symmetric_overlap: the symmetric overlap of one set is one gemm_inner(xx, xx) with the
+//    lower triangle mirrored, in place of the pairwise dots of subspace/util.h:55-62.
+template <class T>
+struct batched_symmetric_overlap : std::false_type {};
+
+// Fused MGS step hook: y_j += c_j x for all j, then dots_j = <y_j, z>, in one pass; returns false
+// when the handler has no fused form (the caller then issues gemm_outer + gemm_inner).  Found by
+// argument-dependent lookup; the HBM overload lives in namespace molpro::linalg::hbm.
+template <class H, class Q, class RefR>
+bool fused_axpy_inner(H&, const std::vector<double>&, const Q&, const RefR&, const Q&, std::vector<double>&) {
+  return false;
+}
+
 }  // namespace molpro::linalg::array

@@ -377,6 +377,16 @@ inline std::shared_ptr<itsolv::ArrayHandlers<Vec, Vec, SparseP>> make_handlers()
       .build_shared();
 }
 
+// Fused MGS step on HBM vectors (array::fused_axpy_inner hook, found by argument-dependent lookup).
+inline bool fused_axpy_inner(array::ArrayHandler<Vec, Vec>&, const std::vector<double>& c, const Vec& x,
+                             const itsolv::VecRef<Vec>& rr, const Vec& z, std::vector<double>& dots) {
+  std::vector<double*> y;
+  for (auto& r : rr) y.push_back(r.get().data());
+  check(ssp_axpy_inner(x.ctx(), c.data(), x.data(), y.data(), int(y.size()), z.data(), x.local_size(), dots.data()),
+        "ssp_axpy_inner");
+  return true;
+}
+
 // Davidson preconditioner on HBM vectors: reference precondition_default (IterativeSolver.h:34-55)
 // as one fused kernel over all working-set vectors (d read once).  Found by argument-dependent
 // lookup from Problem<R>::precondition.
@@ -391,3 +401,9 @@ inline void precondition_default(const itsolv::VecRef<Vec>& action, const std::v
 }
 
 }  // namespace molpro::linalg::hbm
+
+namespace molpro::linalg::array {
+// HBM handlers form symmetric overlaps with one gemm_inner (reads each vector once).
+template <>
+struct batched_symmetric_overlap<hbm::Vec> : std::true_type {};
+}  // namespace molpro::linalg::array

@@ -259,8 +259,34 @@ std::vector<int> modified_gram_schmidt(const VecRef<R>& rparams, const Matrix<do
     }
   };
   orthogonalise(pp, h.rp(), d.oP, pp.size());
-  orthogonalise(qp, h.rq(), d.oQ, qp.size());
-  orthogonalise(dp, h.rq(), d.oD, dp.size());
+  // Q then D: the same handler and the same call sequence as two orthogonalise() sweeps, except
+  // that a handler with a fused form (array::fused_axpy_inner) merges each step's gemm_outer with
+  // the next step's gemm_inner into one pass over R: R is read once per
+  // vector instead of twice, with bit-identical R updates.
+  std::vector<std::pair<const Q*, double>> qd;
+  for (size_t i = 0; i < qp.size(); ++i) qd.emplace_back(&qp.at(i).get(), std::abs(S(d.oQ + i, d.oQ + i)));
+  for (size_t i = 0; i < dp.size(); ++i) qd.emplace_back(&dp.at(i).get(), std::abs(S(d.oD + i, d.oD + i)));
+  if (nR > 0 && !qd.empty()) {
+    auto& hq = h.rq();
+    std::vector<double> dots(nR);
+    auto inner = [&](size_t i) {
+      auto m = hq.gemm_inner(cwrap(rparams), cwrap_arg(*qd[i].first));
+      for (size_t j = 0; j < nR; ++j) dots[j] = m(j, 0);
+    };
+    inner(0);
+    for (size_t i = 0; i < qd.size(); ++i) {
+      std::vector<double> c(nR);
+      for (size_t j = 0; j < nR; ++j) c[j] = -dots[j] / qd[i].second;
+      if (i + 1 < qd.size()) {
+        using array::fused_axpy_inner;
+        if (fused_axpy_inner(hq, c, *qd[i].first, rparams, *qd[i + 1].first, dots)) continue;
+      }
+      Matrix<double> coeff({1, nR});
+      for (size_t j = 0; j < nR; ++j) coeff(0, j) = c[j];
+      hq.gemm_outer(coeff, cwrap_arg(*qd[i].first), rparams);
+      if (i + 1 < qd.size()) inner(i + 1);
+    }
+  }
   std::vector<int> null_params;
   for (size_t i = 0; i < nR; ++i) {
     const double nrm = std::sqrt(std::abs(h.rr().dot(rparams[i], rparams[i])));

@@ -57,10 +57,18 @@ Matrix<double> overlap(const CVecRef<L>& left, const CVecRef<Rt>& right, array::
   }
 }
 
-// Symmetric overlap of one set by pairwise dots over the lower triangle (subspace/util.h:55-62).
+// Symmetric overlap of one set by pairwise dots over the lower triangle (subspace/util.h:55-62),
+// or by one batched gemm_inner where the handlers support it (array::batched_symmetric_overlap).
 template <class R>
 Matrix<double> overlap(const CVecRef<R>& params, array::ArrayHandler<R, R>& handler) {
   Matrix<double> m({params.size(), params.size()});
+  if constexpr (array::batched_symmetric_overlap<R>::value) {
+    if (params.empty()) return m;
+    auto g = handler.gemm_inner(params, params);
+    for (size_t i = 0; i < m.rows(); ++i)
+      for (size_t j = 0; j <= i; ++j) m(i, j) = m(j, i) = g(i, j);
+    return m;
+  }
   for (size_t i = 0; i < m.rows(); ++i)
     for (size_t j = 0; j <= i; ++j) m(i, j) = m(j, i) = handler.dot(params[i], params[j]);
   return m;

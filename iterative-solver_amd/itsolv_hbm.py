@@ -108,7 +108,9 @@ def load_library():
 def _call(fn, args, nout):
     res = Result()
     out = np.zeros(max(1, nout))
-    code = fn(*args, C.byref(res), out.ctypes.data_as(C.POINTER(C.c_double)))
+    # nout == 0: no solution copy-back (null pointer; the C side then skips the download)
+    ptr = out.ctypes.data_as(C.POINTER(C.c_double)) if nout > 0 else None
+    code = fn(*args, C.byref(res), ptr)
     if code != 0:
         raise RuntimeError(f"{fn.__name__}: {load_library().itsolv_last_error().decode()}")
     return res.as_dict(), out

@@ -100,6 +100,30 @@ def test_gemm_outer(ctx, k, m, n):
         v.free()
 
 
+@pytest.mark.parametrize("m", [1, 3, 8, 16, 19])
+@pytest.mark.parametrize("n", [1, 2, 1003, 100_003])
+def test_axpy_inner_fused_mgs_step(ctx, m, n):
+    # ssp_axpy_inner == gemm_outer({x} -> yy) then gemm_inner(yy, {z}): yy bit-identical to the
+    # device gemm_outer, dots within the reduction bound of the oracle's sequential sums.
+    r = rng(m * 7 + n)
+    x, z = r.uniform(-1, 1, n), r.uniform(-1, 1, n)
+    ys = [r.uniform(-1, 1, n) for _ in range(m)]
+    c = r.uniform(-1, 1, m)
+    dx, dz = ctx.upload(x), ctx.upload(z)
+    dy = [ctx.upload(v) for v in ys]
+    ey = [ctx.upload(v) for v in ys]
+    dots = ctx.axpy_inner(c, dx, dy, dz)
+    ctx.gemm_outer(c.reshape(1, m), [dx], ey)
+    for a, b in zip(dy, ey):
+        assert np.array_equal(a.numpy(), b.numpy())
+    ynew = oracle.gemm_outer(c.reshape(1, m), [x], ys)
+    ref = oracle.gemm_inner(ynew, [z])[:, 0]
+    for j in range(m):
+        assert abs(dots[j] - ref[j]) <= red_tol(ynew[j] * z) + 4 * EPS * np.sum(np.abs(z) * (np.abs(ys[j]) + abs(c[j]) * np.abs(x)))
+    for v in [dx, dz] + dy + ey:
+        v.free()
+
+
 def test_gemm_outer_rejects_aliasing(ctx):
     import subspace_hip as sh
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: GPU tests, bench, kernel-trace profile.  Each GPU step has its own time limit;
 # a fault / abort / timeout ends the session (no retries).  Outputs land in gpurun_out/.
-# Usage: tools/gpu_session.sh [tests|bench|prof|pmc|all] [extra bench args...]
+# Usage: tools/gpu_session.sh [tests|bench|prof|pmc|ledger|all] [extra bench args...]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -54,5 +54,13 @@ if [ "$what" = pmc ] || [ "$what" = all ]; then
     rc=$?
     if [ $rc -ne 0 ]; then exit $rc; fi
   done
+fi
+if [ "$what" = ledger ] || [ "$what" = all ]; then
+  step shapes 600 python tools/shapes_bench.py --out "$OUT/shapes.json"
+  rc=$?
+  if [ $rc -ne 0 ]; then exit $rc; fi
+  step solver_ledger 900 python tools/solver_ledger.py --out "$OUT/solver_ledger.json"
+  rc=$?
+  if [ $rc -ne 0 ]; then exit $rc; fi
 fi
 echo "session done"

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""In-solver ledger: run whole solves on one MI355X with the per-op HIP-event
+ledger enabled and report, per handler operation, calls, kernel time, algorithmic bytes and GB/s,
+plus the solve's wall time.  Complements bench.py (a fixed subspace-update step) with the op mix
+of real Davidson / DIIS iterations.
+
+usage: python tools/solver_ledger.py [--configs C2,C3,C5] [--out profiles/r1/solver_ledger.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "iterative-solver_amd"))
+
+import itsolv_hbm as ih  # noqa: E402
+import subspace_hip as sh  # noqa: E402
+
+CONFIGS = {
+    # name: (solver, n, kwargs) -- H = diag(1 + i) + rho * sum_l u_l u_l^T (rank 8 for steady state)
+    "C2": ("davidson", 10_000_000, dict(rho=0.1, rank=8, seed=1, nroots=4, max_size_qspace=24, reset_D=8,
+                                         convergence_threshold=1e-8)),
+    "C3": ("davidson", 100_000_000, dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48,
+                                          reset_D=8, convergence_threshold=1e-8)),
+    "C5": ("diis", 100_000_000, dict(rho=0.01, rank=3, seed=3, max_size_qspace=6, convergence_threshold=1e-8)),
+}
+
+
+def run(ctx, name, repeat=2):
+    """Solves `repeat` times in one context and reports the last (HBM arena warm); the first
+    (cold: every vector block is a fresh hipMalloc) wall time is reported beside it."""
+    cold = None
+    for _ in range(repeat - 1):
+        cold = run_once(ctx, name)["wall_s"]
+    out = run_once(ctx, name)
+    out["wall_s_cold"] = cold
+    print(json.dumps({k: out[k] for k in ("config", "iterations", "wall_s", "wall_s_cold", "kernel_ms", "kernel_GBs",
+                                            "wall_GBs")}), flush=True)
+    return out
+
+
+def run_once(ctx, name):
+    solver, n, kw = CONFIGS[name]
+    kw = dict(kw)
+    rho, rank, seed = kw.pop("rho"), kw.pop("rank"), kw.pop("seed")
+    ctx.ledger_reset()
+    ctx.ledger_enable(True)
+    t0 = time.perf_counter()
+    if solver == "davidson":
+        r = ih.davidson_synthetic(ctx, n, rho, rank, seed, n_local=0, **kw)
+    else:
+        r = ih.diis_synthetic(ctx, n, rho, rank, seed, n_local=0, **kw)
+    wall = time.perf_counter() - t0
+    ctx.ledger_enable(False)
+    led = ctx.ledger()
+    ms = sum(v["ms"] for v in led.values())
+    nb = sum(v["bytes"] for v in led.values())
+    ops = {op: {"calls": v["calls"], "ms": round(v["ms"], 3), "GB": round(v["bytes"] / 1e9, 3),
+                "GBs": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] > 0 else None,
+                "share_of_kernel_time": round(v["ms"] / ms, 4) if ms else None}
+           for op, v in sorted(led.items(), key=lambda kv: -kv[1]["ms"])}
+    out = {"config": name, "solver": solver, "n": n, "options": CONFIGS[name][2], "converged": r["converged"],
+           "iterations": r["iterations"], "wall_s": round(wall, 3), "kernel_ms": round(ms, 3),
+           "algorithmic_GB": round(nb / 1e9, 3), "kernel_GBs": round(nb / (ms / 1e3) / 1e9, 1) if ms else None,
+           "wall_GBs": round(nb / wall / 1e9, 1), "ops": ops}
+    if solver == "davidson":
+        out["eigenvalues"] = [float(e) for e in r["eigenvalues"]]
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C2,C3,C5")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "solver_ledger.json"))
+    a = ap.parse_args()
+    ctx = sh.Context(0)
+    res = [run(ctx, c) for c in a.configs.split(",")]
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    json.dump(res, open(a.out, "w"), indent=1)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
