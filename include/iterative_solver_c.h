@@ -1,0 +1,99 @@
+/*
+ * iterative_solver_c.h — the reference's reverse-communication C API (what Molpro's Fortran and
+ * the Python extension bind) on the MI355X back end, exported by libitsolv_hbm.so.
+ *
+ * Every declaration below has the name, argument list and meaning of the reference's
+ * src/molpro/linalg/IterativeSolverC.h:6-73 (implementation IterativeSolverCMPI.cpp:158-534):
+ *  - R vectors are the caller's host arrays, `buffer_size` vectors of length `dimension` stored
+ *    one after the other; this rank works on [range_begin, range_end) of each (the reference's
+ *    make_distribution_spread_remainder layout), returned by the *Initialize calls;
+ *  - with `sync` != 0 the updated vectors are gathered in full on every rank;
+ *  - Q (and D) vectors live in HBM instead of DistrArrayFile: every subspace operation runs on the
+ *    device, and R crosses PCIe once per call in each direction;
+ *  - the solver instances form a stack; only the top one is active (as in the reference).
+ *
+ * Differences:
+ *  - `fcomm` (a Fortran MPI communicator) is ignored: ranks and the device are taken from the
+ *    context set by IterativeSolverHbmSetContext (an ssp_ctx with an RCCL or host communicator
+ *    attached), or a single-rank context on device 0 is created.
+ *  - Supported algorithms: LinearEigensystem "Davidson" (or "") and NonLinearEquations "DIIS"
+ *    (or "").  IterativeSolverLinearEquationsInitialize and IterativeSolverOptimizeInitialize
+ *    throw std::logic_error (next), as the reference throws for unknown
+ *    algorithms.
+ *  - IterativeSolverAddVector on a non-linear solver (DIIS) passes the vector through the solver's
+ *    own add_vector (residual norm, convergence flag, least-important-vector deletion), as the
+ *    reference's solve() driver does; the reference's C layer reaches the generic vector-list
+ *    overload, which skips that logic.
+ *  - Errors are thrown as C++ exceptions, exactly as the reference's extern "C" functions do,
+ *    unless IterativeSolverHbmSetThrow(0) selects recorded errors (IterativeSolverHbmLastError).
+ */
+#ifndef ITERATIVE_SOLVER_C_H
+#define ITERATIVE_SOLVER_C_H
+#include <stddef.h>
+#include <stdint.h>
+
+#include "subspace_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+void IterativeSolverLinearEigensystemInitialize(size_t nQ, size_t nroot, size_t* range_begin, size_t* range_end,
+                                                double thresh, double thresh_value, int hermitian, int verbosity,
+                                                const char* fname, int64_t fcomm, const char* algorithm,
+                                                const char* options);
+void IterativeSolverLinearEquationsInitialize(size_t n, size_t nroot, size_t* range_begin, size_t* range_end,
+                                              const double* rhs, double aughes, double thresh, double thresh_value,
+                                              int hermitian, int verbosity, const char* fname, int64_t fcomm,
+                                              const char* algorithm, const char* options);
+void IterativeSolverNonLinearEquationsInitialize(size_t n, size_t* range_begin, size_t* range_end, double thresh,
+                                                 int verbosity, const char* fname, int64_t fcomm,
+                                                 const char* algorithm, const char* options);
+void IterativeSolverOptimizeInitialize(size_t n, size_t* range_begin, size_t* range_end, double thresh,
+                                       double thresh_value, int verbosity, int minimize, const char* fname,
+                                       int64_t fcomm, const char* algorithm, const char* options);
+void IterativeSolverFinalize(void);
+size_t IterativeSolverAddVector(size_t buffer_size, double* parameters, double* action, int sync);
+void IterativeSolverSolution(int nroot, int* roots, double* parameters, double* action, int sync);
+size_t IterativeSolverAddValue(double value, double* parameters, double* action, int sync);
+size_t IterativeSolverEndIteration(size_t buffer_size, double* solution, double* residual, int sync);
+int IterativeSolverEndIterationNeeded(void);
+size_t IterativeSolverAddP(size_t buffer_size, size_t nP, const size_t* offsets, const size_t* indices,
+                           const double* coefficients, const double* pp, double* parameters, double* action, int sync,
+                           void (*func)(const double*, double*, const size_t, const size_t*));
+void IterativeSolverErrors(double* errors);
+void IterativeSolverEigenvalues(double* eigenvalues);
+void IterativeSolverWorkingSetEigenvalues(double* eigenvalues);
+size_t IterativeSolverSuggestP(const double* solution, const double* residual, size_t maximumNumber, double threshold,
+                               size_t* indices);
+void IterativeSolverPrintStatistics(void);
+int IterativeSolverNonLinear(void);
+int IterativeSolverHasValues(void);
+int IterativeSolverHasEigenvalues(void);
+void IterativeSolverSetDiagonals(const double* diagonals);
+void IterativeSolverDiagonals(double* diagonals);
+double IterativeSolverValue(void);
+int IterativeSolverVerbosity(void);
+int IterativeSolverMaxIter(void);
+void IterativeSolverSetMaxIter(int max_iter);
+int64_t mpicomm_self(void);
+int64_t mpicomm_global(void);
+int64_t IterativeSolver_mpicomm_global(void);
+int64_t IterativeSolver_mpicomm_self(void);
+
+/* ---- extension: device / communicator selection ----------------------------------------- */
+/* Use `ctx` (not owned) for the instances initialised after this call; NULL restores the
+ * default (a private single-rank context on device 0).  Returns 0. */
+int IterativeSolverHbmSetContext(ssp_ctx* ctx);
+/* enable = 0: errors are recorded (IterativeSolverHbmLastError, cleared by every call) instead of
+ * thrown, and the failing call returns 0 -- for callers that cannot unwind C++ exceptions
+ * (ctypes, Fortran).  Default 1 (throw, as the reference does).  Returns 0. */
+int IterativeSolverHbmSetThrow(int enable);
+/* Statistics of the top instance: iterations, R and Q creations (for tests and reports). */
+int IterativeSolverHbmStatistics(int* iterations, int* r_creations, int* q_creations);
+const char* IterativeSolverHbmLastError(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -168,6 +168,29 @@ inline void general_eigen(size_t n, const std::vector<double>& a, std::vector<st
     c = x / r;
     s = y / r;
   };
+  // Unitary reduction to upper Hessenberg form (Givens rotations, accumulated in Q): the shifted
+  // QR sweeps below and their subdiagonal deflation test assume it.
+  for (size_t j = 0; j + 2 < n; ++j)
+    for (size_t i = n - 1; i >= j + 2; --i) {
+      const cd x = T[(i - 1) + n * j], y = T[i + n * j];
+      if (std::abs(y) == 0) continue;
+      cd c, s;
+      givens(0, x, y, c, s);
+      for (size_t k = 0; k < n; ++k) {
+        const cd a = T[(i - 1) + n * k], b = T[i + n * k];
+        T[(i - 1) + n * k] = std::conj(c) * a + std::conj(s) * b;
+        T[i + n * k] = -s * a + c * b;
+      }
+      for (size_t k = 0; k < n; ++k) {
+        const cd a = T[k + n * (i - 1)], b = T[k + n * i];
+        T[k + n * (i - 1)] = a * c + b * s;
+        T[k + n * i] = -a * std::conj(s) + b * std::conj(c);
+        const cd qa = Q[k + n * (i - 1)], qb = Q[k + n * i];
+        Q[k + n * (i - 1)] = qa * c + qb * s;
+        Q[k + n * i] = -qa * std::conj(s) + qb * std::conj(c);
+      }
+      T[i + n * j] = 0;
+    }
   for (size_t hi = n; hi > 1;) {
     int iter = 0;
     for (;;) {

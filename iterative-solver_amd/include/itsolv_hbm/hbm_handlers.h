@@ -194,14 +194,16 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
     if (alphas.rows() != xx.size())
       throw std::out_of_range("gemm_outer: dimensions of xx and alphas are different: " + std::to_string(alphas.rows()) +
                               " " + std::to_string(xx.size()));
-    if (alphas.cols() != yy.size())
+    // As gemm_outer_default (util/gemm.h:257-265): alphas.cols() destinations, the first of yy
+    // (construct_solution fills a batch of roots into a larger parameter buffer).
+    if (alphas.cols() > yy.size())
       throw std::out_of_range("gemm_outer: dimensions of yy and alphas are different: " + std::to_string(alphas.cols()) +
                               " " + std::to_string(yy.size()));
     for (auto& x : xx) same(x.get(), yy.front().get(), "gemm_outer");
     auto xp = detail::cptrs(xx);
     auto yp = detail::mptrs(yy);
     const auto& y0 = yy.front().get();
-    check(ssp_gemm_outer(y0.ctx(), alphas.data().data(), xp.data(), int(xx.size()), yp.data(), int(yy.size()),
+    check(ssp_gemm_outer(y0.ctx(), alphas.data().data(), xp.data(), int(xx.size()), yp.data(), int(alphas.cols()),
                          y0.local_size()),
           "ssp_gemm_outer");
   }
@@ -313,7 +315,7 @@ class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
   void gemm_outer(const Matrix<double> alphas, const CVecRef<SparseP>& xx, const VecRef<Vec>& yy) override {
     m_counter->gemm_outer++;
     if (xx.empty() || yy.empty()) return;
-    if (alphas.rows() != xx.size() || alphas.cols() != yy.size())
+    if (alphas.rows() != xx.size() || alphas.cols() > yy.size())
       throw std::out_of_range("gemm_outer (sparse): dimensions of alphas do not match xx, yy");
     std::vector<size_t> ptr, idx;
     std::vector<double> val;
@@ -321,7 +323,7 @@ class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
     auto yp = detail::mptrs(yy);
     const auto& y0 = yy.front().get();
     check(ssp_gemm_outer_sparse(y0.ctx(), alphas.data().data(), ptr.data(), idx.data(), val.data(), int(xx.size()),
-                                yp.data(), int(yy.size()), y0.local_size(), y0.offset()),
+                                yp.data(), int(alphas.cols()), y0.local_size(), y0.offset()),
           "ssp_gemm_outer_sparse");
   }
   Matrix<double> gemm_inner(const CVecRef<Vec>& xx, const CVecRef<SparseP>& yy) override {

@@ -1,0 +1,364 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY — never shipped, never loaded by the product libraries.
+//
+// A host-memory emulation of the libsubspace_hip.so C ABI (include/subspace_hip.h), so that the
+// product's HOST code -- the restated solvers, the HBM handlers, the reverse-communication C API
+// (iterative-solver_amd/host/*.cpp) -- can be linked against it (oracle/build/libitsolv_emul.so)
+// and exercised on CPU-only machines, including several ranks over the host communicator
+// (ssp_ctx_attach_host_comm + gloo or sockets).  Every "device" pointer is host memory; every
+// operation is the reference's sequential loop (oracle_ops.c, ArrayHandlerIterable.h:46-102),
+// reductions are summed locally and then over ranks through the callbacks, selection is the
+// reference heap (util/select.h:28-55) per rank followed by the same merge rule ssp_select_merge
+// documents.  GPU parity is proven by tests/test_*_gpu.py against the real library, not here.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "oracle_ops.h"
+#include "subspace_hip.h"
+
+struct ssp_ctx {
+  int rank = 0;
+  int nranks = 1;
+  ssp_host_allreduce_fn allreduce = nullptr;
+  ssp_host_allgather_fn allgather = nullptr;
+  void* user = nullptr;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& m) {
+  g_err = m;
+  return code;
+}
+
+int reduce(ssp_ctx* c, double* v, size_t n) {
+  if (c->nranks <= 1 || n == 0) return SSP_OK;
+  if (!c->allreduce || c->allreduce(v, n, c->user) != 0) return fail(SSP_ERR_COMM, "emul: allreduce failed");
+  return SSP_OK;
+}
+
+uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+uint64_t stream_key(uint64_t seed, uint64_t stream) { return splitmix64(seed ^ (stream * 0xD1B54A32D192ED03ull)); }
+double sign_of(uint64_t key, uint64_t g) { return (splitmix64(key ^ g) & 1) ? -1.0 : 1.0; }
+
+void filter(const size_t* idx, const double* val, size_t nnz, size_t n, size_t off, std::vector<size_t>& li,
+            std::vector<double>& lv) {
+  for (size_t e = 0; e < nnz; ++e)
+    if (idx[e] >= off && idx[e] < off + n) {
+      li.push_back(idx[e] - off);
+      lv.push_back(val[e]);
+    }
+}
+}  // namespace
+
+extern "C" {
+
+const char* ssp_last_error(void) { return g_err.c_str(); }
+const char* ssp_version(void) { return "ssp-emul (host emulation, test infrastructure)"; }
+int ssp_device_count(void) { return 0; }
+int ssp_ctx_create(int, ssp_ctx** out) {
+  *out = new ssp_ctx();
+  return SSP_OK;
+}
+int ssp_ctx_destroy(ssp_ctx* c) {
+  delete c;
+  return SSP_OK;
+}
+void* ssp_ctx_stream(ssp_ctx*) { return nullptr; }
+int ssp_synchronize(ssp_ctx*) { return SSP_OK; }
+int ssp_alloc(ssp_ctx*, size_t n, double** out) {
+  *out = static_cast<double*>(std::calloc(std::max<size_t>(n, 1), sizeof(double)));
+  return *out ? SSP_OK : fail(SSP_ERR_NOMEM, "emul: calloc");
+}
+int ssp_free(ssp_ctx*, double* p) {
+  std::free(p);
+  return SSP_OK;
+}
+int ssp_release_cached(ssp_ctx*) { return SSP_OK; }
+int ssp_memory_stats(ssp_ctx*, size_t* a, size_t* b) {
+  *a = *b = 0;
+  return SSP_OK;
+}
+int ssp_upload(ssp_ctx*, double* d, const double* h, size_t n) {
+  if (n) std::memcpy(d, h, n * sizeof(double));
+  return SSP_OK;
+}
+int ssp_download(ssp_ctx*, double* h, const double* d, size_t n) {
+  if (n) std::memcpy(h, d, n * sizeof(double));
+  return SSP_OK;
+}
+int ssp_comm_unique_id(char* id) {
+  std::memset(id, 0, SSP_UNIQUE_ID_BYTES);
+  return SSP_OK;
+}
+int ssp_ctx_attach_comm(ssp_ctx*, int nranks, int, const char*) {
+  return nranks == 1 ? SSP_OK : fail(SSP_ERR_UNSUPPORTED, "emul: no RCCL; use ssp_ctx_attach_host_comm");
+}
+int ssp_ctx_attach_host_comm(ssp_ctx* c, int nranks, int rank, ssp_host_allreduce_fn ar, ssp_host_allgather_fn ag,
+                             void* user) {
+  c->nranks = nranks;
+  c->rank = rank;
+  c->allreduce = ar;
+  c->allgather = ag;
+  c->user = user;
+  return SSP_OK;
+}
+int ssp_ctx_rank(ssp_ctx* c) { return c->rank; }
+int ssp_ctx_nranks(ssp_ctx* c) { return c->nranks; }
+int ssp_allreduce_sum(ssp_ctx* c, double* v, size_t n) { return reduce(c, v, n); }
+int ssp_allgather_host(ssp_ctx* c, const void* s, void* r, size_t bytes) {
+  if (c->nranks <= 1) {
+    if (bytes) std::memcpy(r, s, bytes);
+    return SSP_OK;
+  }
+  if (!c->allgather || c->allgather(s, r, bytes, c->user) != 0) return fail(SSP_ERR_COMM, "emul: allgather failed");
+  return SSP_OK;
+}
+int ssp_shard_range(size_t n, int nranks, int rank, size_t* off, size_t* len) {
+  const size_t p = size_t(nranks), r = size_t(rank), b = n / p, e = n % p;
+  *off = r * b + std::min(r, e);
+  *len = b + (r < e ? 1 : 0);
+  return SSP_OK;
+}
+int ssp_ledger_enable(ssp_ctx*, int) { return SSP_OK; }
+int ssp_ledger_reset(ssp_ctx*) { return SSP_OK; }
+int ssp_ledger_count(ssp_ctx*) { return 0; }
+int ssp_ledger_entry(ssp_ctx*, int, const char**, long long*, double*, double*) {
+  return fail(SSP_ERR_ARG, "emul: no ledger");
+}
+
+int ssp_fill(ssp_ctx*, double a, double* x, size_t n) {
+  for (size_t i = 0; i < n; ++i) x[i] = a;
+  return SSP_OK;
+}
+int ssp_scal(ssp_ctx*, double a, double* x, size_t n) {
+  for (size_t i = 0; i < n; ++i) x[i] *= a;
+  return SSP_OK;
+}
+int ssp_copy(ssp_ctx*, double* x, const double* y, size_t n) {
+  if (n && x != y) std::memmove(x, y, n * sizeof(double));
+  return SSP_OK;
+}
+int ssp_axpy(ssp_ctx*, double a, const double* x, double* y, size_t n) {
+  for (size_t i = 0; i < n; ++i) y[i] += a * x[i];
+  return SSP_OK;
+}
+int ssp_dot(ssp_ctx* c, const double* x, const double* y, size_t n, double* out) {
+  double s = 0;
+  for (size_t i = 0; i < n; ++i) s += x[i] * y[i];
+  *out = s;
+  return reduce(c, out, 1);
+}
+int ssp_gemm_inner(ssp_ctx* c, const double* const* xx, int m, const double* const* yy, int k, size_t n, double* out) {
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < k; ++j) {
+      double s = 0;
+      for (size_t e = 0; e < n; ++e) s += xx[i][e] * yy[j][e];
+      out[size_t(i) * k + j] = s;
+    }
+  return reduce(c, out, size_t(m) * k);
+}
+int ssp_gemm_outer(ssp_ctx*, const double* al, const double* const* xx, int k, double* const* yy, int m, size_t n) {
+  for (int j = 0; j < m; ++j)
+    for (int i = 0; i < k; ++i) {
+      const double a = al[size_t(i) * m + j];
+      for (size_t e = 0; e < n; ++e) yy[j][e] += a * xx[i][e];
+    }
+  return SSP_OK;
+}
+int ssp_axpy_inner(ssp_ctx* c, const double* cc, const double* x, double* const* yy, int m, const double* z, size_t n,
+                   double* out) {
+  for (int j = 0; j < m; ++j) {
+    double s = 0;
+    for (size_t e = 0; e < n; ++e) {
+      yy[j][e] += cc[j] * x[e];
+      s += yy[j][e] * z[e];
+    }
+    out[j] = s;
+  }
+  return reduce(c, out, size_t(m));
+}
+int ssp_precondition(ssp_ctx*, double* const* a, int nvec, const double* d, const double* shift, size_t n) {
+  for (int v = 0; v < nvec; ++v)
+    for (size_t i = 0; i < n; ++i) a[v][i] = a[v][i] / ((d[i] - shift[v]) + 1e-15);
+  return SSP_OK;
+}
+
+int ssp_select_merge(int nranks, const size_t* counts, size_t stride, const size_t* idx, const double* val,
+                     size_t nsel, int max, size_t* io, double* vo, size_t* nout) {
+  struct It {
+    double key;
+    size_t idx;
+    double val;
+  };
+  std::vector<It> all;
+  for (int r = 0; r < nranks; ++r)
+    for (size_t e = 0; e < counts[r]; ++e) {
+      const size_t s = size_t(r) * stride + e;
+      double k = max ? val[s] : -val[s];
+      if (k == 0) k = 0;  // -0 and +0 compare equal in the heap's pair order
+      all.push_back({k, idx[s], val[s]});
+    }
+  std::sort(all.begin(), all.end(),
+            [](const It& a, const It& b) { return a.key > b.key || (a.key == b.key && a.idx > b.idx); });
+  if (all.size() > nsel) all.resize(nsel);
+  std::sort(all.begin(), all.end(), [](const It& a, const It& b) { return a.idx < b.idx; });
+  for (size_t e = 0; e < all.size(); ++e) {
+    if (io) io[e] = all[e].idx;
+    if (vo) vo[e] = all[e].val;
+  }
+  *nout = all.size();
+  return SSP_OK;
+}
+
+static int select_common(ssp_ctx* c, const std::vector<size_t>& li, const std::vector<double>& lv, size_t offset,
+                         size_t nsel, int max, size_t* io, double* vo, size_t* nout) {
+  const int nr = c->nranks;
+  std::vector<size_t> sidx(nsel, 0), gidx(nsel * size_t(nr));
+  std::vector<double> sval(nsel, 0.0), gval(nsel * size_t(nr));
+  for (size_t e = 0; e < li.size(); ++e) {
+    sidx[e] = li[e] + offset;
+    sval[e] = lv[e];
+  }
+  size_t cnt = li.size();
+  std::vector<size_t> counts(nr);
+  if (int s = ssp_allgather_host(c, &cnt, counts.data(), sizeof(size_t))) return s;
+  if (nsel) {
+    if (int s = ssp_allgather_host(c, sidx.data(), gidx.data(), nsel * sizeof(size_t))) return s;
+    if (int s = ssp_allgather_host(c, sval.data(), gval.data(), nsel * sizeof(double))) return s;
+  }
+  return ssp_select_merge(nr, counts.data(), nsel, gidx.data(), gval.data(), nsel, max, io, vo, nout);
+}
+
+int ssp_select(ssp_ctx* c, const double* x, size_t n, size_t offset, size_t nsel, int max, int ignore_sign,
+               size_t* io, double* vo, size_t* nout) {
+  const size_t k = std::min(n, nsel);
+  std::vector<size_t> li(std::max<size_t>(k, 1));
+  std::vector<double> lv(std::max<size_t>(k, 1));
+  size_t got = 0;
+  if (k) or_select(x, n, k, max, ignore_sign, li.data(), lv.data(), &got);
+  li.resize(got);
+  lv.resize(got);
+  return select_common(c, li, lv, offset, nsel, max, io, vo, nout);
+}
+int ssp_select_max_dot(ssp_ctx* c, const double* x, const double* y, size_t n, size_t offset, size_t nsel, size_t* io,
+                       double* vo, size_t* nout) {
+  const size_t k = std::min(n, nsel);
+  std::vector<size_t> li(std::max<size_t>(k, 1));
+  std::vector<double> lv(std::max<size_t>(k, 1));
+  size_t got = 0;
+  if (k) or_select_max_dot(x, y, n, k, li.data(), lv.data(), &got);
+  li.resize(got);
+  lv.resize(got);
+  return select_common(c, li, lv, offset, nsel, 1, io, vo, nout);
+}
+
+int ssp_sparse_copy(ssp_ctx*, double* x, size_t n, size_t off, const size_t* idx, const double* val, size_t nnz) {
+  std::vector<size_t> li;
+  std::vector<double> lv;
+  filter(idx, val, nnz, n, off, li, lv);
+  for (size_t i = 0; i < n; ++i) x[i] = 0;
+  for (size_t e = 0; e < li.size(); ++e) x[li[e]] = lv[e];
+  return SSP_OK;
+}
+int ssp_sparse_axpy(ssp_ctx*, double a, const size_t* idx, const double* val, size_t nnz, double* x, size_t n,
+                    size_t off) {
+  std::vector<size_t> li;
+  std::vector<double> lv;
+  filter(idx, val, nnz, n, off, li, lv);
+  for (size_t e = 0; e < li.size(); ++e) x[li[e]] += a * lv[e];
+  return SSP_OK;
+}
+int ssp_gemm_inner_sparse(ssp_ctx* c, const double* const* xx, int m, size_t n, size_t off, const size_t* ptr,
+                          const size_t* idx, const double* val, int k, double* out) {
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < k; ++j) {
+      std::vector<size_t> li;
+      std::vector<double> lv;
+      filter(idx + ptr[j], val + ptr[j], ptr[j + 1] - ptr[j], n, off, li, lv);
+      double s = 0;
+      for (size_t e = 0; e < li.size(); ++e) s += xx[i][li[e]] * lv[e];
+      out[size_t(i) * k + j] = s;
+    }
+  return reduce(c, out, size_t(m) * k);
+}
+int ssp_sparse_dot(ssp_ctx* c, const double* x, size_t n, size_t off, const size_t* idx, const double* val, size_t nnz,
+                   double* out) {
+  const size_t ptr[2] = {0, nnz};
+  const double* xx[1] = {x};
+  return ssp_gemm_inner_sparse(c, xx, 1, n, off, ptr, idx, val, 1, out);
+}
+int ssp_gemm_outer_sparse(ssp_ctx*, const double* al, const size_t* ptr, const size_t* idx, const double* val, int k,
+                          double* const* yy, int m, size_t n, size_t off) {
+  for (int j = 0; j < m; ++j)
+    for (int i = 0; i < k; ++i) {
+      std::vector<size_t> li;
+      std::vector<double> lv;
+      filter(idx + ptr[i], val + ptr[i], ptr[i + 1] - ptr[i], n, off, li, lv);
+      for (size_t e = 0; e < li.size(); ++e) yy[j][li[e]] += al[size_t(i) * m + j] * lv[e];
+    }
+  return SSP_OK;
+}
+
+int sspx_synthetic_action(ssp_ctx* c, const double* const* xx, double* const* yy, int nvec, size_t n, size_t off,
+                          double rho, int rank, unsigned long long seed) {
+  std::vector<double> coef(size_t(nvec) * rank, 0.0);
+  std::vector<uint64_t> key(rank);
+  for (int l = 0; l < rank; ++l) key[l] = stream_key(seed, 1000 + l);
+  for (int v = 0; v < nvec; ++v)
+    for (int l = 0; l < rank; ++l) {
+      double s = 0;
+      for (size_t i = 0; i < n; ++i) s += (l == 0 ? 1.0 : sign_of(key[l], off + i)) * xx[v][i];
+      coef[size_t(v) * rank + l] = s;
+    }
+  if (int s = reduce(c, coef.data(), coef.size())) return s;
+  for (int v = 0; v < nvec; ++v)
+    for (size_t i = 0; i < n; ++i) {
+      double t = 0;
+      for (int l = 0; l < rank; ++l) t += (l == 0 ? 1.0 : sign_of(key[l], off + i)) * coef[size_t(v) * rank + l];
+      yy[v][i] = (1.0 + double(off + i)) * xx[v][i] + rho * t;
+    }
+  return SSP_OK;
+}
+int sspx_synthetic_add_lowrank(ssp_ctx*, double* const* yy, int nvec, size_t n, size_t off, double rho, int rank,
+                               unsigned long long seed, const double* w) {
+  for (int v = 0; v < nvec; ++v)
+    for (size_t i = 0; i < n; ++i) {
+      double t = 0;
+      for (int l = 0; l < rank; ++l)
+        t += (l == 0 ? 1.0 : sign_of(stream_key(seed, 1000 + l), off + i)) * w[size_t(v) * rank + l];
+      yy[v][i] += rho * t;
+    }
+  return SSP_OK;
+}
+int sspx_synthetic_diagonal(ssp_ctx*, double* d, size_t n, size_t off, double rho, int rank) {
+  for (size_t i = 0; i < n; ++i) d[i] = 1.0 + double(off + i) + rank * rho;
+  return SSP_OK;
+}
+int sspx_fill_random(ssp_ctx*, double* x, size_t n, size_t off, unsigned long long seed, unsigned long long vec) {
+  const uint64_t key = stream_key(seed, vec);
+  for (size_t i = 0; i < n; ++i) x[i] = double(splitmix64(key ^ (off + i)) >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+  return SSP_OK;
+}
+int sspx_dense_action(ssp_ctx*, const double* a, size_t ng, const double* const* xx, double* const* yy, int nvec,
+                      size_t n, size_t off) {
+  for (int v = 0; v < nvec; ++v)
+    for (size_t r = 0; r < n; ++r) {
+      double s = 0;
+      for (size_t j = 0; j < ng; ++j) s += a[(off + r) * ng + j] * xx[v][j];
+      yy[v][r] = s;
+    }
+  return SSP_OK;
+}
+
+}  // extern "C"

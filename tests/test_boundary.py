@@ -13,14 +13,28 @@ LIBDIR = os.path.join(ROOT, "iterative-solver_amd", "lib")
 HEADERS = {
     "subspace_hip.h": "libsubspace_hip.so",
     "itsolv_hbm.h": "libitsolv_hbm.so",
+    "iterative_solver_c.h": "libitsolv_hbm.so",
 }
+# The reverse-communication API keeps the reference's names (src/molpro/linalg/IterativeSolverC.h).
+REFERENCE_C_API = [
+    "IterativeSolverLinearEigensystemInitialize", "IterativeSolverLinearEquationsInitialize",
+    "IterativeSolverNonLinearEquationsInitialize", "IterativeSolverOptimizeInitialize", "IterativeSolverFinalize",
+    "IterativeSolverAddVector", "IterativeSolverSolution", "IterativeSolverAddValue", "IterativeSolverEndIteration",
+    "IterativeSolverEndIterationNeeded", "IterativeSolverAddP", "IterativeSolverErrors", "IterativeSolverEigenvalues",
+    "IterativeSolverWorkingSetEigenvalues", "IterativeSolverSuggestP", "IterativeSolverPrintStatistics",
+    "IterativeSolverNonLinear", "IterativeSolverHasValues", "IterativeSolverHasEigenvalues",
+    "IterativeSolverSetDiagonals", "IterativeSolverDiagonals", "IterativeSolverValue", "IterativeSolverVerbosity",
+    "IterativeSolverMaxIter", "IterativeSolverSetMaxIter", "mpicomm_self", "mpicomm_global",
+    "IterativeSolver_mpicomm_global", "IterativeSolver_mpicomm_self",
+]
 
 
 def declared_functions(header):
     text = open(os.path.join(INCLUDE, header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     text = re.sub(r"//[^\n]*", "", text)
-    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b((?:ssp|sspx|itsolv)_\w+)\s*\(", text, flags=re.M)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b((?:ssp|sspx|itsolv)_\w+|IterativeSolver\w+|mpicomm_\w+)\s*\(",
+                       text, flags=re.M)
     return sorted(set(names))
 
 
@@ -35,6 +49,13 @@ def test_library_exports_every_declared_symbol(header, lib):
     assert len(names) > 5
     missing = [n for n in names if not hasattr(so, n)]
     assert not missing, f"{lib} lacks {missing}"
+
+
+def test_reverse_communication_api_is_the_reference_name_set():
+    declared = declared_functions("iterative_solver_c.h")
+    assert set(REFERENCE_C_API) <= set(declared)
+    extra = sorted(set(declared) - set(REFERENCE_C_API))
+    assert all(n.startswith("IterativeSolverHbm") for n in extra), extra
 
 
 def test_python_binding_lists_every_symbol():

@@ -1,0 +1,150 @@
+"""The reverse-communication C API (include/iterative_solver_c.h, the reference's
+IterativeSolverC.h) and its Python binding (iterative_solver) on the GPU.
+
+* test_diagonalize / test_nonlinear_equations follow the reference's own Python tests
+  (python/test/test_rayleigh_quotient.py:101-150) with their assertions (7 decimal places).
+* Parity: the C-API loop driven from Python on the dense fixtures takes the same iterations as the
+  reference CPU path (oracle.davidson_dense, the restated solve()), eigenvalues within 1e-10.
+* P space through IterativeSolverAddP with a caller-side apply-P callback, as the reference's
+  examples/LinearEigensystemExampleF-Pspace.F90 drives it (n = 200, 3 roots, 30 P functions).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import iterative_solver
+import oracle
+from test_python_api import RayleighQuotient
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+BIG = 1.7976931348623157e308
+
+
+def test_diagonalize():
+    problem = RayleighQuotient(8, 0.1)
+    nroot = 2
+    parameters = np.zeros([nroot, problem.size])
+    residual = np.zeros([nroot, problem.size])
+    solver = iterative_solver.LinearEigensystem(problem.size, nroot)
+    solver.solve(parameters, residual, problem, generate_initial_guess=True)
+    solver.solution(list(range(nroot)), parameters, residual)
+    assert solver.errors.size == nroot
+    for e in solver.errors:
+        assert e == pytest.approx(0.0, abs=1e-7)
+    ev = solver.eigenvalues
+    for root in range(nroot):
+        parameters[root] /= np.sqrt(np.dot(parameters[root], parameters[root]))
+        value = problem.residual(parameters[root], residual[root])
+        assert ev[root] == pytest.approx(problem.eigenvalues[root], abs=1e-7)
+        assert value == pytest.approx(ev[root], abs=1e-7)
+        assert np.all(np.abs(residual[root]) < 1e-7)
+    solver.finalize()
+
+
+def test_nonlinear_equations():
+    problem = RayleighQuotient(4, 0.01)
+    parameters = np.zeros(problem.size)
+    parameters[0] = 1
+    residual = np.zeros(problem.size)
+    solver = iterative_solver.NonLinearEquations(problem.size)
+    solver.solve(parameters, residual, problem)
+    solver.solution([0], parameters, residual)
+    parameters = parameters * problem.eigenvectors[0, 0] / parameters[0]
+    value = problem.residual(parameters, residual)
+    assert value == pytest.approx(problem.eigenvalues[0], abs=1e-7)
+    np.testing.assert_allclose(residual, 0.0, atol=1e-7)
+    np.testing.assert_allclose(parameters, problem.eigenvectors[:, 0], atol=1e-7)
+    solver.finalize()
+
+
+@pytest.mark.parametrize("cls,args", [("LinearEquations", (np.ones((1, 4)),)), ("Optimize", (4,))])
+def test_unavailable_solvers_raise(cls, args):
+    with pytest.raises(RuntimeError, match="not available"):
+        getattr(iterative_solver, cls)(*args)
+
+
+class Dense(iterative_solver.Problem):
+    """Dense symmetric H with the C++ default preconditioner a / ((d - shift) + 1e-15)
+    (reference IterativeSolver.h:47-55), as the oracle's dense problem uses."""
+
+    def __init__(self, h):
+        super().__init__()
+        self.h = h
+
+    def action(self, parameters, actions):
+        np.matmul(parameters, self.h, out=actions)
+
+    def diagonals(self, d):
+        d[: self.h.shape[0]] = np.diag(self.h)
+        return True
+
+    def precondition(self, residual, shift=None, diagonals=None):
+        for i in range(residual.shape[0]):
+            residual[i] = residual[i] / ((diagonals - shift[i]) + 1e-15)
+
+
+def hamiltonian(name, split):
+    t = open(os.path.join(GOLD, name + ".hamiltonian")).read().split()
+    n = int(t[0])
+    return np.array(t[1:1 + n * n], dtype=float).reshape(n, n) + np.diag(split * np.arange(n))
+
+
+@pytest.mark.parametrize("name,split,nroot", [("he", 0.0, 1), ("hf", 1e-8, 1), ("hf", 1e-8, 3), ("bh", 1e-8, 1),
+                                              ("bh", 1e-8, 3)])
+def test_c_api_loop_matches_reference_path(name, split, nroot):
+    h = hamiltonian(name, split)
+    n = h.shape[0]
+    kw = dict(nroots=nroot, convergence_threshold=1e-8, max_size_qspace=6 * nroot, reset_D=8)
+    cpu = oracle.davidson_dense(h, **kw)
+    solver = iterative_solver.LinearEigensystem(n, nroot, thresh=1e-8, thresh_value=BIG, hermitian=True,
+                                                options=f"MAX_SIZE_QSPACE={6 * nroot},RESET_D=8")
+    x, g = np.zeros((nroot, n)), np.zeros((nroot, n))
+    # the C++ solve()'s initial guess: unit vectors on the nroot smallest diagonals, in index order
+    for k, i in enumerate(sorted(np.argsort(np.diag(h), kind="stable")[:nroot])):
+        x[k, i] = 1.0
+    solver.solve(x, g, Dense(h))
+    st = solver.statistics()
+    assert st["iterations"] == cpu["iterations"]
+    ev = solver.eigenvalues
+    assert np.max(np.abs(ev - cpu["eigenvalues"])) <= 1e-10 * max(1.0, np.max(np.abs(cpu["eigenvalues"])))
+    gold = json.load(open(os.path.join(GOLD, "eigen_golden.json")))[name]["eigenvalues"][:nroot]
+    assert np.max(np.abs(ev - np.array(gold))) < 1e-10
+    assert np.all(solver.errors <= 2e-8)
+    solver.finalize()
+
+
+def test_add_p_with_caller_callback():
+    # reference examples/LinearEigensystemExampleF-Pspace.F90: m = 1 + diag(3 i), P = first 30 unit vectors
+    n, nroot, nP = 200, 3, 30
+    m = np.ones((n, n)) + np.diag(3.0 * np.arange(1, n + 1))
+    pidx = np.arange(nP)
+    solver = iterative_solver.LinearEigensystem(n, nroot, thresh=1e-8, thresh_value=BIG, hermitian=True)
+    c, g = np.zeros((nroot, n)), np.zeros((nroot, n))
+    calls = []
+
+    def apply_p(pc, gl, ranges):
+        calls.append(pc.shape[0])
+        for k in range(pc.shape[0]):
+            r0, r1 = ranges[k]
+            gl[k * n:k * n + (r1 - r0)] += m[r0:r1][:, pidx] @ pc[k]
+
+    nwork = solver.add_p([{int(i): 1.0} for i in pidx], m[np.ix_(pidx, pidx)], c, g, apply_p)
+    d = np.diag(m)
+    for _ in range(100):
+        ev = solver.working_set_eigenvalues(nwork)
+        for k in range(nwork):
+            g[k] = g[k] / ((d - ev[k]) + 1e-15)
+        nwork = solver.end_iteration(c, g)
+        if nwork == 0:
+            break
+        g[:nwork] = c[:nwork] @ m
+        nwork = solver.add_vector(c[:nwork], g[:nwork])
+        if nwork == 0:
+            break
+    assert nwork == 0 and calls
+    np.testing.assert_allclose(solver.eigenvalues, np.linalg.eigvalsh(m)[:nroot], rtol=0, atol=1e-8)
+    assert np.all(solver.errors <= 1e-8)
+    solver.finalize()

@@ -139,3 +139,16 @@ def test_config_c3_n1e8_eight_roots_pspace(ctx):
     assert r["converged"]
     np.testing.assert_allclose(r["eigenvalues"], oracle.rank_one_eigenvalues(n, rho, 8), rtol=1e-10, atol=0)
     assert np.all(r["residual_norms"] <= 1e-7)
+
+
+@pytest.mark.parametrize("param", [1.0, 0.1])
+@pytest.mark.parametrize("nh", [0.0, 0.1, 0.2])
+@pytest.mark.parametrize("nroot", [1, 3])
+def test_nonhermitian_davidson_gpu_vs_cpu(ctx, param, nh, nroot):
+    from test_solver_oracle import nonhermitian_matrix
+
+    h = nonhermitian_matrix(6, param, nh)
+    kw = dict(nroots=nroot, hermitian=0, convergence_threshold=1e-9)
+    gpu, cpu = ih.davidson_dense(ctx, h, **kw), oracle.davidson_dense(h, **kw)
+    assert gpu["converged"] and cpu["converged"] and gpu["iterations"] == cpu["iterations"]
+    np.testing.assert_allclose(gpu["eigenvalues"], cpu["eigenvalues"], rtol=0, atol=1e-10)

@@ -102,3 +102,23 @@ def test_rank_r_synthetic_dense_reference():
                                       max_size_qspace=24, reset_D=8)
         assert r["converged"]
         assert np.max(np.abs(r["eigenvalues"] - ref)) < 1e-10
+
+
+def nonhermitian_matrix(n, param, non_hermiticity):
+    # reference test_LinearEigensystem.cpp:40-50: H = 1, H_ii = i*param, lower triangle *(1 - nh)
+    h = np.ones((n, n))
+    h[np.diag_indices(n)] = np.arange(n) * param
+    h[np.tril_indices(n, -1)] *= 1 - non_hermiticity
+    return h
+
+
+@pytest.mark.parametrize("param", [1.0, 0.1])
+@pytest.mark.parametrize("nh", [0.0, 0.1, 0.2])
+@pytest.mark.parametrize("nroot", [1, 2, 3])
+def test_nonhermitian_eigen(param, nh, nroot):
+    # reference test_LinearEigensystem.cpp:364-375 (n = 6), checked against numpy's general eigensolver
+    h = nonhermitian_matrix(6, param, nh)
+    r = oracle.davidson_dense(h, nroots=nroot, hermitian=0, convergence_threshold=1e-9)
+    assert r["converged"]
+    exact = np.sort(np.linalg.eigvals(h).real)[:nroot]
+    assert np.max(np.abs(r["eigenvalues"] - exact)) < 1e-10
