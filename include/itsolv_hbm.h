@@ -35,6 +35,7 @@ typedef struct {
   int hermitian;
   int generate_initial_guess;  /* 1: initial guess from the n smallest diagonals           */
   int verbosity;               /* 0 none .. 3 detailed                                     */
+  double augmented_hessian;    /* LinearEquationsDavidson augmented-Hessian parameter (0: off) */
 } itsolv_options;
 
 typedef struct {
@@ -69,6 +70,11 @@ int itsolv_diis_synthetic(ssp_ctx* ctx, size_t n, double rho, int rank, unsigned
                           const itsolv_options* opt, itsolv_result* out, double* x_out);
 
 /* DIIS on r(x) = H (x - 1) for a dense row-major H (reference test_NonLinearEquations.cpp:38-49). */
+/* LinearEquationsDavidson (reference itsolv/LinearEquationsDavidson.h): A x_r = b_r for nrhs
+ * right-hand sides b (row-major nrhs x n, host), dense row-major A resident in HBM (single rank).
+ * x_out (nrhs x n, host) may be NULL. */
+int itsolv_linear_equations_dense(ssp_ctx* ctx, const double* a, size_t n, const double* rhs, int nrhs,
+                                  const itsolv_options* opt, itsolv_result* out, double* x_out);
 int itsolv_diis_dense(ssp_ctx* ctx, const double* h, size_t n, const itsolv_options* opt, itsolv_result* out,
                       double* x_out);
 

@@ -29,6 +29,7 @@ namespace {
 using Solver = it::IterativeSolverTemplate<Vec, Vec, SparseP>;
 using Davidson = it::LinearEigensystemDavidson<Vec, Vec, SparseP>;
 using DIIS = it::NonLinearEquationsDIIS<Vec, Vec, SparseP>;
+using LinEq = it::LinearEquationsDavidson<Vec, Vec, SparseP>;
 typedef void (*Apply_on_p_fort)(const double*, double*, const size_t, const size_t*);
 
 thread_local std::string g_error;
@@ -176,11 +177,37 @@ void IterativeSolverLinearEigensystemInitialize(size_t nQ, size_t nroot, size_t*
   });
 }
 
-void IterativeSolverLinearEquationsInitialize(size_t, size_t, size_t*, size_t*, const double*, double, double, double,
-                                              int, int, const char*, int64_t, const char*, const char*) {
-  guarded([] {
-    throw std::logic_error(
-        "IterativeSolverLinearEquationsInitialize: LinearEquationsDavidson is not available on the HBM back end");
+void IterativeSolverLinearEquationsInitialize(size_t n, size_t nroot, size_t* range_begin, size_t* range_end,
+                                              const double* rhs, double aughes, double thresh, double thresh_value,
+                                              int hermitian, int verbosity, const char* fname, int64_t fcomm,
+                                              const char* algorithm, const char* options) {
+  guarded([&] {
+    (void)fname;
+    (void)fcomm;
+    const std::string alg = algorithm ? algorithm : "";
+    if (!alg.empty() && alg != "Davidson")
+      throw std::runtime_error("IterativeSolverLinearEquationsInitialize: algorithm " + alg +
+                               " not available on the HBM back end (Davidson only)");
+    Instance in;
+    in.dev = make_device();
+    setup(in, n, range_begin, range_end);
+    auto solver = std::make_unique<LinEq>(molpro::linalg::hbm::make_handlers());
+    // reference IterativeSolverCMPI.cpp:199-225: rhs as R vectors, then options
+    std::vector<Vec> b;
+    for (size_t r = 0; r < nroot; ++r) {
+      b.emplace_back(in.dev, n);
+      check(ssp_upload(in.dev->ctx(), b.back().data(), rhs + r * n + in.offset, in.local), "ssp_upload");
+    }
+    if (options && *options) solver->set_options(it::LinearEquationsDavidsonOptions(it::parse_options(options)));
+    solver->set_hermiticity(hermitian != 0);
+    solver->set_n_roots(nroot);
+    solver->add_equations(b);
+    solver->set_convergence_threshold(thresh);
+    solver->set_convergence_threshold_value(thresh_value);
+    if (aughes > 0) solver->set_augmented_hessian(aughes);
+    solver->set_verbosity(verbosity_of(verbosity));
+    in.solver = std::move(solver);
+    instances.push(std::move(in));
   });
 }
 

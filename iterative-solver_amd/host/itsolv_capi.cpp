@@ -268,6 +268,39 @@ int itsolv_diis_synthetic(ssp_ctx* ctx, size_t n, double rho, int rank, unsigned
   });
 }
 
+int itsolv_linear_equations_dense(ssp_ctx* ctx, const double* a, size_t n, const double* rhs, int nrhs,
+                                  const itsolv_options* opt, itsolv_result* out, double* x_out) {
+  return guarded([&] {
+    auto dev = borrow(ctx);
+    const auto o = opts_or_default(opt);
+    DenseProblem problem(dev, a, n);
+    std::memset(out, 0, sizeof(*out));
+    std::vector<Vec> b;
+    for (int r = 0; r < nrhs; ++r) {
+      b.emplace_back(dev, n);
+      check(ssp_upload(dev->ctx(), b.back().data(), rhs + size_t(r) * n + b.back().offset(), b.back().local_size()),
+            "ssp_upload");
+    }
+    pr::run_linear_equations<Vec, Vec, SparseP>(
+        molpro::linalg::hbm::make_handlers(), problem, [&] { return zero_vec(dev, n); }, b,
+        [&](const Vec& x, size_t r) {
+          Vec ax(dev, x.size());
+          problem.action(CVecRef<Vec>{std::cref(x)}, VecRef<Vec>{std::ref(ax)});
+          check(ssp_axpy(dev->ctx(), -1.0, b[r].data(), ax.data(), ax.local_size()), "ssp_axpy");
+          double rr = 0, bb = 0;
+          check(ssp_dot(dev->ctx(), ax.data(), ax.data(), ax.local_size(), &rr), "ssp_dot");
+          check(ssp_dot(dev->ctx(), b[r].data(), b[r].data(), b[r].local_size(), &bb), "ssp_dot");
+          return std::sqrt(std::abs(rr) / (bb > 0 ? bb : 1.0));
+        },
+        o, *out,
+        [&](size_t r, const Vec& x) {
+          if (!x_out) return;
+          auto v = x.local_values();
+          std::memcpy(x_out + r * n, v.data(), v.size() * sizeof(double));
+        });
+  });
+}
+
 int itsolv_diis_dense(ssp_ctx* ctx, const double* h, size_t n, const itsolv_options* opt, itsolv_result* out,
                       double* x_out) {
   return guarded([&] {

@@ -147,6 +147,14 @@ struct LinearEigensystemDavidsonOptions : Options {
   std::optional<bool> hermiticity;
 };
 
+struct LinearEquationsDavidsonOptions : LinearEigensystemDavidsonOptions {
+  LinearEquationsDavidsonOptions() = default;
+  explicit LinearEquationsDavidsonOptions(const options_map& opt) : LinearEigensystemDavidsonOptions(opt) {
+    if (opt.count("AUGMENTED_HESSIAN")) augmented_hessian = std::stod(opt.at("AUGMENTED_HESSIAN"));
+  }
+  std::optional<double> augmented_hessian;
+};
+
 struct NonLinearEquationsDIISOptions : Options {
   NonLinearEquationsDIISOptions() = default;
   explicit NonLinearEquationsDIISOptions(const options_map& opt) : Options(opt) {

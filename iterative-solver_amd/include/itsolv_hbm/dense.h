@@ -493,6 +493,39 @@ inline void eigenproblem(std::vector<double>& eigenvectors, std::vector<double>&
   (void)verbosity;
 }
 
+// Householder QR solve of a square system A X = B (A column-major n x n, B column-major n x m),
+// the role of Eigen's householderQr().solve.
+inline void householder_qr_solve(size_t n, std::vector<double> A, std::vector<double>& B, size_t m) {
+  std::vector<double> v(n);
+  for (size_t k = 0; k < n; ++k) {
+    double norm = 0;
+    for (size_t i = k; i < n; ++i) norm += A[i + n * k] * A[i + n * k];
+    norm = std::sqrt(norm);
+    if (norm == 0) continue;
+    const double alpha = A[k + n * k] > 0 ? -norm : norm;
+    double vnorm = 0;
+    for (size_t i = k; i < n; ++i) {
+      v[i] = A[i + n * k] - (i == k ? alpha : 0.0);
+      vnorm += v[i] * v[i];
+    }
+    if (vnorm == 0) continue;
+    auto reflect = [&](double* col) {
+      double d = 0;
+      for (size_t i = k; i < n; ++i) d += v[i] * col[i];
+      d *= 2 / vnorm;
+      for (size_t i = k; i < n; ++i) col[i] -= d * v[i];
+    };
+    for (size_t j = k; j < n; ++j) reflect(&A[n * j]);
+    for (size_t j = 0; j < m; ++j) reflect(&B[n * j]);
+  }
+  for (size_t j = 0; j < m; ++j)
+    for (size_t i = n; i-- > 0;) {
+      double s = B[i + n * j];
+      for (size_t l = i + 1; l < n; ++l) s -= A[i + n * l] * B[l + n * j];
+      B[i + n * j] = A[i + n * i] != 0 ? s / A[i + n * i] : 0.0;
+    }
+}
+
 // DIIS extrapolation coefficients (reference :619-669).  matrix: column-major dimension^2.
 inline void solve_DIIS(std::vector<double>& solution, const std::vector<double>& matrix, const size_t dimension,
                        double svdThreshold, int verbosity = 0) {
@@ -519,6 +552,52 @@ inline void solve_DIIS(std::vector<double>& solution, const std::vector<double>&
   }
   (void)svdThreshold;
   (void)verbosity;
+}
+
+// Subspace linear equations (reference helper-implementation.h:553-617).  matrix: row-major
+// nX x nX; rhs: the row-major nX x nroot EqnData::rhs block.  solution[k + nX*root].
+//  * augmented_hessian == 0: H c = rhs by Householder QR (the reference's householderQr().solve);
+//  * augmented_hessian > 0: for each root the lowest eigenpair of [[H, -a r], [-a r^T, 0]] with
+//    metric diag(S, 1), c = v_head / (a v_last).  As in the reference, H is read column-major
+//    (its transpose) and the rhs of root `root` as rhs[i + nX*root] in this branch.
+inline void solve_LinearEquations(std::vector<double>& solution, std::vector<double>& eigenvalues,
+                                  const std::vector<double>& matrix, const std::vector<double>& metric,
+                                  const std::vector<double>& rhs, const size_t dimension, size_t nroot,
+                                  double augmented_hessian, double svdThreshold, int verbosity) {
+  const size_t nX = dimension;
+  solution.assign(nX * nroot, 0.0);
+  if (augmented_hessian > 0) {
+    const size_t na = nX + 1;
+    eigenvalues.resize(nroot);
+    for (size_t root = 0; root < nroot; ++root) {
+      std::vector<double> M(na * na, 0.0), Sa(na * na, 0.0);  // row-major for eigenproblem()
+      for (size_t i = 0; i < nX; ++i)
+        for (size_t j = 0; j < nX; ++j) {
+          M[i * na + j] = matrix[j * nX + i];   // Eigen::Map column-major view of the row-major H
+          Sa[i + na * j] = metric[i + nX * j];  // metric read column-major, as eigenproblem() does
+        }
+      for (size_t i = 0; i < nX; ++i) M[i * na + nX] = M[nX * na + i] = -augmented_hessian * rhs[i + nX * root];
+      Sa[nX + na * nX] = 1;
+      std::vector<double> evec, eval;
+      eigenproblem(evec, eval, M, Sa, na, false, svdThreshold, verbosity, true);
+      if (eval.empty()) throw std::runtime_error("solve_LinearEquations: empty augmented-Hessian eigenproblem");
+      size_t imax = 0;
+      for (size_t i = 0; i < eval.size(); ++i)
+        if (eval[i] < eval[imax]) imax = i;
+      eigenvalues[root] = eval[imax];
+      const double last = evec[nX + na * imax];
+      for (size_t k = 0; k < nX; ++k) solution[k + nX * root] = evec[k + na * imax] / (augmented_hessian * last);
+    }
+  } else {
+    std::vector<double> A(nX * nX), B(nX * nroot);
+    for (size_t i = 0; i < nX; ++i) {
+      for (size_t j = 0; j < nX; ++j) A[i + nX * j] = matrix[i * nX + j];
+      for (size_t r = 0; r < nroot; ++r) B[i + nX * r] = rhs[i * nroot + r];
+    }
+    householder_qr_solve(nX, A, B, nroot);
+    for (size_t r = 0; r < nroot; ++r)
+      for (size_t k = 0; k < nX; ++k) solution[k + nX * r] = B[k + nX * r];
+  }
 }
 
 }  // namespace molpro::linalg::itsolv

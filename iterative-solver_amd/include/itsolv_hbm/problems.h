@@ -100,6 +100,53 @@ void run_davidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Proble
   }
 }
 
+// Runs LinearEquationsDavidson::solve on A x = b for the given right-hand sides and fills `out`;
+// residual_norms are |A x - b| / |b| recomputed by residual_norm(x, root).
+template <class R, class Q, class P>
+void run_linear_equations(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R, P>& problem,
+                          const std::function<R()>& make_vec, std::vector<R>& rhs,
+                          const std::function<double(const R&, size_t)>& residual_norm, const itsolv_options& o,
+                          itsolv_result& out, const std::function<void(size_t, const R&)>& emit) {
+  LinearEquationsDavidson<R, Q, P> solver(handlers);
+  solver.add_equations(rhs);
+  LinearEquationsDavidsonOptions opt;
+  apply_options(o, opt);
+  opt.n_roots = int(rhs.size());
+  if (o.max_size_qspace > 0) opt.max_size_qspace = o.max_size_qspace;
+  if (o.reset_D > 0) opt.reset_D = o.reset_D;
+  if (o.reset_D_max_Q_size > 0) opt.reset_D_max_Q_size = o.reset_D_max_Q_size;
+  opt.hermiticity = o.hermitian != 0;
+  if (o.augmented_hessian > 0) opt.augmented_hessian = o.augmented_hessian;
+  solver.set_options(opt);
+  const size_t nwork = rhs.size();
+  std::vector<R> params, actions;
+  for (size_t i = 0; i < nwork; ++i) {
+    params.push_back(make_vec());
+    actions.push_back(make_vec());
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  out.converged = solver.solve(params, actions, problem, o.generate_initial_guess != 0);
+  out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const auto& st = solver.statistics();
+  out.iterations = st.iterations;
+  out.r_creations = st.r_creations;
+  out.q_creations = st.q_creations;
+  out.nroots = int(std::min<size_t>(nwork, ITSOLV_MAX_ROOTS));
+  out.n_eig_trace = 0;
+  for (int i = 0; i < out.nroots; ++i) {
+    out.eigenvalues[i] = 0;
+    out.errors[i] = i < int(solver.errors().size()) ? solver.errors()[i] : 0.0;
+  }
+  for (int r = 0; r < out.nroots; ++r) {
+    std::vector<R> x, g;
+    x.push_back(make_vec());
+    g.push_back(make_vec());
+    solver.solution(std::vector<int>{r}, x, g);
+    out.residual_norms[r] = residual_norm(x[0], size_t(r));
+    if (emit) emit(size_t(r), x[0]);
+  }
+}
+
 // Runs NonLinearEquationsDIIS::solve from x0 (set by init) and fills `out`.
 template <class R, class Q, class P>
 void run_diis(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R, P>& problem,
@@ -138,6 +185,7 @@ inline void default_options(itsolv_options* o) {
   o->max_size_qspace = 0;
   o->reset_D = 0;
   o->reset_D_max_Q_size = 0;
+  o->augmented_hessian = 0;
   o->max_p = 0;
   o->p_threshold = 0;
   o->convergence_threshold = 1e-8;

@@ -163,6 +163,12 @@ class SubspaceSolverLinEig : public SubspaceSolver {
  public:
   explicit SubspaceSolverLinEig(std::shared_ptr<Logger> log) : m_logger(std::move(log)) {}
   void solve(const subspace::SubspaceData& data, size_t nroots_max) override {
+    // reference SubspaceSolverLinEig.h:27-34: linear equations when a rhs block is present
+    const auto rhs = data.find(EqnData::rhs);
+    if (rhs != data.end() && !rhs->second.empty()) {
+      solve_linear_equations(data);
+      return;
+    }
     const auto& h = data.at(EqnData::H);
     const auto& s = data.at(EqnData::S);
     const size_t dim = h.rows();
@@ -177,6 +183,23 @@ class SubspaceSolverLinEig : public SubspaceSolver {
     m_errors.assign(nroots, std::numeric_limits<double>::max());
     if (m_logger->data_dump) m_logger->msg("eigenvectors = " + as_string(m_solutions), Logger::Info);
   }
+  // reference SubspaceSolverLinEig.h:62-85
+  void solve_linear_equations(const subspace::SubspaceData& data) {
+    const auto& h = data.at(EqnData::H);
+    const auto& s = data.at(EqnData::S);
+    const auto& rhs = data.at(EqnData::rhs);
+    const size_t dim = h.rows(), nsol = rhs.cols();
+    std::vector<double> solution;
+    m_eigenvalues.assign(nsol, 0);
+    solve_LinearEquations(solution, m_eigenvalues, h.data(), s.data(), rhs.data(), dim, nsol, m_augmented_hessian,
+                          m_svd_solver_threshold, 0);
+    m_solutions = Matrix<double>({nsol, dim});
+    for (size_t r = 0; r < nsol; ++r)
+      for (size_t k = 0; k < dim; ++k) m_solutions(r, k) = solution[k + dim * r];
+    m_errors.assign(nsol, std::numeric_limits<double>::max());
+  }
+  void set_augmented_hessian(double a) { m_augmented_hessian = a; }
+  double get_augmented_hessian() const { return m_augmented_hessian; }
   void set_hermiticity(bool h) { m_hermitian = h; }
   bool get_hermiticity() const { return m_hermitian; }
   double m_svd_solver_threshold = 1.0e-14;
@@ -184,6 +207,7 @@ class SubspaceSolverLinEig : public SubspaceSolver {
  private:
   std::shared_ptr<Logger> m_logger;
   bool m_hermitian = false;
+  double m_augmented_hessian = 0;
 };
 
 class SubspaceSolverDIIS : public SubspaceSolver {
@@ -486,21 +510,21 @@ class IterativeSolverTemplate {
 
 // ---- Davidson ----------------------------------------------------------------------------------
 
-template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>
-class LinearEigensystemDavidson : public IterativeSolverTemplate<R, Q, P> {
+// What LinearEigensystemDavidson and LinearEquationsDavidson share (reference
+// LinearEigensystemDavidson.h:63-83 and LinearEquationsDavidson.h:48-62 have the same end_iteration,
+// both over detail::propose_rspace, propose_rspace.h:553-624, and the DSpaceResetter).
+template <class R, class Q, class P>
+class DavidsonSolver : public IterativeSolverTemplate<R, Q, P> {
   using Base = IterativeSolverTemplate<R, Q, P>;
 
  public:
-  explicit LinearEigensystemDavidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers,
-                                     std::shared_ptr<Logger> logger = std::make_shared<Logger>())
+  DavidsonSolver(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, std::shared_ptr<Logger> logger)
       : Base(std::move(handlers), std::make_shared<SubspaceSolverLinEig>(logger), logger) {
-    set_hermiticity(m_hermiticity);
     this->m_normalise_solution = false;
   }
 
   bool nonlinear() const override { return false; }
 
-  // reference LinearEigensystemDavidson.h:63-83
   size_t end_iteration(const VecRef<R>& parameters, const VecRef<R>& action) override {
     if (m_resetter.do_reset(size_t(this->m_stats->iterations), this->m_xspace->dimensions())) {
       m_resetting = true;
@@ -517,13 +541,6 @@ class LinearEigensystemDavidson : public IterativeSolverTemplate<R, Q, P> {
   }
   using Base::end_iteration;
 
-  std::vector<double> eigenvalues() const { return this->m_subspace_solver->eigenvalues(); }
-  std::vector<double> working_set_eigenvalues() const override {
-    std::vector<double> e;
-    for (auto i : this->working_set()) e.push_back(this->m_subspace_solver->eigenvalues().at(i));
-    return e;
-  }
-
   void set_reset_D(size_t n) { m_resetter.set_nreset(n); }
   int get_reset_D() const { return m_resetter.get_nreset(); }
   void set_reset_D_maxQ_size(size_t n) { m_resetter.set_max_Qsize(n); }
@@ -536,38 +553,24 @@ class LinearEigensystemDavidson : public IterativeSolverTemplate<R, Q, P> {
   void set_hermiticity(bool h) {
     m_hermiticity = h;
     this->m_xspace->set_hermiticity(h);
-    std::static_pointer_cast<SubspaceSolverLinEig>(this->m_subspace_solver)->set_hermiticity(h);
+    subspace_solver().set_hermiticity(h);
   }
   bool get_hermiticity() const { return m_hermiticity; }
-
-  void set_options(const Options& o) override {
-    Base::set_options(o);
-    if (auto* d = dynamic_cast<const LinearEigensystemDavidsonOptions*>(&o)) {
-      if (d->reset_D) set_reset_D(size_t(*d->reset_D));
-      if (d->reset_D_max_Q_size) set_reset_D_maxQ_size(size_t(*d->reset_D_max_Q_size));
-      if (d->max_size_qspace) set_max_size_qspace(*d->max_size_qspace);
-      if (d->norm_thresh) norm_thresh = *d->norm_thresh;
-      if (d->svd_thresh) svd_thresh = *d->svd_thresh;
-      if (d->hermiticity) set_hermiticity(*d->hermiticity);
-    }
-  }
 
   double norm_thresh = 1e-10;  // propose_rspace_norm_thresh
   double svd_thresh = 1e-12;   // propose_rspace_svd_thresh
 
  protected:
-  void set_value_errors() override {
-    const auto cur = this->m_subspace_solver->eigenvalues();
-    this->m_value_errors.assign(cur.size(), std::numeric_limits<double>::max());
-    for (size_t i = 0; i < std::min(m_last_values.size(), cur.size()); ++i)
-      this->m_value_errors[i] = std::abs(cur[i] - m_last_values[i]);
-    if (!m_resetting) m_last_values = cur;
-  }
+  SubspaceSolverLinEig& subspace_solver() { return static_cast<SubspaceSolverLinEig&>(*this->m_subspace_solver); }
 
-  // r_i -= lambda_i x_i (reference LinearEigensystemDavidson.h:186-192)
-  void construct_residual(const std::vector<int>& roots, const CVecRef<R>& params, const VecRef<R>& actions) override {
-    const auto& ev = eigenvalues();
-    for (size_t i = 0; i < roots.size(); ++i) this->m_handlers->rr().axpy(-ev.at(roots[i]), params.at(i), actions.at(i));
+  template <class O>
+  void set_davidson_options(const O& d) {
+    if (d.reset_D) set_reset_D(size_t(*d.reset_D));
+    if (d.reset_D_max_Q_size) set_reset_D_maxQ_size(size_t(*d.reset_D_max_Q_size));
+    if (d.max_size_qspace) set_max_size_qspace(*d.max_size_qspace);
+    if (d.norm_thresh) norm_thresh = *d.norm_thresh;
+    if (d.svd_thresh) svd_thresh = *d.svd_thresh;
+    if (d.hermiticity) set_hermiticity(*d.hermiticity);
   }
 
   // reference propose_rspace.h:553-624
@@ -604,8 +607,94 @@ class LinearEigensystemDavidson : public IterativeSolverTemplate<R, Q, P> {
   int m_max_size_qspace = std::numeric_limits<int>::max();
   detail::DSpaceResetter<Q> m_resetter;
   bool m_hermiticity = false;
-  std::vector<double> m_last_values;
   bool m_resetting = false;
+};
+
+template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>
+class LinearEigensystemDavidson : public DavidsonSolver<R, Q, P> {
+  using Base = DavidsonSolver<R, Q, P>;
+
+ public:
+  explicit LinearEigensystemDavidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers,
+                                     std::shared_ptr<Logger> logger = std::make_shared<Logger>())
+      : Base(std::move(handlers), std::move(logger)) {
+    this->set_hermiticity(this->m_hermiticity);
+  }
+
+  std::vector<double> eigenvalues() const { return this->m_subspace_solver->eigenvalues(); }
+  std::vector<double> working_set_eigenvalues() const override {
+    std::vector<double> e;
+    for (auto i : this->working_set()) e.push_back(this->m_subspace_solver->eigenvalues().at(i));
+    return e;
+  }
+
+  void set_options(const Options& o) override {
+    Base::set_options(o);
+    if (auto* d = dynamic_cast<const LinearEigensystemDavidsonOptions*>(&o)) this->set_davidson_options(*d);
+  }
+
+ protected:
+  void set_value_errors() override {
+    const auto cur = this->m_subspace_solver->eigenvalues();
+    this->m_value_errors.assign(cur.size(), std::numeric_limits<double>::max());
+    for (size_t i = 0; i < std::min(m_last_values.size(), cur.size()); ++i)
+      this->m_value_errors[i] = std::abs(cur[i] - m_last_values[i]);
+    if (!this->m_resetting) m_last_values = cur;
+  }
+
+  // r_i -= lambda_i x_i (reference LinearEigensystemDavidson.h:186-192)
+  void construct_residual(const std::vector<int>& roots, const CVecRef<R>& params, const VecRef<R>& actions) override {
+    const auto& ev = eigenvalues();
+    for (size_t i = 0; i < roots.size(); ++i) this->m_handlers->rr().axpy(-ev.at(roots[i]), params.at(i), actions.at(i));
+  }
+
+  std::vector<double> m_last_values;
+};
+
+// A x = b for several right-hand sides in the same Krylov/P/D subspace machinery
+// (reference LinearEquationsDavidson.h:27-191).  Residuals are scaled by 1/|b| (:175-186).
+template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>
+class LinearEquationsDavidson : public DavidsonSolver<R, Q, P> {
+  using Base = DavidsonSolver<R, Q, P>;
+
+ public:
+  explicit LinearEquationsDavidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers,
+                                   std::shared_ptr<Logger> logger = std::make_shared<Logger>())
+      : Base(std::move(handlers), std::move(logger)) {
+    this->set_hermiticity(true);  // reference LinearEquationsDavidson.h:189 (m_hermiticity = true)
+  }
+
+  // reference :73-78
+  void add_equations(const CVecRef<R>& rhs) {
+    this->m_xspace->add_rhs_equations(rhs);
+    this->set_n_roots(this->m_xspace->dimensions().nRHS);
+  }
+  void add_equations(const R& rhs) { add_equations(cwrap_arg(rhs)); }
+  void add_equations(const std::vector<R>& rhs) { add_equations(cwrap(rhs)); }
+  CVecRef<Q> rhs() const { return this->m_xspace->rhs(); }
+
+  //! Augmented-Hessian parameter of the subspace solve; 0 = plain linear equations (reference :119-127)
+  void set_augmented_hessian(double a) { this->subspace_solver().set_augmented_hessian(a); }
+  double get_augmented_hessian() { return this->subspace_solver().get_augmented_hessian(); }
+
+  void set_options(const Options& o) override {
+    Base::set_options(o);
+    if (auto* d = dynamic_cast<const LinearEquationsDavidsonOptions*>(&o)) {
+      this->set_davidson_options(*d);
+      if (d->augmented_hessian) set_augmented_hessian(*d->augmented_hessian);
+    }
+  }
+
+ protected:
+  // r_i = (A x_i - b_i) / |b_i| (reference :175-186)
+  void construct_residual(const std::vector<int>& roots, const CVecRef<R>& params, const VecRef<R>& actions) override {
+    const auto& norm = this->m_xspace->rhs_norm();
+    for (size_t i = 0; i < roots.size(); ++i) {
+      const auto ii = size_t(roots[i]);
+      this->m_handlers->rq().axpy(-1, rhs().at(ii), actions.at(i));
+      if (norm.at(ii) != 0) this->m_handlers->rr().scal(1 / norm[ii], actions.at(i));
+    }
+  }
 };
 
 // ---- DIIS --------------------------------------------------------------------------------------

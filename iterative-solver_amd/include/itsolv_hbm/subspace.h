@@ -302,6 +302,7 @@ class XSpace {
     update_rhs_with_pspace();
   }
   CVecRef<Q> rhs() const { return cwrap(m_rhs); }
+  const std::vector<double>& rhs_norm() const { return m_rhs_norm; }
 
   void eraseq(size_t i) {
     qspace.erase(i);

@@ -16,7 +16,7 @@ MAX_ROOTS = 64
 
 EXPORTS = [
     "itsolv_last_error", "itsolv_default_options", "itsolv_davidson_synthetic", "itsolv_davidson_dense",
-    "itsolv_diis_synthetic", "itsolv_diis_dense",
+    "itsolv_diis_synthetic", "itsolv_diis_dense", "itsolv_linear_equations_dense",
 ]
 
 
@@ -34,6 +34,7 @@ class Options(C.Structure):
         ("hermitian", C.c_int),
         ("generate_initial_guess", C.c_int),
         ("verbosity", C.c_int),
+        ("augmented_hessian", C.c_double),
     ]
 
 
@@ -69,7 +70,8 @@ class Result(C.Structure):
 
 def make_options(**kw) -> Options:
     o = Options(nroots=1, nwork=0, max_iter=100, max_size_qspace=0, reset_D=0, reset_D_max_Q_size=0, max_p=0,
-                p_threshold=0.0, convergence_threshold=1e-8, hermitian=1, generate_initial_guess=1, verbosity=0)
+                p_threshold=0.0, convergence_threshold=1e-8, hermitian=1, generate_initial_guess=1, verbosity=0,
+                augmented_hessian=0.0)
     for k, v in kw.items():
         if not hasattr(o, k):
             raise KeyError(k)
@@ -96,6 +98,7 @@ def load_library():
             "itsolv_davidson_dense": (I, [P, PD, Z, PO, PR, PD]),
             "itsolv_diis_synthetic": (I, [P, Z, D, I, U, PO, PR, PD]),
             "itsolv_diis_dense": (I, [P, PD, Z, PO, PR, PD]),
+            "itsolv_linear_equations_dense": (I, [P, PD, Z, PD, I, PO, PR, PD]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -150,4 +153,17 @@ def diis_dense(ctx: sh.Context, h: np.ndarray, **opts):
     r, x = _call(load_library().itsolv_diis_dense, (ctx.handle, h.ctypes.data_as(C.POINTER(C.c_double)), n,
                                                     C.byref(o)), n)
     r["x"] = x[:n]
+    return r
+
+
+def linear_equations_dense(ctx: sh.Context, a: np.ndarray, rhs: np.ndarray, **opts):
+    """LinearEquationsDavidson on A x_r = b_r (rows of rhs); returns the result dict with "x"."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(np.atleast_2d(rhs), dtype=np.float64)
+    n, nrhs = a.shape[0], b.shape[0]
+    o = make_options(**opts)
+    r, x = _call(load_library().itsolv_linear_equations_dense,
+                 (ctx.handle, a.ctypes.data_as(C.POINTER(C.c_double)), n, b.ctypes.data_as(C.POINTER(C.c_double)),
+                  nrhs, C.byref(o)), n * nrhs)
+    r["x"] = x[:n * nrhs].reshape(nrhs, n)
     return r

@@ -333,6 +333,32 @@ int oracle_diis_synthetic(size_t n, double rho, int rank, unsigned long long see
   return diis(p, n, opt, out, x_out);
 }
 
+int oracle_linear_equations_dense(const double* h, size_t n, const double* rhs, int nrhs, const itsolv_options* opt,
+                                  itsolv_result* out, double* x_out) {
+  DenseCpu p(h, n);
+  return guarded([&] {
+    std::memset(out, 0, sizeof(*out));
+    std::vector<V> b;
+    for (int r = 0; r < nrhs; ++r) b.emplace_back(rhs + size_t(r) * n, rhs + size_t(r + 1) * n);
+    pr::run_linear_equations<V, V, SP>(
+        cpu_handlers(), p, [&] { return V(n, 0.0); }, b,
+        [&](const V& x, size_t r) {
+          V ax(n);
+          p.apply(x, ax);
+          double rr = 0, bb = 0;
+          for (size_t i = 0; i < n; ++i) {
+            rr += (ax[i] - b[r][i]) * (ax[i] - b[r][i]);
+            bb += b[r][i] * b[r][i];
+          }
+          return std::sqrt(rr / (bb > 0 ? bb : 1.0));
+        },
+        opts_or_default(opt), *out,
+        [&](size_t r, const V& x) {
+          if (x_out) std::memcpy(x_out + r * n, x.data(), n * sizeof(double));
+        });
+  });
+}
+
 int oracle_diis_dense(const double* h, size_t n, const itsolv_options* opt, itsolv_result* out, double* x_out) {
   DenseCpu p(h, n);
   return diis(p, n, opt, out, x_out);

@@ -207,6 +207,7 @@ def itsolv_lib():
             "oracle_davidson_dense": [PDd, Z, PO, PR, PDd],
             "oracle_diis_synthetic": [Z, D, I, U, PO, PR, PDd],
             "oracle_diis_dense": [PDd, Z, PO, PR, PDd],
+            "oracle_linear_equations_dense": [PDd, Z, PDd, I, PO, PR, PDd],
         }.items():
             f = getattr(L, name)
             f.restype = I
@@ -263,6 +264,19 @@ def diis_dense(h, **opts):
     o = make_options(**opts)
     r, x = _solve(itsolv_lib().oracle_diis_dense, (_d(h), n, C.byref(o)), n)
     r["x"] = x[:n]
+    return r
+
+
+def linear_equations_dense(a, rhs, **opts):
+    """The reference CPU path of LinearEquationsDavidson on A x_r = b_r (rows of rhs)."""
+    from itsolv_hbm import make_options
+
+    a = _f64(a)
+    b = np.ascontiguousarray(np.atleast_2d(rhs), dtype=np.float64)
+    n, nrhs = a.shape[0], b.shape[0]
+    o = make_options(**opts)
+    r, x = _solve(itsolv_lib().oracle_linear_equations_dense, (_d(a), n, _d(b), nrhs, C.byref(o)), n * nrhs)
+    r["x"] = x[:n * nrhs].reshape(nrhs, n)
     return r
 
 

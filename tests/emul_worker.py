@@ -54,6 +54,11 @@ def case_api():
     x = x * problem.eigenvectors[0, 0] / x[0]
     assert abs(problem.residual(x, g) - problem.eigenvalues[0]) < 1e-7
     s.finalize()
+    # reference test_rayleigh_quotient.py:152-215: LinearEquations through the C API
+    import test_python_api_gpu as tg
+
+    tg.test_linear_equations()
+    tg.test_simple_linear_equations()
     # C-API loop vs the restated solve() of the CPU reference path: same iterations
     for name, split, nroot in (("he", 0.0, 1), ("hf", 1e-8, 3), ("bh", 1e-8, 3)):
         h = hamiltonian(name, split)

@@ -60,10 +60,49 @@ def test_nonlinear_equations():
     solver.finalize()
 
 
-@pytest.mark.parametrize("cls,args", [("LinearEquations", (np.ones((1, 4)),)), ("Optimize", (4,))])
-def test_unavailable_solvers_raise(cls, args):
+def test_unavailable_solvers_raise():
     with pytest.raises(RuntimeError, match="not available"):
-        getattr(iterative_solver, cls)(*args)
+        iterative_solver.Optimize(4)
+
+
+def test_linear_equations():
+    # reference test_rayleigh_quotient.py:152-181
+    problem = RayleighQuotient(33, 0.1)
+    nroot = 2
+    parameters = np.zeros([nroot, problem.size])
+    residual = np.zeros([nroot, problem.size])
+    rhs = np.array([problem.eigenvalues[r] * problem.eigenvectors[:, r] for r in range(nroot)])
+    solver = iterative_solver.LinearEquations(rhs=rhs, thresh=1e-9)
+    solver.solve(parameters, residual, problem, generate_initial_guess=True)
+    solver.solution(list(range(nroot)), parameters, residual)
+    assert solver.errors.size == nroot
+    assert np.all(np.abs(solver.errors) < 1e-7)
+    for root in range(nroot):
+        v = problem.eigenvectors[0, root] * parameters[root] / parameters[root, 0]
+        np.testing.assert_allclose(v, problem.eigenvectors[:, root], atol=1e-7)
+        np.testing.assert_allclose(residual[root], 0.0, atol=1e-7)
+    solver.finalize()
+
+
+def test_simple_linear_equations():
+    # reference test_rayleigh_quotient.py:183-215: M_ij = i + j + 1 (+1 diagonal), x_r = r + 1
+    class Simple(RayleighQuotient):
+        @property
+        def matrix(self):
+            return np.add.outer(np.arange(self.size), np.arange(self.size)) + 1.0 + np.eye(self.size)
+
+    problem = Simple(8)
+    nroot = 2
+    parameters = np.zeros([nroot, 8])
+    residual = np.zeros([nroot, 8])
+    rhs = np.array([[(r + 1) * (8 * 9 / 2 + i * 8 + 1) for i in range(8)] for r in range(nroot)])
+    solver = iterative_solver.LinearEquations(rhs=rhs)
+    solver.solve(parameters, residual, problem, generate_initial_guess=True)
+    solver.solution(list(range(nroot)), parameters, residual)
+    assert np.all(np.abs(solver.errors) < 1e-7)
+    np.testing.assert_allclose(parameters, np.outer([1.0, 2.0], np.ones(8)), atol=1e-7)
+    np.testing.assert_allclose(residual, 0.0, atol=1e-7)
+    solver.finalize()
 
 
 class Dense(iterative_solver.Problem):

@@ -152,3 +152,15 @@ def test_nonhermitian_davidson_gpu_vs_cpu(ctx, param, nh, nroot):
     gpu, cpu = ih.davidson_dense(ctx, h, **kw), oracle.davidson_dense(h, **kw)
     assert gpu["converged"] and cpu["converged"] and gpu["iterations"] == cpu["iterations"]
     np.testing.assert_allclose(gpu["eigenvalues"], cpu["eigenvalues"], rtol=0, atol=1e-10)
+
+
+@pytest.mark.parametrize("n,nroot", [(3, 1), (12, 3), (33, 2), (33, 13)])
+def test_linear_equations_gpu_vs_cpu(ctx, n, nroot):
+    from test_solver_oracle import simple_system
+
+    a, rhs = simple_system(n, nroot)
+    kw = dict(nroots=nroot, convergence_threshold=1e-10)
+    gpu, cpu = ih.linear_equations_dense(ctx, a, rhs, **kw), oracle.linear_equations_dense(a, rhs, **kw)
+    assert gpu["converged"] and cpu["converged"] and gpu["iterations"] == cpu["iterations"]
+    np.testing.assert_allclose(gpu["x"], np.outer(np.arange(1, nroot + 1), np.ones(n)), atol=1e-5, rtol=0)
+    np.testing.assert_allclose(gpu["x"], cpu["x"], atol=1e-8, rtol=0)

@@ -122,3 +122,38 @@ def test_nonhermitian_eigen(param, nh, nroot):
     assert r["converged"]
     exact = np.sort(np.linalg.eigvals(h).real)[:nroot]
     assert np.max(np.abs(r["eigenvalues"] - exact)) < 1e-10
+
+
+def simple_system(n, nroot):
+    # reference test_LinearEquations.cpp:17-38: A_ij = i + j + 1 (+1 on the diagonal), x_r = r + 1
+    a = np.add.outer(np.arange(n), np.arange(n)) + 1.0 + np.eye(n)
+    rhs = np.array([[(r + 1) * (n * (n + 1) / 2 + j * n + 1) for j in range(n)] for r in range(nroot)])
+    return a, rhs
+
+
+@pytest.mark.parametrize("n", [3, 6, 12, 21, 33])
+@pytest.mark.parametrize("nroot", [1, 2, 3, 13])
+def test_linear_equations_symmetric_system(n, nroot):
+    # reference test_LinearEquations.cpp:59-99 (threshold 1e-10, solution to 1e-5)
+    if nroot > n:
+        pytest.skip("more roots than the dimension")
+    a, rhs = simple_system(n, nroot)
+    r = oracle.linear_equations_dense(a, rhs, nroots=nroot, convergence_threshold=1e-10)
+    assert r["converged"]
+    np.testing.assert_allclose(r["x"], np.outer(np.arange(1, nroot + 1), np.ones(n)), atol=1e-5, rtol=0)
+    assert np.all(r["residual_norms"][:nroot] <= 1e-9)
+
+
+@pytest.mark.parametrize("aug", [0.5, 1.0])
+def test_linear_equations_augmented_hessian_subspace_solve(aug):
+    # Augmented Hessian (reference helper-implementation.h:561-594): the subspace solution is
+    # x = (A - e)^-1 b with e the lowest eigenvalue of [[A, -a b], [-a b^T, 0]].  Once the subspace
+    # spans the whole space (n = 4) that is the full-space value; the residual A x - b then stays
+    # e x, so the run ends unconverged when no new direction remains.
+    n = 4
+    a = np.full((n, n), 0.1) + np.diag(np.arange(1.0, n + 1))
+    rhs = np.sin(np.arange(n) + 1.0)[None, :]
+    r = oracle.linear_equations_dense(a, rhs, nroots=1, convergence_threshold=1e-10, augmented_hessian=aug, max_iter=20)
+    m = np.block([[a, -aug * rhs.T], [-aug * rhs, np.zeros((1, 1))]])
+    e = np.linalg.eigvalsh(m)[0]
+    np.testing.assert_allclose(r["x"][0], np.linalg.solve(a - e * np.eye(n), rhs[0]), atol=1e-12)
