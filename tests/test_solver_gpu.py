@@ -163,4 +163,5 @@ def test_linear_equations_gpu_vs_cpu(ctx, n, nroot):
     gpu, cpu = ih.linear_equations_dense(ctx, a, rhs, **kw), oracle.linear_equations_dense(a, rhs, **kw)
     assert gpu["converged"] and cpu["converged"] and gpu["iterations"] == cpu["iterations"]
     np.testing.assert_allclose(gpu["x"], np.outer(np.arange(1, nroot + 1), np.ones(n)), atol=1e-5, rtol=0)
-    np.testing.assert_allclose(gpu["x"], cpu["x"], atol=1e-8, rtol=0)
+    # both stop at |A x - b| <= 1e-10 |b| (|b| ~ 1e4 here), so x agrees to ~|b| * 1e-10 / sigma_min
+    np.testing.assert_allclose(gpu["x"], cpu["x"], atol=2e-6, rtol=0)
