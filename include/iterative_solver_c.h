@@ -17,9 +17,7 @@
  *    context set by IterativeSolverHbmSetContext (an ssp_ctx with an RCCL or host communicator
  *    attached), or a single-rank context on device 0 is created.
  *  - Supported algorithms: LinearEigensystem and LinearEquations "Davidson" (or ""),
- *    NonLinearEquations "DIIS" (or "").  IterativeSolverOptimizeInitialize throws
- *    std::logic_error (Optimize solvers are not on this back end), as the reference throws for
- *    unknown algorithms.
+ *    NonLinearEquations "DIIS" (or ""), Optimize "BFGS" (or "") and "SD"; minimize = 0 throws.
  *  - IterativeSolverAddVector on a non-linear solver (DIIS) passes the vector through the solver's
  *    own add_vector (residual norm, convergence flag, least-important-vector deletion), as the
  *    reference's solve() driver does; the reference's C layer reaches the generic vector-list

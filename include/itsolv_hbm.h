@@ -75,6 +75,11 @@ int itsolv_diis_synthetic(ssp_ctx* ctx, size_t n, double rho, int rank, unsigned
  * x_out (nrhs x n, host) may be NULL. */
 int itsolv_linear_equations_dense(ssp_ctx* ctx, const double* a, size_t n, const double* rhs, int nrhs,
                                   const itsolv_options* opt, itsolv_result* out, double* x_out);
+/* OptimizeBFGS (algorithm 0) or OptimizeSD (1) minimising the Rayleigh quotient x.Hx / x.x of a
+ * dense row-major H (HBM, single rank) from x = e_0; eigenvalues[0] = final function value, x_out
+ * (n, host) may be NULL. */
+int itsolv_optimize_dense(ssp_ctx* ctx, const double* h, size_t n, int algorithm, const itsolv_options* opt,
+                          itsolv_result* out, double* x_out);
 int itsolv_diis_dense(ssp_ctx* ctx, const double* h, size_t n, const itsolv_options* opt, itsolv_result* out,
                       double* x_out);
 

@@ -30,6 +30,8 @@ using Solver = it::IterativeSolverTemplate<Vec, Vec, SparseP>;
 using Davidson = it::LinearEigensystemDavidson<Vec, Vec, SparseP>;
 using DIIS = it::NonLinearEquationsDIIS<Vec, Vec, SparseP>;
 using LinEq = it::LinearEquationsDavidson<Vec, Vec, SparseP>;
+using BFGS = it::OptimizeBFGS<Vec, Vec, SparseP>;
+using SD = it::OptimizeSD<Vec, Vec, SparseP>;
 typedef void (*Apply_on_p_fort)(const double*, double*, const size_t, const size_t*);
 
 thread_local std::string g_error;
@@ -233,9 +235,37 @@ void IterativeSolverNonLinearEquationsInitialize(size_t n, size_t* range_begin, 
   });
 }
 
-void IterativeSolverOptimizeInitialize(size_t, size_t*, size_t*, double, double, int, int, const char*, int64_t,
-                                       const char*, const char*) {
-  guarded([] { throw std::logic_error("IterativeSolverOptimizeInitialize: Optimize solvers are not available on the HBM back end"); });
+void IterativeSolverOptimizeInitialize(size_t n, size_t* range_begin, size_t* range_end, double thresh,
+                                       double thresh_value, int verbosity, int minimize, const char* fname,
+                                       int64_t fcomm, const char* algorithm, const char* options) {
+  guarded([&] {
+    (void)fname;
+    (void)fcomm;
+    if (!minimize) throw std::runtime_error("IterativeSolverOptimizeInitialize: maximisation is not implemented");
+    const std::string alg = algorithm && *algorithm ? algorithm : "BFGS";
+    Instance in;
+    in.dev = make_device();
+    std::unique_ptr<Solver> solver;
+    if (alg == "BFGS") {
+      auto b = std::make_unique<BFGS>(molpro::linalg::hbm::make_handlers());
+      if (options && *options) b->set_options(it::OptimizeBFGSOptions(it::parse_options(options)));
+      solver = std::move(b);
+    } else if (alg == "SD") {
+      solver = std::make_unique<SD>(molpro::linalg::hbm::make_handlers());
+      if (options && *options) solver->set_options(it::Options(it::parse_options(options)));
+    } else {
+      throw std::runtime_error("IterativeSolverOptimizeInitialize: unknown algorithm " + alg + " (BFGS, SD)");
+    }
+    // reference IterativeSolverCMPI.cpp:245-264
+    solver->set_n_roots(1);
+    solver->set_convergence_threshold(thresh);
+    solver->set_convergence_threshold_value(thresh_value);
+    solver->set_verbosity(verbosity_of(verbosity));
+    in.solver = std::move(solver);
+    in.has_values = true;
+    setup(in, n, range_begin, range_end);
+    instances.push(std::move(in));
+  });
 }
 
 void IterativeSolverFinalize(void) {
@@ -287,9 +317,21 @@ void IterativeSolverSolution(int nroot, int* roots, double* parameters, double* 
   });
 }
 
-size_t IterativeSolverAddValue(double, double*, double*, int) {
-  return guarded([]() -> size_t {
-    throw std::logic_error("IterativeSolverAddValue: Optimize solvers are not available on the HBM back end");
+size_t IterativeSolverAddValue(double value, double* parameters, double* action, int sync) {
+  return guarded([&]() -> size_t {
+    auto& in = top();
+    ensure_r(in, 1);
+    upload(in, in.rp, 1, parameters);
+    upload(in, in.ra, 1, action);
+    // reference IterativeSolverCMPI.cpp:270-298: working set of one, or none when line-searching
+    const int r = in.solver->add_vector(in.rp[0], in.ra[0], value);
+    download(in, in.rp, 1, parameters);
+    download(in, in.ra, 1, action);
+    if (sync) {
+      synchronize(in, 1, parameters);
+      synchronize(in, 1, action);
+    }
+    return r > 0 ? 1 : 0;
   });
 }
 
@@ -424,7 +466,9 @@ void IterativeSolverDiagonals(double* diagonals) {
 
 // reference IterativeSolverTemplate::value (IterativeSolverTemplate.h:312-315): NaN unless the
 // subspace carries a value block (Optimize only).
-double IterativeSolverValue(void) { return std::nan("molpro::linalg::itsolv::IterativeSolver::value"); }
+double IterativeSolverValue(void) {
+  return guarded([] { return top().solver->value(); });
+}
 
 int IterativeSolverVerbosity(void) {
   return guarded([] {

@@ -173,6 +173,23 @@ class DenseProblem : public Problem<Vec, SparseP> {
   double* m_dh = nullptr;
 };
 
+// f(x) = x.Hx / x.x with gradient 2 (Hx - f x) / x.x: the objective of the reference's Python
+// Rayleigh-quotient tests (python/test/test_rayleigh_quotient.py:8-33), H dense in HBM.
+class RayleighProblem : public DenseProblem {
+ public:
+  using DenseProblem::DenseProblem;
+  double residual(const Vec& x, Vec& g) const override {
+    action(CVecRef<Vec>{std::cref(x)}, VecRef<Vec>{std::ref(g)});
+    double xx = 0, xg = 0;
+    check(ssp_dot(x.ctx(), x.data(), x.data(), x.local_size(), &xx), "ssp_dot");
+    check(ssp_dot(x.ctx(), x.data(), g.data(), x.local_size(), &xg), "ssp_dot");
+    const double f = xg / xx;
+    check(ssp_axpy(x.ctx(), -f, x.data(), g.data(), g.local_size()), "ssp_axpy");
+    check(ssp_scal(x.ctx(), 2 / xx, g.data(), g.local_size()), "ssp_scal");
+    return f;
+  }
+};
+
 template <class P>
 double residual_norm(const P& problem, const std::shared_ptr<Device>& dev, const Vec& x, double e) {
   Vec ax(dev, x.size());
@@ -297,6 +314,29 @@ int itsolv_linear_equations_dense(ssp_ctx* ctx, const double* a, size_t n, const
           if (!x_out) return;
           auto v = x.local_values();
           std::memcpy(x_out + r * n, v.data(), v.size() * sizeof(double));
+        });
+  });
+}
+
+int itsolv_optimize_dense(ssp_ctx* ctx, const double* h, size_t n, int algorithm, const itsolv_options* opt,
+                          itsolv_result* out, double* x_out) {
+  return guarded([&] {
+    auto dev = borrow(ctx);
+    const auto o = opts_or_default(opt);
+    RayleighProblem problem(dev, h, n);
+    std::memset(out, 0, sizeof(*out));
+    pr::run_optimize<Vec, Vec, SparseP>(
+        molpro::linalg::hbm::make_handlers(), problem, [&] { return zero_vec(dev, n); },
+        [&](Vec& x) {
+          const size_t i0 = 0;
+          const double one = 1.0;
+          check(ssp_sparse_copy(x.ctx(), x.data(), x.local_size(), x.offset(), &i0, &one, 1), "ssp_sparse_copy");
+        },
+        algorithm, o, *out,
+        [&](const Vec& x) {
+          if (!x_out) return;
+          auto v = x.local_values();
+          std::memcpy(x_out, v.data(), v.size() * sizeof(double));
         });
   });
 }

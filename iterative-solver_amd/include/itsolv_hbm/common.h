@@ -155,6 +155,28 @@ struct LinearEquationsDavidsonOptions : LinearEigensystemDavidsonOptions {
   std::optional<double> augmented_hessian;
 };
 
+struct OptimizeBFGSOptions : Options {
+  OptimizeBFGSOptions() = default;
+  explicit OptimizeBFGSOptions(const options_map& opt) : Options(opt) {
+    auto flag = [](std::string v) {
+      std::transform(v.begin(), v.end(), v.begin(), [](unsigned char c) { return std::tolower(c); });
+      return v == "true" || v == "1" || v == "yes";
+    };
+    if (opt.count("MAX_SIZE_QSPACE")) max_size_qspace = std::stoi(opt.at("MAX_SIZE_QSPACE"));
+    if (opt.count("STRONG_WOLFE")) strong_Wolfe = flag(opt.at("STRONG_WOLFE"));
+    if (opt.count("WOLFE_1")) Wolfe_1 = std::stod(opt.at("WOLFE_1"));
+    if (opt.count("WOLFE_2")) Wolfe_2 = std::stod(opt.at("WOLFE_2"));
+    if (opt.count("LINESEARCH_TOLERANCE")) linesearch_tolerance = std::stod(opt.at("LINESEARCH_TOLERANCE"));
+    if (opt.count("LINESEARCH_GROW_FACTOR")) linesearch_grow_factor = std::stod(opt.at("LINESEARCH_GROW_FACTOR"));
+  }
+  std::optional<int> max_size_qspace;
+  std::optional<bool> strong_Wolfe;
+  std::optional<double> Wolfe_1;
+  std::optional<double> Wolfe_2;
+  std::optional<double> linesearch_tolerance;
+  std::optional<double> linesearch_grow_factor;
+};
+
 struct NonLinearEquationsDIISOptions : Options {
   NonLinearEquationsDIISOptions() = default;
   explicit NonLinearEquationsDIISOptions(const options_map& opt) : Options(opt) {

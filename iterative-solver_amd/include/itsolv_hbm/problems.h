@@ -147,6 +147,48 @@ void run_linear_equations(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, cons
   }
 }
 
+// Runs OptimizeBFGS (algorithm 0) or OptimizeSD (1) from x0 (set by init); eigenvalues[0] is
+// the final function value (reference OptimizeBFGS.h, OptimizeSD.h).
+template <class R, class Q, class P>
+void run_optimize(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R, P>& problem,
+                  const std::function<R()>& make_vec, const std::function<void(R&)>& init, int algorithm,
+                  const itsolv_options& o, itsolv_result& out, const std::function<void(const R&)>& emit) {
+  std::unique_ptr<IterativeSolverTemplate<R, Q, P>> solver;
+  if (algorithm == 0) {
+    auto b = std::make_unique<OptimizeBFGS<R, Q, P>>(handlers);
+    OptimizeBFGSOptions opt;
+    apply_options(o, opt);
+    opt.n_roots = 1;
+    if (o.max_size_qspace > 0) opt.max_size_qspace = o.max_size_qspace;
+    b->set_options(opt);
+    solver = std::move(b);
+  } else {
+    solver = std::make_unique<OptimizeSD<R, Q, P>>(handlers);
+    Options opt;
+    apply_options(o, opt);
+    opt.n_roots = 1;
+    solver->set_options(opt);
+  }
+  R x = make_vec(), g = make_vec();
+  init(x);
+  const auto t0 = std::chrono::steady_clock::now();
+  out.converged = solver->solve(x, g, problem);
+  out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const auto& st = solver->statistics();
+  out.iterations = st.iterations;
+  out.r_creations = st.r_creations;
+  out.q_creations = st.q_creations;
+  out.nroots = 1;
+  out.errors[0] = solver->errors().empty() ? 0.0 : solver->errors().front();
+  out.eigenvalues[0] = solver->value();
+  out.n_eig_trace = 0;
+  R xs = make_vec(), gs = make_vec();
+  solver->solution(xs, gs);
+  problem.residual(xs, gs);
+  out.residual_norms[0] = std::sqrt(std::abs(handlers->rr().dot(gs, gs)));
+  if (emit) emit(xs);
+}
+
 // Runs NonLinearEquationsDIIS::solve from x0 (set by init) and fills `out`.
 template <class R, class Q, class P>
 void run_diis(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R, P>& problem,

@@ -25,6 +25,7 @@
 #include <stdexcept>
 #include <vector>
 
+#include "interpolate.h"
 #include "rspace.h"
 
 namespace molpro::linalg::itsolv {
@@ -330,6 +331,12 @@ class IterativeSolverTemplate {
   const std::vector<double>& errors() const { return m_errors; }
   const Statistics& statistics() const { return *m_stats; }
   const subspace::Dimensions& dimensions() const { return m_xspace->dimensions(); }
+  //! Latest function value of an Optimize solver, NaN otherwise (reference IterativeSolverTemplate.h:312-315)
+  double value() const {
+    const auto it = m_xspace->data.find(EqnData::value);
+    return it != m_xspace->data.end() && !it->second.empty() ? it->second(0, 0)
+                                                               : std::nan("molpro::linalg::itsolv::IterativeSolver::value");
+  }
   void set_convergence_threshold(double t) { m_convergence_threshold = t; }
   double convergence_threshold() const { return m_convergence_threshold; }
   void set_convergence_threshold_value(double t) { m_convergence_threshold_value = t; }
@@ -787,6 +794,219 @@ class NonLinearEquationsDIIS : public IterativeSolverTemplate<R, Q, P> {
   double m_norm_thresh = 1e-10;
   double m_svd_thresh = 1e-12;
   int m_max_size_qspace = std::numeric_limits<int>::max();
+};
+
+// ---- Optimize ------------------------------------------------------------------------------------
+
+// Subspace "solution" of the optimisers: the latest point (reference SubspaceSolverOptBFGS.h:27-46,
+// SubspaceSolverOptSD.h); the step itself is formed in end_iteration.
+class SubspaceSolverOptLatest : public SubspaceSolver {
+ public:
+  void solve(const subspace::SubspaceData& data, size_t) override {
+    const size_t dim = data.at(EqnData::H).rows();
+    m_solutions = Matrix<double>({1, dim});
+    m_solutions.fill(0);
+    if (dim) m_solutions(0, 0) = 1;
+    m_errors.assign(1, dim ? data.at(EqnData::H)(0, 0) : 0.0);
+  }
+  const std::vector<double>& eigenvalues() const override {
+    throw std::logic_error("eigenvalues() not available in non-linear method");
+  }
+};
+
+template <class R, class Q, class P>
+class OptimizeSolver : public IterativeSolverTemplate<R, Q, P> {
+  using Base = IterativeSolverTemplate<R, Q, P>;
+
+ public:
+  OptimizeSolver(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, std::shared_ptr<Logger> logger)
+      : Base(std::move(handlers), std::make_shared<SubspaceSolverOptLatest>(), std::move(logger)) {}
+  bool nonlinear() const override { return true; }
+
+ protected:
+  // reference OptimizeBFGS.h:208-213, OptimizeSD.h:57-62
+  void set_value_errors() override {
+    auto& v = this->m_xspace->data[EqnData::value];
+    this->m_value_errors.assign(1, std::numeric_limits<double>::max());
+    if (this->m_xspace->size() > 1 && v(0, 0) < v(1, 0)) this->m_value_errors.front() = v(1, 0) - v(0, 0);
+  }
+  void construct_residual(const std::vector<int>&, const CVecRef<R>&, const VecRef<R>&) override {}
+};
+
+// Steepest descent with the caller's preconditioner (reference itsolv/OptimizeSD.h:20-104).
+template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>
+class OptimizeSD : public OptimizeSolver<R, Q, P> {
+  using Base = OptimizeSolver<R, Q, P>;
+
+ public:
+  explicit OptimizeSD(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers,
+                      std::shared_ptr<Logger> logger = std::make_shared<Logger>())
+      : Base(std::move(handlers), std::move(logger)) {}
+
+  int add_vector(R& parameters, R& residual, double value) override {
+    auto& v = this->m_xspace->data[EqnData::value];
+    v.resize({this->m_xspace->dimensions().nX + 1, 1});
+    v(0, 0) = value;
+    return IterativeSolverTemplate<R, Q, P>::add_vector(wrap_arg(parameters), wrap_arg(residual));
+  }
+  using Base::add_vector;
+
+  size_t end_iteration(const VecRef<R>& parameters, const VecRef<R>& action) override {
+    this->solution_params(this->m_working_set, parameters);
+    this->m_end_iteration_needed = false;
+    if (this->m_errors.front() < this->m_convergence_threshold) {
+      this->m_working_set.clear();
+      return 0;
+    }
+    this->m_working_set.assign(1, 0);
+    this->m_handlers->rr().axpy(-1, action.front(), parameters.front());
+    this->m_stats->iterations++;
+    return 1;
+  }
+  using Base::end_iteration;
+};
+
+// Limited-memory quasi-Newton (BFGS two-loop recursion over the Q space) with a cubic line search
+// under the Wolfe conditions (reference itsolv/OptimizeBFGS.h:20-265).
+template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>
+class OptimizeBFGS : public OptimizeSolver<R, Q, P> {
+  using Base = OptimizeSolver<R, Q, P>;
+
+ public:
+  explicit OptimizeBFGS(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers,
+                        std::shared_ptr<Logger> logger = std::make_shared<Logger>())
+      : Base(std::move(handlers), std::move(logger)) {}
+
+  // reference :38-106; returns -1 when a line-search point was proposed in `parameters`
+  int add_vector(R& parameters, R& residual, double value) override {
+    auto& xs = *this->m_xspace;
+    auto& xdata = xs.data;
+    while (xs.size() >= size_t(m_max_size_qspace)) xs.eraseq(xs.size() - 1);
+    auto& val = xdata[EqnData::value];
+    const Matrix<double> old = val;
+    val.resize({xs.size() + 1, 1});
+    for (size_t i = 0; i < xs.size(); ++i) val(i + 1, 0) = old(i, 0);
+    val(0, 0) = value;
+    const int nwork = IterativeSolverTemplate<R, Q, P>::add_vector(wrap_arg(parameters), wrap_arg(residual));
+    const auto& H = xdata.at(EqnData::H);
+    const auto& S = xdata.at(EqnData::S);
+    if (xs.size() > 1) {  // line search needed?
+      const auto& V = xdata.at(EqnData::value);
+      const double fprev = V(1, 0), fcur = V(0, 0);
+      const double gprev = H(0, 1) - H(1, 1), gcur = H(0, 0) - H(1, 0);
+      const bool wolfe1 = fcur <= fprev + m_Wolfe_1 * gprev;
+      const bool wolfe2 = m_strong_Wolfe ? gcur >= m_Wolfe_2 * gprev : std::abs(gcur) <= m_Wolfe_2 * std::abs(gprev);
+      (void)S;
+      if (!(wolfe1 && wolfe2)) {
+        Interpolate inter({-1, fprev, gprev}, {0, fcur, gcur});
+        const auto p = inter.minimize(-1 - m_linesearch_grow_factor, m_linesearch_grow_factor);
+        if (std::abs(p.x) > m_linesearch_tolerance) {
+          this->m_logger->msg("Line search step taken", Logger::Info);
+          this->m_handlers->rr().scal(1 + p.x, parameters);
+          this->m_handlers->rq().axpy(-p.x, xs.cparamsq().at(1).get(), parameters);
+          xs.eraseq(fprev < fcur ? 0 : 1);
+          m_linesearch = true;
+          return -1;
+        }
+      }
+    }
+    m_linesearch = false;
+    this->m_logger->msg("Quasi-Newton step taken", Logger::Info);
+    for (bool again = true; again;) {
+      again = false;
+      const auto& Hc = xdata.at(EqnData::H);
+      for (size_t a = 0; a < m_alpha.size() && a + 1 < xs.size(); ++a)
+        if (std::abs(curv(Hc, a)) < std::max(5e-14 * std::abs(Hc(a, a)), 1e-15)) {
+          xs.eraseq(a + 1);
+          this->m_logger->msg("Erase redundant Q", Logger::Info);
+          again = true;
+          break;
+        }
+    }
+    bfgs_update_1(residual);
+    return nwork;
+  }
+  using Base::add_vector;
+
+  // reference :170-205
+  size_t end_iteration(const VecRef<R>& parameters, const VecRef<R>& action) override {
+    this->m_working_set = {0};
+    this->m_end_iteration_needed = false;
+    if (!m_linesearch) {
+      m_last_linesearching = false;
+      this->solution_params(this->m_working_set, parameters);
+      if (this->m_errors.front() < this->m_convergence_threshold) {
+        this->m_working_set.clear();
+        return 0;
+      }
+      this->m_working_set.assign(1, 0);
+      auto& z = action.front().get();
+      bfgs_update_2(z);
+      this->m_handlers->rr().axpy(-1, z, parameters.front());
+    } else {
+      this->m_stats->line_search_steps++;
+      if (!m_last_linesearching) this->m_stats->line_searches++;
+      m_last_linesearching = true;
+    }
+    this->m_stats->iterations++;
+    return this->errors().front() < this->m_convergence_threshold ? 0 : 1;
+  }
+  using Base::end_iteration;
+
+  void set_max_size_qspace(int n) { m_max_size_qspace = n; }
+  int get_max_size_qspace() const { return m_max_size_qspace; }
+  void set_options(const Options& o) override {
+    Base::set_options(o);
+    if (auto* b = dynamic_cast<const OptimizeBFGSOptions*>(&o)) {
+      if (b->max_size_qspace) set_max_size_qspace(*b->max_size_qspace);
+      if (b->strong_Wolfe) m_strong_Wolfe = *b->strong_Wolfe;
+      if (b->Wolfe_1) m_Wolfe_1 = *b->Wolfe_1;
+      if (b->Wolfe_2) m_Wolfe_2 = *b->Wolfe_2;
+      if (b->linesearch_tolerance) m_linesearch_tolerance = *b->linesearch_tolerance;
+      if (b->linesearch_grow_factor) m_linesearch_grow_factor = *b->linesearch_grow_factor;
+    }
+  }
+
+ private:
+  static double curv(const Matrix<double>& H, size_t a) { return H(a, a) - H(a, a + 1) - H(a + 1, a) + H(a + 1, a + 1); }
+
+  // first loop of the two-loop recursion (reference :108-120)
+  void bfgs_update_1(R& residual) {
+    auto& xs = *this->m_xspace;
+    const auto& H = xs.data.at(EqnData::H);
+    m_alpha.assign(xs.size() ? xs.size() - 1 : 0, 0.0);
+    const auto q = xs.cparamsq();
+    const auto u = xs.cactionsq();
+    auto& h = *this->m_handlers;
+    for (size_t a = 0; a < m_alpha.size(); ++a) {
+      m_alpha[a] = (h.rq().dot(residual, q[a].get()) - h.rq().dot(residual, q[a + 1].get())) / curv(H, a);
+      h.rq().axpy(-m_alpha[a], u[a].get(), residual);
+      h.rq().axpy(m_alpha[a], u[a + 1].get(), residual);
+    }
+  }
+  // second loop (reference :122-132)
+  void bfgs_update_2(R& z) {
+    auto& xs = *this->m_xspace;
+    const auto& H = xs.data.at(EqnData::H);
+    const auto q = xs.cparamsq();
+    const auto u = xs.cactionsq();
+    auto& h = *this->m_handlers;
+    for (int a = int(m_alpha.size()) - 1; a >= 0; --a) {
+      const double beta = (h.rq().dot(z, u[a].get()) - h.rq().dot(z, u[a + 1].get())) / curv(H, size_t(a));
+      h.rq().axpy(m_alpha[a] - beta, q[a].get(), z);
+      h.rq().axpy(-m_alpha[a] + beta, q[a + 1].get(), z);
+    }
+  }
+
+  std::vector<double> m_alpha;
+  bool m_linesearch = false;
+  bool m_last_linesearching = false;
+  int m_max_size_qspace = std::numeric_limits<int>::max();
+  bool m_strong_Wolfe = true;
+  double m_Wolfe_1 = 1e-4;
+  double m_Wolfe_2 = 0.9;
+  double m_linesearch_tolerance = .2;
+  double m_linesearch_grow_factor = 2;
 };
 
 }  // namespace molpro::linalg::itsolv

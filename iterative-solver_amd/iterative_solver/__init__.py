@@ -4,8 +4,8 @@ libitsolv_hbm.so (include/iterative_solver_c.h).  Class names, constructor argum
 follow the reference (iterative_solver_extension.pyx); the Q space and all subspace operations
 live in HBM, the parameter/residual arrays the caller passes stay numpy arrays.
 
-Available: LinearEigensystem and LinearEquations (Davidson), NonLinearEquations (DIIS).  Optimize
-raises RuntimeError at construction (not on this back end).
+Available: LinearEigensystem and LinearEquations (Davidson), NonLinearEquations (DIIS), Optimize
+(BFGS, SD).
 """
 from __future__ import annotations
 

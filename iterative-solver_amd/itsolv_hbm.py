@@ -16,7 +16,7 @@ MAX_ROOTS = 64
 
 EXPORTS = [
     "itsolv_last_error", "itsolv_default_options", "itsolv_davidson_synthetic", "itsolv_davidson_dense",
-    "itsolv_diis_synthetic", "itsolv_diis_dense", "itsolv_linear_equations_dense",
+    "itsolv_diis_synthetic", "itsolv_diis_dense", "itsolv_linear_equations_dense", "itsolv_optimize_dense",
 ]
 
 
@@ -99,6 +99,7 @@ def load_library():
             "itsolv_diis_synthetic": (I, [P, Z, D, I, U, PO, PR, PD]),
             "itsolv_diis_dense": (I, [P, PD, Z, PO, PR, PD]),
             "itsolv_linear_equations_dense": (I, [P, PD, Z, PD, I, PO, PR, PD]),
+            "itsolv_optimize_dense": (I, [P, PD, Z, I, PO, PR, PD]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -166,4 +167,16 @@ def linear_equations_dense(ctx: sh.Context, a: np.ndarray, rhs: np.ndarray, **op
                  (ctx.handle, a.ctypes.data_as(C.POINTER(C.c_double)), n, b.ctypes.data_as(C.POINTER(C.c_double)),
                   nrhs, C.byref(o)), n * nrhs)
     r["x"] = x[:n * nrhs].reshape(nrhs, n)
+    return r
+
+
+def optimize_dense(ctx: sh.Context, h: np.ndarray, algorithm: str = "BFGS", **opts):
+    """OptimizeBFGS / OptimizeSD on the Rayleigh quotient of h from e_0 (function value in eigenvalues[0])."""
+    h = np.ascontiguousarray(h, dtype=np.float64)
+    n = h.shape[0]
+    o = make_options(**opts)
+    r, x = _call(load_library().itsolv_optimize_dense,
+                 (ctx.handle, h.ctypes.data_as(C.POINTER(C.c_double)), n, 0 if algorithm == "BFGS" else 1,
+                  C.byref(o)), n)
+    r["x"] = x[:n]
     return r

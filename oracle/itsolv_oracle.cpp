@@ -254,6 +254,25 @@ class DenseCpu : public Problem<V, SP> {
   size_t m_n;
 };
 
+class RayleighCpu : public DenseCpu {
+ public:
+  using DenseCpu::DenseCpu;
+  double residual(const V& x, V& g) const override {
+    apply(x, g);
+    double xx = 0, xg = 0;
+    for (size_t i = 0; i < x.size(); ++i) {
+      xx += x[i] * x[i];
+      xg += x[i] * g[i];
+    }
+    const double f = xg / xx;
+    for (size_t i = 0; i < x.size(); ++i) {
+      g[i] += -f * x[i];
+      g[i] *= 2 / xx;
+    }
+    return f;
+  }
+};
+
 template <class P>
 double residual_norm(const P& problem, const V& x, double e) {
   V ax(x.size());
@@ -355,6 +374,19 @@ int oracle_linear_equations_dense(const double* h, size_t n, const double* rhs, 
         opts_or_default(opt), *out,
         [&](size_t r, const V& x) {
           if (x_out) std::memcpy(x_out + r * n, x.data(), n * sizeof(double));
+        });
+  });
+}
+
+int oracle_optimize_dense(const double* h, size_t n, int algorithm, const itsolv_options* opt, itsolv_result* out,
+                          double* x_out) {
+  RayleighCpu p(h, n);
+  return guarded([&] {
+    std::memset(out, 0, sizeof(*out));
+    pr::run_optimize<V, V, SP>(
+        cpu_handlers(), p, [&] { return V(n, 0.0); }, [](V& x) { x.at(0) = 1.0; }, algorithm, opts_or_default(opt),
+        *out, [&](const V& x) {
+          if (x_out) std::memcpy(x_out, x.data(), n * sizeof(double));
         });
   });
 }

@@ -208,6 +208,7 @@ def itsolv_lib():
             "oracle_diis_synthetic": [Z, D, I, U, PO, PR, PDd],
             "oracle_diis_dense": [PDd, Z, PO, PR, PDd],
             "oracle_linear_equations_dense": [PDd, Z, PDd, I, PO, PR, PDd],
+            "oracle_optimize_dense": [PDd, Z, I, PO, PR, PDd],
         }.items():
             f = getattr(L, name)
             f.restype = I
@@ -277,6 +278,18 @@ def linear_equations_dense(a, rhs, **opts):
     o = make_options(**opts)
     r, x = _solve(itsolv_lib().oracle_linear_equations_dense, (_d(a), n, _d(b), nrhs, C.byref(o)), n * nrhs)
     r["x"] = x[:n * nrhs].reshape(nrhs, n)
+    return r
+
+
+def optimize_dense(h, algorithm="BFGS", **opts):
+    """The reference CPU path of OptimizeBFGS / OptimizeSD on the Rayleigh quotient of h from e_0."""
+    from itsolv_hbm import make_options
+
+    h = _f64(h)
+    n = h.shape[0]
+    o = make_options(**opts)
+    r, x = _solve(itsolv_lib().oracle_optimize_dense, (_d(h), n, 0 if algorithm == "BFGS" else 1, C.byref(o)), n)
+    r["x"] = x[:n]
     return r
 
 

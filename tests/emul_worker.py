@@ -59,6 +59,8 @@ def case_api():
 
     tg.test_linear_equations()
     tg.test_simple_linear_equations()
+    tg.test_optimize("")
+    tg.test_optimize("SD")
     # C-API loop vs the restated solve() of the CPU reference path: same iterations
     for name, split, nroot in (("he", 0.0, 1), ("hf", 1e-8, 3), ("bh", 1e-8, 3)):
         h = hamiltonian(name, split)

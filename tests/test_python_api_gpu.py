@@ -60,9 +60,26 @@ def test_nonlinear_equations():
     solver.finalize()
 
 
-def test_unavailable_solvers_raise():
-    with pytest.raises(RuntimeError, match="not available"):
-        iterative_solver.Optimize(4)
+@pytest.mark.parametrize("algorithm", ["", "SD"])
+def test_optimize(algorithm):
+    # reference test_rayleigh_quotient.py:76-99 (BFGS is the default algorithm, start x = 10).
+    # Plain steepest descent needs a start of unit scale: the Rayleigh gradient scales as 1/|x|.
+    problem = RayleighQuotient(4, 0.01)
+    parameters = np.full(problem.size, 10.0) if algorithm != "SD" else np.eye(problem.size)[0]
+    residual = np.zeros(problem.size)
+    solver = iterative_solver.Optimize(problem.size, algorithm=algorithm)
+    solver.solve(parameters, residual, problem)
+    answer = solver.solution([0], parameters, residual)
+    parameters = parameters * problem.eigenvectors[0, 0] / parameters[0]
+    assert answer == pytest.approx(problem.eigenvalues[0], abs=1e-7)
+    np.testing.assert_allclose(residual, 0.0, atol=1e-7)
+    np.testing.assert_allclose(parameters, problem.eigenvectors[:, 0], atol=1e-7)
+    solver.finalize()
+
+
+def test_maximize_is_rejected():
+    with pytest.raises(RuntimeError, match="maximisation"):
+        iterative_solver.Optimize(4, minimize=False)
 
 
 def test_linear_equations():

@@ -165,3 +165,14 @@ def test_linear_equations_gpu_vs_cpu(ctx, n, nroot):
     np.testing.assert_allclose(gpu["x"], np.outer(np.arange(1, nroot + 1), np.ones(n)), atol=1e-5, rtol=0)
     # both stop at |A x - b| <= 1e-10 |b| (|b| ~ 1e4 here), so x agrees to ~|b| * 1e-10 / sigma_min
     np.testing.assert_allclose(gpu["x"], cpu["x"], atol=2e-6, rtol=0)
+
+
+@pytest.mark.parametrize("n,alg,thresh", [(4, "BFGS", 1e-8), (100, "BFGS", 1e-6), (20, "SD", 1e-6)])
+def test_optimize_gpu_vs_cpu(ctx, n, alg, thresh):
+    from test_solver_oracle import rayleigh_matrix
+
+    m = rayleigh_matrix(n, 0.01)
+    kw = dict(convergence_threshold=thresh, max_iter=200)
+    gpu, cpu = ih.optimize_dense(ctx, m, alg, **kw), oracle.optimize_dense(m, alg, **kw)
+    assert gpu["converged"] and cpu["converged"] and gpu["iterations"] == cpu["iterations"]
+    assert abs(gpu["eigenvalues"][0] - cpu["eigenvalues"][0]) < 1e-12

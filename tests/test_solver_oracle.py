@@ -157,3 +157,19 @@ def test_linear_equations_augmented_hessian_subspace_solve(aug):
     m = np.block([[a, -aug * rhs.T], [-aug * rhs, np.zeros((1, 1))]])
     e = np.linalg.eigvalsh(m)[0]
     np.testing.assert_allclose(r["x"][0], np.linalg.solve(a - e * np.eye(n), rhs[0]), atol=1e-12)
+
+
+def rayleigh_matrix(n, rho):
+    # reference python/test/test_rayleigh_quotient.py:16-22: M_ij = (i + 1) delta_ij + rho
+    return np.full((n, n), rho) + np.diag(np.arange(1.0, n + 1))
+
+
+@pytest.mark.parametrize("n,alg,thresh", [(4, "BFGS", 1e-8), (20, "BFGS", 1e-6), (100, "BFGS", 1e-6),
+                                          (4, "SD", 1e-8), (20, "SD", 1e-6)])
+def test_optimize_rayleigh_quotient(n, alg, thresh):
+    # OptimizeBFGS / OptimizeSD minimising x.Mx / x.x from e_0: the value is the lowest eigenvalue
+    m = rayleigh_matrix(n, 0.01)
+    r = oracle.optimize_dense(m, alg, convergence_threshold=thresh, max_iter=200)
+    assert r["converged"]
+    assert abs(r["eigenvalues"][0] - np.linalg.eigvalsh(m)[0]) < 1e-12
+    assert r["residual_norms"][0] <= thresh
