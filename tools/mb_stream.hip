@@ -140,6 +140,89 @@ __global__ __launch_bounds__(256) void k_o2(const OArgs a) {
   }
 }
 
+// o3: library design (4 sources x U windows) with selectable nontemporal loads of y, and block size BS.
+template <int M, int U, bool NTYL, int BS>
+__global__ __launch_bounds__(BS) void k_o3(const OArgs a) {
+  const int lane = threadIdx.x & 63;
+  const size_t gw = size_t(blockIdx.x) * (BS / 64) + (threadIdx.x >> 6), nw = size_t(gridDim.x) * (BS / 64);
+  const size_t n2 = a.n >> 1, win = 64 * U;
+  for (size_t c = gw; c * win < n2; c += nw) {
+    const size_t p0 = c * win + lane;
+    double2 acc[U][M];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < M; ++j) acc[u][j] = NTYL ? ld2nt(a.y[j] + 2 * (p0 + 64 * u)) : ld2(a.y[j] + 2 * (p0 + 64 * u));
+    for (int i = 0; i + 4 <= a.k; i += 4) {
+      double2 xv[4][U];
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[b][u] = ld2nt(a.x[i + b] + 2 * (p0 + 64 * u));
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          const double al = a.alpha[(i + b) * M + j];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            acc[u][j].x = fma(al, xv[b][u].x, acc[u][j].x);
+            acc[u][j].y = fma(al, xv[b][u].y, acc[u][j].y);
+          }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < M; ++j) st2nt(a.y[j] + 2 * (p0 + 64 * u), acc[u][j]);
+  }
+}
+
+// o4: guarded windows (every load tested against n2), runtime destination count -- the r1 library form.
+template <int M, int U>
+__global__ __launch_bounds__(256) void k_o4(const OArgs a) {
+  const int lane = threadIdx.x & 63;
+  const size_t gw = size_t(blockIdx.x) * 4 + (threadIdx.x >> 6), nw = size_t(gridDim.x) * 4;
+  const size_t n2 = a.n >> 1, win = 64 * U;
+  const double2 z2 = make_double2(0, 0);
+  for (size_t c = gw; c * win < n2; c += nw) {
+    const size_t p0 = c * win + lane;
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ok[u] = p0 + 64 * u < n2;
+    double2 acc[U][M];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < M; ++j) acc[u][j] = (j < a.m && ok[u]) ? ld2nt(a.y[j] + 2 * (p0 + 64 * u)) : z2;
+    for (int i = 0; i + 4 <= a.k; i += 4) {
+      double2 xv[4][U];
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[b][u] = ok[u] ? ld2nt(a.x[i + b] + 2 * (p0 + 64 * u)) : z2;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+          if (j < a.m) {
+            const double al = a.alpha[(i + b) * a.m + j];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              acc[u][j].x = fma(al, xv[b][u].x, acc[u][j].x);
+              acc[u][j].y = fma(al, xv[b][u].y, acc[u][j].y);
+            }
+          }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (ok[u])
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+          if (j < a.m) st2nt(a.y[j] + 2 * (p0 + 64 * u), acc[u][j]);
+  }
+}
+
 template <bool NT, int U>
 __global__ __launch_bounds__(256) void k_fill(double* y, size_t n, double v) {
   const size_t n2 = n >> 1, stride = size_t(gridDim.x) * 256;
@@ -236,26 +319,10 @@ int main(int argc, char** argv) {
   auto rep = [&](const char* name, int g, float ms, double bytes) {
     printf("%-26s g=%-6d %8.3f ms  %7.1f GB/s\n", name, g, ms, bytes / ms / 1e6);
   };
-  const int mode = argc > 2 ? atoi(argv[2]) : 0;
-  if (mode == 0) {
-    for (int g : {256, 512, 1024, 2048}) {
-      rep("outer o1 B8 nt", g, timeit([&] { hipLaunchKernelGGL((k_o1<8, 8, true>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-      rep("outer o2 B4 U4", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 4, 4>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-      rep("outer o2 B4 U4 ntx", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 4, 4, true, false>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-      rep("outer o2 B4 U4 ntx nty", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 4, 4, true, true>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-      rep("outer o2 B2 U8 ntx", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 2, 8, true, false>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-      rep("outer o2 B4 U2 ntx", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 4, 2, true, false>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
-      rep("outer o2 B8 U4 ntx", g, timeit([&] { hipLaunchKernelGGL((k_o2<8, 8, 4, true, false>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
+  for (int rep_i = 0; rep_i < 3; ++rep_i)
+    for (int g : {512, 2048}) {
+      rep("guarded (r1 lib) U4", g, timeit([&] { hipLaunchKernelGGL((k_o4<8, 4>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
+      rep("guard-free U4", g, timeit([&] { hipLaunchKernelGGL((k_o3<8, 4, true, 256>), dim3(g), dim3(256), 0, 0, a); }, 4), obytes);
     }
-  }
-  for (int g : {2048, 8192, 16384}) {
-    rep("fill U1", g, timeit([&] { hipLaunchKernelGGL((k_fill<false, 1>), dim3(g), dim3(256), 0, 0, vec[0], n, 0.0); }, 10), vb);
-    rep("fill U2", g, timeit([&] { hipLaunchKernelGGL((k_fill<false, 2>), dim3(g), dim3(256), 0, 0, vec[0], n, 0.0); }, 10), vb);
-    rep("axpy U1 nt", g, timeit([&] { hipLaunchKernelGGL((k_axpy<true, 1>), dim3(g), dim3(256), 0, 0, vec[1], vec[2], n, 0.5); }, 10), 3 * vb);
-    rep("axpy U2 nt", g, timeit([&] { hipLaunchKernelGGL((k_axpy<true, 2>), dim3(g), dim3(256), 0, 0, vec[1], vec[2], n, 0.5); }, 10), 3 * vb);
-    rep("axpy U4 nt", g, timeit([&] { hipLaunchKernelGGL((k_axpy<true, 4>), dim3(g), dim3(256), 0, 0, vec[1], vec[2], n, 0.5); }, 10), 3 * vb);
-    rep("dot U2 nt", g, timeit([&] { hipLaunchKernelGGL((k_dot<true, 2>), dim3(g), dim3(256), 0, 0, vec[3], n, partial); }, 10), vb);
-    rep("dot U4 nt", g, timeit([&] { hipLaunchKernelGGL((k_dot<true, 4>), dim3(g), dim3(256), 0, 0, vec[3], n, partial); }, 10), vb);
-  }
   return 0;
 }
