@@ -170,12 +170,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=float, default=1e8, help="global vector length")
+    # not "--n": torch.distributed.run would take it as an abbreviation of its own --nnodes/--nproc-per-node
+    ap.add_argument("--n-global", type=float, default=1e8, help="global vector length")
     ap.add_argument("--roots", type=int, default=8)
     ap.add_argument("--qsize", type=int, default=48)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ledger-steps", type=int, default=3)
+    ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
+                    help="rank transport at N > 1: RCCL (the product path) or the host socket hub, which "
+                         "lets tests run several ranks on ONE device (RCCL refuses duplicate GPUs)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r1", "pmc_traffic_n1e8.json"),
                     help="rocprofv3 --pmc summary of this workload (roofline.traffic)")
     args = ap.parse_args()
@@ -186,14 +190,20 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
-    uid, uid_path = rendezvous_uid(rank, world) if world > 1 else (None, None)
-    ctx = sh.Context(local_rank)
-    if world > 1:
-        ctx.attach_comm(world, rank, uid)  # collective: returns once every rank has joined
-        if uid_path:
-            os.remove(uid_path)
+    if args.comm == "host":
+        ctx = sh.Context(local_rank % max(1, sh.device_count()))
+        if world > 1:
+            port = int(os.environ.get("MASTER_PORT", "29500")) + 1
+            ctx.attach_host_comm(sh.HubComm(rank, world, os.environ.get("MASTER_ADDR", "127.0.0.1"), port))
+    else:
+        uid, uid_path = rendezvous_uid(rank, world) if world > 1 else (None, None)
+        ctx = sh.Context(local_rank)
+        if world > 1:
+            ctx.attach_comm(world, rank, uid)  # collective: returns once every rank has joined
+            if uid_path:
+                os.remove(uid_path)
 
-    n_global = int(args.n)
+    n_global = int(args.n_global)
     m, k = args.roots, args.qsize
     borders = distribution(n_global, world)
     n_local, offset = borders[rank + 1] - borders[rank], borders[rank]
@@ -257,7 +267,8 @@ def main():
                 "n_local_rank0": n_local,
                 "roots": m,
                 "qspace": k,
-                "parallelism": f"index-range shards x{world} (RCCL allreduce for reductions)",
+                "parallelism": f"index-range shards x{world} ("
+                               + ("RCCL" if args.comm == "rccl" else "host-hub") + " allreduce for reductions)",
                 "bytes_per_step": step_bytes(n_global, m, k),
             },
             "roofline": {

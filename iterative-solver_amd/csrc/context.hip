@@ -112,8 +112,8 @@ int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev) {
 }
 
 int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n) {
-  if (ctx->nranks <= 1 || n == 0) return SSP_OK;
-  if (ctx->host_allreduce) {
+  if (n == 0) return SSP_OK;
+  if (ctx->host_allreduce && ctx->nranks > 1) {
     // Host-callback communicator: stage through the host (test / fallback transport only).
     std::vector<double> h(n);
     SSP_TRY_HIP(hipMemcpyAsync(h.data(), buf, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
@@ -394,7 +394,8 @@ int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id) {
   ctx->host_user = nullptr;
   ctx->nranks = nranks;
   ctx->rank = rank;
-  if (nranks == 1) return SSP_OK;
+  // A one-rank communicator is created too: its collectives run through RCCL like any other, which
+  // is how the RCCL calls are exercised on a one-GPU machine (tests/test_rccl_gpu.py).
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, uid, rank);
@@ -451,7 +452,7 @@ int ssp_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes)
       return ssp::set_error(SSP_ERR_COMM, "host allgather callback failed");
     return SSP_OK;
   }
-  if (!ctx->comm || ctx->nranks <= 1) {
+  if (!ctx->comm) {
     if (bytes) std::memcpy(recv, send, bytes);
     return SSP_OK;
   }

@@ -1,0 +1,87 @@
+"""bench.py: the driver's contract (one JSON line from rank 0 with the required keys) and its helpers.
+
+CPU: shard borders, algorithmic bytes per step, the PMC-summary lookup, the CPU baseline leg.
+GPU: a short N = 1 run, and N = 2 launched exactly as the driver launches it
+(`python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 ...`)
+with `--comm host`, two ranks on the box's one device (RCCL refuses duplicate GPUs; the RCCL calls
+themselves are covered by test_rccl_gpu.py).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+import oracle
+from test_distributed import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+@pytest.mark.parametrize("n,p", [(10**8, 1), (10**8, 8), (10**8 + 3, 8), (7, 3)])
+def test_distribution_is_reference(n, p):
+    assert bench.distribution(n, p) == oracle.distribution(n, p).tolist()
+
+
+def test_step_bytes():
+    # 2 x gemm_inner 8N(m+k) + 2 m fills 8N + 2 x gemm_outer 8N(k+2m) + m axpy 24N + m dot 8N
+    n, m, k = 10**8, 8, 48
+    assert bench.step_bytes(n, m, k) == 8 * n * (2 * (m + k) + 2 * m + 2 * (k + 2 * m) + 3 * m + m)
+    assert bench.step_bytes(n, m, k) == 230.4e9
+
+
+def test_pmc_traffic_lookup():
+    path = os.path.join(ROOT, "profiles", "r1", "pmc_traffic_n1e8.json")
+    t, src = bench.pmc_traffic(path, "gemm_outer", 10**8, 8, 48, 1)
+    assert t is not None and src.startswith("profiles/r1/pmc_traffic_n1e8.json:k_gemm_outer")
+    assert abs(t - 8 * 10**8 * (48 + 16)) / t < 0.02  # algorithmic bytes: no re-reads
+    assert bench.pmc_traffic(path, "gemm_outer", 10**8, 8, 48, 2) == (None, None)  # other workload
+    assert bench.pmc_traffic("/nonexistent.json", "dot", 1, 1, 1, 1) == (None, None)
+
+
+def test_cpu_baseline_leg():
+    cb = bench.cpu_baseline(2, 3, 0.05)
+    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["unit"] == "GB/s" and cb["value"] > 0
+
+
+def parse(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-3000:]
+    d = json.loads(lines[0])
+    assert KEYS <= set(d), set(KEYS) - set(d)
+    assert d["value"] > 0 and d["unit"] == "GB/s" and d["dtype"] == "f64" and d["higher_is_better"] is True
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1.0
+    return d
+
+
+@pytest.mark.gpu
+def test_bench_single_gpu():
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--n-global", "4e6",
+           "--cpu-seconds", "0.5"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = parse(r.stdout)
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["cpu_baseline"]["value"] > 0
+    assert d["config"]["n_global"] == 4_000_000
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_host_hub():
+    env = dict(os.environ)
+    for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--n-global", "4000001", "--comm", "host"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = parse(r.stdout)
+    assert d["n_gpus"] == 2 and d["cpu_baseline"] is None
+    assert d["config"]["n_local_rank0"] == 2_000_001  # spread-remainder: rank 0 takes the extra element

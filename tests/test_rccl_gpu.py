@@ -1,0 +1,77 @@
+"""The RCCL code path of libsubspace_hip.so on real hardware, on a one-GPU machine.
+
+RCCL refuses two ranks on one device, so the multi-rank tests on one MI355X reduce through the host
+communicator (test_distributed_gpu.py).  A ONE-rank RCCL communicator is legal, and with one attached
+every reduction of the library goes through ncclAllReduce / ncclAllGather on the context stream
+(context.hip: allreduce_dev, ssp_allgather_host) — the calls bench.py and a multi-GPU solver make
+at N > 1.  Each reducing op and a whole Davidson / DIIS solve must give bit-identical results with
+and without the communicator (a one-rank sum is the identity).
+"""
+import numpy as np
+import pytest
+
+import itsolv_hbm as ih
+import subspace_hip as sh
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pair():
+    if sh.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on an MI355X")
+    plain, comm = sh.Context(0), sh.Context(0)
+    comm.attach_comm(1, 0, sh.Context.unique_id())
+    yield plain, comm
+    comm.close()
+    plain.close()
+
+
+def both(pair, fn):
+    return [fn(c) for c in pair]
+
+
+def test_comm_attached(pair):
+    plain, comm = pair
+    assert comm.lib.ssp_ctx_nranks(comm.handle) == 1 and comm.lib.ssp_ctx_rank(comm.handle) == 0
+
+
+@pytest.mark.parametrize("n", [1, 1003, 1_000_003])
+def test_reductions_through_rccl(pair, n):
+    r = np.random.default_rng(n)
+    xs = [r.uniform(-1, 1, n) for _ in range(8)]
+    ys = [r.uniform(-1, 1, n) for _ in range(5)]
+    a, b = both(pair, lambda c: c.dot(c.upload(xs[0]), c.upload(ys[0])))
+    assert a == b
+    a, b = both(pair, lambda c: c.gemm_inner([c.upload(v) for v in xs], [c.upload(v) for v in ys]))
+    assert np.array_equal(a, b)
+    ps = [{0: 1.0}, {n - 1: -2.0, n // 2: 0.5}]
+    a, b = both(pair, lambda c: c.gemm_inner_sparse([c.upload(v) for v in xs[:3]], ps))
+    assert np.array_equal(a, b)
+
+
+def test_select_through_rccl_allgather(pair):
+    x = np.round(np.random.default_rng(5).uniform(-30, 30, 100_003))
+    (ia, va), (ib, vb) = both(pair, lambda c: c.select(c.upload(x), 16))
+    assert ia.tolist() == ib.tolist() and np.array_equal(va, vb)
+    (ia, va), (ib, vb) = both(pair, lambda c: c.select_max_dot(c.upload(x), c.upload(np.ones_like(x)), 5))
+    assert ia.tolist() == ib.tolist() and np.array_equal(va, vb)
+
+
+def test_allgather_and_barrier(pair):
+    _, comm = pair
+    assert comm.allgather_bytes(b"rank0-payload") == [b"rank0-payload"]
+    comm.barrier()
+    comm.barrier()
+
+
+def test_davidson_and_diis_through_rccl(pair):
+    kw = dict(nroots=4, convergence_threshold=1e-8, max_size_qspace=24, reset_D=8)
+    a, b = both(pair, lambda c: ih.davidson_synthetic(c, 200_000, 0.1, 8, 7, **kw))
+    assert a["iterations"] == b["iterations"]
+    assert np.array_equal(a["eigenvalues"], b["eigenvalues"])
+    assert np.array_equal(a["solutions"], b["solutions"])
+    kw = dict(nroots=1, convergence_threshold=1e-8, max_size_qspace=6)
+    a, b = both(pair, lambda c: ih.diis_synthetic(c, 100_000, 0.1, 1, 3, **kw))
+    assert a["iterations"] == b["iterations"]
+    assert np.array_equal(a["x"], b["x"])
