@@ -26,9 +26,17 @@ inline unsigned long long stream_key(unsigned long long seed, unsigned long long
   return splitmix64(seed ^ (stream * 0xD1B54A32D192ED03ull));
 }
 
-__device__ __forceinline__ double sign_of(unsigned long long key, unsigned long long g) {
-  return (splitmix64(key ^ g) & 1ull) ? -1.0 : 1.0;
+// Bit l of the mask is set when u_l(g) = -1 (u_0 = 1 always): the R - 1 hashes of an element are
+// computed once and shared by every vector of the launch.
+template <int R>
+__device__ __forceinline__ unsigned sign_mask(const unsigned long long (&key)[16], unsigned long long g) {
+  unsigned m = 0;
+#pragma unroll
+  for (int l = 1; l < R; ++l) m |= unsigned(splitmix64(key[l] ^ g) & 1ull) << l;
+  return m;
 }
+
+__device__ __forceinline__ double flip(unsigned mask, int l, double v) { return ((mask >> l) & 1u) ? -v : v; }
 
 struct SynthArgs {
   const double* x[kMaxVec];
@@ -56,54 +64,93 @@ __device__ __forceinline__ double block_sum(double v, double* wsum) {
   return s;
 }
 
+// Per-block partial sums of u_l . x_v, vectors in groups of G (R x G accumulators per thread).
+template <int R, int G>
 __global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a) {
   __shared__ double wsum[kBlock / 64];
   const size_t stride = size_t(gridDim.x) * kBlock;
-  for (int v = 0; v < a.nvec; ++v) {
-    double s[kMaxRank];
+  for (int v0 = 0; v0 < a.nvec; v0 += G) {
+    double s[G][R];
 #pragma unroll
-    for (int l = 0; l < kMaxRank; ++l) s[l] = 0;
+    for (int v = 0; v < G; ++v)
+#pragma unroll
+      for (int l = 0; l < R; ++l) s[v][l] = 0;
     for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
-      const double xv = a.x[v][i];
+      const unsigned mask = sign_mask<R>(a.key, a.offset + i);
 #pragma unroll
-      for (int l = 0; l < kMaxRank; ++l)
-        if (l < a.rank) s[l] = fma(l == 0 ? 1.0 : sign_of(a.key[l], a.offset + i), xv, s[l]);
+      for (int v = 0; v < G; ++v) {
+        if (v0 + v < a.nvec) {
+          const double xv = __builtin_nontemporal_load(a.x[v0 + v] + i);
+#pragma unroll
+          for (int l = 0; l < R; ++l) s[v][l] += flip(mask, l, xv);
+        }
+      }
     }
 #pragma unroll
-    for (int l = 0; l < kMaxRank; ++l) {
-      if (l < a.rank) {
-        const double t = block_sum(s[l], wsum);
-        if (threadIdx.x == 0) a.partial[size_t(blockIdx.x) * a.nvec * a.rank + v * a.rank + l] = t;
+    for (int v = 0; v < G; ++v) {
+      if (v0 + v < a.nvec) {
+#pragma unroll
+        for (int l = 0; l < R; ++l) {
+          const double t = block_sum(s[v][l], wsum);
+          if (threadIdx.x == 0) a.partial[size_t(blockIdx.x) * a.nvec * R + (v0 + v) * R + l] = t;
+        }
       }
     }
   }
 }
 
+// y_v = d x_v + rho sum_l u_l coeff[v][l]   (ADD = false)
+// y_v += rho sum_l u_l coeff[v][l]          (ADD = true, the P-space low-rank term)
+template <int R, bool ADD>
 __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
   const size_t stride = size_t(gridDim.x) * kBlock;
   for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
     const unsigned long long g = a.offset + i;
+    const unsigned mask = sign_mask<R>(a.key, g);
     const double d = 1.0 + double(g);
-    double u[kMaxRank];
-    for (int l = 0; l < a.rank; ++l) u[l] = l == 0 ? 1.0 : sign_of(a.key[l], g);
     for (int v = 0; v < a.nvec; ++v) {
       double s = 0;
-      for (int l = 0; l < a.rank; ++l) s = fma(u[l], a.coeff[v * a.rank + l], s);
-      a.y[v][i] = fma(d, a.x[v][i], a.rho * s);
+#pragma unroll
+      for (int l = 0; l < R; ++l) s += flip(mask, l, a.coeff[v * R + l]);
+      if (ADD)
+        a.y[v][i] = fma(a.rho, s, a.y[v][i]);
+      else
+        a.y[v][i] = fma(d, __builtin_nontemporal_load(a.x[v] + i), a.rho * s);
     }
   }
 }
 
-// y[v][i] += rho * sum_l u_l(g) coeff[v*rank + l]
-__global__ __launch_bounds__(kBlock) void k_synth_add(const SynthArgs a) {
-  const size_t stride = size_t(gridDim.x) * kBlock;
-  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
-    const unsigned long long g = a.offset + i;
-    for (int v = 0; v < a.nvec; ++v) {
-      double s = 0;
-      for (int l = 0; l < a.rank; ++l) s = fma(l == 0 ? 1.0 : sign_of(a.key[l], g), a.coeff[v * a.rank + l], s);
-      a.y[v][i] = fma(a.rho, s, a.y[v][i]);
-    }
+template <int R>
+void launch_coeff(unsigned grid, hipStream_t st, const SynthArgs& a) {
+  if (a.nvec <= 2 || R > 8)
+    hipLaunchKernelGGL((k_synth_coeff<R, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_synth_coeff<R, 4>), dim3(grid), dim3(kBlock), 0, st, a);
+}
+
+#define SSP_RANK_CASES(F) \
+  F(1) F(2) F(3) F(4) F(5) F(6) F(7) F(8) F(9) F(10) F(11) F(12) F(13) F(14) F(15) F(16)
+
+void synth_coeff(unsigned grid, hipStream_t st, const SynthArgs& a) {
+  switch (a.rank) {
+#define F(r) \
+  case r:    \
+    launch_coeff<r>(grid, st, a); \
+    break;
+    SSP_RANK_CASES(F)
+#undef F
+  }
+}
+
+template <bool ADD>
+void synth_apply(unsigned grid, hipStream_t st, const SynthArgs& a) {
+  switch (a.rank) {
+#define F(r)                                                                       \
+  case r:                                                                          \
+    hipLaunchKernelGGL((k_synth_apply<r, ADD>), dim3(grid), dim3(kBlock), 0, st, a); \
+    break;
+    SSP_RANK_CASES(F)
+#undef F
   }
 }
 
@@ -171,7 +218,7 @@ int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* 
     SSP_TRY(ssp::ensure_result(ctx, nc));
     a.partial = ctx->partial;
     if (n > 0) {
-      hipLaunchKernelGGL(k_synth_coeff, dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      synth_coeff(grid, ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
       SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, nc, ctx->result_dev, nc, 0, 0));
     } else {
@@ -186,7 +233,7 @@ int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* 
     SSP_TRY_HIP(hipMemcpyAsync(coeff, ctx->result_dev, nc * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
     a.coeff = static_cast<const double*>(coeff);
     if (n > 0) {
-      hipLaunchKernelGGL(k_synth_apply, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, a);
+      synth_apply<false>(ssp::stream_grid(ctx, n, 1), ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
     }
   }
@@ -211,7 +258,7 @@ int sspx_synthetic_add_lowrank(ssp_ctx* ctx, double* const* yy, int nvec, size_t
     void* coeff;
     SSP_TRY(ssp::upload_small(ctx, w + size_t(v0) * rank, size_t(a.nvec) * rank * sizeof(double), &coeff));
     a.coeff = static_cast<const double*>(coeff);
-    hipLaunchKernelGGL(k_synth_add, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, a);
+    synth_apply<true>(ssp::stream_grid(ctx, n, 1), ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
   return SSP_OK;

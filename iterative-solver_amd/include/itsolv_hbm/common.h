@@ -138,7 +138,13 @@ struct LinearEigensystemDavidsonOptions : Options {
       std::transform(v.begin(), v.end(), v.begin(), [](unsigned char c) { return std::tolower(c); });
       hermiticity = (v == "true" || v == "1" || v == "yes");
     }
+    if (opt.count("BLOCK_GRAM_SCHMIDT")) {  // extension, see itsolv_options.block_gram_schmidt
+      auto v = opt.at("BLOCK_GRAM_SCHMIDT");
+      std::transform(v.begin(), v.end(), v.begin(), [](unsigned char c) { return std::tolower(c); });
+      block_gram_schmidt = (v == "true" || v == "1" || v == "yes");
+    }
   }
+  std::optional<bool> block_gram_schmidt;
   std::optional<int> reset_D;
   std::optional<int> reset_D_max_Q_size;
   std::optional<int> max_size_qspace;

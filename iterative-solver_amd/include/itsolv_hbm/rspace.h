@@ -242,6 +242,27 @@ std::tuple<std::vector<Q>, std::vector<Q>> construct_dspace(const Matrix<double>
   return {std::move(newp), std::move(newa)};
 }
 
+// Sequential self-orthonormalisation of R; indices whose norm is below norm_thresh are returned
+// as null (reference propose_rspace.h:450-465).
+template <class R>
+std::vector<int> orthonormalise_among(const VecRef<R>& rparams, double norm_thresh, array::ArrayHandler<R, R>& hr) {
+  std::vector<int> null_params;
+  const size_t nR = rparams.size();
+  for (size_t i = 0; i < nR; ++i) {
+    const double nrm = std::sqrt(std::abs(hr.dot(rparams[i], rparams[i])));
+    if (nrm > norm_thresh) {
+      hr.scal(1. / nrm, rparams[i]);
+      for (size_t j = i + 1; j < nR; ++j) {
+        const double ov = hr.dot(rparams[i], rparams[j]);
+        hr.axpy(-ov, rparams[i], rparams[j]);
+      }
+    } else {
+      null_params.push_back(int(i));
+    }
+  }
+  return null_params;
+}
+
 // Orthogonalise R against P, Q, D (in that order) and among themselves (reference :421-466).
 template <class R, class Q, class P>
 std::vector<int> modified_gram_schmidt(const VecRef<R>& rparams, const Matrix<double>& S, const Dimensions& d,
@@ -287,20 +308,44 @@ std::vector<int> modified_gram_schmidt(const VecRef<R>& rparams, const Matrix<do
       if (i + 1 < qd.size()) inner(i + 1);
     }
   }
-  std::vector<int> null_params;
-  for (size_t i = 0; i < nR; ++i) {
-    const double nrm = std::sqrt(std::abs(h.rr().dot(rparams[i], rparams[i])));
-    if (nrm > norm_thresh) {
-      h.rr().scal(1. / nrm, rparams[i]);
-      for (size_t j = i + 1; j < nR; ++j) {
-        const double ov = h.rr().dot(rparams[i], rparams[j]);
-        h.rr().axpy(-ov, rparams[i], rparams[j]);
+  return orthonormalise_among(rparams, norm_thresh, h.rr());
+}
+
+// Option block_gram_schmidt (extension): the same projection as
+// modified_gram_schmidt above, R_j <- R_j + sum_i c(i,j) x_i over x = P, Q, D in that order, with
+// c(i,j) = -<R_j^(i-1), x_i> / |S_ii| and <R_j^(i-1), x_i> = <R_j, x_i> + sum_{l<i} c(l,j) S_li.
+// <R_j, x_i> are the rows `rows` of `full` (append_overlap_with_r, already computed for the
+// redundancy screen), so the coefficients come from a forward substitution on the host and R is
+// updated by one gemm_outer per space instead of one gemm_inner + gemm_outer per x_i. Identical
+// in exact arithmetic; the rounding differs from the sequential sweep.
+template <class R, class Q, class P>
+std::vector<int> block_gram_schmidt(const VecRef<R>& rparams, const Matrix<double>& full,
+                                    const std::vector<size_t>& rows, const Dimensions& d, const CVecRef<P>& pp,
+                                    const CVecRef<Q>& qp, const CVecRef<Q>& dp, double norm_thresh,
+                                    ArrayHandlers<R, Q, P>& h) {
+  const size_t nR = rparams.size(), nX = d.nX;
+  if (nR > 0 && nX > 0) {
+    Matrix<double> c({nX, nR});
+    for (size_t j = 0; j < nR; ++j)
+      for (size_t i = 0; i < nX; ++i) {
+        double t = full(rows[j], i);
+        for (size_t l = 0; l < i; ++l) t += c(l, j) * full(l, i);
+        c(i, j) = -t / std::abs(full(i, i));
       }
-    } else {
-      null_params.push_back(int(i));
+    auto block = [&](size_t o, size_t n) {
+      Matrix<double> a({n, nR});
+      for (size_t i = 0; i < n; ++i)
+        for (size_t j = 0; j < nR; ++j) a(i, j) = c(o + i, j);
+      return a;
+    };
+    if (d.nP) h.rp().gemm_outer(block(d.oP, d.nP), pp, rparams);
+    if (d.nQ + d.nD) {
+      CVecRef<Q> qd(qp.begin(), qp.end());
+      qd.insert(qd.end(), dp.begin(), dp.end());
+      h.rq().gemm_outer(block(d.oQ, d.nQ + d.nD), qd, rparams);
     }
   }
-  return null_params;
+  return orthonormalise_among(rparams, norm_thresh, h.rr());
 }
 
 // Indices among the last nR parameters made redundant by near-null singular vectors (reference :481-512).

@@ -578,8 +578,14 @@ class DavidsonSolver : public IterativeSolverTemplate<R, Q, P> {
     if (d.norm_thresh) norm_thresh = *d.norm_thresh;
     if (d.svd_thresh) svd_thresh = *d.svd_thresh;
     if (d.hermiticity) set_hermiticity(*d.hermiticity);
+    if (d.block_gram_schmidt) m_block_gram_schmidt = *d.block_gram_schmidt;
   }
 
+ public:
+  void set_block_gram_schmidt(bool on) { m_block_gram_schmidt = on; }
+  bool block_gram_schmidt() const { return m_block_gram_schmidt; }
+
+ protected:
   // reference propose_rspace.h:553-624
   std::vector<int> propose_rspace(const VecRef<R>& parameters, const VecRef<R>& residuals) {
     auto& xs = *this->m_xspace;
@@ -602,9 +608,16 @@ class DavidsonSolver : public IterativeSolverTemplate<R, Q, P> {
     const auto full = detail::append_overlap_with_r(xs.data.at(EqnData::S), cwrap(wres), xs.cparamsp(), xs.cparamsq(),
                                                     xs.cparamsd(), h);
     auto redundant = detail::redundant_parameters(full, xs.dimensions().nX, wres.size(), svd_thresh, log);
+    std::vector<size_t> rows(wres.size());
+    std::iota(rows.begin(), rows.end(), xs.dimensions().nX);
     detail::delete_parameters(redundant, wres);
-    auto null_params = detail::modified_gram_schmidt(wres, xs.data.at(EqnData::S), xs.dimensions(), xs.cparamsp(),
-                                                     xs.cparamsq(), xs.cparamsd(), norm_thresh, h);
+    detail::delete_parameters(redundant, rows);
+    auto null_params =
+        m_block_gram_schmidt
+            ? detail::block_gram_schmidt(wres, full, rows, xs.dimensions(), xs.cparamsp(), xs.cparamsq(),
+                                         xs.cparamsd(), norm_thresh, h)
+            : detail::modified_gram_schmidt(wres, xs.data.at(EqnData::S), xs.dimensions(), xs.cparamsp(),
+                                            xs.cparamsq(), xs.cparamsd(), norm_thresh, h);
     detail::delete_parameters(null_params, wres);
     detail::normalise(wres, h.rr(), log);
     for (size_t i = 0; i < wres.size(); ++i) h.rr().copy(parameters.at(i), wres.at(i));
@@ -615,6 +628,7 @@ class DavidsonSolver : public IterativeSolverTemplate<R, Q, P> {
   detail::DSpaceResetter<Q> m_resetter;
   bool m_hermiticity = false;
   bool m_resetting = false;
+  bool m_block_gram_schmidt = false;
 };
 
 template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>

@@ -35,6 +35,7 @@ class Options(C.Structure):
         ("generate_initial_guess", C.c_int),
         ("verbosity", C.c_int),
         ("augmented_hessian", C.c_double),
+        ("block_gram_schmidt", C.c_int),
     ]
 
 
@@ -71,7 +72,7 @@ class Result(C.Structure):
 def make_options(**kw) -> Options:
     o = Options(nroots=1, nwork=0, max_iter=100, max_size_qspace=0, reset_D=0, reset_D_max_Q_size=0, max_p=0,
                 p_threshold=0.0, convergence_threshold=1e-8, hermitian=1, generate_initial_guess=1, verbosity=0,
-                augmented_hessian=0.0)
+                augmented_hessian=0.0, block_gram_schmidt=0)
     for k, v in kw.items():
         if not hasattr(o, k):
             raise KeyError(k)

@@ -176,3 +176,32 @@ def test_optimize_gpu_vs_cpu(ctx, n, alg, thresh):
     gpu, cpu = ih.optimize_dense(ctx, m, alg, **kw), oracle.optimize_dense(m, alg, **kw)
     assert gpu["converged"] and cpu["converged"] and gpu["iterations"] == cpu["iterations"]
     assert abs(gpu["eigenvalues"][0] - cpu["eigenvalues"][0]) < 1e-12
+
+
+# block_gram_schmidt on the HIP handlers against the reference CPU path (sequential MGS): the bar of
+# the default path (same iterations and R creations, eigenvalues within 1e-10).
+@pytest.mark.parametrize("name,split,nroot,np_", [("hf", 1e-8, 1, 0), ("hf", 1e-8, 3, 0), ("bh", 1e-8, 3, 0),
+                                                  ("bh", 1e-8, 3, 6)])
+def test_block_gram_schmidt_fixture_gpu_vs_reference(ctx, name, split, nroot, np_):
+    h = hamiltonian(name, split)
+    kw = dict(nroots=nroot, max_p=np_, convergence_threshold=1e-8, max_size_qspace=6 * nroot, reset_D=8)
+    assert_same_run(ih.davidson_dense(ctx, h, block_gram_schmidt=1, **kw), oracle.davidson_dense(h, **kw))
+
+
+@pytest.mark.parametrize("rank,nroot,np_", [(1, 4, 0), (4, 8, 0), (4, 8, 16)])
+def test_block_gram_schmidt_synthetic_gpu_vs_reference(ctx, rank, nroot, np_):
+    n, rho, seed = 100_003, 0.1, 20251015
+    kw = dict(nroots=nroot, max_p=np_, convergence_threshold=1e-8, max_size_qspace=6 * nroot, reset_D=8)
+    gpu = ih.davidson_synthetic(ctx, n, rho, rank, seed, block_gram_schmidt=1, **kw)
+    assert_same_run(gpu, oracle.davidson_synthetic(n, rho, rank, seed, **kw))
+    assert np.all(gpu["residual_norms"] <= 1e-7)
+
+
+def test_block_gram_schmidt_config_c3(ctx):
+    n, rho = 100_000_000, 0.1
+    kw = dict(nroots=8, max_p=16, convergence_threshold=1e-8, max_size_qspace=48, reset_D=8)
+    seq = ih.davidson_synthetic(ctx, n, rho, 1, 1, **kw)
+    blk = ih.davidson_synthetic(ctx, n, rho, 1, 1, block_gram_schmidt=1, **kw)
+    assert blk["converged"] and blk["iterations"] == seq["iterations"]
+    np.testing.assert_allclose(blk["eigenvalues"], oracle.rank_one_eigenvalues(n, rho, 8), rtol=1e-10, atol=0)
+    assert np.all(blk["residual_norms"] <= 1e-7)

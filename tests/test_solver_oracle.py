@@ -173,3 +173,39 @@ def test_optimize_rayleigh_quotient(n, alg, thresh):
     assert r["converged"]
     assert abs(r["eigenvalues"][0] - np.linalg.eigvalsh(m)[0]) < 1e-12
     assert r["residual_norms"][0] <= thresh
+
+
+# Option block_gram_schmidt (extension, itsolv_options.block_gram_schmidt): the MGS projection from
+# the overlaps append_overlap_with_r already holds + one gemm_outer per space.  Its own parity
+# sign-off against the reference's sequential sweep: the same iterations and
+# eigenvalues within 1e-10 on the reference fixtures, P space included, and on synthetic problems.
+@pytest.mark.parametrize("name,split,nroot,np_", [("he", 0.0, 1, 0), ("hf", 1e-8, 1, 0), ("hf", 1e-8, 3, 0),
+                                                  ("bh", 1e-8, 1, 0), ("bh", 1e-8, 3, 0), ("bh", 1e-8, 6, 0),
+                                                  ("bh", 1e-8, 3, 6), ("hf", 1e-8, 1, 4)])
+def test_block_gram_schmidt_matches_sequential_fixtures(name, split, nroot, np_):
+    h = hamiltonian(name, split)
+    kw = dict(nroots=nroot, max_p=np_, convergence_threshold=1e-8, max_size_qspace=6 * nroot, reset_D=8)
+    ref, blk = oracle.davidson_dense(h, **kw), oracle.davidson_dense(h, block_gram_schmidt=1, **kw)
+    assert blk["converged"] and blk["iterations"] == ref["iterations"] and blk["r_creations"] == ref["r_creations"]
+    np.testing.assert_allclose(blk["eigenvalues"], ref["eigenvalues"], rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("n,rank,rho,nroot,maxq,np_", [(1000, 1, 0.1, 1, 6, 0), (1000, 4, 0.1, 4, 24, 0),
+                                                       (20_000, 8, 0.1, 8, 48, 0), (20_000, 8, 0.1, 8, 48, 16),
+                                                       (50_000, 3, 0.01, 2, 12, 8)])
+def test_block_gram_schmidt_matches_sequential_synthetic(n, rank, rho, nroot, maxq, np_):
+    kw = dict(nroots=nroot, convergence_threshold=1e-8, max_size_qspace=maxq, reset_D=8, max_p=np_)
+    ref = oracle.davidson_synthetic(n, rho, rank, 1, **kw)
+    blk = oracle.davidson_synthetic(n, rho, rank, 1, block_gram_schmidt=1, **kw)
+    assert blk["converged"] and blk["iterations"] == ref["iterations"]
+    np.testing.assert_allclose(blk["eigenvalues"], ref["eigenvalues"], rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("n,nroot", [(12, 3), (33, 2)])
+def test_block_gram_schmidt_linear_equations(n, nroot):
+    a, rhs = simple_system(n, nroot)
+    kw = dict(nroots=nroot, convergence_threshold=1e-10)
+    ref = oracle.linear_equations_dense(a, rhs, **kw)
+    blk = oracle.linear_equations_dense(a, rhs, block_gram_schmidt=1, **kw)
+    assert blk["converged"] and blk["iterations"] == ref["iterations"]
+    np.testing.assert_allclose(blk["x"], ref["x"], atol=2e-6, rtol=0)

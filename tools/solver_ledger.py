@@ -4,7 +4,7 @@ ledger enabled and report, per handler operation, calls, kernel time, algorithmi
 plus the solve's wall time.  Complements bench.py (a fixed subspace-update step) with the op mix
 of real Davidson / DIIS iterations.
 
-usage: python tools/solver_ledger.py [--configs C2,C3,C5] [--out profiles/r1/solver_ledger.json]
+usage: python tools/solver_ledger.py [--configs C2,C2-bgs,C3,C3-bgs,C5] [--out profiles/r1/solver_ledger.json]
 """
 import argparse
 import json
@@ -24,6 +24,11 @@ CONFIGS = {
                                          convergence_threshold=1e-8)),
     "C3": ("davidson", 100_000_000, dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48,
                                           reset_D=8, convergence_threshold=1e-8)),
+    # C3 with the block Gram-Schmidt option (itsolv_options.block_gram_schmidt)
+    "C3-bgs": ("davidson", 100_000_000, dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48,
+                                              reset_D=8, convergence_threshold=1e-8, block_gram_schmidt=1)),
+    "C2-bgs": ("davidson", 10_000_000, dict(rho=0.1, rank=8, seed=1, nroots=4, max_size_qspace=24, reset_D=8,
+                                             convergence_threshold=1e-8, block_gram_schmidt=1)),
     "C5": ("diis", 100_000_000, dict(rho=0.01, rank=3, seed=3, max_size_qspace=6, convergence_threshold=1e-8)),
 }
 
@@ -72,7 +77,7 @@ def run_once(ctx, name):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="C2,C3,C5")
+    ap.add_argument("--configs", default="C2,C2-bgs,C3,C3-bgs,C5")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "solver_ledger.json"))
     a = ap.parse_args()
     ctx = sh.Context(0)
