@@ -155,6 +155,7 @@ def cpu_baseline(m, k, seconds):
                 break
     except OSError:
         pass
+    hp = host_parallel(m, k, max(1.0, seconds / 3))
     return {
         "value": step_bytes(n, m, k) * steps / dt / 1e9,
         "unit": "GB/s",
@@ -162,7 +163,31 @@ def cpu_baseline(m, k, seconds):
         "kind": "port",
         "sample": f"{steps} step(s) of the same op sequence at N=1e6 (m={m}, k={k}) on 1 core of "
                   f"{cpu} (nproc={os.cpu_count()}), {dt:.1f} s, oracle/oracle_ops.c (reference loops)",
+        "host_parallel": hp,
     }
+
+
+def host_parallel(m, k, seconds):
+    """SURVEY.md §8d's second CPU figure: the same op sequence with OpenMP on all the host threads
+    this process may use and cache-blocked gemm (oracle/host_parallel.c) -- "host-parallel", not
+    the reference."""
+    import oracle  # test infrastructure: the CPU baseline leg only
+
+    n = 4_000_000
+    runner = oracle.HostParallelStep(n, m, k, SEED)
+    runner.step()
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        runner.step()
+        steps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": step_bytes(n, m, k) * steps / dt / 1e9, "unit": "GB/s", "cores": runner.threads,
+            "kind": "host-parallel",
+            "sample": f"{steps} step(s) at N=4e6 (m={m}, k={k}), OpenMP x{runner.threads}, {dt:.1f} s, "
+                      "oracle/host_parallel.c (blocked gemm, not the reference's pairwise loops)"}
 
 
 def main():

@@ -326,6 +326,40 @@ class CpuUpdateStep:
             _c(L.or_dot(_d(self.ra[i]), n, _d(self.ra[i]), n, C.byref(out)))
 
 
+class HostParallelStep:
+    """bench.py's host-parallel baseline: the same op sequence with OpenMP over
+    all host threads and cache-blocked gemm (oracle/host_parallel.c); not the reference's loops."""
+
+    def __init__(self, n, m, k, seed):
+        path = os.path.join(_HERE, "build", "libhost_parallel.so")
+        if not os.path.exists(path):
+            build()
+        self.L = C.CDLL(path)
+        self.L.hp_update_step.argtypes = [C.c_void_p] * 4 + [C.c_int, C.c_int, C.c_size_t] + [C.c_void_p] * 3
+        self.L.hp_update_step.restype = C.c_int
+        self.L.hp_first_touch.argtypes = [C.c_void_p, C.c_size_t, C.c_double]
+        self.n, self.m, self.k = n, m, k
+        self.vecs = []
+        for v in range(2 * (m + k)):
+            a = np.empty(n)
+            self.L.hp_first_touch(a.ctypes.data, n, 1e-3 * (v + 1))
+            self.vecs.append(a)
+        self.p = [_ptrs(self.vecs[o:o + c]) for o, c in ((0, m), (m, m), (2 * m, k), (2 * m + k, k))]
+        r = np.random.default_rng(seed)
+        self.coef = np.ascontiguousarray(r.uniform(-0.1, 0.1, (k, m)))
+        self.lam = r.uniform(0.5, 2.0, m)
+        self.out = np.zeros(m * k)
+
+    @property
+    def threads(self):
+        return int(self.L.hp_threads())
+
+    def step(self):
+        if self.L.hp_update_step(*[C.cast(p, C.c_void_p) for p in self.p], self.m, self.k, self.n,
+                                 self.coef.ctypes.data, self.lam.ctypes.data, self.out.ctypes.data):
+            raise RuntimeError("hp_update_step: shape beyond its limits")
+
+
 # ---- synthetic problem restated in numpy (checker for sspx_*) ------------------------------------
 _M64 = (1 << 64) - 1
 

@@ -48,6 +48,8 @@ def test_pmc_traffic_lookup():
 def test_cpu_baseline_leg():
     cb = bench.cpu_baseline(2, 3, 0.05)
     assert cb["kind"] == "port" and cb["cores"] == 1 and cb["unit"] == "GB/s" and cb["value"] > 0
+    hp = cb["host_parallel"]
+    assert hp["kind"] == "host-parallel" and hp["cores"] >= 1 and hp["value"] > 0
 
 
 def parse(out):
