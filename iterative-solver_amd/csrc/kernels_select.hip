@@ -7,11 +7,16 @@
 //   select_max_dot:  v' = |x*y|,                                     returned value = v'
 // so among equal v' the larger index wins; the result map is ordered by index.
 //
-// GPU: each workgroup sorts a tile of up to 2048 (key, index) candidates in LDS with a bitonic
-// network (descending) and keeps its best n; levels repeat until one tile remains.  key is the
-// order-preserving 64-bit image of v', ties broken by index, so the order is exactly the
-// reference's (v', i) order.  Ranks then all-gather their local best n and every rank merges the
-// same candidate set with the same order on the host (deterministic, identical on all ranks).
+// GPU: the order is that of the 128-bit composite (key, i) -- key the order-preserving 64-bit image
+// of v', i the index, larger first -- which is exactly the reference's (v', i) order.
+//  1. Radix threshold (shards longer than kRadixMin): histogram passes over 12-bit digits of the
+//     composite, each restricted to the elements matching the digits fixed so far, until the
+//     elements at or above the threshold T fit kRadixCap (typically 1-2 passes over the shard);
+//     one compaction pass then collects them.
+//  2. Each workgroup sorts a tile of up to 2048 candidates in LDS with a bitonic network
+//     (descending) and keeps its best n; levels repeat until one tile remains.
+// Ranks then all-gather their local best n and every rank merges the same candidate set with the
+// same order on the host (deterministic, identical on all ranks).
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -22,6 +27,7 @@ namespace {
 
 using ssp::kBlock;
 constexpr int kTile = ssp::kSelectTile;
+constexpr int kTileBlock = 1024;  // one compare-exchange per thread per bitonic stage
 
 struct Cand {
   unsigned long long key;
@@ -33,13 +39,6 @@ __host__ __device__ inline unsigned long long order_key(double v) {
   unsigned long long b;
   memcpy(&b, &v, sizeof(b));
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-
-inline double key_value(unsigned long long k) {
-  unsigned long long b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
-  double v;
-  std::memcpy(&v, &b, sizeof(v));
-  return v;
 }
 
 __device__ __forceinline__ bool better(const Cand& a, const Cand& b) {
@@ -60,10 +59,10 @@ struct SelectArgs {
   Cand* out;     // [gridDim.x][keep]
 };
 
-__global__ __launch_bounds__(kBlock) void k_select_tile(const SelectArgs a) {
+__global__ __launch_bounds__(kTileBlock) void k_select_tile(const SelectArgs a) {
   __shared__ Cand tile[kTile];
   const size_t t0 = size_t(blockIdx.x) * kTile;
-  for (int s = threadIdx.x; s < kTile; s += kBlock) {
+  for (int s = threadIdx.x; s < kTile; s += kTileBlock) {
     const size_t g = t0 + s;
     Cand c{0ull, 0ull};  // padding sorts after every real candidate (key 0 is a NaN image)
     if (g < a.count) {
@@ -87,7 +86,7 @@ __global__ __launch_bounds__(kBlock) void k_select_tile(const SelectArgs a) {
   // Bitonic sort, descending by (key, idx).
   for (int k = 2; k <= kTile; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < kTile / 2; t += kBlock) {
+      for (int t = threadIdx.x; t < kTile / 2; t += kTileBlock) {
         const int i = 2 * j * (t / j) + (t % j);
         const int l = i + j;
         const bool desc = ((i & k) == 0);
@@ -101,7 +100,200 @@ __global__ __launch_bounds__(kBlock) void k_select_tile(const SelectArgs a) {
       __syncthreads();
     }
   }
-  for (int s = threadIdx.x; s < a.keep; s += kBlock) a.out[size_t(blockIdx.x) * a.keep + s] = tile[s];
+  for (int s = threadIdx.x; s < a.keep; s += kTileBlock) a.out[size_t(blockIdx.x) * a.keep + s] = tile[s];
+}
+
+constexpr size_t kRadixMin = size_t(1) << 17;  // shorter shards go straight to the tile sort
+constexpr size_t kRadixCap = size_t(1) << 16;  // candidates handed to the tile sort
+constexpr int kDigitBits = 12;
+constexpr int kBins = 1 << kDigitBits;
+
+struct RadixArgs {
+  const double* x;
+  const double* y;
+  size_t n;
+  int mode;
+  int max;
+  int ignore_sign;
+  int bits;   // composite bits fixed so far (0..128): key bits 63.., then local index bits 63..
+  int width;  // digit width (<= 12), bits + width <= 64 or bits >= 64
+  unsigned long long tkey, tidx;  // threshold composite (fixed bits, zeros below)
+  unsigned* hist;                 // [gridDim.x][kBins]
+  Cand* cand;                     // compaction output
+  unsigned long long* counter;
+};
+
+__device__ __forceinline__ unsigned long long value_key(const RadixArgs& a, double xv, double yv) {
+  double v;
+  if (a.mode == 1)
+    v = fabs(xv * yv);
+  else
+    v = a.max ? (a.ignore_sign ? fabs(xv) : xv) : (a.ignore_sign ? -fabs(xv) : -xv);
+  return order_key(v);
+}
+
+// Keys of elements 2p and 2p+1 (16-byte loads; a missing second element gets valid = false).
+constexpr int kRadixU = 4;  // double2 slots per thread per iteration
+__device__ __forceinline__ void load_pair(const RadixArgs& a, size_t p, unsigned long long (&k)[2], bool (&ok)[2]) {
+  const size_t i = 2 * p;
+  ok[0] = i < a.n;
+  ok[1] = i + 1 < a.n;
+  double2 xv = make_double2(0, 0), yv = make_double2(0, 0);
+  if (ok[1]) {
+    xv = ssp::ld2nt(a.x + i);
+    if (a.mode == 1) yv = ssp::ld2nt(a.y + i);
+  } else if (ok[0]) {
+    xv.x = a.x[i];
+    if (a.mode == 1) yv.x = a.y[i];
+  }
+  k[0] = value_key(a, xv.x, yv.x);
+  k[1] = value_key(a, xv.y, yv.y);
+}
+
+// Digit of (key, i) at composite bit position a.bits, or -1 when the fixed prefix differs.
+__device__ __forceinline__ int elem_digit(const RadixArgs& a, unsigned long long key, unsigned long long i) {
+  const unsigned mask = (1u << a.width) - 1u;
+  if (a.bits < 64) {
+    if (a.bits > 0 && (key >> (64 - a.bits)) != (a.tkey >> (64 - a.bits))) return -1;
+    return int((key >> (64 - a.bits - a.width)) & mask);
+  }
+  const int ib = a.bits - 64;
+  if (key != a.tkey || (ib > 0 && (i >> (64 - ib)) != (a.tidx >> (64 - ib)))) return -1;
+  return int((i >> (64 - ib - a.width)) & mask);
+}
+
+__device__ __forceinline__ void hist_add(unsigned* h, int d) {
+  // Concentrated data sends whole waves to one bin: one atomic per wave then.
+  const int d0 = __builtin_amdgcn_readfirstlane(d);
+  const unsigned long long same = __ballot(d == d0);
+  if (same == __ballot(1)) {
+    if (d0 >= 0 && __lane_id() == 0) atomicAdd(&h[d0], unsigned(__popcll(same)));
+  } else if (d >= 0) {
+    atomicAdd(&h[d], 1u);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_radix_hist(const RadixArgs a) {
+  __shared__ unsigned h[kBins];
+  for (int s = threadIdx.x; s < kBins; s += kBlock) h[s] = 0;
+  __syncthreads();
+  const size_t stride = size_t(gridDim.x) * kBlock, n2 = (a.n + 1) / 2;
+  // Every lane of a wave makes the same trips (the ballots in hist_add need the whole wave).
+  for (size_t p0 = size_t(blockIdx.x) * kBlock; p0 < n2; p0 += kRadixU * stride) {
+    unsigned long long k[kRadixU][2];
+    bool ok[kRadixU][2];
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) load_pair(a, p0 + threadIdx.x + u * stride, k[u], ok[u]);
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const unsigned long long i = 2 * (p0 + threadIdx.x + u * stride) + e;
+        hist_add(h, ok[u][e] ? elem_digit(a, k[u][e], i) : -1);
+      }
+  }
+  __syncthreads();
+  for (int s = threadIdx.x; s < kBins; s += kBlock) a.hist[size_t(blockIdx.x) * kBins + s] = h[s];
+}
+
+// out[b] = sum over blocks of hist[block][b] (fixed order).
+__global__ __launch_bounds__(kBlock) void k_radix_hist_sum(const unsigned* hist, int nblocks, unsigned* out) {
+  const int b = blockIdx.x * kBlock + threadIdx.x;
+  if (b >= kBins) return;
+  unsigned s = 0;
+  for (int k = 0; k < nblocks; ++k) s += hist[size_t(k) * kBins + b];
+  out[b] = s;
+}
+
+// Every element whose composite is >= (tkey, tidx).
+__global__ __launch_bounds__(kBlock) void k_radix_compact(const RadixArgs a, size_t offset) {
+  const size_t stride = size_t(gridDim.x) * kBlock, n2 = (a.n + 1) / 2;
+  for (size_t p0 = size_t(blockIdx.x) * kBlock + threadIdx.x; p0 < n2; p0 += kRadixU * stride) {
+    unsigned long long k[kRadixU][2];
+    bool ok[kRadixU][2];
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) load_pair(a, p0 + u * stride, k[u], ok[u]);
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const unsigned long long i = 2 * (p0 + u * stride) + e;
+        if (ok[u][e] && (k[u][e] > a.tkey || (k[u][e] == a.tkey && i >= a.tidx))) {
+          const unsigned long long slot = atomicAdd(a.counter, 1ull);
+          if (slot < kRadixCap) a.cand[slot] = Cand{k[u][e], offset + i};
+        }
+      }
+  }
+}
+
+// Fixes digits of the composite threshold until at most kRadixCap elements lie at or above it,
+// then compacts them into `cand`; returns their number in *count.
+int radix_candidates(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t n, size_t offset,
+                     size_t nsel, int max, int ignore_sign, Cand* cand, unsigned* hist, unsigned* hsum,
+                     unsigned long long* counter, unsigned grid, size_t* count) {
+  RadixArgs a{};
+  a.x = x;
+  a.y = y;
+  a.n = n;
+  a.mode = mode;
+  a.max = max;
+  a.ignore_sign = ignore_sign;
+  a.hist = hist;
+  int idx_bits = 1;
+  while (idx_bits < 64 && ((n - 1) >> idx_bits) != 0) ++idx_bits;
+  size_t need = nsel, above = 0;
+  std::vector<unsigned> h(kBins);
+  for (;;) {
+    a.width = a.bits < 64 ? std::min(kDigitBits, 64 - a.bits) : std::min(kDigitBits, 128 - a.bits);
+    hipLaunchKernelGGL(k_radix_hist, dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_TRY_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_radix_hist_sum, dim3((kBins + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, hist,
+                       int(grid), hsum);
+    SSP_TRY_HIP(hipGetLastError());
+    SSP_TRY_HIP(hipMemcpyAsync(h.data(), hsum, sizeof(unsigned) * kBins, hipMemcpyDeviceToHost, ctx->stream));
+    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    const int nb = 1 << a.width;
+    size_t cum = 0;
+    int b = nb - 1;
+    for (; b > 0; --b) {
+      if (cum + h[b] >= need) break;
+      cum += h[b];
+    }
+    if (a.bits < 64)
+      a.tkey |= (unsigned long long)b << (64 - a.bits - a.width);
+    else
+      a.tidx |= (unsigned long long)b << (64 - (a.bits - 64) - a.width);
+    above += cum;
+    need -= cum;
+    a.bits += a.width;
+    if (above + h[b] <= kRadixCap || a.bits >= 128) {
+      *count = above + h[b];
+      break;
+    }
+    if (a.bits == 64) a.bits = 128 - idx_bits;  // local indices have no bits above idx_bits
+  }
+  if (*count > kRadixCap) return ssp::set_error(SSP_ERR_UNSUPPORTED, "ssp_select: radix threshold did not converge");
+  a.cand = cand;
+  a.counter = counter;
+  SSP_TRY_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), ctx->stream));
+  hipLaunchKernelGGL(k_radix_compact, dim3(grid), dim3(kBlock), 0, ctx->stream, a, offset);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+// Returned values recomputed from the selected elements as the reference returns them
+// (select.h:52: max ? v' : -v', so the sign of a zero is the element's, not the key's).
+__global__ void k_select_values(const double* x, const double* y, const unsigned long long* li, int cnt, int mode,
+                                int max, int ignore_sign, double* out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= cnt) return;
+  const double xv = x[li[e]];
+  if (mode == 1) {
+    out[e] = fabs(xv * y[li[e]]);
+  } else {
+    const double v = max ? (ignore_sign ? fabs(xv) : xv) : (ignore_sign ? -fabs(xv) : -xv);
+    out[e] = max ? v : -v;
+  }
 }
 
 int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t n, size_t offset, size_t nsel,
@@ -115,26 +307,45 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
   const int keep = int(nsel);
   std::vector<Cand> local;
   if (keep > 0 && n > 0) {
-    // Level 0 reads the shard; later levels read the previous level's survivors.
-    size_t count = n;
+    ssp::LedgerScope ls(ctx, mode == 1 ? "select_max_dot" : "select", (mode == 1 ? 16.0 : 8.0) * n);
+    // Level 0 reads the shard (short shards) or the radix candidates; later levels read the
+    // previous level's survivors.
+    const bool radix = n > kRadixMin;
+    size_t count = radix ? kRadixCap : n;
     size_t tiles = (count + kTile - 1) / kTile;
-    // Workspace: two candidate buffers sized for level 0's output.
-    const size_t cap = tiles * size_t(keep);
-    SSP_TRY(ssp::ensure_partial(ctx, 4 * cap + 4));
+    const size_t cap = tiles * size_t(keep);  // Cands per level buffer
+    const unsigned grid = radix ? std::min<unsigned>(ssp::stream_grid(ctx, n, 4), unsigned(ctx->num_cus) * 4) : 0;
+    // Workspace (doubles): two level buffers, radix candidates, per-block and summed histograms,
+    // the compaction counter.
+    const size_t w_lvl = 2 * cap * 2, w_cand = radix ? 2 * kRadixCap : 0;
+    const size_t w_hist = radix ? (size_t(grid) + 1) * kBins / 2 : 0;
+    SSP_TRY(ssp::ensure_partial(ctx, w_lvl + w_cand + w_hist + 2));
     Cand* buf0 = reinterpret_cast<Cand*>(ctx->partial);
     Cand* buf1 = buf0 + cap;
+    Cand* cand = buf1 + cap;
+    unsigned* hist = reinterpret_cast<unsigned*>(ctx->partial + w_lvl + w_cand);
+    unsigned* hsum = hist + size_t(grid) * kBins;
+    auto* counter = reinterpret_cast<unsigned long long*>(ctx->partial + w_lvl + w_cand + w_hist);
     SelectArgs a{};
-    a.x = x;
-    a.y = y;
-    a.count = count;
-    a.offset = offset;
-    a.mode = mode;
-    a.max = max;
-    a.ignore_sign = ignore_sign;
     a.keep = keep;
     a.out = buf0;
-    ssp::LedgerScope ls(ctx, mode == 1 ? "select_max_dot" : "select", (mode == 1 ? 16.0 : 8.0) * n);
-    hipLaunchKernelGGL(k_select_tile, dim3(unsigned(tiles)), dim3(kBlock), 0, ctx->stream, a);
+    if (radix) {
+      SSP_TRY(radix_candidates(ctx, mode, x, y, n, offset, nsel, max, ignore_sign, cand, hist, hsum, counter, grid,
+                               &count));
+      tiles = (count + kTile - 1) / kTile;
+      a.in = cand;
+      a.count = count;
+      a.mode = 2;
+    } else {
+      a.x = x;
+      a.y = y;
+      a.count = count;
+      a.offset = offset;
+      a.mode = mode;
+      a.max = max;
+      a.ignore_sign = ignore_sign;
+    }
+    hipLaunchKernelGGL(k_select_tile, dim3(unsigned(tiles)), dim3(kTileBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
     count = tiles * size_t(keep);
     Cand* cur = buf0;
@@ -147,7 +358,7 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
       b.mode = 2;
       b.keep = keep;
       b.out = nxt;
-      hipLaunchKernelGGL(k_select_tile, dim3(unsigned(tiles)), dim3(kBlock), 0, ctx->stream, b);
+      hipLaunchKernelGGL(k_select_tile, dim3(unsigned(tiles)), dim3(kTileBlock), 0, ctx->stream, b);
       SSP_TRY_HIP(hipGetLastError());
       count = tiles * size_t(keep);
       std::swap(cur, nxt);
@@ -162,10 +373,20 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
   // slots per rank plus the real count, and the same host merge on every rank.
   std::vector<size_t> lidx(nsel, 0);
   std::vector<double> lval(nsel, 0.0);
-  for (size_t e = 0; e < local.size(); ++e) {
-    const double v = key_value(local[e].key);
-    lidx[e] = size_t(local[e].idx);
-    lval[e] = (mode == 0 && !max) ? -v : v;
+  if (!local.empty()) {
+    std::vector<unsigned long long> li(local.size());
+    for (size_t e = 0; e < local.size(); ++e) {
+      lidx[e] = size_t(local[e].idx);
+      li[e] = local[e].idx - offset;
+    }
+    void* dli;
+    SSP_TRY(ssp::upload_small(ctx, li.data(), li.size() * sizeof(unsigned long long), &dli));
+    SSP_TRY(ssp::ensure_result(ctx, li.size()));
+    hipLaunchKernelGGL(k_select_values, dim3(unsigned((li.size() + 255) / 256)), dim3(256), 0, ctx->stream, x, y,
+                       static_cast<const unsigned long long*>(dli), int(li.size()), mode, max, ignore_sign,
+                       ctx->result_dev);
+    SSP_TRY_HIP(hipGetLastError());
+    SSP_TRY(ssp::fetch_result(ctx, lval.data(), li.size()));
   }
   const int nr = ctx->nranks;
   std::vector<size_t> counts(nr), gidx(nsel * size_t(nr)), gval_bits(nsel * size_t(nr));

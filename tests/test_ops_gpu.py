@@ -161,6 +161,52 @@ def test_select_bit_exact(ctx, n, nsel, mode):
     assert np.array_equal(val, rval)
 
 
+# Shards above kRadixMin (2^17) take the radix-threshold path (kernels_select.hip): distributions
+# that end the digit search early (spread values), late (narrow ranges, heavy ties -> index digits)
+# and in the index phase (constant vectors), with signed zeros and a shard offset.
+def _radix_inputs(n, r):
+    return {
+        "uniform": r.uniform(-1, 1, n),
+        "narrow": 1.0 + r.integers(0, 1 << 20, n) * 2.0**-52,  # differ in the low mantissa bits only
+        "ties": np.round(r.uniform(-3, 3, n)),
+        "constant": np.full(n, 2.5),
+        "zeros": np.where(r.random(n) < 0.5, 0.0, -0.0),
+        "diag": 1.0 + np.arange(n, dtype=float)[::-1].copy(),
+    }
+
+
+@pytest.mark.parametrize("kind", ["uniform", "narrow", "ties", "constant", "zeros", "diag"])
+@pytest.mark.parametrize("nsel", [1, 16, 1024])
+@pytest.mark.parametrize("mode", [(False, False), (True, False), (False, True), (True, True)])
+def test_select_radix_path_bit_exact(ctx, kind, nsel, mode):
+    n = 300_007
+    x = _radix_inputs(n, rng(nsel + len(kind)))[kind]
+    mx, ab = mode
+    idx, val = ctx.select(ctx.upload(x), nsel, max=mx, ignore_sign=ab)
+    ridx, rval = oracle.select(x, nsel, max=mx, ignore_sign=ab)
+    assert idx.tolist() == ridx.tolist()
+    assert np.array_equal(val, rval) and np.array_equal(np.signbit(val), np.signbit(rval))
+
+
+def test_select_radix_path_offset_and_large(ctx):
+    n, off = 5_000_011, 123_456_789
+    x = rng(5).uniform(-1, 1, n)
+    idx, val = ctx.select(ctx.upload(x), 100, offset=off)
+    ridx, rval = oracle.select(x, 100)
+    assert idx.tolist() == (ridx + off).tolist() and np.array_equal(val, rval)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "ties", "constant"])
+def test_select_max_dot_radix_path(ctx, kind):
+    n = 400_003
+    r = rng(9)
+    x = _radix_inputs(n, r)[kind]
+    y = np.round(r.uniform(-3, 3, n))
+    idx, val = ctx.select_max_dot(ctx.upload(x), ctx.upload(y), 37)
+    ridx, rval = oracle.select_max_dot(x, y, 37)
+    assert idx.tolist() == ridx.tolist() and np.array_equal(val, rval)
+
+
 def test_select_diagonal_guess(ctx):
     # initial guess / P-space selection on diagonals (reference IterativeSolverTemplate.h:340, :354)
     d = oracle.synthetic_diagonal(200_000, 0.1, 1)[::-1].copy()
