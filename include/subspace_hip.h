@@ -116,6 +116,15 @@ int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, 
  * pass over yy (reference propose_rspace.h:430-443 issues them as separate handler calls). */
 int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const* yy, int m, const double* z, size_t n,
                    double* out);
+/* Steps of the sequential self-orthonormalisation of the new R vectors (reference
+ * propose_rspace.h:450-465: scal(1/|r_i|, r_i); for j > i: r_j -= <r_i, r_j> r_i), fused so that
+ * each step is two passes:
+ *   ssp_scal_inner:  x *= alpha, then out[j] = <x, yy[j]> summed over ranks   (= ssp_scal then
+ *                    ssp_gemm_inner({x}, yy), x bit-identical)                 bytes 8N(2 + m)
+ *   ssp_axpy_norm:   yy[j] += c[j] * x, then *out = <yy[0], yy[0]> summed over ranks (= ssp_gemm_outer
+ *                    then ssp_dot(yy[0], yy[0]), yy bit-identical)             bytes 8N(1 + 2m) */
+int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* yy, int m, size_t n, double* out);
+int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const* yy, int m, size_t n, double* out);
 /* a[v][i] /= (d[i] - shift[v] + 1e-15) for v in [0,nvec)   reference itsolv/IterativeSolver.h:34-55 */
 int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n);
 

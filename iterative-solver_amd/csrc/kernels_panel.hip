@@ -270,6 +270,102 @@ __global__ __launch_bounds__(kBlock) void k_axpy_inner(const AxpyInnerArgs a) {
   }
 }
 
+// Per-block sums of acc[0..M) over the block's waves into partial[block][m].
+template <int M>
+__device__ __forceinline__ void block_partials(const double (&acc)[M], int m, double* partial) {
+  __shared__ double red[kBlock / 64][M];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    double v = acc[j];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) red[wave][j] = v;
+  }
+  __syncthreads();
+  if (int(threadIdx.x) < m) {
+    double s = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+    partial[size_t(blockIdx.x) * m + threadIdx.x] = s;
+  }
+}
+
+// x *= alpha; acc_j += x_scaled * y_j.
+struct ScalInnerArgs {
+  double* x;
+  const double* y[ssp::kOuterDst];
+  double alpha;
+  int m;
+  size_t n;
+  double* partial;  // [gridDim.x][m]
+};
+
+template <int M>
+__global__ __launch_bounds__(kBlock) void k_scal_inner(const ScalInnerArgs a) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  const size_t n2 = a.n >> 1, stride = size_t(gridDim.x) * kBlock;
+  double acc[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) acc[j] = 0;
+  for (size_t p = size_t(blockIdx.x) * kBlock + threadIdx.x; p < n2; p += stride) {
+    double2 xv = ld2nt(a.x + 2 * p);
+    xv.x *= a.alpha;
+    xv.y *= a.alpha;
+    st2nt(a.x + 2 * p, xv);
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      if (j < a.m) {
+        const double2 y = ld2nt(a.y[j] + 2 * p);
+        acc[j] = fma(xv.x, y.x, acc[j]);
+        acc[j] = fma(xv.y, y.y, acc[j]);
+      }
+    }
+  }
+  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const size_t e = a.n - 1;
+    const double xs = a.x[e] * a.alpha;
+    a.x[e] = xs;
+    for (int j = 0; j < a.m; ++j) acc[j] = fma(xs, a.y[j][e], acc[j]);
+  }
+  block_partials<M>(acc, a.m, a.partial);
+}
+
+// y_j += c_j x; acc += y_0_new^2.
+template <int M>
+__global__ __launch_bounds__(kBlock) void k_axpy_norm(const AxpyInnerArgs a) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  const size_t n2 = a.n >> 1, stride = size_t(gridDim.x) * kBlock;
+  double acc[1] = {0};
+  for (size_t p = size_t(blockIdx.x) * kBlock + threadIdx.x; p < n2; p += stride) {
+    const double2 xv = ld2nt(a.x + 2 * p);
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      if (j < a.m) {
+        double2 y = ld2nt(a.y[j] + 2 * p);
+        y.x = fma(a.c[j], xv.x, y.x);
+        y.y = fma(a.c[j], xv.y, y.y);
+        st2nt(a.y[j] + 2 * p, y);
+        if (j == 0) {
+          acc[0] = fma(y.x, y.x, acc[0]);
+          acc[0] = fma(y.y, y.y, acc[0]);
+        }
+      }
+    }
+  }
+  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const size_t e = a.n - 1;
+    for (int j = 0; j < a.m; ++j) {
+      const double y = fma(a.c[j], a.x[e], a.y[j][e]);
+      a.y[j][e] = y;
+      if (j == 0) acc[0] = fma(y, y, acc[0]);
+    }
+  }
+  block_partials<1>(acc, 1, a.partial);
+}
+
 int check_ptrs(const double* const* v, int count, size_t n, const char* what) {
   if (count > 0 && !v) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null vector list");
   if (n == 0) return SSP_OK;
@@ -426,6 +522,91 @@ int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, 
     }
   }
   return SSP_OK;
+}
+
+int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* yy, int m, size_t n, double* out) {
+  SSP_CHECK_CTX(ctx);
+  if (m < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_scal_inner: negative dimension");
+  if (m > 0 && !out) return ssp::set_error(SSP_ERR_ARG, "ssp_scal_inner: null out");
+  SSP_TRY(check_ptrs(const_cast<const double* const*>(&x), 1, n, "ssp_scal_inner"));
+  SSP_TRY(check_ptrs(yy, m, n, "ssp_scal_inner"));
+  for (int j = 0; j < m; ++j)
+    if (yy[j] == x) return ssp::set_error(SSP_ERR_ARG, "ssp_scal_inner: a vector of yy aliases x");
+  if (m == 0 || m > ssp::kOuterDst) {  // no dots, or more than one launch: the unfused pair
+    SSP_TRY(ssp_scal(ctx, alpha, x, n));
+    return m == 0 ? SSP_OK : ssp_gemm_inner(ctx, const_cast<const double* const*>(&x), 1, yy, m, n, out);
+  }
+  SSP_TRY(ssp::ensure_result(ctx, size_t(m)));
+  if (n == 0) {
+    SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, size_t(m) * sizeof(double), ctx->stream));
+  } else {
+    ssp::LedgerScope ls(ctx, "scal_inner", 8.0 * n * (2.0 + m));
+    const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 1);
+    ScalInnerArgs a{};
+    a.x = x;
+    a.alpha = alpha;
+    a.m = m;
+    a.n = n;
+    for (int j = 0; j < m; ++j) a.y[j] = yy[j];
+    SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * m));
+    a.partial = ctx->partial;
+    if (m <= 1)
+      hipLaunchKernelGGL((k_scal_inner<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else if (m <= 4)
+      hipLaunchKernelGGL((k_scal_inner<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else if (m <= 8)
+      hipLaunchKernelGGL((k_scal_inner<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else
+      hipLaunchKernelGGL((k_scal_inner<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_TRY_HIP(hipGetLastError());
+    SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, m, ctx->result_dev, m, 0, 0));
+  }
+  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, size_t(m)));
+  return ssp::fetch_result(ctx, out, size_t(m));
+}
+
+int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const* yy, int m, size_t n, double* out) {
+  SSP_CHECK_CTX(ctx);
+  if (m < 1) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_norm: needs at least one destination");
+  if (!c || !out) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_norm: null coefficients or out");
+  SSP_TRY(check_ptrs(&x, 1, n, "ssp_axpy_norm"));
+  SSP_TRY(check_ptrs(const_cast<const double* const*>(yy), m, n, "ssp_axpy_norm"));
+  for (int j = 0; j < m; ++j)
+    if (yy[j] == x) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_norm: a destination aliases x");
+  if (m > ssp::kOuterDst) {  // more than one launch: the unfused pair
+    std::vector<double> alpha(c, c + m);
+    SSP_TRY(ssp_gemm_outer(ctx, alpha.data(), &x, 1, yy, m, n));
+    return ssp_dot(ctx, yy[0], yy[0], n, out);
+  }
+  SSP_TRY(ssp::ensure_result(ctx, 1));
+  if (n == 0) {
+    SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, sizeof(double), ctx->stream));
+  } else {
+    ssp::LedgerScope ls(ctx, "axpy_norm", 8.0 * n * (1.0 + 2.0 * m));
+    const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 1);
+    AxpyInnerArgs a{};
+    a.x = x;
+    a.m = m;
+    a.n = n;
+    for (int j = 0; j < m; ++j) {
+      a.y[j] = yy[j];
+      a.c[j] = c[j];
+    }
+    SSP_TRY(ssp::ensure_partial(ctx, size_t(grid)));
+    a.partial = ctx->partial;
+    if (m <= 1)
+      hipLaunchKernelGGL((k_axpy_norm<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else if (m <= 4)
+      hipLaunchKernelGGL((k_axpy_norm<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else if (m <= 8)
+      hipLaunchKernelGGL((k_axpy_norm<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else
+      hipLaunchKernelGGL((k_axpy_norm<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_TRY_HIP(hipGetLastError());
+    SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, 1, ctx->result_dev, 1, 0, 0));
+  }
+  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, 1));
+  return ssp::fetch_result(ctx, out, 1);
 }
 
 int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const* yy, int m, const double* z, size_t n,

@@ -180,4 +180,12 @@ bool fused_axpy_inner(H&, const std::vector<double>&, const Q&, const RefR&, con
   return false;
 }
 
+// Hook for a fused sequential self-orthonormalisation of R (reference propose_rspace.h:450-465):
+// returns false when the handler has no fused form (the caller then runs the reference loop of
+// dot / scal / dot / axpy calls).  Found by argument-dependent lookup.
+template <class H, class RefR>
+bool fused_orthonormalise(H&, const RefR&, double, std::vector<int>&) {
+  return false;
+}
+
 }  // namespace molpro::linalg::array

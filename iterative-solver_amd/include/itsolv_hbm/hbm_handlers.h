@@ -389,6 +389,42 @@ inline bool fused_axpy_inner(array::ArrayHandler<Vec, Vec>&, const std::vector<d
   return true;
 }
 
+// Sequential self-orthonormalisation of R (reference propose_rspace.h:450-465) in two passes per
+// vector: ssp_scal_inner (r_i *= 1/|r_i|, then <r_i, r_j> for j > i) and ssp_axpy_norm
+// (r_j -= <r_i, r_j> r_i for j > i, then |r_{i+1}|^2).  The vector updates are the reference loop's
+// scal and axpys, element for element; the dots are taken from the same values (array::
+// fused_orthonormalise hook, found by argument-dependent lookup).
+inline bool fused_orthonormalise(array::ArrayHandler<Vec, Vec>&, const itsolv::VecRef<Vec>& rr, double norm_thresh,
+                                 std::vector<int>& null_params) {
+  const size_t nR = rr.size();
+  if (nR == 0) return true;
+  ssp_ctx* ctx = rr[0].get().ctx();
+  const size_t n = rr[0].get().local_size();
+  double nrm2 = 0;
+  check(ssp_dot(ctx, rr[0].get().data(), rr[0].get().data(), n, &nrm2), "ssp_dot");
+  for (size_t i = 0; i < nR; ++i) {
+    const double nrm = std::sqrt(std::abs(nrm2));
+    if (nrm > norm_thresh) {
+      std::vector<const double*> yc;
+      std::vector<double*> y;
+      for (size_t j = i + 1; j < nR; ++j) {
+        yc.push_back(rr[j].get().data());
+        y.push_back(rr[j].get().data());
+      }
+      std::vector<double> ov(std::max<size_t>(1, y.size()));
+      check(ssp_scal_inner(ctx, 1. / nrm, rr[i].get().data(), yc.data(), int(yc.size()), n, ov.data()),
+            "ssp_scal_inner");
+      if (y.empty()) break;
+      for (auto& o : ov) o = -o;
+      check(ssp_axpy_norm(ctx, ov.data(), rr[i].get().data(), y.data(), int(y.size()), n, &nrm2), "ssp_axpy_norm");
+    } else {
+      null_params.push_back(int(i));
+      if (i + 1 < nR) check(ssp_dot(ctx, rr[i + 1].get().data(), rr[i + 1].get().data(), n, &nrm2), "ssp_dot");
+    }
+  }
+  return true;
+}
+
 // Davidson preconditioner on HBM vectors: reference precondition_default (IterativeSolver.h:34-55)
 // as one fused kernel over all working-set vectors (d read once).  Found by argument-dependent
 // lookup from Problem<R>::precondition.

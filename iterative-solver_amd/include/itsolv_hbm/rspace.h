@@ -247,6 +247,8 @@ std::tuple<std::vector<Q>, std::vector<Q>> construct_dspace(const Matrix<double>
 template <class R>
 std::vector<int> orthonormalise_among(const VecRef<R>& rparams, double norm_thresh, array::ArrayHandler<R, R>& hr) {
   std::vector<int> null_params;
+  using array::fused_orthonormalise;
+  if (fused_orthonormalise(hr, rparams, norm_thresh, null_params)) return null_params;
   const size_t nR = rparams.size();
   for (size_t i = 0; i < nR; ++i) {
     const double nrm = std::sqrt(std::abs(hr.dot(rparams[i], rparams[i])));

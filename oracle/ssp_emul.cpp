@@ -188,6 +188,23 @@ int ssp_axpy_inner(ssp_ctx* c, const double* cc, const double* x, double* const*
   }
   return reduce(c, out, size_t(m));
 }
+int ssp_scal_inner(ssp_ctx* c, double alpha, double* x, const double* const* yy, int m, size_t n, double* out) {
+  for (size_t e = 0; e < n; ++e) x[e] *= alpha;
+  for (int j = 0; j < m; ++j) {
+    double s = 0;
+    for (size_t e = 0; e < n; ++e) s += x[e] * yy[j][e];
+    out[j] = s;
+  }
+  return reduce(c, out, size_t(m));
+}
+int ssp_axpy_norm(ssp_ctx* c, const double* cc, const double* x, double* const* yy, int m, size_t n, double* out) {
+  for (int j = 0; j < m; ++j)
+    for (size_t e = 0; e < n; ++e) yy[j][e] += cc[j] * x[e];
+  double s = 0;
+  for (size_t e = 0; e < n; ++e) s += yy[0][e] * yy[0][e];
+  *out = s;
+  return reduce(c, out, 1);
+}
 int ssp_precondition(ssp_ctx*, double* const* a, int nvec, const double* d, const double* shift, size_t n) {
   for (int v = 0; v < nvec; ++v)
     for (size_t i = 0; i < n; ++i) a[v][i] = a[v][i] / ((d[i] - shift[v]) + 1e-15);

@@ -5,6 +5,8 @@ Tolerances: elementwise ops are within 1 ulp (the GPU fuses y + a*x into one fma
 not); reductions reorder the sum, so |gpu - oracle| <= 64 * eps * sum|x_i y_i| (the deterministic
 order error bound, well inside the solver's 1e-10).  Integer/index results (select) are bit-exact.
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -122,6 +124,37 @@ def test_axpy_inner_fused_mgs_step(ctx, m, n):
         assert abs(dots[j] - ref[j]) <= red_tol(ynew[j] * z) + 4 * EPS * np.sum(np.abs(z) * (np.abs(ys[j]) + abs(c[j]) * np.abs(x)))
     for v in [dx, dz] + dy + ey:
         v.free()
+
+
+@pytest.mark.parametrize("m", [0, 1, 3, 8, 16, 17])
+@pytest.mark.parametrize("n", [1, 1003, 100_003])
+def test_scal_inner_and_axpy_norm_fused_orthonormalisation(ctx, m, n):
+    # ssp_scal_inner == scal then gemm_inner({x}, yy); ssp_axpy_norm == gemm_outer({x} -> yy) then
+    # dot(yy[0], yy[0]): vectors bit-identical to the unfused calls, dots to reduction rounding.
+    r = rng(m * 7 + n)
+    x = r.uniform(-1, 1, n)
+    ys = [r.uniform(-1, 1, n) for _ in range(m)]
+    dx, dy = ctx.upload(x), [ctx.upload(v) for v in ys]
+    got = ctx.scal_inner(0.37, dx, dy)
+    xs = oracle.scal(0.37, x)
+    assert np.array_equal(dx.numpy(), xs)
+    for j in range(m):
+        assert abs(got[j] - oracle.dot(xs, ys[j])) <= red_tol(xs * ys[j])
+    if m == 0:
+        return
+    c = r.uniform(-1, 1, m)
+    nrm2 = ctx.axpy_norm(c, dx, dy)
+    ref = [oracle.axpy(c[j], xs, ys[j]) for j in range(m)]
+    for v, e in zip(dy, ref):
+        np.testing.assert_allclose(v.numpy(), e, rtol=2 * EPS, atol=4 * EPS)
+    ctx2 = [ctx.upload(v) for v in ys]
+    ctx.gemm_outer(c.reshape(1, m), [dx], ctx2)
+    for v, w in zip(dy, ctx2):
+        assert np.array_equal(v.numpy(), w.numpy())  # bit-identical to the unfused gemm_outer
+    y0 = dy[0].numpy()
+    # all terms positive: against the exactly rounded sum (the oracle's sequential sum has its own
+    # O(n eps) error here, larger than the GPU's tree-sum error)
+    assert abs(nrm2 - math.fsum(y0 * y0)) <= red_tol(y0 * y0)
 
 
 def test_gemm_outer_rejects_aliasing(ctx):
