@@ -111,6 +111,11 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
  * reference util/gemm.h:186-203 (distributed) and :257-265 (pairwise default) */
 int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
                    size_t n);
+/* yy[j] = sum_i alphas[i*m + j] * xx[i]: ssp_fill(0) on every destination followed by ssp_gemm_outer,
+ * bit-identical, in one pass that does not read the destinations (construct_solution,
+ * reference IterativeSolverTemplate.h:33-65).  k = 0 zero-fills. */
+int ssp_gemm_outer_set(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
+                       size_t n);
 /* Fused modified-Gram-Schmidt step: yy[j] += c[j] * x, then out[j] = <yy[j], z> summed over ranks.
  * Equals ssp_gemm_outer({x} -> yy) followed by ssp_gemm_inner(yy, {z}) with bit-identical yy; one
  * pass over yy (reference propose_rspace.h:430-443 issues them as separate handler calls). */
@@ -162,6 +167,15 @@ int ssp_gemm_inner_sparse(ssp_ctx* ctx, const double* const* xx, int m, size_t n
 /* yy[j] += sum_i alphas[i*m + j] * p_i; p_i = entries [ptr[i], ptr[i+1]). */
 int ssp_gemm_outer_sparse(ssp_ctx* ctx, const double* alphas, const size_t* ptr, const size_t* idx,
                           const double* val, int k, double* const* yy, int m, size_t n, size_t offset);
+
+/* construct_solution (reference IterativeSolverTemplate.h:33-65: fill(0), then gemm_outer over the
+ * P, Q and D spaces) in one pass that does not read the destinations:
+ *   yy[j] = sum_i palphas[i*m + j] p_i  +  sum_s alphas[s*m + j] xx[s]
+ * with P = CSR (ptr, idx, val) of kp sparse vectors (global indices), bit-identical to
+ * ssp_fill(0) + ssp_gemm_outer_sparse + ssp_gemm_outer (Q and D sources concatenated). */
+int ssp_construct_solution(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const size_t* idx,
+                           const double* val, int kp, const double* alphas, const double* const* xx, int k,
+                           double* const* yy, int m, size_t n, size_t offset);
 
 /* ---- synthetic problem (harness only; not a reference operation) ----------------------------
  * H = diag(1 + g) + rho * sum_{l<rank} u_l u_l^T, g = global index, u_0 = 1 and for l > 0

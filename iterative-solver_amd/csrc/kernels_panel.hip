@@ -123,6 +123,7 @@ struct OuterArgs {
   double* y[ssp::kOuterDst];
   int k;
   int m;
+  int set;  // 1: yy[j] = sum (destinations not read: fill(0) + gemm_outer in one pass)
   size_t n;
   double alpha[ssp::kOuterAlpha];  // alpha[i*m + j]
 };
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int j = 0; j < M; ++j) acc[u][j] = (j < a.m && ok[u]) ? ld2nt(a.y[j] + 2 * (p0 + 64 * u)) : z2;
+      for (int j = 0; j < M; ++j) acc[u][j] = (j < a.m && ok[u] && !a.set) ? ld2nt(a.y[j] + 2 * (p0 + 64 * u)) : z2;
     int i = 0;
     for (; i + 4 <= a.k; i += 4) {
       double2 xv[4][U];
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
   if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x < a.m) {
     const size_t e = a.n - 1;
     const int j = threadIdx.x;
-    double v = a.y[j][e];
+    double v = a.set ? 0.0 : a.y[j][e];
     for (int i = 0; i < a.k; ++i) v = fma(a.alpha[i * a.m + j], a.x[i][e], v);
     a.y[j][e] = v;
   }
@@ -492,10 +493,17 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
   return SSP_OK;
 }
 
-int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
-                   size_t n) {
+}  // extern "C"
+
+namespace {
+int gemm_outer_impl(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
+                    size_t n, bool set) {
   SSP_CHECK_CTX(ctx);
   if (m < 0 || k < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_outer: negative dimension");
+  if (set && k == 0) {
+    for (int j = 0; j < m; ++j) SSP_TRY(ssp_fill(ctx, 0.0, yy[j], n));
+    return SSP_OK;
+  }
   if (m == 0 || k == 0 || n == 0) return SSP_OK;
   if (!alphas) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_outer: null alphas");
   SSP_TRY(check_ptrs(xx, k, n, "ssp_gemm_outer"));
@@ -505,7 +513,7 @@ int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, 
       if (yy[j] == xx[i]) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_outer: a destination aliases a source");
   // Destinations are independent; sources are applied in increasing order, in groups that fit
   // the kernel argument block, so each destination sees the reference's summation order.
-  ssp::LedgerScope ls(ctx, "gemm_outer", 8.0 * n * (k + 2.0 * m));
+  ssp::LedgerScope ls(ctx, set ? "gemm_outer_set" : "gemm_outer", 8.0 * n * (k + (set ? 1.0 : 2.0) * m));
   for (int j0 = 0; j0 < m; j0 += ssp::kOuterDst) {
     const int mm = std::min(ssp::kOuterDst, m - j0);
     const int kmax = std::max(1, std::min(ssp::kOuterSrc, ssp::kOuterAlpha / mm));
@@ -513,6 +521,7 @@ int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, 
       OuterArgs a{};
       a.m = mm;
       a.k = std::min(kmax, k - i0);
+      a.set = (set && i0 == 0) ? 1 : 0;
       a.n = n;
       for (int i = 0; i < a.k; ++i) a.x[i] = xx[i0 + i];
       for (int j = 0; j < mm; ++j) a.y[j] = yy[j0 + j];
@@ -522,6 +531,19 @@ int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, 
     }
   }
   return SSP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
+                   size_t n) {
+  return gemm_outer_impl(ctx, alphas, xx, k, yy, m, n, false);
+}
+
+int ssp_gemm_outer_set(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
+                       size_t n) {
+  return gemm_outer_impl(ctx, alphas, xx, k, yy, m, n, true);
 }
 
 int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* yy, int m, size_t n, double* out) {

@@ -70,6 +70,42 @@ __global__ void k_sparse_outer(const SparseOuterArgs a) {
   }
 }
 
+// construct_solution fix-up at the indices the P vectors touch: the dense pass (ssp_gemm_outer_set)
+// summed Q and D from zero there, the reference sums P first.  One lane per (index, destination)
+// recomputes the reference's sequence: v = 0; v += alpha(i,j) * p_i[idx] for P vectors i and their
+// entries in order (no contraction); then v = fma(beta(s,j), x_s[idx], v) for the dense sources s in
+// order, the arithmetic of k_gemm_outer.
+struct ConstructFixArgs {
+  const unsigned long long* uidx;  // distinct local indices touched by P
+  size_t nu;
+  int m;
+  int kp;
+  int k;
+  const unsigned long long* ptr;   // kp+1 offsets into li/v
+  const unsigned long long* li;
+  const double* v;
+  const double* palpha;            // kp x m
+  const double* alpha;             // k x m
+  const double* const* x;          // k dense sources
+  double* const* y;                // m destinations
+};
+
+__global__ void k_construct_fixup(const ConstructFixArgs a) {
+  const size_t t = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= a.nu * size_t(a.m)) return;
+  const size_t u = t / a.m;
+  const int j = int(t % a.m);
+  const unsigned long long g = a.uidx[u];
+  double v = 0;
+  for (int i = 0; i < a.kp; ++i) {
+    const double al = a.palpha[size_t(i) * a.m + j];
+    for (unsigned long long e = a.ptr[i]; e < a.ptr[i + 1]; ++e)
+      if (a.li[e] == g) v += al * a.v[e];
+  }
+  for (int s = 0; s < a.k; ++s) v = fma(a.alpha[size_t(s) * a.m + j], a.x[s][g], v);
+  a.y[j][g] = v;
+}
+
 // Local entries of one sparse vector: indices in [offset, offset+n), converted to local indices.
 void filter_local(const size_t* idx, const double* val, size_t nnz, size_t n, size_t offset,
                   std::vector<unsigned long long>& li, std::vector<double>& lv) {
@@ -221,6 +257,57 @@ int ssp_gemm_outer_sparse(ssp_ctx* ctx, const double* alphas, const size_t* ptr,
     hipLaunchKernelGGL(k_sparse_outer, dim3(1), dim3(64), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
+  return SSP_OK;
+}
+
+int ssp_construct_solution(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const size_t* idx,
+                           const double* val, int kp, const double* alphas, const double* const* xx, int k,
+                           double* const* yy, int m, size_t n, size_t offset) {
+  SSP_CHECK_CTX(ctx);
+  if (m < 0 || k < 0 || kp < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_construct_solution: negative dimension");
+  if (m == 0) return SSP_OK;
+  if (kp > 0 && (!palphas || !ptr)) return ssp::set_error(SSP_ERR_ARG, "ssp_construct_solution: null P argument");
+  SSP_TRY(ssp_gemm_outer_set(ctx, alphas, xx, k, yy, m, n));
+  if (kp == 0 || n == 0) return SSP_OK;
+  std::vector<unsigned long long> lptr{0}, li;
+  std::vector<double> lv;
+  for (int i = 0; i < kp; ++i) {
+    SSP_TRY(check_entries(idx + ptr[i], val + ptr[i], ptr[i + 1] - ptr[i], "ssp_construct_solution"));
+    filter_local(idx + ptr[i], val + ptr[i], ptr[i + 1] - ptr[i], n, offset, li, lv);
+    lptr.push_back(li.size());
+  }
+  if (li.empty()) return SSP_OK;
+  std::vector<unsigned long long> uidx(li);
+  std::sort(uidx.begin(), uidx.end());
+  uidx.erase(std::unique(uidx.begin(), uidx.end()), uidx.end());
+  ConstructFixArgs a{};
+  unsigned long long *dptr, *dli;
+  double* dv;
+  SSP_TRY(upload_entries(ctx, lptr, li, lv, &dptr, &dli, &dv));
+  a.ptr = dptr;
+  a.li = dli;
+  a.v = dv;
+  void* p;
+  SSP_TRY(ssp::upload_small(ctx, uidx.data(), uidx.size() * sizeof(unsigned long long), &p));
+  a.uidx = static_cast<const unsigned long long*>(p);
+  SSP_TRY(ssp::upload_small(ctx, palphas, size_t(kp) * m * sizeof(double), &p));
+  a.palpha = static_cast<const double*>(p);
+  if (k > 0) {
+    SSP_TRY(ssp::upload_small(ctx, alphas, size_t(k) * m * sizeof(double), &p));
+    a.alpha = static_cast<const double*>(p);
+    SSP_TRY(ssp::upload_small(ctx, xx, size_t(k) * sizeof(double*), &p));
+    a.x = static_cast<const double* const*>(p);
+  }
+  SSP_TRY(ssp::upload_small(ctx, yy, size_t(m) * sizeof(double*), &p));
+  a.y = static_cast<double* const*>(p);
+  a.nu = uidx.size();
+  a.m = m;
+  a.kp = kp;
+  a.k = k;
+  ssp::LedgerScope ls(ctx, "sparse", 8.0 * a.nu * m * (2.0 + k));
+  const size_t threads = a.nu * size_t(m);
+  hipLaunchKernelGGL(k_construct_fixup, dim3(unsigned((threads + 255) / 256)), dim3(256), 0, ctx->stream, a);
+  SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
 

@@ -180,6 +180,16 @@ bool fused_axpy_inner(H&, const std::vector<double>&, const Q&, const RefR&, con
   return false;
 }
 
+// Hook for construct_solution (reference IterativeSolverTemplate.h:33-65: fill(0), then gemm_outer
+// over the P, Q and D spaces) as one pass that writes the destinations without reading them:
+// returns false when the handler has no such form.  `hp` is the R x P handler; the Q and D
+// sources arrive concatenated (`qd`, coefficients `cqd`).  Found by argument-dependent lookup.
+template <class HP, class RefP, class RefQ, class RefR>
+bool fused_construct_solution(HP&, const Matrix<double>&, const RefP&, const Matrix<double>&, const RefQ&,
+                              const RefR&) {
+  return false;
+}
+
 // Hook for a fused sequential self-orthonormalisation of R (reference propose_rspace.h:450-465):
 // returns false when the handler has no fused form (the caller then runs the reference loop of
 // dot / scal / dot / axpy calls).  Found by argument-dependent lookup.

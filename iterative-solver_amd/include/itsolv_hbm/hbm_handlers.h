@@ -389,6 +389,27 @@ inline bool fused_axpy_inner(array::ArrayHandler<Vec, Vec>&, const std::vector<d
   return true;
 }
 
+// construct_solution as one pass (array::fused_construct_solution hook): ssp_construct_solution
+// writes the destinations without reading them, bit-identical to fill(0) + the three gemm_outer.
+inline bool fused_construct_solution(array::ArrayHandler<Vec, SparseP>&, const itsolv::subspace::Matrix<double>& cp,
+                                     const itsolv::CVecRef<SparseP>& pp, const itsolv::subspace::Matrix<double>& cqd,
+                                     const itsolv::CVecRef<Vec>& qd, const itsolv::VecRef<Vec>& yy) {
+  if (yy.empty() || cqd.cols() > yy.size() || cqd.rows() != qd.size() || cp.rows() != pp.size() ||
+      (!pp.empty() && cp.cols() != cqd.cols()))
+    return false;
+  std::vector<size_t> ptr{0}, idx;
+  std::vector<double> val;
+  if (!pp.empty()) detail::pack(pp, ptr, idx, val);
+  auto xp = detail::cptrs(qd);
+  auto yp = detail::mptrs(yy);
+  const auto& y0 = yy.front().get();
+  check(ssp_construct_solution(y0.ctx(), cp.data().data(), ptr.data(), idx.data(), val.data(), int(pp.size()),
+                               cqd.data().data(), xp.data(), int(qd.size()), yp.data(), int(cqd.cols()),
+                               y0.local_size(), y0.offset()),
+        "ssp_construct_solution");
+  return true;
+}
+
 // Sequential self-orthonormalisation of R (reference propose_rspace.h:450-465) in two passes per
 // vector: ssp_scal_inner (r_i *= 1/|r_i|, then <r_i, r_j> for j > i) and ssp_axpy_norm
 // (r_j -= <r_i, r_j> r_i for j > i, then |r_{i+1}|^2).  The vector updates are the reference loop's

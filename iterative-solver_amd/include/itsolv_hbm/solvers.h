@@ -83,6 +83,20 @@ void construct_solution(const VecRef<R>& params, const std::vector<int>& roots, 
                         const CVecRef<P>& pp, const CVecRef<Q>& qp, const CVecRef<Q>& dp, size_t oP, size_t oQ,
                         size_t oD, ArrayHandlers<R, Q, P>& h) {
   if (roots.empty()) return;
+  {
+    // Handlers with a one-pass form write the solutions without reading them: each destination
+    // still sums its sources from zero in the order P, Q, D.
+    Matrix<double> cp({pp.size(), roots.size()}), cqd({qp.size() + dp.size(), roots.size()});
+    for (size_t i = 0; i < roots.size(); ++i) {
+      for (size_t j = 0; j < pp.size(); ++j) cp(j, i) = sol(roots[i], oP + j);
+      for (size_t j = 0; j < qp.size(); ++j) cqd(j, i) = sol(roots[i], oQ + j);
+      for (size_t j = 0; j < dp.size(); ++j) cqd(qp.size() + j, i) = sol(roots[i], oD + j);
+    }
+    CVecRef<Q> qd(qp.begin(), qp.end());
+    qd.insert(qd.end(), dp.begin(), dp.end());
+    using array::fused_construct_solution;
+    if (fused_construct_solution(h.rp(), cp, pp, cqd, qd, params)) return;
+  }
   for (size_t i = 0; i < roots.size(); ++i) h.rr().fill(0, params.at(i));
   Matrix<double> cp({pp.size(), roots.size()}), cq({qp.size(), roots.size()}), cd({dp.size(), roots.size()});
   for (size_t i = 0; i < roots.size(); ++i) {

@@ -35,8 +35,9 @@ EXPORTS = [
     "ssp_allreduce_sum", "ssp_allgather_host", "ssp_ctx_attach_host_comm", "ssp_shard_range", "ssp_select_merge",
     "ssp_ledger_enable", "ssp_ledger_reset", "ssp_ledger_count",
     "ssp_ledger_entry", "ssp_fill", "ssp_scal", "ssp_copy", "ssp_axpy", "ssp_dot",
-    "ssp_gemm_inner", "ssp_gemm_outer", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_precondition", "ssp_select", "ssp_select_max_dot",
+    "ssp_gemm_inner", "ssp_gemm_outer", "ssp_gemm_outer_set", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_precondition", "ssp_select", "ssp_select_max_dot",
     "ssp_sparse_copy", "ssp_sparse_axpy", "ssp_sparse_dot", "ssp_gemm_inner_sparse", "ssp_gemm_outer_sparse",
+    "ssp_construct_solution",
     "sspx_synthetic_action", "sspx_synthetic_add_lowrank", "sspx_synthetic_diagonal", "sspx_fill_random", "sspx_dense_action",
 ]
 
@@ -107,6 +108,7 @@ def _declare(lib):
         "ssp_dot": (I, [P, P, P, Z, PD]),
         "ssp_gemm_inner": (I, [P, P, I, P, I, Z, PD]),
         "ssp_gemm_outer": (I, [P, PD, P, I, P, I, Z]),
+        "ssp_gemm_outer_set": (I, [P, PD, P, I, P, I, Z]),
         "ssp_axpy_inner": (I, [P, PD, P, P, I, P, Z, PD]),
         "ssp_scal_inner": (I, [P, C.c_double, P, P, I, Z, PD]),
         "ssp_axpy_norm": (I, [P, PD, P, P, I, Z, PD]),
@@ -118,6 +120,7 @@ def _declare(lib):
         "ssp_sparse_dot": (I, [P, P, Z, Z, PZ, PD, Z, PD]),
         "ssp_gemm_inner_sparse": (I, [P, P, I, Z, Z, PZ, PZ, PD, I, PD]),
         "ssp_gemm_outer_sparse": (I, [P, PD, PZ, PZ, PD, I, P, I, Z, Z]),
+        "ssp_construct_solution": (I, [P, PD, PZ, PZ, PD, I, PD, P, I, P, I, Z, Z]),
         "sspx_synthetic_action": (I, [P, P, P, I, Z, Z, D, I, C.c_ulonglong]),
         "sspx_synthetic_add_lowrank": (I, [P, P, I, Z, Z, D, I, C.c_ulonglong, PD]),
         "sspx_synthetic_diagonal": (I, [P, P, Z, Z, D, I]),
@@ -480,6 +483,12 @@ class Context:
         n = yy[0].n if m else 0
         _check(self.lib.ssp_gemm_outer(self.handle, _dptr(alphas), _ptrs(xx), k, _ptrs(yy), m, n))
 
+    def gemm_outer_set(self, alphas: np.ndarray, xx: Sequence[DeviceVector], yy: Sequence[DeviceVector]):
+        """yy[j] = sum_i alphas[i, j] xx[i] (fill(0) + gemm_outer in one pass)."""
+        alphas = np.ascontiguousarray(alphas, dtype=np.float64).reshape(len(xx), len(yy))
+        n = yy[0].n if yy else 0
+        _check(self.lib.ssp_gemm_outer_set(self.handle, _dptr(alphas), _ptrs(xx), len(xx), _ptrs(yy), len(yy), n))
+
     def axpy_inner(self, c: Sequence[float], x: DeviceVector, yy: Sequence[DeviceVector], z: DeviceVector) -> np.ndarray:
         """yy[j] += c[j] x, then returns <yy[j], z> (fused MGS step)."""
         cc = np.ascontiguousarray(c, dtype=np.float64)
@@ -557,6 +566,18 @@ class Context:
         _check(self.lib.ssp_gemm_inner_sparse(self.handle, _ptrs(xx), m, n, offset, _zptr(ptr), _zptr(idx),
                                               _dptr(val), k, _dptr(out)))
         return out
+
+    def construct_solution(self, palphas: np.ndarray, ps: Sequence[dict], alphas: np.ndarray,
+                           xx: Sequence[DeviceVector], yy: Sequence[DeviceVector], offset: int = 0):
+        """yy[j] = sum_i palphas[i, j] p_i + sum_s alphas[s, j] xx[s] (fill(0) + sparse and dense
+        gemm_outer in one pass, reference construct_solution)."""
+        m = len(yy)
+        pa = np.ascontiguousarray(palphas, dtype=np.float64).reshape(len(ps), m)
+        al = np.ascontiguousarray(alphas, dtype=np.float64).reshape(len(xx), m)
+        ptr, idx, val = self._pack_sparse(ps)
+        n = yy[0].n if m else 0
+        _check(self.lib.ssp_construct_solution(self.handle, _dptr(pa), _zptr(ptr), _zptr(idx), _dptr(val), len(ps),
+                                               _dptr(al), _ptrs(xx), len(xx), _ptrs(yy), m, n, offset))
 
     def gemm_outer_sparse(self, alphas: np.ndarray, ps: Sequence[dict], yy: Sequence[DeviceVector], offset: int = 0):
         ptr, idx, val = self._pack_sparse(ps)

@@ -168,6 +168,22 @@ int ssp_gemm_inner(ssp_ctx* c, const double* const* xx, int m, const double* con
     }
   return reduce(c, out, size_t(m) * k);
 }
+int ssp_gemm_outer_sparse(ssp_ctx*, const double* alphas, const size_t* ptr, const size_t* idx, const double* val,
+                          int k, double* const* yy, int m, size_t n, size_t offset);
+int ssp_construct_solution(ssp_ctx* c, const double* palphas, const size_t* ptr, const size_t* idx,
+                           const double* val, int kp, const double* alphas, const double* const* xx, int k,
+                           double* const* yy, int m, size_t n, size_t offset) {
+  for (int j = 0; j < m; ++j)
+    for (size_t e = 0; e < n; ++e) yy[j][e] = 0;
+  if (kp > 0) ssp_gemm_outer_sparse(c, palphas, ptr, idx, val, kp, yy, m, n, offset);
+  return ssp_gemm_outer(c, alphas, xx, k, yy, m, n);
+}
+int ssp_gemm_outer_set(ssp_ctx* c, const double* al, const double* const* xx, int k, double* const* yy, int m,
+                       size_t n) {
+  for (int j = 0; j < m; ++j)
+    for (size_t e = 0; e < n; ++e) yy[j][e] = 0;
+  return ssp_gemm_outer(c, al, xx, k, yy, m, n);
+}
 int ssp_gemm_outer(ssp_ctx*, const double* al, const double* const* xx, int k, double* const* yy, int m, size_t n) {
   for (int j = 0; j < m; ++j)
     for (int i = 0; i < k; ++i) {

@@ -157,6 +157,51 @@ def test_scal_inner_and_axpy_norm_fused_orthonormalisation(ctx, m, n):
     assert abs(nrm2 - math.fsum(y0 * y0)) <= red_tol(y0 * y0)
 
 
+@pytest.mark.parametrize("k,m", [(0, 3), (1, 1), (48, 8), (60, 8), (5, 16), (65, 17)])
+@pytest.mark.parametrize("n", [1, 1003, 100_003])
+def test_gemm_outer_set_equals_fill_then_gemm_outer(ctx, k, m, n):
+    r = rng(k * 100 + m + n)
+    xs = [r.uniform(-1, 1, n) for _ in range(k)]
+    al = r.uniform(-1, 1, (k, m))
+    dx = [ctx.upload(v) for v in xs]
+    a = [ctx.upload(r.uniform(-1, 1, n)) for _ in range(m)]  # garbage the set form must not read
+    b = [ctx.upload(r.uniform(-1, 1, n)) for _ in range(m)]
+    ctx.gemm_outer_set(al, dx, a)
+    for v in b:
+        ctx.fill(0.0, v)
+    if k:
+        ctx.gemm_outer(al, dx, b)
+    for u, v in zip(a, b):
+        assert np.array_equal(u.numpy(), v.numpy())
+
+
+@pytest.mark.parametrize("nq,np_", [(0, 0), (5, 0), (48, 0), (0, 3), (6, 4), (56, 16)])
+def test_construct_solution_one_pass_bit_exact(ctx, nq, np_):
+    # ssp_construct_solution == fill(0) + gemm_outer_sparse(P) + gemm_outer(Q+D), bit for bit,
+    # including P entries shared by several P vectors and entries outside the shard.
+    n, off, m = 100_003, 1000, 8
+    r = rng(nq * 31 + np_)
+    xs = [r.uniform(-1, 1, n) for _ in range(nq)]
+    ps = [{off + int(i): 1.0} for i in r.choice(n, np_, replace=False)]
+    if np_ >= 2:
+        ps[1][next(iter(ps[0]))] = 0.5  # an index shared with p_0
+        ps[-1][off + n + 7] = 2.0  # outside this shard
+        ps[-1][off - 1] = 3.0
+    pal, al = r.uniform(-1, 1, (np_, m)), r.uniform(-1, 1, (nq, m))
+    dx = [ctx.upload(v) for v in xs]
+    a = [ctx.upload(r.uniform(-1, 1, n)) for _ in range(m)]
+    b = [ctx.alloc(n) for _ in range(m)]
+    ctx.construct_solution(pal, ps, al, dx, a, offset=off)
+    for v in b:
+        ctx.fill(0.0, v)
+    if np_:
+        ctx.gemm_outer_sparse(pal, ps, b, offset=off)
+    if nq:
+        ctx.gemm_outer(al, dx, b)
+    for u, v in zip(a, b):
+        assert np.array_equal(u.numpy(), v.numpy())
+
+
 def test_gemm_outer_rejects_aliasing(ctx):
     import subspace_hip as sh
 
