@@ -222,7 +222,8 @@ def main():
             ctx.attach_host_comm(sh.HubComm(rank, world, os.environ.get("MASTER_ADDR", "127.0.0.1"), port))
     else:
         uid, uid_path = rendezvous_uid(rank, world) if world > 1 else (None, None)
-        ctx = sh.Context(local_rank)
+        # one GPU per rank; a launcher that narrows HIP_VISIBLE_DEVICES per rank leaves one visible
+        ctx = sh.Context(local_rank % max(1, sh.device_count()))
         if world > 1:
             ctx.attach_comm(world, rank, uid)  # collective: returns once every rank has joined
             if uid_path:
