@@ -125,7 +125,8 @@ struct OuterArgs {
   int m;
   int set;  // 1: yy[j] = sum (destinations not read: fill(0) + gemm_outer in one pass)
   size_t n;
-  double alpha[ssp::kOuterAlpha];  // alpha[i*m + j]
+  const double* alpha_dev;         // k*m > kOuterAlpha: alpha[i*m + j] in device memory
+  double alpha[ssp::kOuterAlpha];  // alpha[i*m + j] in the argument block
 };
 static_assert(sizeof(OuterArgs) <= 4000, "kernel argument block too large");
 
@@ -137,10 +138,14 @@ static_assert(sizeof(OuterArgs) <= 4000, "kernel argument block too large");
 // lane and plain accesses).
 constexpr int kOuterWin = 4;
 
-template <int M>
+template <int M, bool DEV>
 __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
   using ssp::ld2nt;
   using ssp::st2nt;
+  // Device-resident alphas are read through the constant address space (scalar loads, as the
+  // argument block's are): they are uniform across the wave and read-only in the kernel.
+  using cdouble = const __attribute__((address_space(4))) double;
+  const auto alpha = [&](int idx) { return DEV ? ((cdouble*)a.alpha_dev)[idx] : a.alpha[idx]; };
   constexpr int U = M > 8 ? 2 : kOuterWin;  // 16 destinations: 2 windows keep 2 waves per SIMD
   const int lane = threadIdx.x & 63;
   const size_t gw = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
@@ -169,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
 #pragma unroll
         for (int j = 0; j < M; ++j) {
           if (j < a.m) {
-            const double al = a.alpha[(i + b) * a.m + j];
+            const double al = alpha((i + b) * a.m + j);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
               acc[u][j].x = fma(al, xv[b][u].x, acc[u][j].x);
@@ -185,7 +190,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
 #pragma unroll
       for (int j = 0; j < M; ++j) {
         if (j < a.m) {
-          const double al = a.alpha[i * a.m + j];
+          const double al = alpha(i * a.m + j);
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             acc[u][j].x = fma(al, xv[u].x, acc[u][j].x);
@@ -205,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
     const size_t e = a.n - 1;
     const int j = threadIdx.x;
     double v = a.set ? 0.0 : a.y[j][e];
-    for (int i = 0; i < a.k; ++i) v = fma(a.alpha[i * a.m + j], a.x[i][e], v);
+    for (int i = 0; i < a.k; ++i) v = fma(alpha(i * a.m + j), a.x[i][e], v);
     a.y[j][e] = v;
   }
 }
@@ -377,8 +382,10 @@ int check_ptrs(const double* const* v, int count, size_t n, const char* what) {
   return SSP_OK;
 }
 
-// Column groups per launch for MG row groups (accumulator registers: MG * NG doubles per lane).
-constexpr int ng_max(int mg) { return mg == 1 ? 16 : mg == 2 ? 12 : mg == 3 ? 8 : 6; }
+// Column groups per launch for MG row groups (accumulator registers: MG * NG doubles per lane):
+// 16 (64 columns, the launch maximum) for every row-group count, so one launch reads every vector
+// once (tools/mb_inner.hip: 16 x 64 at 5.9 TB/s in one launch against 4.3 TB/s in three).
+constexpr int ng_max(int) { return 16; }
 
 // Workgroups per gemm_inner launch: 4 per CU (16 waves) when n allows, else one wave per chunk.
 unsigned inner_grid(const ssp_ctx* ctx, size_t n) {
@@ -422,18 +429,26 @@ int launch_inner(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
   }
 }
 
+template <bool DEV>
+void launch_outer_t(ssp_ctx* ctx, unsigned grid, const OuterArgs& a) {
+  if (a.m <= 1)
+    hipLaunchKernelGGL((k_gemm_outer<1, DEV>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  else if (a.m <= 2)
+    hipLaunchKernelGGL((k_gemm_outer<2, DEV>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  else if (a.m <= 4)
+    hipLaunchKernelGGL((k_gemm_outer<4, DEV>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  else if (a.m <= 8)
+    hipLaunchKernelGGL((k_gemm_outer<8, DEV>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  else
+    hipLaunchKernelGGL((k_gemm_outer<16, DEV>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+}
+
 int launch_outer(ssp_ctx* ctx, const OuterArgs& a) {
   const unsigned grid = ssp::stream_grid(ctx, a.n / 2 + 1, kOuterWin);
-  if (a.m <= 1)
-    hipLaunchKernelGGL((k_gemm_outer<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
-  else if (a.m <= 2)
-    hipLaunchKernelGGL((k_gemm_outer<2>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
-  else if (a.m <= 4)
-    hipLaunchKernelGGL((k_gemm_outer<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
-  else if (a.m <= 8)
-    hipLaunchKernelGGL((k_gemm_outer<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  if (a.alpha_dev)
+    launch_outer_t<true>(ctx, grid, a);
   else
-    hipLaunchKernelGGL((k_gemm_outer<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    launch_outer_t<false>(ctx, grid, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -516,17 +531,27 @@ int gemm_outer_impl(ssp_ctx* ctx, const double* alphas, const double* const* xx,
   ssp::LedgerScope ls(ctx, set ? "gemm_outer_set" : "gemm_outer", 8.0 * n * (k + (set ? 1.0 : 2.0) * m));
   for (int j0 = 0; j0 < m; j0 += ssp::kOuterDst) {
     const int mm = std::min(ssp::kOuterDst, m - j0);
-    const int kmax = std::max(1, std::min(ssp::kOuterSrc, ssp::kOuterAlpha / mm));
-    for (int i0 = 0; i0 < k; i0 += kmax) {
+    // Up to kOuterSrc sources per launch; their alphas ride in the argument block when they fit,
+    // else in device memory (one upload), so every destination is read and written once per
+    // kOuterSrc sources.
+    for (int i0 = 0; i0 < k; i0 += ssp::kOuterSrc) {
       OuterArgs a{};
       a.m = mm;
-      a.k = std::min(kmax, k - i0);
+      a.k = std::min(ssp::kOuterSrc, k - i0);
       a.set = (set && i0 == 0) ? 1 : 0;
       a.n = n;
       for (int i = 0; i < a.k; ++i) a.x[i] = xx[i0 + i];
       for (int j = 0; j < mm; ++j) a.y[j] = yy[j0 + j];
+      const bool dev = a.k * mm > ssp::kOuterAlpha;
+      std::vector<double> block(dev ? size_t(a.k) * mm : 0);
+      double* dst = dev ? block.data() : a.alpha;
       for (int i = 0; i < a.k; ++i)
-        for (int j = 0; j < mm; ++j) a.alpha[i * mm + j] = alphas[size_t(i0 + i) * m + j0 + j];
+        for (int j = 0; j < mm; ++j) dst[i * mm + j] = alphas[size_t(i0 + i) * m + j0 + j];
+      if (dev) {
+        void* p;
+        SSP_TRY(ssp::upload_small(ctx, block.data(), block.size() * sizeof(double), &p));
+        a.alpha_dev = static_cast<const double*>(p);
+      }
       SSP_TRY(launch_outer(ctx, a));
     }
   }

@@ -205,6 +205,36 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&a.partial, 8192 * 256 * 8));
   const double bytes = 8.0 * n * (m + k);
   auto report = [&](const char* name, float ms) { printf("%-28s %8.3f ms  %7.1f GB/s\n", name, ms, bytes / ms / 1e6); };
+  if (m == 16 && k == 64) {
+    // 16 x 64: one launch with 16 column groups vs the library's three (6 + 6 + 4 groups)
+    for (int rep = 0; rep < 2; ++rep)
+      for (int grid : {1024, 2048}) {
+        char nm[64];
+        snprintf(nm, 64, "v3 MG4 NG16 1 launch g=%d", grid);
+        report(nm, timeit([&] { hipLaunchKernelGGL((k_v3<4, 16, 1>), dim3(grid), dim3(256), 0, 0, a); }, 5));
+        snprintf(nm, 64, "v3 MG4 NG8 2 launches g=%d", grid);
+        report(nm, timeit([&] {
+                 Args b = a;
+                 for (int h = 0; h < 2; ++h) {
+                   b.k = 32;
+                   for (int j = 0; j < 32; ++j) b.y[j] = a.y[32 * h + j];
+                   hipLaunchKernelGGL((k_v3<4, 8, 1>), dim3(grid), dim3(256), 0, 0, b);
+                 }
+               }, 5));
+        snprintf(nm, 64, "v3 MG4 NG6 3 launches g=%d", grid);
+        report(nm, timeit([&] {
+                 Args b = a;
+                 const int c0[3] = {0, 24, 48}, kk[3] = {24, 24, 16};
+                 for (int h = 0; h < 3; ++h) {
+                   b.k = kk[h];
+                   for (int j = 0; j < kk[h]; ++j) b.y[j] = a.y[c0[h] + j];
+                   if (h < 2) hipLaunchKernelGGL((k_v3<4, 6, 1>), dim3(grid), dim3(256), 0, 0, b);
+                   else hipLaunchKernelGGL((k_v3<4, 4, 1>), dim3(grid), dim3(256), 0, 0, b);
+                 }
+               }, 5));
+      }
+    return 0;
+  }
   for (int grid : {512, 1024, 2048}) {
     char nm[64];
     snprintf(nm, 64, "read g=%d", grid);

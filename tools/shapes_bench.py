@@ -38,7 +38,7 @@ def main():
     cases = []
     for m, k in ((8, 48), (8, 1), (1, 6), (1, 48), (4, 24), (16, 64), (48, 8)):
         cases.append((f"gemm_inner {m}x{k}", "gemm_inner",
-                      lambda m=m, k=k: ctx.gemm_inner(pool[:m], pool[16:16 + k])))
+                      lambda m=m, k=k: ctx.gemm_inner(pool[:m], pool[m:m + k])))
     for k, m in ((48, 8), (1, 8), (6, 1), (8, 8), (24, 4), (64, 16)):
         al = rng.uniform(-0.1, 0.1, (k, m))
         cases.append((f"gemm_outer {k}->{m}", "gemm_outer",
