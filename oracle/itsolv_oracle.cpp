@@ -328,11 +328,165 @@ int diis(const P& problem, size_t n, const itsolv_options* opt, itsolv_result* o
   });
 }
 
+// Reverse-communication twin of include/iterative_solver_c.h over the CPU handlers: the same solver
+// construction and the same per-call routing as iterative-solver_amd/host/iterative_solver_c.cpp
+// (reference IterativeSolverCMPI.cpp:158-534), with host vectors.  Tests drive one loop through both
+// (problems defined in Python: Rosenbrock, trig, quadratic forms) and compare iteration by iteration.
+namespace it = molpro::linalg::itsolv;
+struct RcInstance {
+  std::unique_ptr<it::IterativeSolverTemplate<V, V, SP>> solver;
+  size_t n = 0;
+  std::vector<V> rp, ra;
+  VecRef<V> first(std::vector<V>& v, size_t k) {
+    VecRef<V> r;
+    for (size_t i = 0; i < k; ++i) r.emplace_back(v[i]);
+    return r;
+  }
+  void in(size_t k, const double* x, const double* g) {
+    while (rp.size() < k) {
+      rp.emplace_back(n, 0.0);
+      ra.emplace_back(n, 0.0);
+    }
+    for (size_t i = 0; i < k; ++i) {
+      std::memcpy(rp[i].data(), x + i * n, n * sizeof(double));
+      std::memcpy(ra[i].data(), g + i * n, n * sizeof(double));
+    }
+  }
+  void out(size_t k, double* x, double* g) {
+    for (size_t i = 0; i < k; ++i) {
+      std::memcpy(x + i * n, rp[i].data(), n * sizeof(double));
+      std::memcpy(g + i * n, ra[i].data(), n * sizeof(double));
+    }
+  }
+};
+
 }  // namespace
 
 extern "C" {
 
 const char* oracle_itsolv_last_error(void) { return g_error.c_str(); }
+
+// kind: "LinearEigensystem", "NonLinearEquations" (DIIS), "Optimize" (algorithm BFGS or SD),
+// "LinearEquations" (rhs: nroot x n).  Returns NULL on error (oracle_itsolv_last_error).
+void* oracle_rc_create(const char* kind, size_t n, size_t nroot, const double* rhs, double thresh, double thresh_value,
+                       int hermitian, const char* algorithm, const char* options) {
+  auto* h = new RcInstance;
+  h->n = n;
+  const std::string k = kind ? kind : "", alg = algorithm ? algorithm : "", opt = options ? options : "";
+  const int s = guarded([&] {
+    if (k == "LinearEigensystem") {
+      auto d = std::make_unique<it::LinearEigensystemDavidson<V, V, SP>>(cpu_handlers());
+      if (!opt.empty()) d->set_options(it::LinearEigensystemDavidsonOptions(it::parse_options(opt)));
+      d->set_n_roots(nroot);
+      d->set_hermiticity(hermitian != 0);
+      d->set_convergence_threshold(thresh);
+      d->set_convergence_threshold_value(thresh_value);
+      h->solver = std::move(d);
+    } else if (k == "NonLinearEquations") {
+      auto d = std::make_unique<it::NonLinearEquationsDIIS<V, V, SP>>(cpu_handlers());
+      if (!opt.empty()) d->set_options(it::NonLinearEquationsDIISOptions(it::parse_options(opt)));
+      d->set_convergence_threshold(thresh);
+      h->solver = std::move(d);
+    } else if (k == "Optimize") {
+      std::unique_ptr<it::IterativeSolverTemplate<V, V, SP>> d;
+      if (alg.empty() || alg == "BFGS") {
+        auto b = std::make_unique<it::OptimizeBFGS<V, V, SP>>(cpu_handlers());
+        if (!opt.empty()) b->set_options(it::OptimizeBFGSOptions(it::parse_options(opt)));
+        d = std::move(b);
+      } else if (alg == "SD") {
+        d = std::make_unique<it::OptimizeSD<V, V, SP>>(cpu_handlers());
+        if (!opt.empty()) d->set_options(it::Options(it::parse_options(opt)));
+      } else {
+        throw std::runtime_error("oracle_rc_create: unknown algorithm " + alg);
+      }
+      d->set_n_roots(1);
+      d->set_convergence_threshold(thresh);
+      d->set_convergence_threshold_value(thresh_value);
+      h->solver = std::move(d);
+    } else if (k == "LinearEquations") {
+      auto d = std::make_unique<it::LinearEquationsDavidson<V, V, SP>>(cpu_handlers());
+      std::vector<V> b;
+      for (size_t r = 0; r < nroot; ++r) b.emplace_back(rhs + r * n, rhs + (r + 1) * n);
+      if (!opt.empty()) d->set_options(it::LinearEquationsDavidsonOptions(it::parse_options(opt)));
+      d->set_hermiticity(hermitian != 0);
+      d->set_n_roots(nroot);
+      d->add_equations(b);
+      d->set_convergence_threshold(thresh);
+      d->set_convergence_threshold_value(thresh_value);
+      h->solver = std::move(d);
+    } else {
+      throw std::runtime_error("oracle_rc_create: unknown kind " + k);
+    }
+  });
+  if (s) {
+    delete h;
+    return nullptr;
+  }
+  return h;
+}
+
+void oracle_rc_destroy(void* h) { delete static_cast<RcInstance*>(h); }
+
+long long oracle_rc_add_vector(void* hp, size_t nbuf, double* x, double* g) {
+  auto& h = *static_cast<RcInstance*>(hp);
+  long long r = -1;
+  guarded([&] {
+    h.in(nbuf, x, g);
+    r = h.solver->nonlinear() && nbuf >= 1 ? (long long)h.solver->add_vector(h.rp[0], h.ra[0], 0.0)
+                                           : (long long)h.solver->add_vector(h.first(h.rp, nbuf), h.first(h.ra, nbuf));
+    h.out(nbuf, x, g);
+  });
+  return r;
+}
+
+long long oracle_rc_add_value(void* hp, double value, double* x, double* g) {
+  auto& h = *static_cast<RcInstance*>(hp);
+  long long r = -1;
+  guarded([&] {
+    h.in(1, x, g);
+    r = h.solver->add_vector(h.rp[0], h.ra[0], value) > 0 ? 1 : 0;
+    h.out(1, x, g);
+  });
+  return r;
+}
+
+long long oracle_rc_end_iteration(void* hp, size_t nbuf, double* x, double* g) {
+  auto& h = *static_cast<RcInstance*>(hp);
+  long long r = -1;
+  guarded([&] {
+    h.in(nbuf, x, g);
+    r = (long long)h.solver->end_iteration(h.first(h.rp, nbuf), h.first(h.ra, nbuf));
+    h.out(nbuf, x, g);
+  });
+  return r;
+}
+
+int oracle_rc_solution(void* hp, int nroot, const int* roots, double* x, double* g) {
+  auto& h = *static_cast<RcInstance*>(hp);
+  return guarded([&] {
+    h.in(size_t(nroot), x, g);
+    h.solver->solution(std::vector<int>(roots, roots + nroot), h.first(h.rp, size_t(nroot)),
+                       h.first(h.ra, size_t(nroot)));
+    h.out(size_t(nroot), x, g);
+  });
+}
+
+// iterations, r_creations, errors (nroot), value, eigenvalues (nroot; Davidson only)
+int oracle_rc_stats(void* hp, int* iterations, int* r_creations, double* errors, double* value, double* eigenvalues) {
+  auto& h = *static_cast<RcInstance*>(hp);
+  return guarded([&] {
+    const auto& st = h.solver->statistics();
+    *iterations = st.iterations;
+    *r_creations = st.r_creations;
+    size_t k = 0;
+    for (double e : h.solver->errors()) errors[k++] = e;
+    *value = h.solver->value();
+    if (auto* d = dynamic_cast<it::LinearEigensystemDavidson<V, V, SP>*>(h.solver.get())) {
+      k = 0;
+      for (double e : d->eigenvalues()) eigenvalues[k++] = e;
+    }
+  });
+}
 
 int oracle_davidson_synthetic(size_t n, double rho, int rank, unsigned long long seed, const itsolv_options* opt,
                               itsolv_result* out, double* solutions_out) {

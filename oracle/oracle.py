@@ -214,8 +214,74 @@ def itsolv_lib():
             f.restype = I
             f.argtypes = args
         L.oracle_itsolv_last_error.restype = C.c_char_p
+        P, LL = C.c_void_p, C.c_longlong
+        L.oracle_rc_create.restype = P
+        L.oracle_rc_create.argtypes = [C.c_char_p, Z, Z, PDd, D, D, I, C.c_char_p, C.c_char_p]
+        L.oracle_rc_destroy.argtypes = [P]
+        for name, args in {"oracle_rc_add_vector": [P, Z, PDd, PDd], "oracle_rc_add_value": [P, D, PDd, PDd],
+                           "oracle_rc_end_iteration": [P, Z, PDd, PDd]}.items():
+            getattr(L, name).restype = LL
+            getattr(L, name).argtypes = args
+        L.oracle_rc_solution.restype = I
+        L.oracle_rc_solution.argtypes = [P, I, C.POINTER(C.c_int), PDd, PDd]
+        L.oracle_rc_stats.restype = I
+        L.oracle_rc_stats.argtypes = [P, C.POINTER(I), C.POINTER(I), PDd, PDd, PDd]
         _itsolv = L
     return _itsolv
+
+
+class RcSolver:
+    """The reference CPU path behind the reverse-communication C API's call sequence
+    (oracle_rc_*: the same solver construction and routing as iterative_solver_c.cpp, CPU
+    handlers).  Method names and arguments follow iterative_solver.IterativeSolver."""
+
+    def __init__(self, kind, n, nroot=1, rhs=None, thresh=1e-10, thresh_value=1e50, hermitian=True, algorithm="",
+                 options=""):
+        L = itsolv_lib()
+        self.n, self.nroot = n, nroot
+        b = None if rhs is None else np.ascontiguousarray(rhs, dtype=np.float64)
+        self._h = L.oracle_rc_create(kind.encode(), n, nroot, None if b is None else _d(b), thresh, thresh_value,
+                                     int(hermitian), algorithm.encode(), options.encode())
+        if not self._h:
+            raise RuntimeError(L.oracle_itsolv_last_error().decode())
+        self._rhs = b
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            itsolv_lib().oracle_rc_destroy(self._h)
+            self._h = None
+
+    def _r(self, v):
+        if v < 0:
+            raise RuntimeError(itsolv_lib().oracle_itsolv_last_error().decode())
+        return int(v)
+
+    @staticmethod
+    def _nbuf(a):
+        return a.shape[0] if a.ndim > 1 else 1
+
+    def add_vector(self, parameters, action):
+        return self._r(itsolv_lib().oracle_rc_add_vector(self._h, self._nbuf(parameters), _d(parameters), _d(action)))
+
+    def add_value(self, value, parameters, action):
+        return self._r(itsolv_lib().oracle_rc_add_value(self._h, float(value), _d(parameters), _d(action)))
+
+    def end_iteration(self, parameters, residual):
+        return self._r(itsolv_lib().oracle_rc_end_iteration(self._h, self._nbuf(parameters), _d(parameters),
+                                                            _d(residual)))
+
+    def solution(self, roots, parameters, residual):
+        r = (C.c_int * max(1, len(roots)))(*roots)
+        if itsolv_lib().oracle_rc_solution(self._h, len(roots), r, _d(parameters), _d(residual)):
+            raise RuntimeError(itsolv_lib().oracle_itsolv_last_error().decode())
+
+    def stats(self):
+        it, rc = C.c_int(), C.c_int()
+        err, ev, val = np.zeros(max(1, self.nroot)), np.zeros(max(1, self.nroot)), np.zeros(1)
+        if itsolv_lib().oracle_rc_stats(self._h, C.byref(it), C.byref(rc), _d(err), _d(val), _d(ev)):
+            raise RuntimeError(itsolv_lib().oracle_itsolv_last_error().decode())
+        return {"iterations": it.value, "r_creations": rc.value, "errors": err[:self.nroot], "value": float(val[0]),
+                "eigenvalues": ev[:self.nroot]}
 
 
 def _solve(fn, args, nout):

@@ -1,0 +1,120 @@
+"""Reverse-communication loops of the reference's solver tests, written once and driven through
+either back end: oracle.RcSolver (the reference CPU path) or the iterative_solver package (the
+C API on the HIP handlers).  Each driver returns a trace (per-iteration return values and
+parameters) so the two paths can be compared step by step.
+
+Problems and loops follow the reference's tests:
+  quadratic form     test_Optimize.cpp:20-112 / test_NonLinearEquations.cpp:20-110
+                     (h = 1 + diag((i + 2) param), minimum / root at x = 1, start x = e_0)
+  Rosenbrock         test_Optimize.cpp:124-156
+  trig1d             test_Optimize.cpp:158-176, test_NonLinearEquations.cpp:252-270
+  trig (n = 1, 2)    test_NonLinearEquations.cpp:160-250 (calc, trigProblem)
+"""
+import numpy as np
+
+
+def quadratic_matrix(n, param):
+    h = np.ones((n, n))
+    h[np.diag_indices(n)] = (np.arange(n) + 2) * param
+    return h
+
+
+def quadratic_action(h, x, g):
+    """f = 0.5 (x - 1).h.(x - 1), g = h (x - 1) (test_Optimize.cpp:32-46)."""
+    d = x - 1.0
+    g[:] = h @ d
+    return 0.5 * d @ (h @ d)
+
+
+def loop_quadratic(solver, h, optimize, max_iter=1000):
+    """test_Optimize.cpp:60-88 (optimize) / test_NonLinearEquations.cpp:62-86 (DIIS)."""
+    n = h.shape[0]
+    x, g = np.zeros(n), np.zeros(n)
+    x[0] = 1.0
+    trace, nwork, n_iter = [], 1, 1
+    for _ in range(1, max_iter):
+        if nwork <= 0:
+            break
+        value = quadratic_action(h, x, g)
+        precon = solver.add_value(value, x, g) if optimize else solver.add_vector(x, g)
+        if precon > 0:
+            g /= np.diag(h)
+        nwork = solver.end_iteration(x, g)
+        trace.append((precon, nwork, x.copy()))
+        n_iter += 1
+    return trace, n_iter
+
+
+def rosenbrock(x, a=1.0, b=100.0):
+    """test_Optimize.cpp:124-133"""
+    f, f1 = 0.0, np.zeros_like(x)
+    for i in range(x.size - 1):
+        f += (a - x[i]) ** 2 + b * (x[i] ** 2 - x[i + 1]) ** 2
+        f1[i] -= 2 * (a - x[i])
+        f1[i] += 4 * b * x[i] * (x[i] ** 2 - x[i + 1])
+        f1[i + 1] -= 2 * b * (x[i] ** 2 - x[i + 1])
+    return f, f1
+
+
+def loop_rosenbrock(solver, n, max_iter=10000):
+    """test_Optimize.cpp:135-156: x = (-3, -4, ..., -4), preconditioner g / 2."""
+    x = np.full(n, -4.0)
+    x[0] = -3.0
+    g = np.zeros(n)
+    trace = []
+    for _ in range(max_iter):
+        value, g[:] = rosenbrock(x)
+        precon = solver.add_value(value, x, g) > 0
+        if precon:
+            g /= 2
+        nwork = solver.end_iteration(x, g)
+        trace.append((int(precon), nwork, x.copy()))
+        if nwork == 0:
+            break
+    return trace, x
+
+
+def loop_trig1d(solver, optimize, max_iter=100):
+    """test_Optimize.cpp:158-176 / test_NonLinearEquations.cpp:252-270: f = sin x, g = cos x, x = 1."""
+    x, g = np.ones(1), np.zeros(1)
+    trace = []
+    for _ in range(max_iter):
+        value = np.sin(x[0])
+        g[0] = np.cos(x[0])
+        precon = solver.add_value(value, x, g) if optimize else solver.add_vector(x, g)
+        nwork = solver.end_iteration(x, g)
+        trace.append((precon, nwork, x.copy()))
+        if nwork == 0:
+            break
+    return trace, x
+
+
+def trig_calc(x, g):
+    """test_NonLinearEquations.cpp:160-173"""
+    n = x.size
+    value = 0.0
+    couple = 1e-2
+    for i in range(n):
+        value += np.sin((i + 1) * x[i]) ** 2
+        g[i] = 2 * (i + 1) * np.sin((i + 1) * x[i]) * np.cos((i + 1) * x[i])
+        for j in range(n):
+            value += couple * x[i] * x[j]
+            g[i] += 2 * couple * x[j]
+    return value
+
+
+def loop_trig(solver, n, max_iter=100):
+    """test_NonLinearEquations.cpp:215-250 through IterativeSolverTemplate::solve's loop for a
+    non-linear problem (IterativeSolverTemplate.h:371-405): residual, add_vector, precondition when
+    asked, end_iteration.  The reference trigProblem's precondition divides a COPY of each residual
+    (`auto g = gr.get()`, :186), so it leaves the residual unchanged; so does this loop."""
+    x, g = np.full(n, 0.05), np.zeros(n)
+    trace = []
+    for _ in range(max_iter):
+        trig_calc(x, g)
+        nwork = solver.add_vector(x, g)
+        nwork = solver.end_iteration(x, g)
+        trace.append((nwork, x.copy()))
+        if nwork == 0:
+            break
+    return trace, x
