@@ -461,6 +461,50 @@ long long oracle_rc_end_iteration(void* hp, size_t nbuf, double* x, double* g) {
   return r;
 }
 
+// IterativeSolverAddP's twin: func(pcoeff (nvec x nP), actions (nvec rows of n), nvec, ranges).
+long long oracle_rc_add_p(void* hp, size_t nbuf, size_t nP, const size_t* offsets, const size_t* indices,
+                          const double* coefficients, const double* pp, double* x, double* g,
+                          void (*func)(const double*, double*, const size_t, const size_t*)) {
+  auto& h = *static_cast<RcInstance*>(hp);
+  long long r = -1;
+  guarded([&] {
+    h.in(nbuf, x, g);
+    std::vector<SP> pvectors(nP);
+    for (size_t p = 0; p < nP; ++p)
+      for (size_t k = offsets[p]; k < offsets[p + 1]; ++k) pvectors[p].emplace(indices[k], coefficients[k]);
+    const size_t npp = (h.solver->dimensions().oP + nP) * nP;
+    std::vector<double> ppm(pp, pp + npp);
+    // stored by the solver and called again from later add_vector / solution calls: capture by value
+    const size_t n = h.n;
+    auto apply = [n, func](const std::vector<std::vector<double>>& pvecs, const CVecRef<SP>&, const VecRef<V>& act) {
+      const size_t nu = pvecs.size();
+      std::vector<double> flat;
+      for (const auto& v : pvecs) flat.insert(flat.end(), v.begin(), v.end());
+      std::vector<size_t> ranges;
+      for (size_t k = 0; k < nu; ++k) {
+        ranges.push_back(0);
+        ranges.push_back(n);
+      }
+      std::vector<double> host(nu * n);
+      for (size_t k = 0; k < nu; ++k) std::memcpy(host.data() + k * n, act[k].get().data(), n * sizeof(double));
+      func(flat.data(), host.data(), nu, ranges.data());
+      for (size_t k = 0; k < nu; ++k) std::memcpy(act[k].get().data(), host.data() + k * n, n * sizeof(double));
+    };
+    r = (long long)h.solver->add_p(molpro::linalg::itsolv::cwrap(pvectors), ppm, h.first(h.rp, nbuf),
+                                   h.first(h.ra, nbuf), apply);
+    h.out(nbuf, x, g);
+  });
+  return r;
+}
+
+int oracle_rc_working_set_eigenvalues(void* hp, double* ev) {
+  auto& h = *static_cast<RcInstance*>(hp);
+  return guarded([&] {
+    size_t k = 0;
+    for (double e : h.solver->working_set_eigenvalues()) ev[k++] = e;
+  });
+}
+
 int oracle_rc_solution(void* hp, int nroot, const int* roots, double* x, double* g) {
   auto& h = *static_cast<RcInstance*>(hp);
   return guarded([&] {

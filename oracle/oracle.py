@@ -222,6 +222,10 @@ def itsolv_lib():
                            "oracle_rc_end_iteration": [P, Z, PDd, PDd]}.items():
             getattr(L, name).restype = LL
             getattr(L, name).argtypes = args
+        L.oracle_rc_add_p.restype = LL
+        L.oracle_rc_add_p.argtypes = [P, Z, Z, C.POINTER(Z), C.POINTER(Z), PDd, PDd, PDd, PDd, C.c_void_p]
+        L.oracle_rc_working_set_eigenvalues.restype = I
+        L.oracle_rc_working_set_eigenvalues.argtypes = [P, PDd]
         L.oracle_rc_solution.restype = I
         L.oracle_rc_solution.argtypes = [P, I, C.POINTER(C.c_int), PDd, PDd]
         L.oracle_rc_stats.restype = I
@@ -269,6 +273,39 @@ class RcSolver:
     def end_iteration(self, parameters, residual):
         return self._r(itsolv_lib().oracle_rc_end_iteration(self._h, self._nbuf(parameters), _d(parameters),
                                                             _d(residual)))
+
+    def add_p(self, pvectors, pp, parameters, action, apply_p):
+        """As iterative_solver.IterativeSolver.add_p (IterativeSolverAddP)."""
+        offsets = np.zeros(len(pvectors) + 1, dtype=np.uint64)
+        idx, coef = [], []
+        for k, p in enumerate(pvectors):
+            for i in sorted(p):
+                idx.append(i)
+                coef.append(p[i])
+            offsets[k + 1] = len(idx)
+        idx = np.array(idx if idx else [0], dtype=np.uint64)
+        coef = np.array(coef if coef else [0.0], dtype=np.float64)
+        ppm = np.ascontiguousarray(pp, dtype=np.float64)
+        n, nP = self.n, len(pvectors)
+        fn_t = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_size_t, C.POINTER(C.c_size_t))
+
+        def tramp(pbuf, gbuf, nvec, ranges):
+            pc = np.ctypeslib.as_array(pbuf, shape=(nvec * nP,)).reshape(nvec, nP)
+            rg = np.ctypeslib.as_array(ranges, shape=(2 * nvec,)).reshape(nvec, 2).astype(np.int64)
+            g = np.ctypeslib.as_array(gbuf, shape=(nvec * n,))
+            apply_p(pc, g, rg)
+
+        self._apply_p = fn_t(tramp)
+        Zp = C.POINTER(C.c_size_t)
+        return self._r(itsolv_lib().oracle_rc_add_p(
+            self._h, self._nbuf(parameters), nP, offsets.ctypes.data_as(Zp), idx.ctypes.data_as(Zp), _d(coef),
+            _d(ppm), _d(parameters), _d(action), C.cast(self._apply_p, C.c_void_p)))
+
+    def working_set_eigenvalues(self, nwork):
+        ev = np.zeros(max(1, self.nroot))
+        if itsolv_lib().oracle_rc_working_set_eigenvalues(self._h, _d(ev)):
+            raise RuntimeError(itsolv_lib().oracle_itsolv_last_error().decode())
+        return ev[:nwork]
 
     def solution(self, roots, parameters, residual):
         r = (C.c_int * max(1, len(roots)))(*roots)

@@ -9,6 +9,9 @@ Problems and loops follow the reference's tests:
   Rosenbrock         test_Optimize.cpp:124-156
   trig1d             test_Optimize.cpp:158-176, test_NonLinearEquations.cpp:252-270
   trig (n = 1, 2)    test_NonLinearEquations.cpp:160-250 (calc, trigProblem)
+  test_eigen         test_LinearEigensystem.cpp:60-330 (file, n, small, symmetry and
+                     non-hermitian matrices; P space through add_p; preconditioner
+                     g *= -1 / (1e-12 - shift + h_ii))
 """
 import numpy as np
 
@@ -118,3 +121,108 @@ def loop_trig(solver, n, max_iter=100):
         if nwork == 0:
             break
     return trace, x
+
+
+# ---- LinearEigensystem: test_LinearEigensystem.cpp:60-330 ---------------------------------------
+def eigen_matrix(n, param=1.0, non_hermiticity=0.0):
+    """load_matrix(n, "", param, non_hermiticity) (test_LinearEigensystem.cpp:41-51)."""
+    h = np.ones((n, n))
+    h[np.diag_indices(n)] = np.arange(n) * param
+    if non_hermiticity:
+        h[np.tril_indices(n, -1)] *= 1 - non_hermiticity
+    return h
+
+
+def symmetry_matrix(n, param=1.0):
+    """symmetry_eigen (test_LinearEigensystem.cpp:387-406): couplings between i % 3 == 0 and the rest removed."""
+    h = eigen_matrix(n, param)
+    for i in range(n):
+        for j in range(n):
+            if (i % 3 == 0 and j % 3 != 0) or (j % 3 == 0 and i % 3 != 0):
+                h[j, i] = 0.0
+    return h
+
+
+def eigen_options(n, nroot, np_, hermitian):
+    """set_options (test_LinearEigensystem.cpp:192-215)."""
+    qmax = max(6 * nroot, min(n, min(1000, 6 * nroot)) - np_)
+    return (f"convergence_threshold=1e-8,max_size_qspace={qmax},reset_D=8,"
+            f"hermiticity={'true' if hermitian else 'false'}")
+
+
+def _lowest_diagonals(h, count):
+    d = list(np.diag(h).copy())
+    out = []
+    for _ in range(count):
+        k = int(np.argmin(d))  # first minimum, as std::min_element
+        out.append(k)
+        d[k] = 1e99
+    return out
+
+
+def eigen_update(h, g, shift):
+    """update(): g_k *= -1 / (1e-12 - shift_k + h_ii) (test_LinearEigensystem.cpp:91-102)."""
+    d = np.diag(h)
+    for k in range(min(g.shape[0], len(shift))):
+        g[k] *= -1.0 / (1e-12 - shift[k] + d)
+
+
+def loop_eigen(solver, h, nroot, np_, max_iter=100):
+    """initialize_subspace + the test_eigen loop (test_LinearEigensystem.cpp:217-283).  Returns the
+    trace of add_vector / end_iteration returns and the iteration count n_iter."""
+    n = h.shape[0]
+    x, g = np.zeros((nroot, n)), np.zeros((nroot, n))
+    trace = []
+    if np_:
+        pidx = _lowest_diagonals(h, np_)
+        pspace = [{k: 1.0} for k in pidx]
+        pp = h[np.ix_(pidx, pidx)].copy()
+
+        def apply_p(pc, gl, ranges):
+            for i in range(pc.shape[0]):
+                for pi, k in enumerate(pidx):
+                    gl[i * n:(i + 1) * n] += h[:, k] * pc[i, pi]
+
+        nwork = solver.add_p(pspace, pp, x, g, apply_p)
+        trace.append(("p", nwork))
+    else:
+        for root, k in enumerate(_lowest_diagonals(h, nroot)):
+            x[root, k] = 1.0
+        g[:] = x @ h.T
+        nwork = solver.add_vector(x, g)
+        trace.append(("v", nwork))
+    eigen_update(h, g, solver.working_set_eigenvalues(nwork))
+    trace.append(("e", solver.end_iteration(x, g)))
+    n_iter = 2
+    for _ in range(1, max_iter):
+        g[:] = x @ h.T
+        nwork = solver.add_vector(x, g)
+        trace.append(("v", nwork))
+        if nwork == 0:
+            break
+        eigen_update(h, g, solver.working_set_eigenvalues(nwork))
+        nwork = solver.end_iteration(x, g)
+        trace.append(("e", nwork))
+        n_iter += 1
+        if nwork == 0:
+            break
+    return trace, n_iter
+
+
+def expected_eigen(h, hermitian):
+    if hermitian:
+        w, v = np.linalg.eigh(h)
+    else:
+        w, v = np.linalg.eig(h)
+        o = np.argsort(w.real, kind="stable")
+        w, v = w[o].real, v[:, o].real
+        v /= np.linalg.norm(v, axis=0)
+    return w, v
+
+
+def eigen_cases(n, hermitian=True):
+    """(nroot, np) pairs of test_eigen (test_LinearEigensystem.cpp:226-229)."""
+    for nroot in range(1, min(n, 28) + 1, max(1, n // 10)):
+        for np_ in range(0, min(n, 100) + 1, max(nroot, n // 5)):
+            if hermitian or np_ == 0:
+                yield nroot, np_
