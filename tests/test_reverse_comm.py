@@ -277,3 +277,48 @@ def test_eigen_gpu(family):
             g.finalize()
     if family not in ROUNDING_CHAOTIC:  # the exact-trace bar applies to every case of these families
         assert not sensitive, sensitive
+
+
+def _solution_case(make, h, nroot, np_):
+    """test_LinearEigensystem.cpp:408-433: after initialize_subspace, solution(working set) gives the
+    residuals the solver handed back."""
+    n = h.shape[0]
+    s = make(n, nroot, True, rp.eigen_options(n, nroot, np_, True))
+    x, g = np.zeros((nroot, n)), np.zeros((nroot, n))
+    if np_:
+        pidx = rp._lowest_diagonals(h, np_)
+        pp = h[np.ix_(pidx, pidx)].copy()
+
+        def apply_p(pc, gl, ranges):
+            for i in range(pc.shape[0]):
+                for pi, k in enumerate(pidx):
+                    gl[i * n:(i + 1) * n] += h[:, k] * pc[i, pi]
+
+        nwork = s.add_p([{k: 1.0} for k in pidx], pp, x, g, apply_p)
+    else:
+        for root, k in enumerate(rp._lowest_diagonals(h, nroot)):
+            x[root, k] = 1.0
+        g[:] = x @ h.T
+        nwork = s.add_vector(x, g)
+    ev = s.working_set_eigenvalues(nwork)
+    rp.eigen_update(h, g, ev)
+    s.end_iteration(x, g)
+    return s, nwork, ev
+
+
+@pytest.mark.parametrize("backend", ["cpu", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_eigen_solution_matches_residual(backend):
+    h = rp.eigen_matrix(10, 1.0)
+    make = cpu_eigen if backend == "cpu" else gpu_eigen
+    for nroot in range(1, 10):
+        for np_ in (0, nroot):
+            s, nwork, _ = _solution_case(make, h, nroot, np_)
+            roots = list(range(nroot))
+            x, g = np.zeros((nroot, 10)), np.zeros((nroot, 10))
+            s.solution(roots, x, g)
+            ev = (s.stats()["eigenvalues"] if backend == "cpu" else s.eigenvalues)[:nroot]
+            r = x @ h.T - ev[:, None] * x
+            # the solver's residual for each root is H x - e x (reference: |g - residual| <= 1e-6)
+            np.testing.assert_allclose(g, r, rtol=0, atol=1e-6, err_msg=f"nroot={nroot} np={np_}")
+            if backend == "gpu":
+                s.finalize()
