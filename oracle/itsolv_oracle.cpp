@@ -366,6 +366,26 @@ extern "C" {
 
 const char* oracle_itsolv_last_error(void) { return g_error.c_str(); }
 
+// The cubic line-search model of OptimizeBFGS (iterative-solver_amd/include/itsolv_hbm/interpolate.h,
+// reference itsolv/Interpolate.cpp): value, first and second derivative at x of the cubic through
+// (x0, f0, g0), (x1, f1, g1); and its analytic minimiser (out: x, f, f1, f2).
+void oracle_interpolate_cubic(const double* p0, const double* p1, double x, double* out) {
+  it::Interpolate inter({p0[0], p0[1], p0[2]}, {p1[0], p1[1], p1[2]});
+  const auto p = inter(x);
+  out[0] = p.x;
+  out[1] = p.f;
+  out[2] = p.f1;
+  out[3] = p.f2;
+}
+void oracle_interpolate_minimize(const double* p0, const double* p1, double xa, double xb, double* out) {
+  it::Interpolate inter({p0[0], p0[1], p0[2]}, {p1[0], p1[1], p1[2]});
+  const auto p = inter.minimize(xa, xb);
+  out[0] = p.x;
+  out[1] = p.f;
+  out[2] = p.f1;
+  out[3] = p.f2;
+}
+
 // kind: "LinearEigensystem", "NonLinearEquations" (DIIS), "Optimize" (algorithm BFGS or SD),
 // "LinearEquations" (rhs: nroot x n).  Returns NULL on error (oracle_itsolv_last_error).
 void* oracle_rc_create(const char* kind, size_t n, size_t nroot, const double* rhs, double thresh, double thresh_value,

@@ -226,12 +226,29 @@ def itsolv_lib():
         L.oracle_rc_add_p.argtypes = [P, Z, Z, C.POINTER(Z), C.POINTER(Z), PDd, PDd, PDd, PDd, C.c_void_p]
         L.oracle_rc_working_set_eigenvalues.restype = I
         L.oracle_rc_working_set_eigenvalues.argtypes = [P, PDd]
+        for name in ("oracle_interpolate_cubic",):
+            getattr(L, name).argtypes = [PDd, PDd, D, PDd]
+        L.oracle_interpolate_minimize.argtypes = [PDd, PDd, D, D, PDd]
         L.oracle_rc_solution.restype = I
         L.oracle_rc_solution.argtypes = [P, I, C.POINTER(C.c_int), PDd, PDd]
         L.oracle_rc_stats.restype = I
         L.oracle_rc_stats.argtypes = [P, C.POINTER(I), C.POINTER(I), PDd, PDd, PDd]
         _itsolv = L
     return _itsolv
+
+
+def interpolate_cubic(p0, p1, x):
+    """(x, f, f', f'') of the cubic through p0 = (x0, f0, g0), p1 (OptimizeBFGS's line-search model)."""
+    out = np.zeros(4)
+    itsolv_lib().oracle_interpolate_cubic(_d(np.array(p0, float)), _d(np.array(p1, float)), float(x), _d(out))
+    return out
+
+
+def interpolate_minimize(p0, p1, xa, xb):
+    out = np.zeros(4)
+    itsolv_lib().oracle_interpolate_minimize(_d(np.array(p0, float)), _d(np.array(p1, float)), float(xa), float(xb),
+                                             _d(out))
+    return out
 
 
 class RcSolver:

@@ -209,3 +209,18 @@ def test_block_gram_schmidt_linear_equations(n, nroot):
     blk = oracle.linear_equations_dense(a, rhs, block_gram_schmidt=1, **kw)
     assert blk["converged"] and blk["iterations"] == ref["iterations"]
     np.testing.assert_allclose(blk["x"], ref["x"], atol=2e-6, rtol=0)
+
+
+def test_interpolate_cubic_constructor():
+    # reference test/itsolv/test_Interpolate.cpp:7-21: f = x (x - 1/2)^2 through (0, 0, 1/4), (1, 1/4, 5/4)
+    p0, p1 = (0.0, 0.0, 0.25), (1.0, 0.25, 1.25)
+    assert oracle.interpolate_cubic(p0, p1, 0.0).tolist() == [0.0, 0.0, 0.25, -2.0]
+    assert oracle.interpolate_cubic(p0, p1, 1.0).tolist() == [1.0, 0.25, 1.25, 4.0]
+    assert oracle.interpolate_cubic(p0, p1, 0.5)[2] == 0.0
+
+
+def test_interpolate_cubic_minimum():
+    # test_Interpolate.cpp:23-41 with the analytic cubic minimiser OptimizeBFGS uses
+    # (OptimizeBFGS.h:95-96; Interpolate.cpp:141-142); the bracketing search is not restated
+    p = oracle.interpolate_minimize((0.0, 0.0, 0.25), (1.0, 0.25, 1.25), 0.0, 1.0)
+    assert abs(p[0] - 0.5) < 1e-13 and abs(p[1]) < 1e-13 and abs(p[2]) < 1e-13 and p[3] > 0
