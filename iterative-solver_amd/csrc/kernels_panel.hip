@@ -36,8 +36,11 @@ struct InnerArgs {
   double* partial;  // [gridDim.x][m][k]
 };
 
-template <int MG, int NG>
+// SYM: xx == yy (a symmetric overlap, MG == NG): each vector is loaded once and used as both
+// operands of the MFMA.
+template <int MG, int NG, bool SYM = false>
 __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
+  static_assert(!SYM || MG == NG, "symmetric panel needs square groups");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 3, p = lane >> 2;
   const double* xp[MG];
@@ -62,7 +65,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
 #pragma unroll
     for (int g = 0; g < MG; ++g) xv[g] = xp[g] ? ld2(xp[g] + e) : z2;
 #pragma unroll
-    for (int h = 0; h < NG; ++h) yv[h] = yp[h] ? ld2(yp[h] + e) : z2;
+    for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : (yp[h] ? ld2(yp[h] + e) : z2);
 #pragma unroll
     for (int g = 0; g < MG; ++g)
 #pragma unroll
@@ -82,8 +85,8 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
     }
 #pragma unroll
     for (int h = 0; h < NG; ++h) {
-      const double y0 = (yp[h] && i0 < a.n) ? yp[h][i0] : 0.0;
-      const double y1 = (yp[h] && i1 < a.n) ? yp[h][i1] : 0.0;
+      const double y0 = SYM ? x0[h] : ((yp[h] && i0 < a.n) ? yp[h][i0] : 0.0);
+      const double y1 = SYM ? x1[h] : ((yp[h] && i1 < a.n) ? yp[h][i1] : 0.0);
 #pragma unroll
       for (int g = 0; g < MG; ++g) {
         acc[g][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(x0[g], y0, acc[g][h], 0, 0, 0);
@@ -115,6 +118,62 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
       for (int w = 1; w < kBlock / 64; ++w) v += red[w][gh][e];
       out[size_t(row) * a.k + col] = v;
     }
+  }
+}
+
+// Panels of 1 x 1 and 1 x 2 (or 2 x 1) vectors: with only one or two MFMA operand rows live, the
+// 4x4x4 layout leaves 3/4 of the lanes idle on loads (tools/shapes_bench.py: 1 x 1 at 3.4 TB/s),
+// so these run on the VALU with every lane streaming 16 B per vector, 4 positions in flight.
+template <int K>
+__global__ __launch_bounds__(kBlock) void k_gemm_inner_row(const InnerArgs a) {
+  using ssp::ld2nt;
+  const size_t n2 = a.n >> 1, stride = size_t(gridDim.x) * kBlock;
+  double acc[K][2] = {};
+  const bool same = K == 1 && a.y[0] == a.x[0];  // a norm: one load stream
+  size_t p = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  for (; p + 3 * stride < n2; p += 4 * stride) {
+    double2 xv[4], yv[K][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xv[u] = ld2nt(a.x[0] + 2 * (p + u * stride));
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) yv[j][u] = same ? xv[u] : ld2nt(a.y[j] + 2 * (p + u * stride));
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[j][u & 1] = fma(xv[u].x, yv[j][u].x, acc[j][u & 1]);
+        acc[j][u & 1] = fma(xv[u].y, yv[j][u].y, acc[j][u & 1]);
+      }
+  }
+  for (; p < n2; p += stride) {
+    const double2 xv = ld2(a.x[0] + 2 * p);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const double2 yv = ld2(a.y[j] + 2 * p);
+      acc[j][0] = fma(xv.x, yv.x, acc[j][0]);
+      acc[j][0] = fma(xv.y, yv.y, acc[j][0]);
+    }
+  }
+  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0)
+#pragma unroll
+    for (int j = 0; j < K; ++j) acc[j][0] = fma(a.x[0][a.n - 1], a.y[j][a.n - 1], acc[j][0]);
+  __shared__ double red[kBlock / 64][K];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    double v = acc[j][0] + acc[j][1];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) red[wave][j] = v;
+  }
+  __syncthreads();
+  if (int(threadIdx.x) < K) {
+    double v = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) v += red[w][threadIdx.x];
+    a.partial[size_t(blockIdx.x) * K + threadIdx.x] = v;
   }
 }
 
@@ -419,6 +478,17 @@ int launch_inner_mg(ssp_ctx* ctx, unsigned grid, const InnerArgs& a, int need) {
   return SSP_OK;
 }
 
+int launch_inner_sym(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
+  switch ((a.m + 3) / 4) {
+    case 1: hipLaunchKernelGGL((k_gemm_inner<1, 1, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    case 2: hipLaunchKernelGGL((k_gemm_inner<2, 2, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    case 3: hipLaunchKernelGGL((k_gemm_inner<3, 3, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    default: hipLaunchKernelGGL((k_gemm_inner<4, 4, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+  }
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
 int launch_inner(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
   const int mg = (a.m + 3) / 4, need = (a.k + 3) / 4;
   switch (mg) {
@@ -481,7 +551,39 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
     std::sort(distinct.begin(), distinct.end());
     const double nvec = double(std::unique(distinct.begin(), distinct.end()) - distinct.begin());
     ssp::LedgerScope ls(ctx, "gemm_inner", 8.0 * n * nvec);
-    for (int r0 = 0; r0 < R; r0 += ssp::kInnerRows) {
+    // 1 x 1 and 1 x 2 panels (rows = the shorter side): VALU row kernel.
+    if (R == 1 && C <= 2) {
+      InnerArgs a{};
+      a.m = 1;
+      a.k = C;
+      a.n = n;
+      a.x[0] = rows[0];
+      for (int j = 0; j < C; ++j) a.y[j] = cols[j];
+      const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 4);
+      SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * C));
+      a.partial = ctx->partial;
+      if (C == 1)
+        hipLaunchKernelGGL((k_gemm_inner_row<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      else
+        hipLaunchKernelGGL((k_gemm_inner_row<2>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_TRY_HIP(hipGetLastError());
+      SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, C, ctx->result_dev, C, 0, 0));
+    }
+    // A symmetric overlap <xx_i, xx_j> of up to 16 vectors: one panel that loads each vector once.
+    bool sym = m == k && m <= ssp::kInnerRows && !(R == 1 && C <= 2);
+    for (int i = 0; sym && i < m; ++i) sym = xx[i] == yy[i];
+    if (sym) {
+      InnerArgs a{};
+      a.m = a.k = m;
+      a.n = n;
+      for (int i = 0; i < m; ++i) a.x[i] = a.y[i] = xx[i];
+      const unsigned grid = inner_grid(ctx, n);
+      SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * m * m));
+      a.partial = ctx->partial;
+      SSP_TRY(launch_inner_sym(ctx, a, grid));
+      SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), m, m, ctx->result_dev, m, 0, 0));
+    }
+    for (int r0 = 0; !sym && !(R == 1 && C <= 2) && r0 < R; r0 += ssp::kInnerRows) {
       const int mr = std::min(ssp::kInnerRows, R - r0);
       const int cols_per_launch = 4 * ng_max((mr + 3) / 4);
       for (int c0 = 0; c0 < C; c0 += cols_per_launch) {

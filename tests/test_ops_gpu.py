@@ -74,6 +74,23 @@ def test_gemm_inner(ctx, m, k, n):
         v.free()
 
 
+@pytest.mark.parametrize("m", [1, 2, 5, 8, 13, 16, 17])
+@pytest.mark.parametrize("n", [1, 33, 1003, 100_003])
+def test_gemm_inner_symmetric_panel(ctx, m, n):
+    # gemm_inner(xx, xx) loads each vector once (SYM panel); the result is bit-identical to the same
+    # overlap of distinct copies and symmetric
+    r = rng(m + n)
+    xs = [r.uniform(-1, 1, n) for _ in range(m)]
+    dx = [ctx.upload(v) for v in xs]
+    dc = [ctx.upload(v) for v in xs]
+    s = ctx.gemm_inner(dx, dx)
+    assert np.array_equal(s, ctx.gemm_inner(dx, dc))
+    assert np.array_equal(s, s.T)
+    for i in range(m):
+        for j in range(m):  # against the exactly rounded sum (positive diagonal terms, see axpy_norm)
+            assert abs(s[i, j] - math.fsum(xs[i] * xs[j])) <= red_tol(xs[i] * xs[j])
+
+
 def test_gemm_inner_asymmetric_layout(ctx):
     # Exact integer data: catches row/col swaps in the MFMA accumulator mapping.
     n = 4096 + 24

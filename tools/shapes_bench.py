@@ -36,7 +36,7 @@ def main():
     ctx.synthetic_diagonal(d, 0.1, 1)
     rng = np.random.default_rng(0)
     cases = []
-    for m, k in ((8, 48), (8, 1), (1, 6), (1, 48), (4, 24), (16, 64), (48, 8)):
+    for m, k in ((8, 48), (8, 1), (1, 6), (1, 48), (4, 24), (16, 64), (48, 8), (1, 1), (1, 2), (2, 2), (1, 3)):
         cases.append((f"gemm_inner {m}x{k}", "gemm_inner",
                       lambda m=m, k=k: ctx.gemm_inner(pool[:m], pool[m:m + k])))
     for k, m in ((48, 8), (1, 8), (6, 1), (8, 8), (24, 4), (64, 16)):
