@@ -319,23 +319,21 @@ int main(int argc, char** argv) {
   auto rep = [&](const char* name, int g, float ms, double bytes) {
     printf("%-26s g=%-6d %8.3f ms  %7.1f GB/s\n", name, g, ms, bytes / ms / 1e6);
   };
-  // Vector placement: separate hipMallocs vs one slab with vector i at i * pitch + i * stagger.
-  const size_t pitch = ((n * 8 + (2u << 20) - 1) / (2u << 20)) * (2u << 20);
-  char* slab;
-  CK(hipMalloc((void**)&slab, (m + k) * pitch + (m + k) * (size_t(1) << 20)));
-  CK(hipMemset(slab, 0, (m + k) * pitch + (m + k) * (size_t(1) << 20)));
-  for (int rep_i = 0; rep_i < 2; ++rep_i) {
-    for (int j = 0; j < m; ++j) a.y[j] = vec[j];
-    for (int i = 0; i < k; ++i) a.x[i] = vec[m + i];
-    rep("separate hipMalloc", 1024, timeit([&] { hipLaunchKernelGGL((k_o4<8, 4>), dim3(1024), dim3(256), 0, 0, a); }, 4), obytes);
-    for (size_t st : {size_t(0), size_t(256), size_t(4096), size_t(65536), size_t(1) << 20, size_t(4096 + 256)}) {
-      auto at = [&](int v) { return reinterpret_cast<double*>(slab + v * pitch + v * st); };
-      for (int j = 0; j < m; ++j) a.y[j] = at(j);
-      for (int i = 0; i < k; ++i) a.x[i] = at(m + i);
-      char name[64];
-      snprintf(name, sizeof name, "slab stagger %zu", st);
-      rep(name, 1024, timeit([&] { hipLaunchKernelGGL((k_o4<8, 4>), dim3(1024), dim3(256), 0, 0, a); }, 4), obytes);
+  // Placement: several independent sets of separately allocated vectors in one process.
+  for (int set = 0; set < 4; ++set) {
+    double* v2[64];
+    for (int i = 0; i < m + k; ++i) {
+      CK(hipMalloc((void**)&v2[i], n * 8));
+      CK(hipMemset(v2[i], 0, n * 8));
     }
+    for (int j = 0; j < m; ++j) a.y[j] = v2[j];
+    for (int i = 0; i < k; ++i) a.x[i] = v2[m + i];
+    char name[64];
+    snprintf(name, sizeof name, "set %d (%p)", set, (void*)v2[0]);
+    for (int r = 0; r < 2; ++r)
+      rep(name, 1024, timeit([&] { hipLaunchKernelGGL((k_o4<8, 4>), dim3(1024), dim3(256), 0, 0, a); }, 4), obytes);
+    if (set < 3)
+      for (int i = 0; i < m + k; ++i) CK(hipFree(v2[i]));
   }
   return 0;
 }
