@@ -319,21 +319,22 @@ int main(int argc, char** argv) {
   auto rep = [&](const char* name, int g, float ms, double bytes) {
     printf("%-26s g=%-6d %8.3f ms  %7.1f GB/s\n", name, g, ms, bytes / ms / 1e6);
   };
-  // Placement: several independent sets of separately allocated vectors in one process.
-  for (int set = 0; set < 4; ++set) {
-    double* v2[64];
-    for (int i = 0; i < m + k; ++i) {
-      CK(hipMalloc((void**)&v2[i], n * 8));
-      CK(hipMemset(v2[i], 0, n * 8));
-    }
-    for (int j = 0; j < m; ++j) a.y[j] = v2[j];
-    for (int i = 0; i < k; ++i) a.x[i] = v2[m + i];
-    char name[64];
-    snprintf(name, sizeof name, "set %d (%p)", set, (void*)v2[0]);
-    for (int r = 0; r < 2; ++r)
+  // Placement: one slab per trial, vector i at i * (pitch + stagger) for large staggers.
+  const size_t MB2 = size_t(2) << 20;
+  const size_t pitch = ((n * 8 + MB2 - 1) / MB2) * MB2;
+  const size_t staggers[] = {0, MB2, 3 * MB2, 7 * MB2, 15 * MB2, 31 * MB2, 63 * MB2, 127 * MB2};
+  for (int rep_i = 0; rep_i < 2; ++rep_i)
+    for (size_t st : staggers) {
+      const size_t step = pitch + st;
+      char* base = nullptr;
+      CK(hipMalloc((void**)&base, step * (m + k)));
+      CK(hipMemset(base, 0, step * (m + k)));
+      for (int j = 0; j < m; ++j) a.y[j] = reinterpret_cast<double*>(base + j * step);
+      for (int i = 0; i < k; ++i) a.x[i] = reinterpret_cast<double*>(base + (m + i) * step);
+      char name[64];
+      snprintf(name, sizeof name, "slab stagger %zu MB", st >> 20);
       rep(name, 1024, timeit([&] { hipLaunchKernelGGL((k_o4<8, 4>), dim3(1024), dim3(256), 0, 0, a); }, 4), obytes);
-    if (set < 3)
-      for (int i = 0; i < m + k; ++i) CK(hipFree(v2[i]));
-  }
+      CK(hipFree(base));
+    }
   return 0;
 }
