@@ -125,6 +125,11 @@ class IterativeSolver:
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
 
+    def mpicomm_compute(self):
+        """The communicator handle of the reference (IterativeSolver_mpicomm_global); on the HBM back
+        end ranks communicate through the context's RCCL communicator and this is 0."""
+        return int(_call("IterativeSolver_mpicomm_global"))
+
     def finalize(self):
         if getattr(self, "_active", False):
             _call("IterativeSolverFinalize")

@@ -72,7 +72,7 @@ def test_classes_mirror_reference_api():
     for name in ("Problem", "IterativeSolver", "LinearEigensystem", "NonLinearEquations", "LinearEquations",
                  "Optimize"):
         assert hasattr(iterative_solver, name)
-    for meth in ("solve", "solution", "add_vector", "end_iteration", "add_value", "add_p"):
+    for meth in ("solve", "solution", "add_vector", "end_iteration", "add_value", "add_p", "mpicomm_compute"):
         assert callable(getattr(iterative_solver.IterativeSolver, meth))
     assert isinstance(iterative_solver.LinearEigensystem.eigenvalues, property)
     assert isinstance(iterative_solver.IterativeSolver.errors, property)
