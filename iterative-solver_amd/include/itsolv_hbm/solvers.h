@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <functional>
+#include <iostream>
 #include <limits>
 #include <map>
 #include <memory>
@@ -65,6 +66,9 @@ class Problem {
                         const VecRef<container_t>& actions) const {
     if (!pparams.empty()) throw std::logic_error("P-space unavailable: unimplemented p_action() in Problem class");
   }
+  // Parameter sets for IterativeSolverTemplate::test_problem (reference IterativeSolver.h:163-171):
+  // fill `parameters` for instance 0, 1, ... and return false when there are no more.
+  virtual bool test_parameters(unsigned int instance, R& parameters) const { return false; }
 };
 
 namespace detail {
@@ -269,6 +273,50 @@ class IterativeSolverTemplate {
   IterativeSolverTemplate(const IterativeSolverTemplate&) = delete;
 
   virtual bool nonlinear() const = 0;
+
+  // Consistency check of a Problem (reference IterativeSolverTemplate.h:420-473): for a non-linear
+  // problem, the change of the value between test parameter sets against the mean residual dotted
+  // with the step; for a linear one, that the action is linear under scaling by 10.
+  bool test_problem(const Problem<R, P>& problem, R& v0, R& v1, int verbosity, double threshold) const {
+    auto& h = *m_handlers;
+    bool success = true;
+    if (nonlinear()) {
+      if (!problem.test_parameters(0, v0)) return true;
+      const auto value0 = problem.residual(v0, v1);
+      Q parameters0{h.qr().copy(v0)};
+      Q residual0{h.qr().copy(v1)};
+      for (unsigned int instance = 1; problem.test_parameters(instance, v0); ++instance) {
+        const auto value1 = problem.residual(v0, v1);
+        Q parameters1{h.qr().copy(v0)};
+        Q residual1{h.qr().copy(v1)};
+        h.rq().copy(v0, residual1);
+        h.rr().scal(0.5, v0);
+        h.rq().axpy(0.5, residual0, v0);
+        h.rq().copy(v1, parameters1);
+        h.rq().axpy(-1, parameters0, v1);
+        const auto dv_analytic = h.rr().dot(v0, v1);
+        success = success && std::abs(dv_analytic - (value1 - value0)) < threshold;
+        if (verbosity > 0 || (verbosity > -1 && !success))
+          std::cout << "{actual, extrapolated} value change: {" << value1 - value0 << ", " << dv_analytic << "}"
+                    << std::endl;
+      }
+    } else {
+      for (unsigned int instance = 0; problem.test_parameters(instance, v0); ++instance) {
+        problem.action(cwrap_arg(v0), wrap_arg(v1));
+        Q residual{h.qr().copy(v1)};
+        const auto norm2_residual = std::sqrt(h.rr().dot(v1, v1));
+        constexpr double scale_factor{10.0};
+        h.rr().scal(scale_factor, v0);
+        problem.action(cwrap_arg(v0), wrap_arg(v1));
+        h.rq().axpy(-scale_factor, residual, v1);
+        const auto norm2 = std::sqrt(h.rr().dot(v1, v1));
+        success = success && std::abs(norm2 / norm2_residual) < threshold;
+        if (verbosity > 0 || (verbosity > -1 && !success))
+          std::cout << "Length of residual: " << norm2_residual << ", scaling defect: " << norm2 << std::endl;
+      }
+    }
+    return success;
+  }
 
   // Adds the working-set parameters and their actions (residuals for non-linear solvers) to the
   // subspace, solves it and returns the new working set in parameters / actions.

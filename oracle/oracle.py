@@ -229,6 +229,8 @@ def itsolv_lib():
         for name in ("oracle_interpolate_cubic",):
             getattr(L, name).argtypes = [PDd, PDd, D, PDd]
         L.oracle_interpolate_minimize.argtypes = [PDd, PDd, D, D, PDd]
+        L.oracle_test_problem_trig.restype = I
+        L.oracle_test_problem_trig.argtypes = [Z, D, I]
         L.oracle_rc_solution.restype = I
         L.oracle_rc_solution.argtypes = [P, I, C.POINTER(C.c_int), PDd, PDd]
         L.oracle_rc_stats.restype = I

@@ -224,3 +224,11 @@ def test_interpolate_cubic_minimum():
     # (OptimizeBFGS.h:95-96; Interpolate.cpp:141-142); the bracketing search is not restated
     p = oracle.interpolate_minimize((0.0, 0.0, 0.25), (1.0, 0.25, 1.25), 0.0, 1.0)
     assert abs(p[0] - 0.5) < 1e-13 and abs(p[1]) < 1e-13 and abs(p[2]) < 1e-13 and p[3] > 0
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_test_problem_trig(n):
+    # reference test_NonLinearEquations.cpp:206-213: test_problem accepts trigProblem at 1e-9 ...
+    assert oracle.itsolv_lib().oracle_test_problem_trig(n, 1e-9, 0) == 1
+    # ... and rejects the same problem with a residual 10 % too large
+    assert oracle.itsolv_lib().oracle_test_problem_trig(n, 1e-9, 1) == 0
