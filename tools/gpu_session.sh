@@ -27,7 +27,7 @@ fatal() {  # statuses after which nothing else may use the GPU in this call
 }
 
 if [ "$what" = tests ] || [ "$what" = all ]; then
-  step pytest_gpu 1100 python -m pytest tests -m gpu -q -rf
+  step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -rf --timeout 120 --timeout-method thread
   rc=$?
   if fatal $rc; then exit $rc; fi
 fi
