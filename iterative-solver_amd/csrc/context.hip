@@ -4,6 +4,8 @@
 // or in MPI-3 windows and reduces with MPI_Allreduce (reference array/util/gemm.h:179-182).  Here
 // every vector shard lives in HBM for the solver's lifetime and reductions are RCCL allreduces on
 // the compute stream.
+#include <immintrin.h>
+
 #include <algorithm>
 #include <cstring>
 #include <mutex>
@@ -74,10 +76,15 @@ int ensure_result(ssp_ctx* ctx, size_t n) {
   size_t cap = std::max(n, size_t(1) << 16);
   if (hipMalloc(&ctx->result_dev, cap * sizeof(double)) != hipSuccess)
     return set_error(SSP_ERR_NOMEM, "hipMalloc of result staging failed");
-  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->result_host), cap * sizeof(double), hipHostMallocDefault) !=
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->result_host), cap * sizeof(double), hipHostMallocCoherent) !=
       hipSuccess)
     return set_error(SSP_ERR_NOMEM, "hipHostMalloc of result staging failed");
   ctx->result_cap = cap;
+  if (!ctx->pub_flag) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->pub_flag), 64, hipHostMallocCoherent) != hipSuccess)
+      return set_error(SSP_ERR_NOMEM, "hipHostMalloc of the result flag failed");
+    __atomic_store_n(ctx->pub_flag, ctx->pub_seq, __ATOMIC_RELEASE);
+  }
   return SSP_OK;
 }
 
@@ -130,10 +137,41 @@ int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n) {
   return SSP_OK;
 }
 
+// Publishes n doubles of the device result into coherent host memory, then the sequence number
+// (system-scope release after every thread's system fence).  One workgroup: n is a reduction result
+// (at most a few thousand doubles).
+__global__ __launch_bounds__(256) void k_publish(const double* src, size_t n, double* dst,
+                                                 unsigned long long* flag, unsigned long long seq) {
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The result is complete when the flag carries this call's sequence number; the kernel is the last
+// one queued, so every operation before it has completed too (stream order).  Polling the flag
+// instead of a D2H copy + hipStreamSynchronize cuts the host-visible latency of a reduction by about
+// a third (tools/sync_probe.hip, profiles/r1/sync_probe.txt).  The stream is queried every few
+// hundred polls so that a failed kernel surfaces as an error instead of a hang; should the stream
+// drain without the flag becoming visible, the result is copied the ordinary way.
 int fetch_result(ssp_ctx* ctx, double* out, size_t n) {
-  SSP_TRY_HIP(hipMemcpyAsync(ctx->result_host, ctx->result_dev, n * sizeof(double), hipMemcpyDeviceToHost,
-                             ctx->stream));
-  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  if (n > ctx->result_cap) return set_error(SSP_ERR_ARG, "fetch_result: result larger than the staging buffer");
+  const unsigned long long seq = ++ctx->pub_seq;
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, ctx->stream, ctx->result_dev, n, ctx->result_host,
+                     ctx->pub_flag, seq);
+  SSP_TRY_HIP(hipGetLastError());
+  for (unsigned spin = 1;; ++spin) {
+    if (__atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq) break;
+    if ((spin & 255) == 0) {
+      const hipError_t e = hipStreamQuery(ctx->stream);
+      if (e == hipErrorNotReady) continue;
+      if (e != hipSuccess) return hip_error(e, "reduction");
+      if (__atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq) break;
+      SSP_TRY_HIP(hipMemcpy(ctx->result_host, ctx->result_dev, n * sizeof(double), hipMemcpyDeviceToHost));
+      break;
+    }
+    _mm_pause();
+  }
   std::memcpy(out, ctx->result_host, n * sizeof(double));
   return SSP_OK;
 }
@@ -280,6 +318,7 @@ int ssp_ctx_destroy(ssp_ctx* ctx) {
   if (ctx->partial) (void)hipFree(ctx->partial);
   if (ctx->result_dev) (void)hipFree(ctx->result_dev);
   if (ctx->result_host) (void)hipHostFree(ctx->result_host);
+  if (ctx->pub_flag) (void)hipHostFree(ctx->pub_flag);
   if (ctx->ring_dev) (void)hipFree(ctx->ring_dev);
   if (ctx->ring_host) (void)hipHostFree(ctx->ring_host);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

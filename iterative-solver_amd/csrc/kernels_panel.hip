@@ -10,7 +10,7 @@
 // lane 16i + 4b + j.  Rows / columns are groups of 4 vectors; the contraction (MFMA k and block b)
 // runs over the vector index n.  The 16 lanes that hold one vector (same l & 3) load 16 B each at
 // position p = l >> 2, i.e. 256 contiguous bytes per vector per load instruction (4 vectors per
-// 1 KiB wave load), which streams at the HBM read rate (6.1 TB/s measured for 8 x 48 at N = 1e8,
+// 1 KiB wave load), which streams at the HBM read rate (6.0-6.2 TB/s measured for 8 x 48 at N = 1e8,
 // against 3.7 TB/s for the 16x16x4 layout, whose 16 x 64 B segments per load halve the load-path
 // efficiency).  The two doubles of each 16 B load feed two MFMAs, so the summation order within a
 // 32-element chunk is a fixed permutation.  Block partials are folded with two lane shuffles, waves
@@ -63,9 +63,9 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
     const size_t e = ch * 32 + 2 * p;
     double2 xv[MG], yv[NG];
 #pragma unroll
-    for (int g = 0; g < MG; ++g) xv[g] = xp[g] ? ld2(xp[g] + e) : z2;
+    for (int g = 0; g < MG; ++g) xv[g] = xp[g] ? ssp::ld2nt(xp[g] + e) : z2;
 #pragma unroll
-    for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : (yp[h] ? ld2(yp[h] + e) : z2);
+    for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : (yp[h] ? ssp::ld2nt(yp[h] + e) : z2);
 #pragma unroll
     for (int g = 0; g < MG; ++g)
 #pragma unroll
@@ -447,6 +447,8 @@ int check_ptrs(const double* const* v, int count, size_t n, const char* what) {
 constexpr int ng_max(int) { return 16; }
 
 // Workgroups per gemm_inner launch: 4 per CU (16 waves) when n allows, else one wave per chunk.
+// 8 per CU measures the same (tools/ab_inner.py, profiles/r1/ab_inner.txt); the nontemporal loads
+// of the main loop gain 3 % over plain ones on the same vectors, with bit-identical results.
 unsigned inner_grid(const ssp_ctx* ctx, size_t n) {
   const size_t chunks = n / 32 + 1;
   const size_t blocks = (chunks + 3) / 4;

@@ -41,10 +41,14 @@ struct ssp_ctx {
   // Device scratch for per-workgroup partial sums (deterministic two-pass reductions).
   double* partial = nullptr;
   size_t partial_cap = 0;  // doubles
-  // Device + pinned host staging for small reduction results.
+  // Device + pinned host staging for small reduction results.  result_host and pub_flag are
+  // coherent host memory: a publish kernel writes the result and then a sequence number, which the
+  // host polls (fetch_result) instead of a D2H copy + stream synchronisation.
   double* result_dev = nullptr;
   double* result_host = nullptr;
   size_t result_cap = 0;  // doubles
+  unsigned long long* pub_flag = nullptr;
+  unsigned long long pub_seq = 0;
 
   // Upload ring: pinned host + device mirror for small per-call operand arrays (sparse index
   // lists).  Regions are reused only after a stream synchronisation at wrap-around.
@@ -83,7 +87,8 @@ int ensure_result(ssp_ctx* ctx, size_t n_doubles);
 int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev);
 // Sums the rank-local device results over ranks (no-op for one rank).
 int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n);
-// Copies n doubles of ctx->result_dev to host `out` after the stream drains.
+// Copies n doubles of ctx->result_dev to host `out` once every operation queued before it has
+// completed (publish kernel + host poll of a sequence flag; see context.hip).
 int fetch_result(ssp_ctx* ctx, double* out, size_t n);
 // Grid size for streaming kernels: enough workgroups to fill 256 CUs, grid-stride beyond.
 // Workgroups for a grid-stride streaming launch: enough for work_items / (kBlock * per_thread),
