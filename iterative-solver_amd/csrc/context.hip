@@ -137,42 +137,79 @@ int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n) {
   return SSP_OK;
 }
 
-// Publishes n doubles of the device result into coherent host memory, then the sequence number
-// (system-scope release after every thread's system fence).  One workgroup: n is a reduction result
-// (at most a few thousand doubles).
+// Publishes n doubles of the device result into coherent host memory (system-scope write-through
+// stores), then, once every wave's stores have completed, the sequence number.  One workgroup: n is
+// a reduction result (at most a few thousand doubles).
 __global__ __launch_bounds__(256) void k_publish(const double* src, size_t n, double* dst,
                                                  unsigned long long* flag, unsigned long long seq) {
-  for (size_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
-  __threadfence_system();
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x)
+    __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The result is complete when the flag carries this call's sequence number; the kernel is the last
-// one queued, so every operation before it has completed too (stream order).  Polling the flag
-// instead of a D2H copy + hipStreamSynchronize cuts the host-visible latency of a reduction by about
-// a third (tools/sync_probe.hip, profiles/r1/sync_probe.txt).  The stream is queried every few
-// hundred polls so that a failed kernel surfaces as an error instead of a hang; should the stream
-// drain without the flag becoming visible, the result is copied the ordinary way.
+// Waits until the flag carries `seq`: the kernel that sets it is the last one queued, so every
+// operation before it has completed too (stream order).  Polling the flag instead of a D2H copy +
+// hipStreamSynchronize cuts the host-visible latency of a reduction (tools/sync_probe.hip,
+// profiles/r1/sync_probe.txt).  The stream is queried every few hundred polls so that a failed
+// kernel surfaces as an error instead of a hang.  *seen is false when the stream drained without the
+// flag becoming visible (the writes of a finished kernel are visible all the same).
+int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen) {
+  *seen = true;
+  for (unsigned spin = 1;; ++spin) {
+    if (__atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq) return SSP_OK;
+    if ((spin & 255) == 0) {
+      const hipError_t e = hipStreamQuery(ctx->stream);
+      if (e == hipErrorNotReady) continue;
+      if (e != hipSuccess) return hip_error(e, "reduction");
+      *seen = __atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq;
+      return SSP_OK;
+    }
+    _mm_pause();
+  }
+}
+
 int fetch_result(ssp_ctx* ctx, double* out, size_t n) {
   if (n > ctx->result_cap) return set_error(SSP_ERR_ARG, "fetch_result: result larger than the staging buffer");
   const unsigned long long seq = ++ctx->pub_seq;
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, ctx->stream, ctx->result_dev, n, ctx->result_host,
                      ctx->pub_flag, seq);
   SSP_TRY_HIP(hipGetLastError());
-  for (unsigned spin = 1;; ++spin) {
-    if (__atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq) break;
-    if ((spin & 255) == 0) {
-      const hipError_t e = hipStreamQuery(ctx->stream);
-      if (e == hipErrorNotReady) continue;
-      if (e != hipSuccess) return hip_error(e, "reduction");
-      if (__atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq) break;
-      SSP_TRY_HIP(hipMemcpy(ctx->result_host, ctx->result_dev, n * sizeof(double), hipMemcpyDeviceToHost));
-      break;
-    }
-    _mm_pause();
-  }
+  bool seen = true;
+  SSP_TRY(wait_flag(ctx, seq, &seen));
+  if (!seen)
+    SSP_TRY_HIP(hipMemcpy(ctx->result_host, ctx->result_dev, n * sizeof(double), hipMemcpyDeviceToHost));
   std::memcpy(out, ctx->result_host, n * sizeof(double));
+  return SSP_OK;
+}
+
+int fold_begin(ssp_ctx* ctx, int nout, FoldTail* t) {
+  SSP_TRY(ensure_result(ctx, size_t(nout)));
+  t->counter = ctx->fold_counter;
+  t->nout = nout;
+  t->flag = ctx->pub_flag;
+  const bool ranks = ctx->comm || (ctx->host_allreduce && ctx->nranks > 1);
+  if (ranks) {
+    t->out = ctx->result_dev;
+    t->host = nullptr;
+    t->seq = 0;
+  } else {
+    t->out = nullptr;
+    t->host = ctx->result_host;
+    t->seq = ++ctx->pub_seq;
+  }
+  return SSP_OK;
+}
+
+int fold_finish(ssp_ctx* ctx, const FoldTail& t, double* out) {
+  if (!t.host) {
+    SSP_TRY(allreduce_dev(ctx, ctx->result_dev, size_t(t.nout)));
+    return fetch_result(ctx, out, size_t(t.nout));
+  }
+  bool seen = true;
+  SSP_TRY(wait_flag(ctx, t.seq, &seen));
+  std::memcpy(out, ctx->result_host, size_t(t.nout) * sizeof(double));
   return SSP_OK;
 }
 
@@ -294,6 +331,12 @@ int ssp_ctx_create(int device, ssp_ctx** out) {
   }
   int s = ssp::ensure_partial(ctx, size_t(1) << 20);
   if (s == SSP_OK) s = ssp::ensure_result(ctx, size_t(1) << 16);
+  if (s == SSP_OK) {
+    const size_t bytes = sizeof(unsigned) * ssp::kFoldLine * (ssp::kFoldShards + 1);
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->fold_counter), bytes) != hipSuccess ||
+        hipMemsetAsync(ctx->fold_counter, 0, bytes, ctx->stream) != hipSuccess)
+      s = ssp::set_error(SSP_ERR_NOMEM, "allocation of the reduction counter failed");
+  }
   if (s != SSP_OK) {
     ssp_ctx_destroy(ctx);
     return s;
@@ -319,6 +362,7 @@ int ssp_ctx_destroy(ssp_ctx* ctx) {
   if (ctx->result_dev) (void)hipFree(ctx->result_dev);
   if (ctx->result_host) (void)hipHostFree(ctx->result_host);
   if (ctx->pub_flag) (void)hipHostFree(ctx->pub_flag);
+  if (ctx->fold_counter) (void)hipFree(ctx->fold_counter);
   if (ctx->ring_dev) (void)hipFree(ctx->ring_dev);
   if (ctx->ring_host) (void)hipHostFree(ctx->ring_host);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -33,7 +33,8 @@ struct InnerArgs {
   int m;
   int k;
   size_t n;
-  double* partial;  // [gridDim.x][m][k]
+  double* partial;     // [gridDim.x][m][k]
+  ssp::FoldTail tail;  // row kernel only: fused fold when tail.counter is set
 };
 
 // SYM: xx == yy (a symmetric overlap, MG == NG): each vector is loaded once and used as both
@@ -173,8 +174,9 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner_row(const InnerArgs a) {
     double v = red[0][threadIdx.x];
 #pragma unroll
     for (int w = 1; w < kBlock / 64; ++w) v += red[w][threadIdx.x];
-    a.partial[size_t(blockIdx.x) * K + threadIdx.x] = v;
+    ssp::store_partial(a.partial + size_t(blockIdx.x) * K + threadIdx.x, v);
   }
+  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
 }
 
 struct OuterArgs {
@@ -284,7 +286,8 @@ struct AxpyInnerArgs {
   double c[ssp::kOuterDst];
   int m;
   size_t n;
-  double* partial;  // [gridDim.x][m]
+  double* partial;     // [gridDim.x][m]
+  ssp::FoldTail tail;  // fused fold when tail.counter is set
 };
 
 template <int M>
@@ -331,8 +334,9 @@ __global__ __launch_bounds__(kBlock) void k_axpy_inner(const AxpyInnerArgs a) {
     double s = red[0][threadIdx.x];
 #pragma unroll
     for (int w = 1; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
-    a.partial[size_t(blockIdx.x) * a.m + threadIdx.x] = s;
+    ssp::store_partial(a.partial + size_t(blockIdx.x) * a.m + threadIdx.x, s);
   }
+  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
 }
 
 // Per-block sums of acc[0..M) over the block's waves into partial[block][m].
@@ -352,7 +356,7 @@ __device__ __forceinline__ void block_partials(const double (&acc)[M], int m, do
     double s = red[0][threadIdx.x];
 #pragma unroll
     for (int w = 1; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
-    partial[size_t(blockIdx.x) * m + threadIdx.x] = s;
+    ssp::store_partial(partial + size_t(blockIdx.x) * m + threadIdx.x, s);
   }
 }
 
@@ -363,7 +367,8 @@ struct ScalInnerArgs {
   double alpha;
   int m;
   size_t n;
-  double* partial;  // [gridDim.x][m]
+  double* partial;     // [gridDim.x][m]
+  ssp::FoldTail tail;  // fused fold when tail.counter is set
 };
 
 template <int M>
@@ -395,6 +400,7 @@ __global__ __launch_bounds__(kBlock) void k_scal_inner(const ScalInnerArgs a) {
     for (int j = 0; j < a.m; ++j) acc[j] = fma(xs, a.y[j][e], acc[j]);
   }
   block_partials<M>(acc, a.m, a.partial);
+  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
 }
 
 // y_j += c_j x; acc += y_0_new^2.
@@ -429,6 +435,7 @@ __global__ __launch_bounds__(kBlock) void k_axpy_norm(const AxpyInnerArgs a) {
     }
   }
   block_partials<1>(acc, 1, a.partial);
+  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
 }
 
 int check_ptrs(const double* const* v, int count, size_t n, const char* what) {
@@ -544,6 +551,7 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
   const int R = swap ? k : m, C = swap ? m : k;
   const size_t total = size_t(R) * C;
   SSP_TRY(ssp::ensure_result(ctx, total));
+  ssp::FoldTail tail{};
   if (n == 0) {
     SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, total * sizeof(double), ctx->stream));
   } else {
@@ -564,12 +572,13 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
       const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 4);
       SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * C));
       a.partial = ctx->partial;
+      SSP_TRY(ssp::fold_begin(ctx, C, &tail));
+      a.tail = tail;
       if (C == 1)
         hipLaunchKernelGGL((k_gemm_inner_row<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       else
         hipLaunchKernelGGL((k_gemm_inner_row<2>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
-      SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, C, ctx->result_dev, C, 0, 0));
     }
     // A symmetric overlap <xx_i, xx_j> of up to 16 vectors: one panel that loads each vector once.
     bool sym = m == k && m <= ssp::kInnerRows && !(R == 1 && C <= 2);
@@ -603,10 +612,15 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
       }
     }
   }
-  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, total));
-  if (!swap) return ssp::fetch_result(ctx, out, total);
-  std::vector<double> t(total);
-  SSP_TRY(ssp::fetch_result(ctx, t.data(), total));
+  std::vector<double> t(swap ? total : 0);
+  double* dst = swap ? t.data() : out;
+  if (tail.counter) {
+    SSP_TRY(ssp::fold_finish(ctx, tail, dst));
+  } else {
+    SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, total));
+    SSP_TRY(ssp::fetch_result(ctx, dst, total));
+  }
+  if (!swap) return SSP_OK;
   for (int i = 0; i < m; ++i)
     for (int j = 0; j < k; ++j) out[size_t(i) * k + j] = t[size_t(j) * m + i];
   return SSP_OK;
@@ -688,9 +702,11 @@ int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* y
     return m == 0 ? SSP_OK : ssp_gemm_inner(ctx, const_cast<const double* const*>(&x), 1, yy, m, n, out);
   }
   SSP_TRY(ssp::ensure_result(ctx, size_t(m)));
+  ssp::FoldTail tail{};
   if (n == 0) {
     SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, size_t(m) * sizeof(double), ctx->stream));
   } else {
+    SSP_TRY(ssp::fold_begin(ctx, m, &tail));
     ssp::LedgerScope ls(ctx, "scal_inner", 8.0 * n * (2.0 + m));
     const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 1);
     ScalInnerArgs a{};
@@ -701,6 +717,7 @@ int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* y
     for (int j = 0; j < m; ++j) a.y[j] = yy[j];
     SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * m));
     a.partial = ctx->partial;
+    a.tail = tail;
     if (m <= 1)
       hipLaunchKernelGGL((k_scal_inner<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (m <= 4)
@@ -710,8 +727,8 @@ int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* y
     else
       hipLaunchKernelGGL((k_scal_inner<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
-    SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, m, ctx->result_dev, m, 0, 0));
   }
+  if (tail.counter) return ssp::fold_finish(ctx, tail, out);
   SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, size_t(m)));
   return ssp::fetch_result(ctx, out, size_t(m));
 }
@@ -730,9 +747,11 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
     return ssp_dot(ctx, yy[0], yy[0], n, out);
   }
   SSP_TRY(ssp::ensure_result(ctx, 1));
+  ssp::FoldTail tail{};
   if (n == 0) {
     SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, sizeof(double), ctx->stream));
   } else {
+    SSP_TRY(ssp::fold_begin(ctx, 1, &tail));
     ssp::LedgerScope ls(ctx, "axpy_norm", 8.0 * n * (1.0 + 2.0 * m));
     const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 1);
     AxpyInnerArgs a{};
@@ -745,6 +764,7 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
     }
     SSP_TRY(ssp::ensure_partial(ctx, size_t(grid)));
     a.partial = ctx->partial;
+    a.tail = tail;
     if (m <= 1)
       hipLaunchKernelGGL((k_axpy_norm<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (m <= 4)
@@ -754,8 +774,8 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
     else
       hipLaunchKernelGGL((k_axpy_norm<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
-    SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, 1, ctx->result_dev, 1, 0, 0));
   }
+  if (tail.counter) return ssp::fold_finish(ctx, tail, out);
   SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, 1));
   return ssp::fetch_result(ctx, out, 1);
 }
@@ -772,9 +792,11 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
   for (int j = 0; j < m; ++j)
     if (yy[j] == x || yy[j] == z) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_inner: a destination aliases x or z");
   SSP_TRY(ssp::ensure_result(ctx, size_t(m)));
+  ssp::FoldTail tail{};
   if (n == 0) {
     SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, size_t(m) * sizeof(double), ctx->stream));
   } else {
+    if (m <= ssp::kOuterDst) SSP_TRY(ssp::fold_begin(ctx, m, &tail));  // one launch: fused fold
     ssp::LedgerScope ls(ctx, "axpy_inner", 8.0 * n * (2.0 + 2.0 * m));
     const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 1);
     for (int j0 = 0; j0 < m; j0 += ssp::kOuterDst) {
@@ -789,6 +811,7 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
       }
       SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * a.m));
       a.partial = ctx->partial;
+      a.tail = tail;
       if (a.m <= 1)
         hipLaunchKernelGGL((k_axpy_inner<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       else if (a.m <= 4)
@@ -798,9 +821,11 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
       else
         hipLaunchKernelGGL((k_axpy_inner<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
-      SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, a.m, ctx->result_dev, m, 0, j0));
+      if (!tail.counter)
+        SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, a.m, ctx->result_dev, m, 0, j0));
     }
   }
+  if (tail.counter) return ssp::fold_finish(ctx, tail, out);
   SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, size_t(m)));
   return ssp::fetch_result(ctx, out, size_t(m));
 }

@@ -5,8 +5,9 @@
 // Each is HBM-bound (<= 0.25 flop/B).  Layout: 16-byte (double2) accesses per lane, 4 independent
 // accesses per lane in flight, grid-stride.  Grid caps and nontemporal accesses follow the sweep in
 // tools/mb_stream.hip (profiles/r1/mb_stream*.txt): fill and axpy run best with one pass over a
-// large grid (64 workgroups per CU), dot with 8 per CU and nontemporal loads.  Reductions are two
-// pass and deterministic: one partial per workgroup in a fixed grid, then a fixed-order tree.
+// large grid (64 workgroups per CU), dot with 8 per CU and nontemporal loads.  Reductions are
+// deterministic: one partial per workgroup in a fixed grid, then a fixed-order fold (by the last
+// workgroup to finish for small results, ssp::fold_tail; else the k_reduce_partials pass).
 #include <algorithm>
 
 #include "ssp_internal.h"
@@ -109,7 +110,8 @@ __global__ __launch_bounds__(kBlock) void k_axpy(const double* __restrict__ x, d
 // SAME: x == y (norms), one load stream.
 template <bool SAME>
 __global__ __launch_bounds__(kBlock) void k_dot_partial(const double* __restrict__ x, const double* __restrict__ y,
-                                                        size_t n, double* __restrict__ partial) {
+                                                        size_t n, double* __restrict__ partial,
+                                                        const ssp::FoldTail tail) {
   const size_t n2 = n >> 1;
   const size_t stride = size_t(gridDim.x) * kBlock;
   size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
@@ -141,7 +143,8 @@ __global__ __launch_bounds__(kBlock) void k_dot_partial(const double* __restrict
   }
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) s0 = fma(x[n - 1], y[n - 1], s0);
   double s = block_sum((s0 + s1) + (s2 + s3));
-  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+  if (threadIdx.x == 0) ssp::store_partial(partial + blockIdx.x, s);
+  ssp::fold_tail(partial, tail);
 }
 
 // out[(row0+r)*ldo + col0+c] = sum_b partial[b*rows*cols + r*cols + c]; one workgroup per output.
@@ -253,22 +256,25 @@ int ssp_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, double* ou
   if (!out) return ssp::set_error(SSP_ERR_ARG, "ssp_dot: null out");
   SSP_TRY(check_vec(x, n, "ssp_dot"));
   SSP_TRY(check_vec(y, n, "ssp_dot"));
-  SSP_TRY(ssp::ensure_result(ctx, 1));
   if (n == 0) {
+    SSP_TRY(ssp::ensure_result(ctx, 1));
     SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, sizeof(double), ctx->stream));
-  } else {
-    const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 4);
-    SSP_TRY(ssp::ensure_partial(ctx, grid));
+    SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, 1));
+    return ssp::fetch_result(ctx, out, 1);
+  }
+  const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 4);
+  SSP_TRY(ssp::ensure_partial(ctx, grid));
+  ssp::FoldTail tail{};
+  SSP_TRY(ssp::fold_begin(ctx, 1, &tail));
+  {
     ssp::LedgerScope ls(ctx, "dot", (x == y ? 8.0 : 16.0) * n);
     if (x == y)
-      hipLaunchKernelGGL(k_dot_partial<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, x, y, n, ctx->partial);
+      hipLaunchKernelGGL(k_dot_partial<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, x, y, n, ctx->partial, tail);
     else
-      hipLaunchKernelGGL(k_dot_partial<false>, dim3(grid), dim3(kBlock), 0, ctx->stream, x, y, n, ctx->partial);
+      hipLaunchKernelGGL(k_dot_partial<false>, dim3(grid), dim3(kBlock), 0, ctx->stream, x, y, n, ctx->partial, tail);
     SSP_TRY_HIP(hipGetLastError());
-    SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, 1, ctx->result_dev, 1, 0, 0));
   }
-  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, 1));
-  return ssp::fetch_result(ctx, out, 1);
+  return ssp::fold_finish(ctx, tail, out);
 }
 
 int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n) {

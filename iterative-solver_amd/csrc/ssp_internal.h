@@ -49,6 +49,8 @@ struct ssp_ctx {
   size_t result_cap = 0;  // doubles
   unsigned long long* pub_flag = nullptr;
   unsigned long long pub_seq = 0;
+  // Arrival counter of the fused reduction tails (FoldTail); zero between launches.
+  unsigned* fold_counter = nullptr;
 
   // Upload ring: pinned host + device mirror for small per-call operand arrays (sparse index
   // lists).  Regions are reused only after a stream synchronisation at wrap-around.
@@ -121,6 +123,113 @@ class LedgerScope {
   int slot_ = -1;
   hipEvent_t start_ = nullptr;
 };
+
+// Sum over the 256 threads of a workgroup; result valid in thread 0.  Fixed order.
+__device__ inline double block_sum256(double v) {
+  __shared__ double wsum[kBlock / 64];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) wsum[wave] = v;
+  __syncthreads();
+  double s = 0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) s += wsum[w];
+  }
+  __syncthreads();  // wsum may be reused by the next call
+  return s;
+}
+
+// Reduction tail fused into the kernel that writes the per-workgroup partials (results of at most
+// a few dozen doubles): the last workgroup to arrive folds partial[grid][nout] in exactly the order
+// of the separate k_reduce_partials pass (per output: thread t sums workgroups t, t + 256, ...,
+// then block_sum256), so results are bit-identical to the two-kernel form.  It then stores the
+// results in device memory (`out`, for a following allreduce) or publishes them straight into
+// coherent host memory followed by the sequence flag (one rank: no second kernel, no D2H copy).
+//
+// Hand-off (cdna_hip_programming.md Guideline 16, write-through form): every partial is stored by
+// wave 0 of its workgroup with an agent-scope write-through store (store_partial, sc1); wave 0 waits
+// for its stores (vmcnt(0)) before lane 0 adds to the arrival counters (agent-scope atomics, two
+// levels); the last arriver reads every partial with sc1 loads.  No __threadfence(): its L2 write-back + invalidate in
+// every workgroup costs more than the launch it saves.
+constexpr unsigned kFoldShards = 8;  // arrival-counter shards (one per XCD's worth of workgroups)
+constexpr unsigned kFoldLine = 32;   // unsigned per 128-B line
+struct FoldTail {
+  unsigned* counter;  // kFoldShards shard counters + the top counter, kFoldLine apart, all zero
+  double* out;                // device results, or nullptr
+  double* host;               // coherent host results, or nullptr
+  unsigned long long* flag;   // with host: set to seq after the results
+  unsigned long long seq;
+  int nout;
+};
+
+// Stores one per-workgroup partial (callers: lanes of wave 0 only).
+__device__ inline void store_partial(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline void fold_tail(const double* partial, const FoldTail& t) {
+  __shared__ unsigned s_last;
+  if (threadIdx.x < 64) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's partial stores have completed
+    if (threadIdx.x == 0) {
+      // Two-level arrival: workgroup b adds to shard b % 8 (each shard on a 128-B line of its own),
+      // the last arriver of a shard resets it and adds to the top counter.  Eight shards keep ~2000
+      // same-address atomics from serialising at the end of a launch (one counter: +15 us at 2048
+      // workgroups, profiles/r1/latency_probe_fused.json).
+      const unsigned G = gridDim.x, sh = blockIdx.x & (kFoldShards - 1);
+      const unsigned nsh = G < kFoldShards ? G : kFoldShards, in_sh = (G - sh + kFoldShards - 1) / kFoldShards;
+      unsigned last = 0;
+      unsigned* c = t.counter + kFoldLine * sh;
+      if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_sh - 1) {
+        __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = __hip_atomic_fetch_add(t.counter + kFoldLine * kFoldShards, 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+      }
+      s_last = last;
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the loads are sc1
+  const int G = int(gridDim.x);
+  for (int o = 0; o < t.nout; ++o) {
+    // Thread t adds workgroups t, t + 256, ... in that order; the loads are issued 8 at a time so
+    // their (cross-XCD) latencies overlap.
+    double s = 0;
+    for (int b0 = threadIdx.x; b0 < G; b0 += 8 * kBlock) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + u * kBlock;
+        v[u] = b < G ? __hip_atomic_load(partial + size_t(b) * t.nout + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (b0 + u * kBlock < G) s += v[u];
+    }
+    s = block_sum256(s);
+    if (threadIdx.x == 0) {
+      if (t.host) __hip_atomic_store(t.host + o, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else t.out[o] = s;
+    }
+  }
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(t.counter + kFoldLine * kFoldShards, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t.host) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the results have reached host memory
+      __hip_atomic_store(t.flag, t.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// Host side of FoldTail (context.hip): fold_begin fills the tail for nout results (host publication
+// when no communicator is attached); fold_finish delivers the nout results to `out` (waiting on the
+// flag, or allreduce + fetch_result).
+int fold_begin(ssp_ctx* ctx, int nout, FoldTail* t);
+int fold_finish(ssp_ctx* ctx, const FoldTail& t, double* out);
 
 // kernels_stream.hip
 int launch_reduce_partials(ssp_ctx* ctx, const double* partial, int nblocks, int rows, int cols, double* out,
