@@ -43,6 +43,9 @@ if [ "$what" = prof ] || [ "$what" = all ]; then
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "$@"
   rc=$?
   if [ $rc -ne 0 ]; then exit $rc; fi
+  # The bench line of the profiled process itself: its HIP-event ledger and the kernel statistics
+  # below come from the same allocation (placement moves gemm_outer by up to 8 % between processes).
+  grep '^{' "$OUT/rocprof.log" >"$OUT/bench_rocprof.json" || true
 fi
 if [ "$what" = pmc ] || [ "$what" = all ]; then
   # HBM traffic counters, one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass);

@@ -1,7 +1,7 @@
 // Read path: register loads against LDS-DMA (global_load_lds_dwordx4) for the panel kernels'
 // many-vector streams at N = 1e8 (development tool, not part of the library).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_glds.hip -o tools/mb_glds
-// Run:   tools/mb_glds [n=1e8] [s = read-pattern sweep]
+// Run:   tools/mb_glds [n=1e8] [s = read-pattern sweep | p = placement: default vs contiguous allocations]
 //
 // The question: MI355X_MICROARCH.md's ldsdma-fill row reads 6.5-6.8 TB/s chip-wide with nt LDS-DMA,
 // against 6.3-6.4 TB/s for register loads (profiles/r1/mb_read_patterns.txt).  Does a 56-vector
@@ -303,6 +303,41 @@ int main(int argc, char** argv) {
   };
   const int reps = 7;
   const double rb = 8.0 * n * NV, ob = 8.0 * n * (48 + 16);
+  if (argc > 2 && argv[2][0] == 'p') {
+    // Placement: the same kernels over freshly allocated vector sets, default hipMalloc against
+    // hipExtMallocWithFlags(hipDeviceMallocContiguous), alternating.
+    for (int i = 0; i < NV; ++i) CK(hipFree(vec[i]));
+    for (int set = 0; set < 8; ++set) {
+      const bool contig = set & 1;
+      bool ok = true;
+      for (int i = 0; i < NV; ++i) {
+        hipError_t e = contig ? hipExtMallocWithFlags((void**)&vec[i], n * 8, hipDeviceMallocContiguous)
+                              : hipMalloc((void**)&vec[i], n * 8);
+        if (e != hipSuccess) {
+          printf("set %d: allocation %d failed: %s\n", set, i, hipGetErrorString(e));
+          for (int j = 0; j < i; ++j) CK(hipFree(vec[j]));
+          ok = false;
+          break;
+        }
+        hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, 0, vec[i], n, unsigned(i));
+      }
+      (void)hipGetLastError();
+      if (!ok) continue;
+      CK(hipDeviceSynchronize());
+      for (int i = 0; i < NV; ++i) a.x[i] = vec[i];
+      for (int i = 0; i < 48; ++i) o.x[i] = vec[8 + i];
+      for (int j = 0; j < 8; ++j) o.y[j] = vec[j];
+      char nm[64];
+      snprintf(nm, 64, "set %d %s outer", set, contig ? "contig " : "default");
+      rep(nm, 2048, timeit([&] { hipLaunchKernelGGL(k_outer_reg, dim3(2048), dim3(256), 0, 0, o); }, reps), ob);
+      snprintf(nm, 64, "set %d %s read56", set, contig ? "contig " : "default");
+      rep(nm, 2048, timeit([&] { hipLaunchKernelGGL((k_reg<4, 4>), dim3(2048), dim3(256), 0, 0, a, NV, out); }, reps), rb);
+      snprintf(nm, 64, "set %d %s quad", set, contig ? "contig " : "default");
+      rep(nm, 2048, timeit([&] { hipLaunchKernelGGL((k_quad<1>), dim3(2048), dim3(256), 0, 0, a, NV, out); }, reps), rb);
+      for (int i = 0; i < NV; ++i) CK(hipFree(vec[i]));
+    }
+    return 0;
+  }
   const bool sweep = argc > 2 && argv[2][0] == 's';
   for (int round = 0; round < 2; ++round) {
     if (sweep) {
