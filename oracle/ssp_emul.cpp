@@ -10,6 +10,7 @@
 // reference heap (util/select.h:28-55) per rank followed by the same merge rule ssp_select_merge
 // documents.  GPU parity is proven by tests/test_*_gpu.py against the real library, not here.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -26,6 +27,14 @@ struct ssp_ctx {
   ssp_host_allreduce_fn allreduce = nullptr;
   ssp_host_allgather_fn allgather = nullptr;
   void* user = nullptr;
+  // Operation ledger (host clock here; HIP events in the real library), same names and bytes.
+  struct Entry {
+    std::string name;
+    long long calls = 0;
+    double ms = 0, bytes = 0;
+  };
+  bool ledger_on = false;
+  std::vector<Entry> ledger;
 };
 
 namespace {
@@ -41,6 +50,24 @@ int reduce(ssp_ctx* c, double* v, size_t n) {
   if (!c->allreduce || c->allreduce(v, n, c->user) != 0) return fail(SSP_ERR_COMM, "emul: allreduce failed");
   return SSP_OK;
 }
+
+struct Led {
+  ssp_ctx* c;
+  const char* name;
+  double bytes;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  Led(ssp_ctx* ctx, const char* op, double b) : c(ctx), name(op), bytes(b) {}
+  ~Led() {
+    if (!c || !c->ledger_on) return;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (auto& e : c->ledger)
+      if (e.name == name) {
+        e.calls++, e.ms += ms, e.bytes += bytes;
+        return;
+      }
+    c->ledger.push_back({name, 1, ms, bytes});
+  }
+};
 
 uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -130,36 +157,57 @@ int ssp_shard_range(size_t n, int nranks, int rank, size_t* off, size_t* len) {
   *len = b + (r < e ? 1 : 0);
   return SSP_OK;
 }
-int ssp_ledger_enable(ssp_ctx*, int) { return SSP_OK; }
-int ssp_ledger_reset(ssp_ctx*) { return SSP_OK; }
-int ssp_ledger_count(ssp_ctx*) { return 0; }
-int ssp_ledger_entry(ssp_ctx*, int, const char**, long long*, double*, double*) {
-  return fail(SSP_ERR_ARG, "emul: no ledger");
+int ssp_ledger_enable(ssp_ctx* c, int on) {
+  c->ledger_on = on != 0;
+  return SSP_OK;
+}
+int ssp_ledger_reset(ssp_ctx* c) {
+  c->ledger.clear();
+  return SSP_OK;
+}
+int ssp_ledger_count(ssp_ctx* c) { return int(c->ledger.size()); }
+int ssp_ledger_entry(ssp_ctx* c, int i, const char** name, long long* calls, double* ms, double* bytes) {
+  if (i < 0 || i >= int(c->ledger.size())) return fail(SSP_ERR_ARG, "ssp_ledger_entry: index out of range");
+  const auto& e = c->ledger[size_t(i)];
+  *name = e.name.c_str();
+  *calls = e.calls;
+  *ms = e.ms;
+  *bytes = e.bytes;
+  return SSP_OK;
 }
 
-int ssp_fill(ssp_ctx*, double a, double* x, size_t n) {
+int ssp_fill(ssp_ctx* c, double a, double* x, size_t n) {
+  Led l(c, "fill", 8.0 * n);
   for (size_t i = 0; i < n; ++i) x[i] = a;
   return SSP_OK;
 }
-int ssp_scal(ssp_ctx*, double a, double* x, size_t n) {
+int ssp_scal(ssp_ctx* c, double a, double* x, size_t n) {
+  Led l(c, "scal", 16.0 * n);
   for (size_t i = 0; i < n; ++i) x[i] *= a;
   return SSP_OK;
 }
-int ssp_copy(ssp_ctx*, double* x, const double* y, size_t n) {
+int ssp_copy(ssp_ctx* c, double* x, const double* y, size_t n) {
+  Led l(c, "copy", 16.0 * n);
   if (n && x != y) std::memmove(x, y, n * sizeof(double));
   return SSP_OK;
 }
-int ssp_axpy(ssp_ctx*, double a, const double* x, double* y, size_t n) {
+int ssp_axpy(ssp_ctx* c, double a, const double* x, double* y, size_t n) {
+  Led l(c, "axpy", 24.0 * n);
   for (size_t i = 0; i < n; ++i) y[i] += a * x[i];
   return SSP_OK;
 }
 int ssp_dot(ssp_ctx* c, const double* x, const double* y, size_t n, double* out) {
+  Led l(c, "dot", (x == y ? 8.0 : 16.0) * n);
   double s = 0;
   for (size_t i = 0; i < n; ++i) s += x[i] * y[i];
   *out = s;
   return reduce(c, out, 1);
 }
 int ssp_gemm_inner(ssp_ctx* c, const double* const* xx, int m, const double* const* yy, int k, size_t n, double* out) {
+  std::vector<const double*> distinct(xx, xx + m);
+  distinct.insert(distinct.end(), yy, yy + k);
+  std::sort(distinct.begin(), distinct.end());
+  Led l(c, "gemm_inner", 8.0 * n * double(std::unique(distinct.begin(), distinct.end()) - distinct.begin()));
   for (int i = 0; i < m; ++i)
     for (int j = 0; j < k; ++j) {
       double s = 0;
@@ -184,7 +232,8 @@ int ssp_gemm_outer_set(ssp_ctx* c, const double* al, const double* const* xx, in
     for (size_t e = 0; e < n; ++e) yy[j][e] = 0;
   return ssp_gemm_outer(c, al, xx, k, yy, m, n);
 }
-int ssp_gemm_outer(ssp_ctx*, const double* al, const double* const* xx, int k, double* const* yy, int m, size_t n) {
+int ssp_gemm_outer(ssp_ctx* c, const double* al, const double* const* xx, int k, double* const* yy, int m, size_t n) {
+  Led l(c, "gemm_outer", 8.0 * n * (k + 2.0 * m));
   for (int j = 0; j < m; ++j)
     for (int i = 0; i < k; ++i) {
       const double a = al[size_t(i) * m + j];

@@ -87,3 +87,43 @@ def test_bench_two_ranks_host_hub():
     d = parse(r.stdout)
     assert d["n_gpus"] == 2 and d["cpu_baseline"] is None
     assert d["config"]["n_local_rank0"] == 2_000_001  # spread-remainder: rank 0 takes the extra element
+
+
+def test_bench_eight_ranks_emulated():
+    """The driver's 8-GPU launch rehearsed on CPU: 8 ranks under torch.distributed.run over the host
+    emulation of the device ABI (--comm host): shard sizes, barriers, max-over-ranks time, ledger and
+    one JSON line from rank 0."""
+    env = dict(os.environ)
+    for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    n = 8 * 12_500 + 5
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "bench_emul.py"), "bench",
+           "--gpus", "8", "--steps", "2", "--warmup", "1", "--ledger-steps", "1", "--n-global", str(n),
+           "--comm", "host"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = parse(r.stdout)
+    assert d["n_gpus"] == 8 and d["cpu_baseline"] is None and d["scaling"] == "strong"
+    assert d["config"]["n_local_rank0"] == bench.distribution(n, 8)[1] == 12_501
+    assert d["config"]["bytes_per_step"] == bench.step_bytes(n, 8, 48)
+    assert set(d["ops"]) == {"gemm_inner", "gemm_outer", "fill", "axpy", "dot"}
+
+
+def test_rccl_id_rendezvous_eight_ranks():
+    """bench.rendezvous_uid: rank 0's RCCL unique id reaches all 8 local ranks (siblings of one
+    launcher process, keyed by MASTER_ADDR/PORT and the parent pid)."""
+    port = str(free_port())
+    procs = []
+    for r in range(8):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="8", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "bench_emul.py"), "uid"],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                                      cwd=ROOT))
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    want = bytes(range(7, 7 + 128)).hex()
+    for r, (p, out) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, out[-2000:]
+        assert f"uid {r} {want}" in out, out[-2000:]
