@@ -3,7 +3,7 @@
 
 Times many back-to-back calls from Python (ctypes) so the figure is host-visible latency per call:
 launch + kernel + (for reductions) the second pass, the D2H of the result and the stream sync.
-Usage: python tools/latency_probe.py [--out file.json]
+Usage: python tools/latency_probe.py [--rccl] [--out file.json]
 """
 import argparse
 import json
@@ -26,9 +26,14 @@ def per_call(f, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
+    ap.add_argument("--rccl", action="store_true",
+                    help="attach a one-rank RCCL communicator: reductions take the multi-rank path "
+                         "(fold -> ncclAllReduce -> publish) instead of the fused host publish")
     args = ap.parse_args()
     res = {}
     with sh.Context(0) as ctx:
+        if args.rccl:
+            ctx.attach_comm(1, 0, sh.Context.unique_id())
         for n in (1024, 1_000_000, 12_500_000):
             reps = 2000 if n <= 1_000_000 else 200
             x = [ctx.alloc(n) for _ in range(56)]
@@ -42,6 +47,7 @@ def main():
                 "dot(x,y)": per_call(lambda: ctx.dot(x[1], x[2]), reps),
                 "gemm_inner 8x48": per_call(lambda: ctx.gemm_inner(x[:8], x[8:56]), max(20, reps // 10)),
                 "sync only": per_call(ctx.synchronize, reps),
+                "barrier": per_call(ctx.barrier, reps),
             }
             res[str(n)] = {k: round(v, 2) for k, v in r.items()}
             print(n, json.dumps(res[str(n)]), flush=True)
