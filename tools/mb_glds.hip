@@ -1,7 +1,7 @@
 // Read path: register loads against LDS-DMA (global_load_lds_dwordx4) for the panel kernels'
 // many-vector streams at N = 1e8 (development tool, not part of the library).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_glds.hip -o tools/mb_glds
-// Run:   tools/mb_glds [n=1e8] [s = read-pattern sweep | p = placement: default vs contiguous allocations]
+// Run:   tools/mb_glds [n=1e8] [s = read-pattern sweep | p = placement: default vs contiguous allocations | o = gemm_outer destination split]
 //
 // The question: MI355X_MICROARCH.md's ldsdma-fill row reads 6.5-6.8 TB/s chip-wide with nt LDS-DMA,
 // against 6.3-6.4 TB/s for register loads (profiles/r1/mb_read_patterns.txt).  Does a 56-vector
@@ -249,6 +249,47 @@ __global__ __launch_bounds__(256) void k_outer_reg(const Args a) {
   }
 }
 
+// Destinations split over the waves of a workgroup: the G = 8 / MW waves of a group share one 4 KiB
+// window and each applies all 48 sources to its MW destinations (the sources' second and later
+// reads of a window are meant to hit the CU's L1 / the XCD's L2).  Fewer accumulator registers per
+// wave: more waves in flight per SIMD.
+template <int MW>
+__global__ __launch_bounds__(256) void k_outer_split(const Args a) {
+  constexpr int K = 48, U = 4, G = 8 / MW, WPB = 4 / G;  // windows per block
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j0 = (wave % G) * MW;
+  const size_t gw = size_t(blockIdx.x) * WPB + wave / G, nw = size_t(gridDim.x) * WPB;
+  const size_t n2 = a.n >> 1, win = 64 * U;
+  for (size_t c = gw; (c + 1) * win <= n2; c += nw) {
+    const size_t p0 = c * win + lane;
+    double2 acc[U][MW];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < MW; ++j) acc[u][j] = ld2nt(a.y[j0 + j] + 2 * (p0 + 64 * u));
+    for (int i = 0; i < K; i += 4) {
+      double2 xv[4][U];
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[b][u] = *reinterpret_cast<const double2*>(a.x[i + b] + 2 * (p0 + 64 * u));
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int j = 0; j < MW; ++j)
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            acc[u][j].x = fma(a.alpha[(i + b) * 8 + j0 + j], xv[b][u].x, acc[u][j].x);
+            acc[u][j].y = fma(a.alpha[(i + b) * 8 + j0 + j], xv[b][u].y, acc[u][j].y);
+          }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < MW; ++j) st2nt(a.y[j0 + j] + 2 * (p0 + 64 * u), acc[u][j]);
+  }
+}
+
 __global__ void k_init(double* x, size_t n, unsigned seed) {
   for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
     x[i] = double((i * 2654435761u + seed) % 1000) * 1e-3 - 0.5;
@@ -303,6 +344,28 @@ int main(int argc, char** argv) {
   };
   const int reps = 7;
   const double rb = 8.0 * n * NV, ob = 8.0 * n * (48 + 16);
+  if (argc > 2 && argv[2][0] == 'o') {
+    // gemm_outer 48 -> 8: library form against destination-split forms, over fresh vector sets.
+    for (int set = 0; set < 4; ++set) {
+      if (set) {
+        for (int i = 0; i < NV; ++i) CK(hipFree(vec[i]));
+        for (int i = 0; i < NV; ++i) {
+          CK(hipMalloc((void**)&vec[i], n * 8));
+          hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, 0, vec[i], n, unsigned(i));
+        }
+        CK(hipDeviceSynchronize());
+        for (int i = 0; i < 48; ++i) o.x[i] = vec[8 + i];
+        for (int j = 0; j < 8; ++j) o.y[j] = vec[j];
+      }
+      printf("-- set %d\n", set);
+      for (int g : {1024, 2048}) {
+        rep("outer reg U4 (library)", g, timeit([&] { hipLaunchKernelGGL(k_outer_reg, dim3(g), dim3(256), 0, 0, o); }, reps), ob);
+        rep("outer split 4 dst/wave", g, timeit([&] { hipLaunchKernelGGL((k_outer_split<4>), dim3(g), dim3(256), 0, 0, o); }, reps), ob);
+        rep("outer split 2 dst/wave", g, timeit([&] { hipLaunchKernelGGL((k_outer_split<2>), dim3(g), dim3(256), 0, 0, o); }, reps), ob);
+      }
+    }
+    return 0;
+  }
   if (argc > 2 && argv[2][0] == 'p') {
     // Placement: the same kernels over freshly allocated vector sets, default hipMalloc against
     // hipExtMallocWithFlags(hipDeviceMallocContiguous), alternating.
