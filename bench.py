@@ -34,6 +34,7 @@ import subspace_hip as sh  # noqa: E402
 
 METRIC = "subspace-update GB/s (gemm_inner+axpy) at N=1e8, 8 roots; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
+MFMA_F64_PEAK_TFLOPS = 78.6  # MI355X dense f64 matrix peak
 SEED = 20251015
 
 
@@ -106,6 +107,19 @@ def pmc_traffic(path, op, n_global, m, k, world):
         base = name.split("<")[0]
         if base in prefixes:
             return v["hbm_bytes_per_dispatch"], os.path.relpath(path, ROOT) + ":" + name
+    return None, None
+
+
+def mfma_util(path, kernel_prefix="k_gemm_inner<2, 12"):
+    """MFMA utilisation of gemm_inner 8x48 from the committed rocprofv3 --pmc MfmaUtil summary."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    for name, v in d.get("bench_step", {}).items():
+        if name.startswith(kernel_prefix):
+            return v["mfma_util_pct"], os.path.relpath(path, ROOT) + ":" + name
     return None, None
 
 
@@ -207,6 +221,8 @@ def main():
                          "lets tests run several ranks on ONE device (RCCL refuses duplicate GPUs)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r1", "pmc_traffic_n1e8.json"),
                     help="rocprofv3 --pmc summary of this workload (roofline.traffic)")
+    ap.add_argument("--mfma-json", default=os.path.join(ROOT, "profiles", "r1", "mfma_util_n1e8.json"),
+                    help="rocprofv3 --pmc MfmaUtil summary of this workload (mfma.mfma_util_pct)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -311,6 +327,15 @@ def main():
             },
             "ops": ops,
         }
+        if "gemm_inner" in led and world == 1:
+            # gemm_inner runs on the f64 matrix cores: live MFMA rate from the ledger (2 m k N flops
+            # per call) against the dense f64 MFMA peak, and the PMC-measured MfmaUtil beside it.
+            gi = led["gemm_inner"]
+            tflops = 2.0 * m * k * n_local * gi["calls"] / (gi["ms"] / 1e3) / 1e12
+            util, util_src = mfma_util(args.mfma_json)
+            result["mfma"] = {"kernel": "gemm_inner", "achieved_tflops": round(tflops, 2),
+                              "peak_tflops": MFMA_F64_PEAK_TFLOPS, "frac": round(tflops / MFMA_F64_PEAK_TFLOPS, 4),
+                              "mfma_util_pct": util, "util_source": util_src}
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline (oracle, 1 core)...")
             result["cpu_baseline"] = cpu_baseline(m, k, args.cpu_seconds)

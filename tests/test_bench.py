@@ -45,6 +45,16 @@ def test_pmc_traffic_lookup():
     assert bench.pmc_traffic("/nonexistent.json", "dot", 1, 1, 1, 1) == (None, None)
 
 
+def test_mfma_util_lookup():
+    path = os.path.join(ROOT, "profiles", "r1", "mfma_util_n1e8.json")
+    util, src = bench.mfma_util(path)
+    assert 0 < util < 100 and src.startswith("profiles/r1/mfma_util_n1e8.json:k_gemm_inner<2, 12")
+    d = json.load(open(path))
+    k = next(v for n, v in d["bench_step"].items() if n.startswith("k_gemm_inner<2, 12"))
+    assert k["mfma_f64_flops_per_dispatch"] == 2 * 8 * 48 * 10**8  # MOPS x 512 = algorithmic flops
+    assert bench.mfma_util("/nonexistent.json") == (None, None)
+
+
 def test_cpu_baseline_leg():
     cb = bench.cpu_baseline(2, 3, 0.05)
     assert cb["kind"] == "port" and cb["cores"] == 1 and cb["unit"] == "GB/s" and cb["value"] > 0

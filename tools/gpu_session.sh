@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: GPU tests, bench, kernel-trace profile.  Each GPU step has its own time limit;
 # a fault / abort / timeout ends the session (no retries).  Outputs land in gpurun_out/.
-# Usage: tools/gpu_session.sh [tests|bench|prof|pmc|ledger|all] [extra bench args...]
+# Usage: tools/gpu_session.sh [tests|bench|prof|pmc|mfma|ledger|all] [extra bench args...]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -57,6 +57,20 @@ if [ "$what" = pmc ] || [ "$what" = all ]; then
     rc=$?
     if [ $rc -ne 0 ]; then exit $rc; fi
   done
+fi
+if [ "$what" = mfma ] || [ "$what" = all ]; then
+  # Matrix-core activity (MfmaUtil, MfmaFlopsF64): the bench step, then the per-shape bench
+  # (gemm_inner 16x64 is the densest panel), one --pmc pass each.
+  rm -rf "$OUT/pmc_mfma" "$OUT/pmc_mfma_shapes"
+  step pmc_mfma 600 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 --kernel-trace -d "$OUT/pmc_mfma" \
+    -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 --no-cpu-baseline "$@"
+  rc=$?
+  if [ $rc -ne 0 ]; then exit $rc; fi
+  step pmc_mfma_shapes 600 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 --kernel-trace \
+    -d "$OUT/pmc_mfma_shapes" -o run --output-format csv -- python3 tools/shapes_bench.py --reps 1 \
+    --out "$OUT/shapes_pmc.json"
+  rc=$?
+  if [ $rc -ne 0 ]; then exit $rc; fi
 fi
 if [ "$what" = ledger ] || [ "$what" = all ]; then
   step shapes 600 python tools/shapes_bench.py --out "$OUT/shapes.json"
