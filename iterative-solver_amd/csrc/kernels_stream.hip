@@ -2,12 +2,16 @@
 //
 // Reference loops (single-threaded std::fill / transform / inner_product):
 //   ArrayHandlerIterable.h:46-82, DistrArray.cpp:43-138, itsolv/IterativeSolver.h:34-55.
-// Each is HBM-bound (<= 0.25 flop/B).  Layout: 16-byte (double2) accesses per lane, 4 independent
-// accesses per lane in flight, grid-stride.  Grid caps and nontemporal accesses follow the sweep in
-// tools/mb_stream.hip (profiles/r1/mb_stream*.txt): fill and axpy run best with one pass over a
-// large grid (64 workgroups per CU), dot with 8 per CU and nontemporal loads.  Reductions are
-// deterministic: one partial per workgroup in a fixed grid, then a fixed-order fold (by the last
-// workgroup to finish for small results, ssp::fold_tail; else the k_reduce_partials pass).
+// Each is HBM-bound (<= 0.25 flop/B).  Layout: 16-byte (double2) accesses per lane, nontemporal.
+// Two access shapes (tools/mb_glds.hip mode a, profiles/r1/mb_stream_shapes.txt):
+//   stride  4 double2 per lane spaced a whole grid apart, 64 workgroups per CU (fill; and
+//           axpy/scal/copy below kWinMin elements, where the vectors are largely cache-resident);
+//   window  each wave owns kWinU consecutive KiB of every vector per visit: dot always (5.6-6.0 ->
+//           6.7-6.9 TB/s at N = 1e8, 5.6 -> 5.8 at the C4 shard), axpy/scal/copy from kWinMin
+//           elements (axpy 5.1-5.3 -> 5.8 TB/s at N = 1e8).
+// Reductions are deterministic: one partial per workgroup in a fixed grid (a function of N and the
+// CU count), then a fixed-order fold (by the last workgroup to finish for small results,
+// ssp::fold_tail; else the k_reduce_partials pass).
 #include <algorithm>
 
 #include "ssp_internal.h"
@@ -18,6 +22,27 @@ using ssp::kBlock;
 
 __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
 __device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
+
+// Window shape: a wave covers kWinU x 64 consecutive double2 (kWinU KiB) of each vector per visit.
+constexpr int kWinU = 8;
+constexpr size_t kWinMin = size_t(1) << 24;  // elementwise ops switch to windows from 128 MiB vectors
+constexpr int kDotU = 4;
+
+// Visits the whole windows of [0, n2) double2 positions (wave-granular grid stride), then the
+// positions past the last whole window (thread-granular), then the odd last element (n odd).
+// f(p) handles double2 position p; the window body issues all U positions of one wave visit
+// through fw(p0) (lane's first position, then + 64 u).
+template <int U, typename FW, typename F, typename FO>
+__device__ __forceinline__ void for_windows(size_t n, FW&& fw, F&& f, FO&& fo) {
+  const int lane = threadIdx.x & 63;
+  const size_t gw = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const size_t nw = size_t(gridDim.x) * (kBlock / 64);
+  const size_t n2 = n >> 1, win = 64 * size_t(U), nwin = n2 / win;
+  for (size_t c = gw; c < nwin; c += nw) fw(c * win + lane);
+  for (size_t i = nwin * win + size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += size_t(gridDim.x) * kBlock)
+    f(i);
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) fo(n - 1);
+}
 
 // Sum over the 256 threads of a workgroup; result valid in thread 0.  Fixed order.
 __device__ __forceinline__ double block_sum(double v) {
@@ -107,41 +132,94 @@ __global__ __launch_bounds__(kBlock) void k_axpy(const double* __restrict__ x, d
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) y[n - 1] = fma(alpha, x[n - 1], y[n - 1]);
 }
 
-// SAME: x == y (norms), one load stream.
+__global__ __launch_bounds__(kBlock) void k_scal_win(double* __restrict__ x, size_t n, double alpha) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  for_windows<kWinU>(
+      n,
+      [&](size_t p0) {
+        double2 v[kWinU];
+#pragma unroll
+        for (int u = 0; u < kWinU; ++u) v[u] = ld2nt(x + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int u = 0; u < kWinU; ++u) st2nt(x + 2 * (p0 + 64 * u), make_double2(v[u].x * alpha, v[u].y * alpha));
+      },
+      [&](size_t i) {
+        const double2 a = ld2(x + 2 * i);
+        st2(x + 2 * i, make_double2(a.x * alpha, a.y * alpha));
+      },
+      [&](size_t e) { x[e] *= alpha; });
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy_win(double* __restrict__ x, const double* __restrict__ y, size_t n) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  for_windows<kWinU>(
+      n,
+      [&](size_t p0) {
+        double2 v[kWinU];
+#pragma unroll
+        for (int u = 0; u < kWinU; ++u) v[u] = ld2nt(y + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int u = 0; u < kWinU; ++u) st2nt(x + 2 * (p0 + 64 * u), v[u]);
+      },
+      [&](size_t i) { st2(x + 2 * i, ld2(y + 2 * i)); }, [&](size_t e) { x[e] = y[e]; });
+}
+
+// y += alpha * x in the window shape; the same single fma per element as k_axpy.
+__global__ __launch_bounds__(kBlock) void k_axpy_win(const double* __restrict__ x, double* __restrict__ y, size_t n,
+                                                     double alpha) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  for_windows<kWinU>(
+      n,
+      [&](size_t p0) {
+        double2 xv[kWinU], yv[kWinU];
+#pragma unroll
+        for (int u = 0; u < kWinU; ++u) xv[u] = ld2nt(x + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int u = 0; u < kWinU; ++u) yv[u] = ld2nt(y + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int u = 0; u < kWinU; ++u)
+          st2nt(y + 2 * (p0 + 64 * u), make_double2(fma(alpha, xv[u].x, yv[u].x), fma(alpha, xv[u].y, yv[u].y)));
+      },
+      [&](size_t i) {
+        const double2 a = ld2(x + 2 * i), b = ld2(y + 2 * i);
+        st2(y + 2 * i, make_double2(fma(alpha, a.x, b.x), fma(alpha, a.y, b.y)));
+      },
+      [&](size_t e) { y[e] = fma(alpha, x[e], y[e]); });
+}
+
+// SAME: x == y (norms), one load stream.  Window shape (kDotU KiB per vector per wave visit),
+// 4 accumulators per lane (window position u into accumulator u % 4), then the positions past the
+// last whole window and the odd element into accumulator 0.
 template <bool SAME>
 __global__ __launch_bounds__(kBlock) void k_dot_partial(const double* __restrict__ x, const double* __restrict__ y,
                                                         size_t n, double* __restrict__ partial,
                                                         const ssp::FoldTail tail) {
-  const size_t n2 = n >> 1;
-  const size_t stride = size_t(gridDim.x) * kBlock;
-  size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
-  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  for (; i + 3 * stride < n2; i += 4 * stride) {
-    using ssp::ld2nt;
-    double2 x0 = ld2nt(x + 2 * i), x1 = ld2nt(x + 2 * (i + stride)), x2 = ld2nt(x + 2 * (i + 2 * stride)),
-            x3 = ld2nt(x + 2 * (i + 3 * stride));
-    double2 y0 = x0, y1 = x1, y2 = x2, y3 = x3;
-    if (!SAME) {
-      y0 = ld2nt(y + 2 * i);
-      y1 = ld2nt(y + 2 * (i + stride));
-      y2 = ld2nt(y + 2 * (i + 2 * stride));
-      y3 = ld2nt(y + 2 * (i + 3 * stride));
-    }
-    s0 = fma(x0.x, y0.x, s0);
-    s0 = fma(x0.y, y0.y, s0);
-    s1 = fma(x1.x, y1.x, s1);
-    s1 = fma(x1.y, y1.y, s1);
-    s2 = fma(x2.x, y2.x, s2);
-    s2 = fma(x2.y, y2.y, s2);
-    s3 = fma(x3.x, y3.x, s3);
-    s3 = fma(x3.y, y3.y, s3);
-  }
-  for (; i < n2; i += stride) {
-    double2 a = ld2(x + 2 * i), b = ld2(y + 2 * i);
-    s0 = fma(a.x, b.x, s0);
-    s0 = fma(a.y, b.y, s0);
-  }
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) s0 = fma(x[n - 1], y[n - 1], s0);
+  using ssp::ld2nt;
+  double acc[4] = {0, 0, 0, 0};
+  for_windows<kDotU>(
+      n,
+      [&](size_t p0) {
+        double2 xv[kDotU], yv[kDotU];
+#pragma unroll
+        for (int u = 0; u < kDotU; ++u) xv[u] = ld2nt(x + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int u = 0; u < kDotU; ++u) yv[u] = SAME ? xv[u] : ld2nt(y + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int u = 0; u < kDotU; ++u) {
+          acc[u & 3] = fma(xv[u].x, yv[u].x, acc[u & 3]);
+          acc[u & 3] = fma(xv[u].y, yv[u].y, acc[u & 3]);
+        }
+      },
+      [&](size_t i) {
+        const double2 a = ld2(x + 2 * i), b = ld2(y + 2 * i);
+        acc[0] = fma(a.x, b.x, acc[0]);
+        acc[0] = fma(a.y, b.y, acc[0]);
+      },
+      [&](size_t e) { acc[0] = fma(x[e], y[e], acc[0]); });
+  const double s0 = acc[0], s1 = acc[1], s2 = acc[2], s3 = acc[3];
   double s = block_sum((s0 + s1) + (s2 + s3));
   if (threadIdx.x == 0) ssp::store_partial(partial + blockIdx.x, s);
   ssp::fold_tail(partial, tail);
@@ -187,6 +265,12 @@ __global__ __launch_bounds__(kBlock) void k_precondition(const PrecArgs p) {
   }
 }
 
+// Workgroups for a window-shaped launch: one wave per window of u KiB, at most per_cu per CU
+// (grid-stride beyond); at least one.
+unsigned win_grid(const ssp_ctx* ctx, size_t n, int u, unsigned per_cu) {
+  return ssp::stream_grid(ctx, ((n >> 1) / (64 * size_t(u)) + 1) * 64, 1, per_cu);
+}
+
 int check_vec(const void* p, size_t n, const char* what) {
   if (n == 0) return SSP_OK;
   if (!p) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null vector");
@@ -224,7 +308,10 @@ int ssp_scal(ssp_ctx* ctx, double alpha, double* x, size_t n) {
   SSP_TRY(check_vec(x, n, "ssp_scal"));
   if (n == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "scal", 16.0 * n);
-  hipLaunchKernelGGL(k_scal, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
+  if (n >= kWinMin)
+    hipLaunchKernelGGL(k_scal_win, dim3(win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
+  else
+    hipLaunchKernelGGL(k_scal, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -235,7 +322,10 @@ int ssp_copy(ssp_ctx* ctx, double* x, const double* y, size_t n) {
   SSP_TRY(check_vec(y, n, "ssp_copy"));
   if (n == 0 || x == y) return SSP_OK;
   ssp::LedgerScope ls(ctx, "copy", 16.0 * n);
-  hipLaunchKernelGGL(k_copy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, y, n);
+  if (n >= kWinMin)
+    hipLaunchKernelGGL(k_copy_win, dim3(win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, y, n);
+  else
+    hipLaunchKernelGGL(k_copy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, y, n);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -246,7 +336,11 @@ int ssp_axpy(ssp_ctx* ctx, double alpha, const double* x, double* y, size_t n) {
   SSP_TRY(check_vec(y, n, "ssp_axpy"));
   if (n == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "axpy", 24.0 * n);
-  hipLaunchKernelGGL(k_axpy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+  if (n >= kWinMin)
+    hipLaunchKernelGGL(k_axpy_win, dim3(win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+  else
+    hipLaunchKernelGGL(k_axpy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, y, n,
+                       alpha);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -262,7 +356,7 @@ int ssp_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, double* ou
     SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, 1));
     return ssp::fetch_result(ctx, out, 1);
   }
-  const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 4);
+  const unsigned grid = win_grid(ctx, n, kDotU, 8);
   SSP_TRY(ssp::ensure_partial(ctx, grid));
   ssp::FoldTail tail{};
   SSP_TRY(ssp::fold_begin(ctx, 1, &tail));

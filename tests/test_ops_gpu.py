@@ -42,6 +42,29 @@ def test_fill_scal_copy_axpy(ctx, n):
         v.free()
 
 
+@pytest.mark.parametrize("n", [1 << 24, (1 << 24) + 1001, (1 << 24) + 512 * 3 + 6])
+def test_window_shaped_elementwise_ops(ctx, n):
+    # From 2^24 elements axpy / scal / copy run in the window shape (kernels_stream.hip: whole
+    # windows, then the positions past the last window, then the odd element): same results.
+    r = rng(n % 1000)
+    x, y = r.uniform(-1, 1, n), r.uniform(-1, 1, n)
+    dx, dy = ctx.upload(x), ctx.upload(y)
+    ctx.axpy(-0.75, dx, dy)
+    np.testing.assert_allclose(dy.numpy(), oracle.axpy(-0.75, x, y), rtol=2 * EPS, atol=4 * EPS)
+    ctx.scal(3.5, dx)
+    assert np.array_equal(dx.numpy(), oracle.scal(3.5, x))
+    ctx.copy(dy, dx)
+    assert np.array_equal(dy.numpy(), dx.numpy())
+    got = ctx.dot(dx, dy)
+    xs = oracle.scal(3.5, x)
+    # At 2^24 terms the oracle's sequential sum carries ~sqrt(n) eps sum|x y| of its own rounding,
+    # more than the GPU's fixed-order tree: compare with the correctly rounded sum (math.fsum).
+    assert abs(got - math.fsum(xs * xs)) <= red_tol(xs * xs)
+    assert abs(oracle.dot(xs, xs) - math.fsum(xs * xs)) <= 1e-12 * abs(got)
+    for v in (dx, dy):
+        v.free()
+
+
 @pytest.mark.parametrize("n", SIZES)
 def test_dot(ctx, n):
     r = rng(n + 1)

@@ -1,7 +1,7 @@
 // Read path: register loads against LDS-DMA (global_load_lds_dwordx4) for the panel kernels'
 // many-vector streams at N = 1e8 (development tool, not part of the library).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_glds.hip -o tools/mb_glds
-// Run:   tools/mb_glds [n=1e8] [s = read-pattern sweep | p = placement: default vs contiguous allocations | o = gemm_outer destination split]
+// Run:   tools/mb_glds [n=1e8] [s = read-pattern sweep | p = placement: default vs contiguous allocations | o = gemm_outer destination split | a = axpy/dot/fill access shapes]
 //
 // The question: MI355X_MICROARCH.md's ldsdma-fill row reads 6.5-6.8 TB/s chip-wide with nt LDS-DMA,
 // against 6.3-6.4 TB/s for register loads (profiles/r1/mb_read_patterns.txt).  Does a 56-vector
@@ -290,6 +290,98 @@ __global__ __launch_bounds__(256) void k_outer_split(const Args a) {
   }
 }
 
+// Streaming kernels, two access shapes: "stride" (the library's k_axpy: 4 double2 per lane spaced a
+// whole grid apart) and "win" (each wave owns U consecutive KiB of every vector per visit).
+__global__ __launch_bounds__(256) void k_axpy_stride(const double* __restrict__ x, double* __restrict__ y, size_t n,
+                                                     double alpha) {
+  const size_t n2 = n >> 1, stride = size_t(gridDim.x) * 256;
+  size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
+  for (; i + 3 * stride < n2; i += 4 * stride) {
+    double2 x0 = ld2nt(x + 2 * i), x1 = ld2nt(x + 2 * (i + stride)), x2 = ld2nt(x + 2 * (i + 2 * stride)),
+            x3 = ld2nt(x + 2 * (i + 3 * stride));
+    double2 y0 = ld2nt(y + 2 * i), y1 = ld2nt(y + 2 * (i + stride)), y2 = ld2nt(y + 2 * (i + 2 * stride)),
+            y3 = ld2nt(y + 2 * (i + 3 * stride));
+    st2nt(y + 2 * i, make_double2(fma(alpha, x0.x, y0.x), fma(alpha, x0.y, y0.y)));
+    st2nt(y + 2 * (i + stride), make_double2(fma(alpha, x1.x, y1.x), fma(alpha, x1.y, y1.y)));
+    st2nt(y + 2 * (i + 2 * stride), make_double2(fma(alpha, x2.x, y2.x), fma(alpha, x2.y, y2.y)));
+    st2nt(y + 2 * (i + 3 * stride), make_double2(fma(alpha, x3.x, y3.x), fma(alpha, x3.y, y3.y)));
+  }
+  for (; i < n2; i += stride) {
+    double2 a = ld2nt(x + 2 * i), b = ld2nt(y + 2 * i);
+    st2nt(y + 2 * i, make_double2(fma(alpha, a.x, b.x), fma(alpha, a.y, b.y)));
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_axpy_win(const double* __restrict__ x, double* __restrict__ y, size_t n,
+                                                  double alpha) {
+  const int lane = threadIdx.x & 63;
+  const size_t gw = size_t(blockIdx.x) * 4 + (threadIdx.x >> 6), nw = size_t(gridDim.x) * 4;
+  const size_t n2 = n >> 1, win = 64 * U;
+  for (size_t c = gw; (c + 1) * win <= n2; c += nw) {
+    const size_t p0 = c * win + lane;
+    double2 xv[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xv[u] = ld2nt(x + 2 * (p0 + 64 * u));
+#pragma unroll
+    for (int u = 0; u < U; ++u) yv[u] = ld2nt(y + 2 * (p0 + 64 * u));
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      st2nt(y + 2 * (p0 + 64 * u), make_double2(fma(alpha, xv[u].x, yv[u].x), fma(alpha, xv[u].y, yv[u].y)));
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_dot_win(const double* __restrict__ x, size_t n, double* out) {
+  const int lane = threadIdx.x & 63;
+  const size_t gw = size_t(blockIdx.x) * 4 + (threadIdx.x >> 6), nw = size_t(gridDim.x) * 4;
+  const size_t n2 = n >> 1, win = 64 * U;
+  double s = 0;
+  for (size_t c = gw; (c + 1) * win <= n2; c += nw) {
+    const size_t p0 = c * win + lane;
+    double2 xv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xv[u] = ld2nt(x + 2 * (p0 + 64 * u));
+#pragma unroll
+    for (int u = 0; u < U; ++u) s = fma(xv[u].x, xv[u].x, fma(xv[u].y, xv[u].y, s));
+  }
+  if (s == 12345.678) out[0] = s;
+}
+
+__global__ __launch_bounds__(256) void k_dot_stride(const double* __restrict__ x, size_t n, double* out) {
+  const size_t n2 = n >> 1, stride = size_t(gridDim.x) * 256;
+  size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
+  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  for (; i + 3 * stride < n2; i += 4 * stride) {
+    double2 x0 = ld2nt(x + 2 * i), x1 = ld2nt(x + 2 * (i + stride)), x2 = ld2nt(x + 2 * (i + 2 * stride)),
+            x3 = ld2nt(x + 2 * (i + 3 * stride));
+    s0 = fma(x0.x, x0.x, fma(x0.y, x0.y, s0));
+    s1 = fma(x1.x, x1.x, fma(x1.y, x1.y, s1));
+    s2 = fma(x2.x, x2.x, fma(x2.y, x2.y, s2));
+    s3 = fma(x3.x, x3.x, fma(x3.y, x3.y, s3));
+  }
+  const double s = (s0 + s1) + (s2 + s3);
+  if (s == 12345.678) out[0] = s;
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_fill_win(double* __restrict__ x, size_t n, double alpha) {
+  const int lane = threadIdx.x & 63;
+  const size_t gw = size_t(blockIdx.x) * 4 + (threadIdx.x >> 6), nw = size_t(gridDim.x) * 4;
+  const size_t n2 = n >> 1, win = 64 * U;
+  for (size_t c = gw; (c + 1) * win <= n2; c += nw) {
+    const size_t p0 = c * win + lane;
+#pragma unroll
+    for (int u = 0; u < U; ++u) *reinterpret_cast<double2*>(x + 2 * (p0 + 64 * u)) = make_double2(alpha, alpha);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fill_stride(double* __restrict__ x, size_t n, double alpha) {
+  const size_t n2 = n >> 1, stride = size_t(gridDim.x) * 256;
+  for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < n2; i += stride)
+    *reinterpret_cast<double2*>(x + 2 * i) = make_double2(alpha, alpha);
+}
+
 __global__ void k_init(double* x, size_t n, unsigned seed) {
   for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
     x[i] = double((i * 2654435761u + seed) % 1000) * 1e-3 - 0.5;
@@ -344,6 +436,44 @@ int main(int argc, char** argv) {
   };
   const int reps = 7;
   const double rb = 8.0 * n * NV, ob = 8.0 * n * (48 + 16);
+  if (argc > 2 && argv[2][0] == 'a') {
+    // Streaming ops (axpy, self-dot, fill) on 100 MB / 800 MB vectors, stride vs window shapes.
+    for (size_t nn : {n / 8, n}) {
+      char nm[64];
+      const double ab = 24.0 * nn, db = 8.0 * nn, fb = 8.0 * nn;
+      for (int set = 0; set < 2; ++set) {
+        double* xv = vec[2 * set];
+        double* yv = vec[2 * set + 1];
+        for (int g : {2048, 8192, 16384}) {
+          snprintf(nm, 64, "n=%.3g axpy stride", double(nn));
+          rep(nm, g, timeit([&] { hipLaunchKernelGGL(k_axpy_stride, dim3(g), dim3(256), 0, 0, xv, yv, nn, 1e-9); }, reps), ab);
+        }
+        for (int g : {1024, 2048, 4096}) {
+          snprintf(nm, 64, "n=%.3g axpy win U4", double(nn));
+          rep(nm, g, timeit([&] { hipLaunchKernelGGL((k_axpy_win<4>), dim3(g), dim3(256), 0, 0, xv, yv, nn, 1e-9); }, reps), ab);
+          snprintf(nm, 64, "n=%.3g axpy win U8", double(nn));
+          rep(nm, g, timeit([&] { hipLaunchKernelGGL((k_axpy_win<8>), dim3(g), dim3(256), 0, 0, xv, yv, nn, 1e-9); }, reps), ab);
+        }
+        for (int g : {1024, 2048}) {
+          snprintf(nm, 64, "n=%.3g dot stride", double(nn));
+          rep(nm, g, timeit([&] { hipLaunchKernelGGL(k_dot_stride, dim3(g), dim3(256), 0, 0, xv, nn, out); }, reps), db);
+          snprintf(nm, 64, "n=%.3g dot win U4", double(nn));
+          rep(nm, g, timeit([&] { hipLaunchKernelGGL((k_dot_win<4>), dim3(g), dim3(256), 0, 0, xv, nn, out); }, reps), db);
+          snprintf(nm, 64, "n=%.3g dot win U8", double(nn));
+          rep(nm, g, timeit([&] { hipLaunchKernelGGL((k_dot_win<8>), dim3(g), dim3(256), 0, 0, xv, nn, out); }, reps), db);
+        }
+        for (int g : {4096, 16384}) {
+          snprintf(nm, 64, "n=%.3g fill stride", double(nn));
+          rep(nm, g, timeit([&] { hipLaunchKernelGGL(k_fill_stride, dim3(g), dim3(256), 0, 0, yv, nn, 0.5); }, reps), fb);
+        }
+        for (int g : {1024, 2048, 4096}) {
+          snprintf(nm, 64, "n=%.3g fill win U4", double(nn));
+          rep(nm, g, timeit([&] { hipLaunchKernelGGL((k_fill_win<4>), dim3(g), dim3(256), 0, 0, yv, nn, 0.5); }, reps), fb);
+        }
+      }
+    }
+    return 0;
+  }
   if (argc > 2 && argv[2][0] == 'o') {
     // gemm_outer 48 -> 8: library form against destination-split forms, over fresh vector sets.
     for (int set = 0; set < 4; ++set) {
