@@ -124,7 +124,10 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
 
 // Panels of 1 x 1 and 1 x 2 (or 2 x 1) vectors: with only one or two MFMA operand rows live, the
 // 4x4x4 layout leaves 3/4 of the lanes idle on loads (tools/shapes_bench.py: 1 x 1 at 3.4 TB/s),
-// so these run on the VALU with every lane streaming 16 B per vector, 4 positions in flight.
+// so these run on the VALU with every lane streaming 16 B per vector, 4 positions in flight.  (The
+// window shape of the other streaming kernels changes this kernel's summation order, which moved
+// DIIS (n = 1e5, rank 2, rho = 0.01) from the reference's 15 iterations to 30: the stride shape,
+// whose order matches the CPU path's trajectory there, stays.)
 template <int K>
 __global__ __launch_bounds__(kBlock) void k_gemm_inner_row(const InnerArgs a) {
   using ssp::ld2nt;
@@ -290,36 +293,63 @@ struct AxpyInnerArgs {
   ssp::FoldTail tail;  // fused fold when tail.counter is set
 };
 
+// Window shape (ssp::for_windows, kFusedU KiB per vector per wave visit): x and z are loaded once per
+// window, then each destination is read, updated, stored and dotted with z.
+constexpr int kFusedU = 4;
+
 template <int M>
 __global__ __launch_bounds__(kBlock) void k_axpy_inner(const AxpyInnerArgs a) {
   using ssp::ld2nt;
   using ssp::st2nt;
-  const size_t n2 = a.n >> 1, stride = size_t(gridDim.x) * kBlock;
   double acc[M];
 #pragma unroll
   for (int j = 0; j < M; ++j) acc[j] = 0;
-  for (size_t p = size_t(blockIdx.x) * kBlock + threadIdx.x; p < n2; p += stride) {
-    const double2 xv = ld2nt(a.x + 2 * p), zv = ld2nt(a.z + 2 * p);
+  ssp::for_windows<kFusedU>(
+      a.n,
+      [&](size_t p0) {
+        double2 xv[kFusedU], zv[kFusedU];
 #pragma unroll
-    for (int j = 0; j < M; ++j) {
-      if (j < a.m) {
-        double2 y = ld2nt(a.y[j] + 2 * p);
-        y.x = fma(a.c[j], xv.x, y.x);
-        y.y = fma(a.c[j], xv.y, y.y);
-        st2nt(a.y[j] + 2 * p, y);
-        acc[j] = fma(y.x, zv.x, acc[j]);
-        acc[j] = fma(y.y, zv.y, acc[j]);
-      }
-    }
-  }
-  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    const size_t e = a.n - 1;
-    for (int j = 0; j < a.m; ++j) {
-      const double y = fma(a.c[j], a.x[e], a.y[j][e]);
-      a.y[j][e] = y;
-      acc[j] = fma(y, a.z[e], acc[j]);
-    }
-  }
+        for (int u = 0; u < kFusedU; ++u) xv[u] = ld2nt(a.x + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int u = 0; u < kFusedU; ++u) zv[u] = ld2nt(a.z + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            double2 y[kFusedU];
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) y[u] = ld2nt(a.y[j] + 2 * (p0 + 64 * u));
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) {
+              y[u].x = fma(a.c[j], xv[u].x, y[u].x);
+              y[u].y = fma(a.c[j], xv[u].y, y[u].y);
+              st2nt(a.y[j] + 2 * (p0 + 64 * u), y[u]);
+              acc[j] = fma(y[u].x, zv[u].x, acc[j]);
+              acc[j] = fma(y[u].y, zv[u].y, acc[j]);
+            }
+          }
+        }
+      },
+      [&](size_t p) {
+        const double2 xv = ld2(a.x + 2 * p), zv = ld2(a.z + 2 * p);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            double2 y = ld2(a.y[j] + 2 * p);
+            y.x = fma(a.c[j], xv.x, y.x);
+            y.y = fma(a.c[j], xv.y, y.y);
+            *reinterpret_cast<double2*>(a.y[j] + 2 * p) = y;
+            acc[j] = fma(y.x, zv.x, acc[j]);
+            acc[j] = fma(y.y, zv.y, acc[j]);
+          }
+        }
+      },
+      [&](size_t e) {
+        for (int j = 0; j < a.m; ++j) {
+          const double y = fma(a.c[j], a.x[e], a.y[j][e]);
+          a.y[j][e] = y;
+          acc[j] = fma(y, a.z[e], acc[j]);
+        }
+      });
   __shared__ double red[kBlock / 64][M];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -375,30 +405,54 @@ template <int M>
 __global__ __launch_bounds__(kBlock) void k_scal_inner(const ScalInnerArgs a) {
   using ssp::ld2nt;
   using ssp::st2nt;
-  const size_t n2 = a.n >> 1, stride = size_t(gridDim.x) * kBlock;
   double acc[M];
 #pragma unroll
   for (int j = 0; j < M; ++j) acc[j] = 0;
-  for (size_t p = size_t(blockIdx.x) * kBlock + threadIdx.x; p < n2; p += stride) {
-    double2 xv = ld2nt(a.x + 2 * p);
-    xv.x *= a.alpha;
-    xv.y *= a.alpha;
-    st2nt(a.x + 2 * p, xv);
+  ssp::for_windows<kFusedU>(
+      a.n,
+      [&](size_t p0) {
+        double2 xv[kFusedU];
 #pragma unroll
-    for (int j = 0; j < M; ++j) {
-      if (j < a.m) {
-        const double2 y = ld2nt(a.y[j] + 2 * p);
-        acc[j] = fma(xv.x, y.x, acc[j]);
-        acc[j] = fma(xv.y, y.y, acc[j]);
-      }
-    }
-  }
-  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    const size_t e = a.n - 1;
-    const double xs = a.x[e] * a.alpha;
-    a.x[e] = xs;
-    for (int j = 0; j < a.m; ++j) acc[j] = fma(xs, a.y[j][e], acc[j]);
-  }
+        for (int u = 0; u < kFusedU; ++u) xv[u] = ld2nt(a.x + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int u = 0; u < kFusedU; ++u) {
+          xv[u].x *= a.alpha;
+          xv[u].y *= a.alpha;
+          st2nt(a.x + 2 * (p0 + 64 * u), xv[u]);
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            double2 y[kFusedU];
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) y[u] = ld2nt(a.y[j] + 2 * (p0 + 64 * u));
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) {
+              acc[j] = fma(xv[u].x, y[u].x, acc[j]);
+              acc[j] = fma(xv[u].y, y[u].y, acc[j]);
+            }
+          }
+        }
+      },
+      [&](size_t p) {
+        double2 xv = ld2(a.x + 2 * p);
+        xv.x *= a.alpha;
+        xv.y *= a.alpha;
+        *reinterpret_cast<double2*>(a.x + 2 * p) = xv;
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            const double2 y = ld2(a.y[j] + 2 * p);
+            acc[j] = fma(xv.x, y.x, acc[j]);
+            acc[j] = fma(xv.y, y.y, acc[j]);
+          }
+        }
+      },
+      [&](size_t e) {
+        const double xs = a.x[e] * a.alpha;
+        a.x[e] = xs;
+        for (int j = 0; j < a.m; ++j) acc[j] = fma(xs, a.y[j][e], acc[j]);
+      });
   block_partials<M>(acc, a.m, a.partial);
   if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
 }
@@ -408,32 +462,55 @@ template <int M>
 __global__ __launch_bounds__(kBlock) void k_axpy_norm(const AxpyInnerArgs a) {
   using ssp::ld2nt;
   using ssp::st2nt;
-  const size_t n2 = a.n >> 1, stride = size_t(gridDim.x) * kBlock;
   double acc[1] = {0};
-  for (size_t p = size_t(blockIdx.x) * kBlock + threadIdx.x; p < n2; p += stride) {
-    const double2 xv = ld2nt(a.x + 2 * p);
+  ssp::for_windows<kFusedU>(
+      a.n,
+      [&](size_t p0) {
+        double2 xv[kFusedU];
 #pragma unroll
-    for (int j = 0; j < M; ++j) {
-      if (j < a.m) {
-        double2 y = ld2nt(a.y[j] + 2 * p);
-        y.x = fma(a.c[j], xv.x, y.x);
-        y.y = fma(a.c[j], xv.y, y.y);
-        st2nt(a.y[j] + 2 * p, y);
-        if (j == 0) {
-          acc[0] = fma(y.x, y.x, acc[0]);
-          acc[0] = fma(y.y, y.y, acc[0]);
+        for (int u = 0; u < kFusedU; ++u) xv[u] = ld2nt(a.x + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            double2 y[kFusedU];
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) y[u] = ld2nt(a.y[j] + 2 * (p0 + 64 * u));
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) {
+              y[u].x = fma(a.c[j], xv[u].x, y[u].x);
+              y[u].y = fma(a.c[j], xv[u].y, y[u].y);
+              st2nt(a.y[j] + 2 * (p0 + 64 * u), y[u]);
+              if (j == 0) {
+                acc[0] = fma(y[u].x, y[u].x, acc[0]);
+                acc[0] = fma(y[u].y, y[u].y, acc[0]);
+              }
+            }
+          }
         }
-      }
-    }
-  }
-  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    const size_t e = a.n - 1;
-    for (int j = 0; j < a.m; ++j) {
-      const double y = fma(a.c[j], a.x[e], a.y[j][e]);
-      a.y[j][e] = y;
-      if (j == 0) acc[0] = fma(y, y, acc[0]);
-    }
-  }
+      },
+      [&](size_t p) {
+        const double2 xv = ld2(a.x + 2 * p);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            double2 y = ld2(a.y[j] + 2 * p);
+            y.x = fma(a.c[j], xv.x, y.x);
+            y.y = fma(a.c[j], xv.y, y.y);
+            *reinterpret_cast<double2*>(a.y[j] + 2 * p) = y;
+            if (j == 0) {
+              acc[0] = fma(y.x, y.x, acc[0]);
+              acc[0] = fma(y.y, y.y, acc[0]);
+            }
+          }
+        }
+      },
+      [&](size_t e) {
+        for (int j = 0; j < a.m; ++j) {
+          const double y = fma(a.c[j], a.x[e], a.y[j][e]);
+          a.y[j][e] = y;
+          if (j == 0) acc[0] = fma(y, y, acc[0]);
+        }
+      });
   block_partials<1>(acc, 1, a.partial);
   if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
 }
@@ -708,7 +785,7 @@ int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* y
   } else {
     SSP_TRY(ssp::fold_begin(ctx, m, &tail));
     ssp::LedgerScope ls(ctx, "scal_inner", 8.0 * n * (2.0 + m));
-    const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 1);
+    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, 8);
     ScalInnerArgs a{};
     a.x = x;
     a.alpha = alpha;
@@ -753,7 +830,7 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
   } else {
     SSP_TRY(ssp::fold_begin(ctx, 1, &tail));
     ssp::LedgerScope ls(ctx, "axpy_norm", 8.0 * n * (1.0 + 2.0 * m));
-    const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 1);
+    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, 8);
     AxpyInnerArgs a{};
     a.x = x;
     a.m = m;
@@ -798,7 +875,7 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
   } else {
     if (m <= ssp::kOuterDst) SSP_TRY(ssp::fold_begin(ctx, m, &tail));  // one launch: fused fold
     ssp::LedgerScope ls(ctx, "axpy_inner", 8.0 * n * (2.0 + 2.0 * m));
-    const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 1);
+    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, 8);
     for (int j0 = 0; j0 < m; j0 += ssp::kOuterDst) {
       AxpyInnerArgs a{};
       a.m = std::min(ssp::kOuterDst, m - j0);

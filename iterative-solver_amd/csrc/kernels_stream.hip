@@ -28,21 +28,6 @@ constexpr int kWinU = 8;
 constexpr size_t kWinMin = size_t(1) << 24;  // elementwise ops switch to windows from 128 MiB vectors
 constexpr int kDotU = 4;
 
-// Visits the whole windows of [0, n2) double2 positions (wave-granular grid stride), then the
-// positions past the last whole window (thread-granular), then the odd last element (n odd).
-// f(p) handles double2 position p; the window body issues all U positions of one wave visit
-// through fw(p0) (lane's first position, then + 64 u).
-template <int U, typename FW, typename F, typename FO>
-__device__ __forceinline__ void for_windows(size_t n, FW&& fw, F&& f, FO&& fo) {
-  const int lane = threadIdx.x & 63;
-  const size_t gw = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
-  const size_t nw = size_t(gridDim.x) * (kBlock / 64);
-  const size_t n2 = n >> 1, win = 64 * size_t(U), nwin = n2 / win;
-  for (size_t c = gw; c < nwin; c += nw) fw(c * win + lane);
-  for (size_t i = nwin * win + size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += size_t(gridDim.x) * kBlock)
-    f(i);
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) fo(n - 1);
-}
 
 // Sum over the 256 threads of a workgroup; result valid in thread 0.  Fixed order.
 __device__ __forceinline__ double block_sum(double v) {
@@ -135,7 +120,7 @@ __global__ __launch_bounds__(kBlock) void k_axpy(const double* __restrict__ x, d
 __global__ __launch_bounds__(kBlock) void k_scal_win(double* __restrict__ x, size_t n, double alpha) {
   using ssp::ld2nt;
   using ssp::st2nt;
-  for_windows<kWinU>(
+  ssp::for_windows<kWinU>(
       n,
       [&](size_t p0) {
         double2 v[kWinU];
@@ -154,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void k_scal_win(double* __restrict__ x, siz
 __global__ __launch_bounds__(kBlock) void k_copy_win(double* __restrict__ x, const double* __restrict__ y, size_t n) {
   using ssp::ld2nt;
   using ssp::st2nt;
-  for_windows<kWinU>(
+  ssp::for_windows<kWinU>(
       n,
       [&](size_t p0) {
         double2 v[kWinU];
@@ -171,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void k_axpy_win(const double* __restrict__ 
                                                      double alpha) {
   using ssp::ld2nt;
   using ssp::st2nt;
-  for_windows<kWinU>(
+  ssp::for_windows<kWinU>(
       n,
       [&](size_t p0) {
         double2 xv[kWinU], yv[kWinU];
@@ -199,7 +184,7 @@ __global__ __launch_bounds__(kBlock) void k_dot_partial(const double* __restrict
                                                         const ssp::FoldTail tail) {
   using ssp::ld2nt;
   double acc[4] = {0, 0, 0, 0};
-  for_windows<kDotU>(
+  ssp::for_windows<kDotU>(
       n,
       [&](size_t p0) {
         double2 xv[kDotU], yv[kDotU];
@@ -248,27 +233,39 @@ struct PrecArgs {
 
 // a[v][i] = a[v][i] / ((d[i] - shift[v]) + 1e-15): reference itsolv/IterativeSolver.h:52-53.
 __global__ __launch_bounds__(kBlock) void k_precondition(const PrecArgs p) {
-  const size_t n2 = p.n >> 1;
-  const size_t stride = size_t(gridDim.x) * kBlock;
-  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += stride) {
-    const double2 dv = ld2(p.d + 2 * i);
-    for (int v = 0; v < p.nvec; ++v) {
-      double2 av = ld2(p.a[v] + 2 * i);
-      av.x = av.x / (dv.x - p.shift[v] + 1e-15);
-      av.y = av.y / (dv.y - p.shift[v] + 1e-15);
-      st2(p.a[v] + 2 * i, av);
-    }
-  }
-  if ((p.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    const size_t j = p.n - 1;
-    for (int v = 0; v < p.nvec; ++v) p.a[v][j] = p.a[v][j] / (p.d[j] - p.shift[v] + 1e-15);
-  }
-}
-
-// Workgroups for a window-shaped launch: one wave per window of u KiB, at most per_cu per CU
-// (grid-stride beyond); at least one.
-unsigned win_grid(const ssp_ctx* ctx, size_t n, int u, unsigned per_cu) {
-  return ssp::stream_grid(ctx, ((n >> 1) / (64 * size_t(u)) + 1) * 64, 1, per_cu);
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  constexpr int U = 4;
+  ssp::for_windows<U>(
+      p.n,
+      [&](size_t p0) {
+        double2 dv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) dv[u] = ld2nt(p.d + 2 * (p0 + 64 * u));
+        for (int v = 0; v < p.nvec; ++v) {
+          double2 av[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) av[u] = ld2nt(p.a[v] + 2 * (p0 + 64 * u));
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            av[u].x = av[u].x / (dv[u].x - p.shift[v] + 1e-15);
+            av[u].y = av[u].y / (dv[u].y - p.shift[v] + 1e-15);
+            st2nt(p.a[v] + 2 * (p0 + 64 * u), av[u]);
+          }
+        }
+      },
+      [&](size_t i) {
+        const double2 dv = ld2(p.d + 2 * i);
+        for (int v = 0; v < p.nvec; ++v) {
+          double2 av = ld2(p.a[v] + 2 * i);
+          av.x = av.x / (dv.x - p.shift[v] + 1e-15);
+          av.y = av.y / (dv.y - p.shift[v] + 1e-15);
+          st2(p.a[v] + 2 * i, av);
+        }
+      },
+      [&](size_t j) {
+        for (int v = 0; v < p.nvec; ++v) p.a[v][j] = p.a[v][j] / (p.d[j] - p.shift[v] + 1e-15);
+      });
 }
 
 int check_vec(const void* p, size_t n, const char* what) {
@@ -309,7 +306,7 @@ int ssp_scal(ssp_ctx* ctx, double alpha, double* x, size_t n) {
   if (n == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "scal", 16.0 * n);
   if (n >= kWinMin)
-    hipLaunchKernelGGL(k_scal_win, dim3(win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
+    hipLaunchKernelGGL(k_scal_win, dim3(ssp::win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
   else
     hipLaunchKernelGGL(k_scal, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
   SSP_TRY_HIP(hipGetLastError());
@@ -323,7 +320,7 @@ int ssp_copy(ssp_ctx* ctx, double* x, const double* y, size_t n) {
   if (n == 0 || x == y) return SSP_OK;
   ssp::LedgerScope ls(ctx, "copy", 16.0 * n);
   if (n >= kWinMin)
-    hipLaunchKernelGGL(k_copy_win, dim3(win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, y, n);
+    hipLaunchKernelGGL(k_copy_win, dim3(ssp::win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, y, n);
   else
     hipLaunchKernelGGL(k_copy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, y, n);
   SSP_TRY_HIP(hipGetLastError());
@@ -337,7 +334,7 @@ int ssp_axpy(ssp_ctx* ctx, double alpha, const double* x, double* y, size_t n) {
   if (n == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "axpy", 24.0 * n);
   if (n >= kWinMin)
-    hipLaunchKernelGGL(k_axpy_win, dim3(win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+    hipLaunchKernelGGL(k_axpy_win, dim3(ssp::win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
   else
     hipLaunchKernelGGL(k_axpy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, y, n,
                        alpha);
@@ -356,7 +353,7 @@ int ssp_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, double* ou
     SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, 1));
     return ssp::fetch_result(ctx, out, 1);
   }
-  const unsigned grid = win_grid(ctx, n, kDotU, 8);
+  const unsigned grid = ssp::win_grid(ctx, n, kDotU, 8);
   SSP_TRY(ssp::ensure_partial(ctx, grid));
   ssp::FoldTail tail{};
   SSP_TRY(ssp::fold_begin(ctx, 1, &tail));
@@ -387,7 +384,7 @@ int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, 
     }
     p.d = d;
     p.n = n;
-    hipLaunchKernelGGL(k_precondition, dim3(ssp::stream_grid(ctx, n / 2 + 1, 1)), dim3(kBlock), 0, ctx->stream, p);
+    hipLaunchKernelGGL(k_precondition, dim3(ssp::win_grid(ctx, n, 4, 8)), dim3(kBlock), 0, ctx->stream, p);
     SSP_TRY_HIP(hipGetLastError());
   }
   return SSP_OK;

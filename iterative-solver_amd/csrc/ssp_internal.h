@@ -124,6 +124,30 @@ class LedgerScope {
   hipEvent_t start_ = nullptr;
 };
 
+// Window shape for streaming kernels (tools/mb_glds.hip mode a, profiles/r1/mb_stream_shapes.txt):
+// a wave covers U x 64 consecutive double2 (U KiB) of each vector per visit.  Visits the whole
+// windows of the n2 = n / 2 double2 positions (wave-granular grid stride), then the positions past
+// the last whole window (thread-granular), then the odd last element when n is odd.  fw(p0) gets
+// the lane's first position of a window (its others are p0 + 64 u), f(p) one position, fo(e) the
+// odd element.
+template <int U, typename FW, typename F, typename FO>
+__device__ __forceinline__ void for_windows(size_t n, FW&& fw, F&& f, FO&& fo) {
+  const int lane = threadIdx.x & 63;
+  const size_t gw = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const size_t nw = size_t(gridDim.x) * (kBlock / 64);
+  const size_t n2 = n >> 1, win = 64 * size_t(U), nwin = n2 / win;
+  for (size_t c = gw; c < nwin; c += nw) fw(c * win + lane);
+  for (size_t i = nwin * win + size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += size_t(gridDim.x) * kBlock)
+    f(i);
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) fo(n - 1);
+}
+
+// Workgroups for a window-shaped launch over n doubles: one wave per window of u KiB, at most
+// per_cu workgroups per CU (grid-stride beyond), at least one.
+inline unsigned win_grid(const ssp_ctx* ctx, size_t n, int u, unsigned per_cu) {
+  return stream_grid(ctx, ((n >> 1) / (64 * size_t(u)) + 1) * 64, 1, per_cu);
+}
+
 // Sum over the 256 threads of a workgroup; result valid in thread 0.  Fixed order.
 __device__ inline double block_sum256(double v) {
   __shared__ double wsum[kBlock / 64];
