@@ -1,7 +1,7 @@
 // Read path: register loads against LDS-DMA (global_load_lds_dwordx4) for the panel kernels'
 // many-vector streams at N = 1e8 (development tool, not part of the library).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_glds.hip -o tools/mb_glds
-// Run:   tools/mb_glds [n=1e8] [s = read-pattern sweep | p = placement: default vs contiguous allocations | o = gemm_outer destination split | a = axpy/dot/fill access shapes]
+// Run:   tools/mb_glds [n=1e8] [s = read-pattern sweep | p = placement: default vs contiguous allocations | o = gemm_outer destination split, ow = wider windows | a = axpy/dot/fill access shapes]
 //
 // The question: MI355X_MICROARCH.md's ldsdma-fill row reads 6.5-6.8 TB/s chip-wide with nt LDS-DMA,
 // against 6.3-6.4 TB/s for register loads (profiles/r1/mb_read_patterns.txt).  Does a 56-vector
@@ -214,6 +214,46 @@ __global__ __launch_bounds__(64) void k_oglds(const Args a) {
 }
 
 // Library-form gemm_outer 48 -> 8 (U = 4 windows of 1 KiB per vector per wave, 4 sources per group).
+__global__ __launch_bounds__(256) void k_outer_reg(const Args a);
+
+// Wider windows: U KiB per vector per wave visit, B sources per load group (U = 8 needs the 512
+// VGPRs of one wave per SIMD).
+template <int U, int B>
+__global__ __launch_bounds__(256) void k_outer_wide(const Args a) {
+  constexpr int K = 48, M = 8;
+  const int lane = threadIdx.x & 63;
+  const size_t gw = size_t(blockIdx.x) * 4 + (threadIdx.x >> 6), nw = size_t(gridDim.x) * 4;
+  const size_t n2 = a.n >> 1, win = 64 * U;
+  for (size_t c = gw; (c + 1) * win <= n2; c += nw) {
+    const size_t p0 = c * win + lane;
+    double2 acc[U][M];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < M; ++j) acc[u][j] = ld2nt(a.y[j] + 2 * (p0 + 64 * u));
+    for (int i = 0; i < K; i += B) {
+      double2 xv[B][U];
+#pragma unroll
+      for (int b = 0; b < B; ++b)
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[b][u] = ld2nt(a.x[i + b] + 2 * (p0 + 64 * u));
+#pragma unroll
+      for (int b = 0; b < B; ++b)
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            acc[u][j].x = fma(a.alpha[(i + b) * M + j], xv[b][u].x, acc[u][j].x);
+            acc[u][j].y = fma(a.alpha[(i + b) * M + j], xv[b][u].y, acc[u][j].y);
+          }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < M; ++j) st2nt(a.y[j] + 2 * (p0 + 64 * u), acc[u][j]);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_outer_reg(const Args a) {
   constexpr int K = 48, M = 8, U = 4;
   const int lane = threadIdx.x & 63;
@@ -490,6 +530,13 @@ int main(int argc, char** argv) {
       printf("-- set %d\n", set);
       for (int g : {1024, 2048}) {
         rep("outer reg U4 (library)", g, timeit([&] { hipLaunchKernelGGL(k_outer_reg, dim3(g), dim3(256), 0, 0, o); }, reps), ob);
+        if (argv[2][1] == 'w') {
+          rep("outer wide U6 B4", g, timeit([&] { hipLaunchKernelGGL((k_outer_wide<6, 4>), dim3(g), dim3(256), 0, 0, o); }, reps), ob);
+          rep("outer wide U8 B2", g, timeit([&] { hipLaunchKernelGGL((k_outer_wide<8, 2>), dim3(g), dim3(256), 0, 0, o); }, reps), ob);
+          rep("outer wide U8 B4", g, timeit([&] { hipLaunchKernelGGL((k_outer_wide<8, 4>), dim3(g), dim3(256), 0, 0, o); }, reps), ob);
+          rep("outer wide U4 B2", g, timeit([&] { hipLaunchKernelGGL((k_outer_wide<4, 2>), dim3(g), dim3(256), 0, 0, o); }, reps), ob);
+          continue;
+        }
         rep("outer split 4 dst/wave", g, timeit([&] { hipLaunchKernelGGL((k_outer_split<4>), dim3(g), dim3(256), 0, 0, o); }, reps), ob);
         rep("outer split 2 dst/wave", g, timeit([&] { hipLaunchKernelGGL((k_outer_split<2>), dim3(g), dim3(256), 0, 0, o); }, reps), ob);
       }
