@@ -28,6 +28,7 @@ namespace {
 
 using Solver = it::IterativeSolverTemplate<Vec, Vec, SparseP>;
 using Davidson = it::LinearEigensystemDavidson<Vec, Vec, SparseP>;
+using RSPT = it::LinearEigensystemRSPT<Vec, Vec, SparseP>;
 using DIIS = it::NonLinearEquationsDIIS<Vec, Vec, SparseP>;
 using LinEq = it::LinearEquationsDavidson<Vec, Vec, SparseP>;
 using BFGS = it::OptimizeBFGS<Vec, Vec, SparseP>;
@@ -160,11 +161,23 @@ void IterativeSolverLinearEigensystemInitialize(size_t nQ, size_t nroot, size_t*
     (void)fname;
     (void)fcomm;
     const std::string alg = algorithm ? algorithm : "";
-    if (!alg.empty() && alg != "Davidson")
-      throw std::runtime_error("IterativeSolverLinearEigensystemInitialize: algorithm " + alg +
-                               " not available on the HBM back end (Davidson only)");
+    if (!alg.empty() && alg != "Davidson" && alg != "RSPT")
+      throw std::runtime_error("IterativeSolverLinearEigensystemInitialize: unknown algorithm " + alg +
+                               " (Davidson, RSPT)");
     Instance in;
     in.dev = make_device();
+    if (alg == "RSPT") {  // reference SolverFactory-implementation.h: create_LinearEigensystem("RSPT")
+      auto solver = std::make_unique<RSPT>(molpro::linalg::hbm::make_handlers());
+      if (options && *options) solver->set_options(it::Options(it::parse_options(options)));
+      solver->set_verbosity(verbosity_of(verbosity));
+      solver->set_convergence_threshold(thresh);
+      solver->set_convergence_threshold_value(thresh_value);
+      in.solver = std::move(solver);
+      in.has_eigenvalues = true;
+      setup(in, nQ, range_begin, range_end);
+      instances.push(std::move(in));
+      return;
+    }
     auto solver = std::make_unique<Davidson>(molpro::linalg::hbm::make_handlers());
     if (options && *options) solver->set_options(it::LinearEigensystemDavidsonOptions(it::parse_options(options)));
     solver->set_n_roots(nroot);
@@ -418,6 +431,9 @@ void IterativeSolverEigenvalues(double* eigenvalues) {
     if (auto* d = dynamic_cast<Davidson*>(top().solver.get())) {
       size_t k = 0;
       for (double e : d->eigenvalues()) eigenvalues[k++] = e;
+    } else if (auto* r = dynamic_cast<RSPT*>(top().solver.get())) {
+      size_t k = 0;
+      for (double e : r->eigenvalues()) eigenvalues[k++] = e;
     }
   });
 }
@@ -427,6 +443,9 @@ void IterativeSolverWorkingSetEigenvalues(double* eigenvalues) {
     if (auto* d = dynamic_cast<Davidson*>(top().solver.get())) {
       size_t k = 0;
       for (double e : d->working_set_eigenvalues()) eigenvalues[k++] = e;
+    } else if (auto* r = dynamic_cast<RSPT*>(top().solver.get())) {
+      size_t k = 0;
+      for (double e : r->working_set_eigenvalues()) eigenvalues[k++] = e;
     }
   });
 }

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <functional>
+#include <iomanip>
 #include <iostream>
 #include <limits>
 #include <map>
@@ -227,6 +228,19 @@ class SubspaceSolverLinEig : public SubspaceSolver {
   std::shared_ptr<Logger> m_logger;
   bool m_hermitian = false;
   double m_augmented_hessian = 0;
+};
+
+// Rayleigh-Schroedinger perturbation theory in the subspace (reference
+// itsolv/subspace/SubspaceSolverRSPT.h:6-25): the variational subspace eigenproblem is solved (for
+// eigenvalues()), then the solution is the unit vector on the first Q parameter.
+class SubspaceSolverRSPT : public SubspaceSolverLinEig {
+ public:
+  using SubspaceSolverLinEig::SubspaceSolverLinEig;
+  void solve(const subspace::SubspaceData& data, size_t nroots_max) override {
+    SubspaceSolverLinEig::solve(data, nroots_max);
+    m_solutions.fill(0);
+    m_solutions(0, 0) = 1;
+  }
 };
 
 class SubspaceSolverDIIS : public SubspaceSolver {
@@ -732,6 +746,76 @@ class LinearEigensystemDavidson : public DavidsonSolver<R, Q, P> {
   }
 
   std::vector<double> m_last_values;
+};
+
+// Lowest eigenvalue by Rayleigh-Schroedinger perturbation theory (reference
+// itsolv/LinearEigensystemRSPT.h:32-198).  The caller's loop (test_RSPT.cpp:105-128) adds x = psi(k)
+// and g = H psi(k); construct_residual appends E(k+1) = <psi(0), H psi(k)> to the perturbation series
+// and forms g = H psi(k) - E(0..) psi(..) from the stored Q parameters (q(j) holds psi(n-j-1)); after
+// the caller's preconditioner end_iteration makes the next correction x = -g (the first one from
+// x = 0).  One root, hermitian, unnormalised solutions.
+template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>
+class LinearEigensystemRSPT : public IterativeSolverTemplate<R, Q, P> {
+  using Base = IterativeSolverTemplate<R, Q, P>;
+
+ public:
+  explicit LinearEigensystemRSPT(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers,
+                                 std::shared_ptr<Logger> logger = std::make_shared<Logger>())
+      : Base(std::move(handlers), std::make_shared<SubspaceSolverRSPT>(logger), logger) {
+    set_hermiticity(true);
+    this->set_n_roots(1);
+    this->m_normalise_solution = false;
+  }
+
+  bool nonlinear() const override { return false; }
+
+  // reference LinearEigensystemRSPT.h:74-81
+  size_t end_iteration(const VecRef<R>& parameters, const VecRef<R>& actions) override {
+    R& x = parameters.front().get();
+    R& g = actions.front().get();
+    if (this->m_xspace->size() == 1) this->m_handlers->rr().fill(0, x);
+    this->m_handlers->rr().axpy(-1, g, x);
+    this->m_end_iteration_needed = false;
+    return this->m_errors.front() < this->m_convergence_threshold ? 0 : 1;
+  }
+  using Base::end_iteration;
+
+  std::vector<double> eigenvalues() const { return this->m_subspace_solver->eigenvalues(); }
+  std::vector<double> working_set_eigenvalues() const override {
+    std::vector<double> e;
+    for (auto i : this->working_set()) e.push_back(this->m_subspace_solver->eigenvalues().at(i));
+    return e;
+  }
+  //! The perturbation series: element k (k >= 1) is the k-th order energy contribution, with
+  //! element 1 = E(0) + E(1) = <psi(0)|H|psi(0)>; element 0 is 0 (LinearEigensystemRSPT.h:175-179).
+  const std::vector<double>& rspt_values() const { return m_rspt_values; }
+
+  void set_hermiticity(bool hermitian) {
+    this->m_xspace->set_hermiticity(hermitian);
+    std::static_pointer_cast<SubspaceSolverRSPT>(this->m_subspace_solver)->set_hermiticity(hermitian);
+  }
+  bool get_hermiticity() const { return true; }
+
+  void report(std::ostream& o = std::cout) const override {
+    o << "Perturbed energies " << std::fixed << std::setprecision(8);
+    for (double e : m_rspt_values) o << e << ", ";
+    o << std::defaultfloat << std::endl;
+  }
+
+ protected:
+  // reference LinearEigensystemRSPT.h:163-190
+  void construct_residual(const std::vector<int>&, const CVecRef<R>& params, const VecRef<R>& actions) override {
+    const auto q = this->m_xspace->cparamsq();
+    const size_t n = q.size();
+    const R& c = params.back().get();
+    R& hc = actions.back().get();
+    if (n == 1) m_rspt_values.assign(1, 0);
+    m_rspt_values.push_back(this->m_handlers->qr().dot(q.at(n - 1).get(), hc));
+    this->m_handlers->rr().axpy(-m_rspt_values[0], c, hc);
+    for (size_t k = 0; k < n; ++k) this->m_handlers->rq().axpy(-m_rspt_values[n - k], q.at(n - k - 1).get(), hc);
+  }
+
+  std::vector<double> m_rspt_values;
 };
 
 // A x = b for several right-hand sides in the same Krylov/P/D subspace machinery

@@ -434,7 +434,13 @@ void* oracle_rc_create(const char* kind, size_t n, size_t nroot, const double* r
   h->n = n;
   const std::string k = kind ? kind : "", alg = algorithm ? algorithm : "", opt = options ? options : "";
   const int s = guarded([&] {
-    if (k == "LinearEigensystem") {
+    if (k == "LinearEigensystem" && alg == "RSPT") {  // LinearEigensystemRSPT.h:32-198
+      auto d = std::make_unique<it::LinearEigensystemRSPT<V, V, SP>>(cpu_handlers());
+      if (!opt.empty()) d->set_options(it::Options(it::parse_options(opt)));
+      d->set_convergence_threshold(thresh);
+      d->set_convergence_threshold_value(thresh_value);
+      h->solver = std::move(d);
+    } else if (k == "LinearEigensystem") {
       auto d = std::make_unique<it::LinearEigensystemDavidson<V, V, SP>>(cpu_handlers());
       if (!opt.empty()) d->set_options(it::LinearEigensystemDavidsonOptions(it::parse_options(opt)));
       d->set_n_roots(nroot);

@@ -12,8 +12,15 @@ Problems and loops follow the reference's tests:
   test_eigen         test_LinearEigensystem.cpp:60-330 (file, n, small, symmetry and
                      non-hermitian matrices; P space through add_p; preconditioner
                      g *= -1 / (1e-12 - shift + h_ii))
+  RSPT               test_RSPT.cpp:31-190: <file>.hamiltonian with H0 = diag(<file>.h0);
+                     Rayleigh-Schroedinger perturbation series (file_eigen) and the
+                     second-order energy as the Hylleraas minimum by BFGS / DIIS (file_Hylleraas)
 """
+import os
+
 import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def quadratic_matrix(n, param):
@@ -226,3 +233,71 @@ def eigen_cases(n, hermitian=True):
         for np_ in range(0, min(n, 100) + 1, max(nroot, n // 5)):
             if hermitian or np_ == 0:
                 yield nroot, np_
+
+
+# ---- RSPT (test_RSPT.cpp) ------------------------------------------------------------------------
+def rspt_problem(name, degeneracy_split=1e-8):
+    """test_RSPT.cpp:31-50: H read row by row, diagonal split by degeneracy_split * i, H0 diagonal."""
+    t = open(os.path.join(GOLDEN, name + ".hamiltonian")).read().split()
+    n = int(t[0])
+    h = np.array(t[1:1 + n * n], dtype=float).reshape(n, n) + np.diag(degeneracy_split * np.arange(n))
+    h0 = np.array(open(os.path.join(GOLDEN, name + ".h0")).read().split()[:n], dtype=float)
+    return h, h0
+
+
+def rspt_update(h0, g):
+    """test_RSPT.cpp:58-66: g /= (1e-12 - e0 + h0), e0 = min h0."""
+    g /= 1e-12 - h0.min() + h0
+
+
+def rspt_initial_guess(h0):
+    x = np.zeros(h0.size)
+    x[int(np.argmin(h0))] = 1.0  # test_RSPT.cpp:68-74
+    return x
+
+
+def loop_rspt(solver, h, h0, niter=9):
+    """test_RSPT.cpp:99-125 (file_eigen): x = psi(k), g = H x; add_vector, update, end_iteration."""
+    x, g = rspt_initial_guess(h0), np.zeros(h0.size)
+    trace = []
+    for _ in range(niter):
+        g[:] = h @ x
+        nwork = solver.add_vector(x, g)
+        rspt_update(h0, g)
+        nend = solver.end_iteration(x, g)
+        trace.append((nwork, nend, x.copy()))
+    return trace
+
+
+def rspt_second_order_energy(h, h0):
+    """Closed form (independent of the solvers): E2 = -sum_{i != 0} H1_{i0}^2 / (h0_i - e0 + 1e-12) with
+    psi(0) = e_0 the minimum of h0 and H1 = H - diag(h0)."""
+    i0 = int(np.argmin(h0))
+    col = h[:, i0].copy()
+    col[i0] = 0.0
+    return -np.sum(col * col / (1e-12 - h0[i0] + h0))
+
+
+def loop_hylleraas(solver, h, h0, optimize, precondition=True, max_iter=20):
+    """test_RSPT.cpp:134-188: minimise the Hylleraas functional
+    e2(x) = 2 x0.(H1 x - e1 x) + x.(H0 x - e0 x) (BFGS: add_value(e2 / 2), DIIS: add_vector) from
+    x = 0 with gradient r = H1 x0 - e1 x0 + H0 x - e0 x; returns the last e2 and the trace."""
+    n = h0.size
+    ham0 = np.diag(h0)
+    ham1 = h - ham0
+    x0 = rspt_initial_guess(h0)
+    e0 = h0 @ x0
+    e1 = x0 @ (ham1 @ x0)
+    x, g = np.zeros(n), np.zeros(n)
+    trace, e2 = [], None
+    for _ in range(1, max_iter):
+        e2 = 2 * (x0 @ (ham1 @ x - e1 * x)) + x @ (ham0 @ x - e0 * x)
+        g[:] = ham1 @ x0 - e1 * x0 + ham0 @ x - e0 * x
+        nwork = solver.add_value(e2 / 2, x, g) if optimize else solver.add_vector(x, g)
+        if precondition:
+            rspt_update(h0, g)
+        nwork = solver.end_iteration(x, g)
+        trace.append((nwork, x.copy()))
+        if nwork < 1:
+            break
+    return e2, trace
