@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "itsolv_hbm/hbm_handlers.h"
+#include "itsolv_hbm/solver_factory.h"
 #include "itsolv_hbm/solvers.h"
 
 using molpro::linalg::hbm::check;
@@ -160,29 +161,16 @@ void IterativeSolverLinearEigensystemInitialize(size_t nQ, size_t nroot, size_t*
   guarded([&] {
     (void)fname;
     (void)fcomm;
-    const std::string alg = algorithm ? algorithm : "";
-    if (!alg.empty() && alg != "Davidson" && alg != "RSPT")
-      throw std::runtime_error("IterativeSolverLinearEigensystemInitialize: unknown algorithm " + alg +
-                               " (Davidson, RSPT)");
     Instance in;
     in.dev = make_device();
-    if (alg == "RSPT") {  // reference SolverFactory-implementation.h: create_LinearEigensystem("RSPT")
-      auto solver = std::make_unique<RSPT>(molpro::linalg::hbm::make_handlers());
-      if (options && *options) solver->set_options(it::Options(it::parse_options(options)));
-      solver->set_verbosity(verbosity_of(verbosity));
-      solver->set_convergence_threshold(thresh);
-      solver->set_convergence_threshold_value(thresh_value);
-      in.solver = std::move(solver);
-      in.has_eigenvalues = true;
-      setup(in, nQ, range_begin, range_end);
-      instances.push(std::move(in));
-      return;
+    // method dispatch and option parsing as the reference's create_LinearEigensystem (SolverFactory.h:114-125)
+    auto solver = it::create_LinearEigensystem(algorithm ? algorithm : "", options ? options : "",
+                                               molpro::linalg::hbm::make_handlers());
+    if (auto* d = dynamic_cast<Davidson*>(solver.get())) {
+      d->set_n_roots(nroot);
+      d->set_hermiticity(hermitian != 0);
     }
-    auto solver = std::make_unique<Davidson>(molpro::linalg::hbm::make_handlers());
-    if (options && *options) solver->set_options(it::LinearEigensystemDavidsonOptions(it::parse_options(options)));
-    solver->set_n_roots(nroot);
     solver->set_verbosity(verbosity_of(verbosity));
-    solver->set_hermiticity(hermitian != 0);
     solver->set_convergence_threshold(thresh);
     solver->set_convergence_threshold_value(thresh_value);
     in.solver = std::move(solver);
@@ -199,21 +187,18 @@ void IterativeSolverLinearEquationsInitialize(size_t n, size_t nroot, size_t* ra
   guarded([&] {
     (void)fname;
     (void)fcomm;
-    const std::string alg = algorithm ? algorithm : "";
-    if (!alg.empty() && alg != "Davidson")
-      throw std::runtime_error("IterativeSolverLinearEquationsInitialize: algorithm " + alg +
-                               " not available on the HBM back end (Davidson only)");
+    auto made = it::create_LinearEquations(algorithm ? algorithm : "", options ? options : "",
+                                           molpro::linalg::hbm::make_handlers());
+    std::unique_ptr<LinEq> solver(static_cast<LinEq*>(made.release()));
     Instance in;
     in.dev = make_device();
     setup(in, n, range_begin, range_end);
-    auto solver = std::make_unique<LinEq>(molpro::linalg::hbm::make_handlers());
     // reference IterativeSolverCMPI.cpp:199-225: rhs as R vectors, then options
     std::vector<Vec> b;
     for (size_t r = 0; r < nroot; ++r) {
       b.emplace_back(in.dev, n);
       check(ssp_upload(in.dev->ctx(), b.back().data(), rhs + r * n + in.offset, in.local), "ssp_upload");
     }
-    if (options && *options) solver->set_options(it::LinearEquationsDavidsonOptions(it::parse_options(options)));
     solver->set_hermiticity(hermitian != 0);
     solver->set_n_roots(nroot);
     solver->add_equations(b);
@@ -232,14 +217,10 @@ void IterativeSolverNonLinearEquationsInitialize(size_t n, size_t* range_begin, 
   guarded([&] {
     (void)fname;
     (void)fcomm;
-    const std::string alg = algorithm ? algorithm : "";
-    if (!alg.empty() && alg != "DIIS")
-      throw std::runtime_error("IterativeSolverNonLinearEquationsInitialize: algorithm " + alg +
-                               " not available on the HBM back end (DIIS only)");
     Instance in;
     in.dev = make_device();
-    auto solver = std::make_unique<DIIS>(molpro::linalg::hbm::make_handlers());
-    if (options && *options) solver->set_options(it::NonLinearEquationsDIISOptions(it::parse_options(options)));
+    auto solver = it::create_NonLinearEquations(algorithm ? algorithm : "", options ? options : "",
+                                                molpro::linalg::hbm::make_handlers());
     solver->set_convergence_threshold(thresh);
     solver->set_verbosity(verbosity_of(verbosity));
     in.solver = std::move(solver);
@@ -255,20 +236,10 @@ void IterativeSolverOptimizeInitialize(size_t n, size_t* range_begin, size_t* ra
     (void)fname;
     (void)fcomm;
     if (!minimize) throw std::runtime_error("IterativeSolverOptimizeInitialize: maximisation is not implemented");
-    const std::string alg = algorithm && *algorithm ? algorithm : "BFGS";
     Instance in;
     in.dev = make_device();
-    std::unique_ptr<Solver> solver;
-    if (alg == "BFGS") {
-      auto b = std::make_unique<BFGS>(molpro::linalg::hbm::make_handlers());
-      if (options && *options) b->set_options(it::OptimizeBFGSOptions(it::parse_options(options)));
-      solver = std::move(b);
-    } else if (alg == "SD") {
-      solver = std::make_unique<SD>(molpro::linalg::hbm::make_handlers());
-      if (options && *options) solver->set_options(it::Options(it::parse_options(options)));
-    } else {
-      throw std::runtime_error("IterativeSolverOptimizeInitialize: unknown algorithm " + alg + " (BFGS, SD)");
-    }
+    auto solver = it::create_Optimize(algorithm ? algorithm : "", options ? options : "",
+                                      molpro::linalg::hbm::make_handlers());
     // reference IterativeSolverCMPI.cpp:245-264
     solver->set_n_roots(1);
     solver->set_convergence_threshold(thresh);

@@ -61,6 +61,23 @@ def case_api():
     tg.test_simple_linear_equations()
     tg.test_optimize("")
     tg.test_optimize("SD")
+    # method dispatch of the C API through the SolverFactory restatement (SolverFactory.h:114-185):
+    # unknown methods raise "Unimplemented method <m>", the named methods construct
+    from test_python_api_gpu import check_factory_dispatch
+
+    check_factory_dispatch()
+    # RSPT (test_RSPT.cpp:191-196) through the product host code: the reference path's steps
+    import rc_problems as rp
+
+    for name in ("he", "hf"):
+        h, h0 = rp.rspt_problem(name)
+        ref = rp.loop_rspt(oracle.RcSolver("LinearEigensystem", h0.size, thresh=1e-8, algorithm="RSPT"), h, h0)
+        s = iterative_solver.LinearEigensystem(h0.size, 1, thresh=1e-8, hermitian=True, algorithm="RSPT")
+        trace = rp.loop_rspt(s, h, h0)
+        assert [t[:-1] for t in trace] == [t[:-1] for t in ref], name
+        for a, b in zip(trace, ref):
+            assert np.max(np.abs(a[-1] - b[-1])) <= 1e-9 * max(1.0, np.max(np.abs(b[-1]))), name
+        s.finalize()
     # C-API loop vs the restated solve() of the CPU reference path: same iterations
     for name, split, nroot in (("he", 0.0, 1), ("hf", 1e-8, 3), ("bh", 1e-8, 3)):
         h = hamiltonian(name, split)

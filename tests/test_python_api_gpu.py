@@ -204,3 +204,35 @@ def test_add_p_with_caller_callback():
     np.testing.assert_allclose(solver.eigenvalues, np.linalg.eigvalsh(m)[:nroot], rtol=0, atol=1e-8)
     assert np.all(solver.errors <= 1e-8)
     solver.finalize()
+
+
+def check_factory_dispatch():
+    rhs = np.ones((1, 4))
+    bad = [
+        lambda: iterative_solver.LinearEigensystem(4, 1, algorithm="Lanczos"),
+        lambda: iterative_solver.LinearEquations(rhs, algorithm="CG"),
+        lambda: iterative_solver.NonLinearEquations(4, algorithm="Newton"),
+        lambda: iterative_solver.Optimize(4, algorithm="LBFGS"),
+    ]
+    for make in bad:
+        try:
+            make()
+        except RuntimeError as e:
+            assert "Unimplemented method" in str(e), str(e)
+        else:
+            raise AssertionError("unknown method accepted")
+    for make in (
+        lambda: iterative_solver.LinearEigensystem(4, 1, algorithm="Davidson"),
+        lambda: iterative_solver.LinearEigensystem(4, 1, algorithm="RSPT", options="max_iter=5"),
+        lambda: iterative_solver.LinearEquations(rhs, algorithm="Davidson"),
+        lambda: iterative_solver.NonLinearEquations(4, algorithm="DIIS"),
+        lambda: iterative_solver.Optimize(4, algorithm="SD"),
+        lambda: iterative_solver.Optimize(4, algorithm=""),
+    ):
+        make().finalize()
+
+
+def test_solver_factory_dispatch():
+    # C API method names through the SolverFactory restatement (reference SolverFactory.h:114-185):
+    # unknown methods raise "Unimplemented method <m>"; Davidson/RSPT/DIIS/BFGS/SD construct
+    check_factory_dispatch()
