@@ -1170,3 +1170,5 @@ class OptimizeBFGS : public OptimizeSolver<R, Q, P> {
 };
 
 }  // namespace molpro::linalg::itsolv
+
+#include "interpolate_morse.h"  // Interpolate("morse") fits by NonLinearEquationsDIIS, defined above

@@ -417,6 +417,24 @@ void oracle_interpolate_cubic(const double* p0, const double* p1, double x, doub
   out[2] = p.f1;
   out[3] = p.f2;
 }
+// Interpolate(p0, p1, interpolant) evaluated at x, and minimize(xa, xb, bracket_grid,
+// max_bracket_grid, analytic) (reference Interpolate.cpp:55-186); out: x, f, f1, f2 then the four
+// parameters.  Returns nonzero with oracle_itsolv_last_error() on a throw (unknown interpolant).
+int oracle_interpolate_ex(const double* p0, const double* p1, const char* interpolant, double x, double xa, double xb,
+                          size_t bracket_grid, size_t max_bracket_grid, int analytic, double* at_x, double* minimum,
+                          double* parameters) {
+  return guarded([&] {
+    it::Interpolate inter({p0[0], p0[1], p0[2]}, {p1[0], p1[1], p1[2]}, interpolant ? interpolant : "cubic", 0);
+    const auto p = inter(x);
+    const auto m = inter.minimize(xa, xb, bracket_grid, max_bracket_grid, analytic != 0);
+    const double v[4] = {p.x, p.f, p.f1, p.f2}, w[4] = {m.x, m.f, m.f1, m.f2};
+    for (int i = 0; i < 4; ++i) {
+      at_x[i] = v[i];
+      minimum[i] = w[i];
+      parameters[i] = inter.parameters()[i];
+    }
+  });
+}
 void oracle_interpolate_minimize(const double* p0, const double* p1, double xa, double xb, double* out) {
   it::Interpolate inter({p0[0], p0[1], p0[2]}, {p1[0], p1[1], p1[2]});
   const auto p = inter.minimize(xa, xb);

@@ -229,6 +229,8 @@ def itsolv_lib():
         for name in ("oracle_interpolate_cubic",):
             getattr(L, name).argtypes = [PDd, PDd, D, PDd]
         L.oracle_interpolate_minimize.argtypes = [PDd, PDd, D, D, PDd]
+        L.oracle_interpolate_ex.restype = I
+        L.oracle_interpolate_ex.argtypes = [PDd, PDd, C.c_char_p, D, D, D, Z, Z, I, PDd, PDd, PDd]
         L.oracle_test_problem_trig.restype = I
         L.oracle_test_problem_trig.argtypes = [Z, D, I]
         L.oracle_rc_solution.restype = I
@@ -251,6 +253,20 @@ def interpolate_minimize(p0, p1, xa, xb):
     itsolv_lib().oracle_interpolate_minimize(_d(np.array(p0, float)), _d(np.array(p1, float)), float(xa), float(xb),
                                              _d(out))
     return out
+
+
+def interpolate(p0, p1, interpolant="cubic", x=0.0, xa=0.0, xb=1.0, bracket_grid=100, max_bracket_grid=100000,
+                analytic=True):
+    """Interpolate(p0, p1, interpolant) (reference Interpolate.cpp:55-186): returns (the point at x,
+    minimize(xa, xb, bracket_grid, max_bracket_grid, analytic), the four parameters), points as
+    (x, f, f', f'')."""
+    L = itsolv_lib()
+    at, mn, par = np.zeros(4), np.zeros(4), np.zeros(4)
+    if L.oracle_interpolate_ex(_d(np.array(p0, float)), _d(np.array(p1, float)), interpolant.encode(), float(x),
+                               float(xa), float(xb), int(bracket_grid), int(max_bracket_grid), 1 if analytic else 0,
+                               _d(at), _d(mn), _d(par)):
+        raise RuntimeError(L.oracle_itsolv_last_error().decode())
+    return at, mn, par
 
 
 class RcSolver:

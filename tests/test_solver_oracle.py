@@ -221,9 +221,51 @@ def test_interpolate_cubic_constructor():
 
 def test_interpolate_cubic_minimum():
     # test_Interpolate.cpp:23-41 with the analytic cubic minimiser OptimizeBFGS uses
-    # (OptimizeBFGS.h:95-96; Interpolate.cpp:141-142); the bracketing search is not restated
+    # (OptimizeBFGS.h:95-96; Interpolate.cpp:141-142)
     p = oracle.interpolate_minimize((0.0, 0.0, 0.25), (1.0, 0.25, 1.25), 0.0, 1.0)
     assert abs(p[0] - 0.5) < 1e-13 and abs(p[1]) < 1e-13 and abs(p[2]) < 1e-13 and p[3] > 0
+
+
+def test_interpolate_minimize_bracketing():
+    # test_Interpolate.cpp:23-41 (Interpolate.minimize): the grid-bracketing + regula-falsi search
+    # (analytic = false) on f = x (x - 1/2)^2, every assertion of the reference test
+    p0, p1 = (0.0, 0.0, 0.25), (1.0, 0.25, 1.25)
+
+    def mini(xa, xb, grid=100, grid_max=100000):
+        return oracle.interpolate(p0, p1, "cubic", xa=xa, xb=xb, bracket_grid=grid, max_bracket_grid=grid_max,
+                                  analytic=False)[1]
+
+    assert abs(mini(0, 1, 5, 1000)[0] - 0.5) < 1e-13
+    assert abs(mini(0, 1)[1]) < 1e-13
+    assert abs(mini(0, 1)[2]) < 1e-13
+    assert mini(0.3, 0.6)[3] > 0
+    assert abs(mini(0, -1)[0] + 1) < 1e-13
+    assert abs(mini(0.51, 1)[0] - 0.51) < 1e-13
+    assert abs(mini(0.1, 2)[0] - 0.5) < 1e-13
+    assert abs(mini(-1200, 2)[0] - 0.5) < 1e-13
+    assert abs(mini(0.4, 200)[0] - 0.5) < 1e-13
+
+
+@pytest.mark.parametrize("interpolant", ["cubic", "morse"])
+def test_interpolate_quadratic(interpolant):
+    # test_Interpolate.cpp:43-58: f = (x - 1/2)^2 + lambda x^3 through (0, 1/4, -1), (1, 1/4 + l, 1 + 3l);
+    # both interpolants' minimum on [0, 1] is the exact one to 1e-8
+    lam = 1e-3
+    p0, p1 = (0.0, 0.25, -1.0), (1.0, 0.25 + lam, 1 + 3 * lam)
+    at0, m, par = oracle.interpolate(p0, p1, interpolant, x=0.0, xa=0.0, xb=1.0)
+    x_expected = (-2.0 + np.sqrt(4.0 + 12 * lam)) / (6 * lam)
+    assert abs(m[0] - x_expected) < 1e-8
+    # the interpolant reproduces the defining values and slopes (the Morse fit's DIIS residual)
+    at1 = oracle.interpolate(p0, p1, interpolant, x=1.0)[0]
+    np.testing.assert_allclose([at0[1], at0[2], at1[1], at1[2]], [p0[1], p0[2], p1[1], p1[2]], atol=1e-9)
+    if interpolant == "morse":
+        # L0 + (k / 2a^2)(1 - exp(-a (y - y0)))^2: minimum L0 at y0
+        assert abs(m[0] - par[3]) < 1e-8 and abs(m[1] - par[0]) < 1e-12
+
+
+def test_interpolate_unknown():
+    with pytest.raises(RuntimeError, match="Unknown interpolant: spline"):
+        oracle.interpolate((0.0, 0.0, 0.25), (1.0, 0.25, 1.25), "spline")
 
 
 @pytest.mark.parametrize("n", [1, 2])
