@@ -427,3 +427,41 @@ def test_rspt_file_hylleraas_gpu(name, method, precondition):
     assert abs(e_gpu - e_ref) <= 1e-11
     assert abs(e_gpu - rp.rspt_second_order_energy(h, h0)) <= 1e-10
     s.finalize()
+
+
+def rspt_dense_problem(n=2000, seed=7):
+    # A perturbation problem at a size the fixtures do not reach: H0 = diag(i / 10 + 1), a weak
+    # symmetric perturbation (|H1| ~ 1e-3), so the series converges fast to the lowest eigenvalue.
+    rng = np.random.default_rng(seed)
+    h0 = 1.0 + 0.1 * np.arange(n)
+    v = rng.uniform(-1e-3, 1e-3, (n, n))
+    return np.diag(h0) + (v + v.T) / 2, h0
+
+
+def rspt_series(trace, h, h0):
+    x0 = rp.rspt_initial_guess(h0)
+    return np.cumsum([x0 @ (h @ x0)] + [x0 @ (h @ t[-1]) for t in trace[:-1]])
+
+
+def test_rspt_dense_2000_cpu():
+    h, h0 = rspt_dense_problem()
+    trace = rp.loop_rspt(rspt_cpu(h0.size), h, h0)
+    series = rspt_series(trace, h, h0)
+    exact = np.linalg.eigvalsh(h)[0]
+    assert abs(series[1] - series[0] - rp.rspt_second_order_energy(h, h0)) <= 1e-15
+    assert abs(series[-1] - exact) < 1e-12
+
+
+@pytest.mark.gpu
+def test_rspt_dense_2000_gpu():
+    # the HBM path (C API, host R buffers) against the CPU path: same steps, each order's energy
+    # and vector to the last digits the reductions' order leaves
+    h, h0 = rspt_dense_problem()
+    ref = rp.loop_rspt(rspt_cpu(h0.size), h, h0)
+    g = rspt_gpu(h0.size)
+    trace = rp.loop_rspt(g, h, h0)
+    assert [t[:-1] for t in trace] == [t[:-1] for t in ref]
+    for a, b in zip(trace, ref):
+        np.testing.assert_allclose(a[-1], b[-1], rtol=0, atol=1e-12 * max(1e-300, np.max(np.abs(b[-1]))))
+    np.testing.assert_allclose(rspt_series(trace, h, h0), rspt_series(ref, h, h0), rtol=1e-14, atol=0)
+    g.finalize()
