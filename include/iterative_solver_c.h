@@ -17,7 +17,8 @@
  *    context set by IterativeSolverHbmSetContext (an ssp_ctx with an RCCL or host communicator
  *    attached), or a single-rank context on device 0 is created.
  *  - Supported algorithms: LinearEigensystem and LinearEquations "Davidson" (or ""),
- *    NonLinearEquations "DIIS" (or ""), Optimize "BFGS" (or "") and "SD"; minimize = 0 throws.
+ *    NonLinearEquations "DIIS" (or ""), Optimize "BFGS" (or "") and "SD"; `minimize` is ignored,
+ *    as in the reference (IterativeSolverCMPI.cpp:250-268).
  *  - IterativeSolverAddVector on a non-linear solver (DIIS) passes the vector through the solver's
  *    own add_vector (residual norm, convergence flag, least-important-vector deletion), as the
  *    reference's solve() driver does; the reference's C layer reaches the generic vector-list
@@ -90,6 +91,12 @@ int IterativeSolverHbmSetThrow(int enable);
 /* Statistics of the top instance: iterations, R and Q creations (for tests and reports). */
 int IterativeSolverHbmStatistics(int* iterations, int* r_creations, int* q_creations);
 const char* IterativeSolverHbmLastError(void);
+/* Id (> 0) of the top instance, 0 when there is none.  Ids are unique within the process. */
+uint64_t IterativeSolverHbmInstanceId(void);
+/* Removes the instance with this id wherever it sits in the stack (a binding whose solver object
+ * is destroyed after a newer one was created must not pop the newer one, which
+ * IterativeSolverFinalize would).  Returns 0, or 1 when no instance has that id. */
+int IterativeSolverHbmFinalizeInstance(uint64_t id);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,8 @@ extern "C" {
 #endif
 
 #define ITSOLV_MAX_ROOTS 64
+#define ITSOLV_TRACE_ITER 256
+#define ITSOLV_TRACE_ROOTS 8
 
 typedef struct {
   int nroots;                  /* n_roots (reference Options::n_roots)                    */
@@ -55,6 +57,14 @@ typedef struct {
   double seconds;      /* wall time of the solve                                            */
   int n_eig_trace;     /* iterations recorded in eig_trace (<= 256)                          */
   double eig_trace[256]; /* lowest eigenvalue after each add_vector                          */
+  /* Per-iteration trace (the parity observables of IterativeSolverTemplate.h:322-408), one row
+   * per solve() iteration, n_eig_trace rows: eigenvalues (Davidson) and errors of the first
+   * trace_roots roots, Q-space size and working-set size after the iteration. */
+  int trace_roots;
+  int trace_nq[ITSOLV_TRACE_ITER];
+  int trace_nwork[ITSOLV_TRACE_ITER];
+  double trace_eigenvalues[ITSOLV_TRACE_ITER * ITSOLV_TRACE_ROOTS];
+  double trace_errors[ITSOLV_TRACE_ITER * ITSOLV_TRACE_ROOTS];
 } itsolv_result;
 
 const char* itsolv_last_error(void);

@@ -8,7 +8,6 @@
 #include <iostream>
 #include <limits>
 #include <memory>
-#include <stack>
 #include <stdexcept>
 #include <string>
 #include <tuple>
@@ -41,6 +40,7 @@ ssp_ctx* g_user_ctx = nullptr;
 bool g_throw = true;
 
 struct Instance {
+  uint64_t id = 0;  // IterativeSolverHbmInstanceId: lets a binding finalize its own instance
   std::shared_ptr<Device> dev;
   std::unique_ptr<Solver> solver;
   size_t dimension = 0, offset = 0, local = 0;
@@ -50,11 +50,20 @@ struct Instance {
   bool has_values = false;
   bool has_eigenvalues = false;
 };
-std::stack<Instance> instances;
+// The instance stack (reference IterativeSolverCMPI.cpp: std::stack<Instance>); the back is the top,
+// the only active instance.  A vector, so that IterativeSolverHbmFinalizeInstance can also remove
+// an instance below the top whose owner has gone away.  Instances are heap-held: the P-space
+// callback keeps a pointer to its instance across pushes and erasures.
+std::vector<std::unique_ptr<Instance>> instances;
+uint64_t g_next_id = 1;
 
 Instance& top() {
   if (instances.empty()) throw std::runtime_error("IterativeSolver not initialised properly");
-  return instances.top();
+  return *instances.back();
+}
+void push(Instance&& in) {
+  in.id = g_next_id++;
+  instances.push_back(std::make_unique<Instance>(std::move(in)));
 }
 
 std::shared_ptr<Device> make_device() {
@@ -147,7 +156,7 @@ const char* IterativeSolverHbmLastError(void) { return g_error.c_str(); }
 
 int IterativeSolverHbmStatistics(int* iterations, int* r_creations, int* q_creations) {
   if (instances.empty()) return 1;
-  const auto& s = instances.top().solver->statistics();
+  const auto& s = instances.back()->solver->statistics();
   if (iterations) *iterations = s.iterations;
   if (r_creations) *r_creations = s.r_creations;
   if (q_creations) *q_creations = s.q_creations;
@@ -176,7 +185,7 @@ void IterativeSolverLinearEigensystemInitialize(size_t nQ, size_t nroot, size_t*
     in.solver = std::move(solver);
     in.has_eigenvalues = true;
     setup(in, nQ, range_begin, range_end);
-    instances.push(std::move(in));
+    push(std::move(in));
   });
 }
 
@@ -207,7 +216,7 @@ void IterativeSolverLinearEquationsInitialize(size_t n, size_t nroot, size_t* ra
     if (aughes > 0) solver->set_augmented_hessian(aughes);
     solver->set_verbosity(verbosity_of(verbosity));
     in.solver = std::move(solver);
-    instances.push(std::move(in));
+    push(std::move(in));
   });
 }
 
@@ -225,7 +234,7 @@ void IterativeSolverNonLinearEquationsInitialize(size_t n, size_t* range_begin, 
     solver->set_verbosity(verbosity_of(verbosity));
     in.solver = std::move(solver);
     setup(in, n, range_begin, range_end);
-    instances.push(std::move(in));
+    push(std::move(in));
   });
 }
 
@@ -235,7 +244,7 @@ void IterativeSolverOptimizeInitialize(size_t n, size_t* range_begin, size_t* ra
   guarded([&] {
     (void)fname;
     (void)fcomm;
-    if (!minimize) throw std::runtime_error("IterativeSolverOptimizeInitialize: maximisation is not implemented");
+    (void)minimize;  // ignored, as the reference does (IterativeSolverCMPI.cpp:250-268)
     Instance in;
     in.dev = make_device();
     auto solver = it::create_Optimize(algorithm ? algorithm : "", options ? options : "",
@@ -248,14 +257,25 @@ void IterativeSolverOptimizeInitialize(size_t n, size_t* range_begin, size_t* ra
     in.solver = std::move(solver);
     in.has_values = true;
     setup(in, n, range_begin, range_end);
-    instances.push(std::move(in));
+    push(std::move(in));
   });
 }
 
 void IterativeSolverFinalize(void) {
   guarded([] {
-    if (!instances.empty()) instances.pop();
+    if (!instances.empty()) instances.pop_back();
   });
+}
+
+uint64_t IterativeSolverHbmInstanceId(void) { return instances.empty() ? 0 : instances.back()->id; }
+
+int IterativeSolverHbmFinalizeInstance(uint64_t id) {
+  for (auto it = instances.begin(); it != instances.end(); ++it)
+    if ((*it)->id == id) {
+      instances.erase(it);
+      return 0;
+    }
+  return 1;
 }
 
 size_t IterativeSolverAddVector(size_t buffer_size, double* parameters, double* action, int sync) {

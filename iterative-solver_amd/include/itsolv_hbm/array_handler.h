@@ -8,14 +8,17 @@
 //   select_max_dot / select -> std::map ordered by index       :212, :222
 //   op Counter feeding Statistics                              :167-176, :224-253
 //   errors throw util::ArrayHandlerError                       :25-27, :268
-//   lazy_handle(): registers dot / axpy and evaluates them on eval() or destruction (:298-432);
-//   here evaluation goes through fused_dot / fused_axpy, which device handlers override with
-//   one gemm_inner / gemm_outer launch.
+//   lazy_handle(): registers dot / axpy and evaluates them on eval() or destruction (:298-437)
+//   through the protected fused_dot / fused_axpy, which device handlers override with one
+//   gemm_inner / gemm_outer launch.
 #pragma once
 #include <cmath>
 #include <complex>
+#include <functional>
+#include <list>
 #include <map>
 #include <memory>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <tuple>
@@ -35,6 +38,65 @@ namespace util {
 struct ArrayHandlerError : public std::logic_error {
   using std::logic_error::logic_error;
 };
+
+// Ordered register of deferred operations (reference ArrayHandler.h:29-57).  push(args...) appends;
+// push<N>(args..., equal) inserts after the last registered operation whose N-th argument equals
+// this one's, so operations sharing that argument end up consecutive, groups in arrival order.
+template <typename... Args>
+struct OperationRegister {
+  using OP = std::tuple<Args...>;
+  std::list<OP> m_register;
+
+  template <int N, class ArgEqual>
+  void push(const Args&... args, ArgEqual equal) {
+    OP op{args...};
+    auto pos = m_register.end();
+    for (auto it = m_register.end(); it != m_register.begin();) {
+      --it;
+      if (equal(std::get<N>(op), std::get<N>(*it))) {
+        pos = std::next(it);
+        break;
+      }
+    }
+    m_register.insert(pos, std::move(op));
+  }
+  void push(const Args&... args) { m_register.emplace_back(args...); }
+  bool empty() { return m_register.empty(); }
+  void clear() { m_register.clear(); }
+};
+
+// Turns a register of (x, y, z) operations into index triples over the distinct x, y and z
+// (first-appearance order, equality by the given predicates) -- reference ArrayHandler.h:59-97.
+template <typename X, typename Y, typename Z, class EqualX, class EqualY, class EqualZ>
+std::tuple<std::vector<std::tuple<size_t, size_t, size_t>>, std::vector<X>, std::vector<Y>, std::vector<Z>>
+remove_duplicates(const std::list<std::tuple<X, Y, Z>>& reg, EqualX equal_x, EqualY equal_y, EqualZ equal_z) {
+  std::vector<std::tuple<size_t, size_t, size_t>> index;
+  std::vector<X> xs;
+  std::vector<Y> ys;
+  std::vector<Z> zs;
+  auto slot = [](auto& seen, const auto& v, auto& eq) {
+    for (size_t i = 0; i < seen.size(); ++i)
+      if (eq(v, seen[i])) return i;
+    seen.push_back(v);
+    return seen.size() - 1;
+  };
+  index.reserve(reg.size());
+  for (const auto& op : reg) {
+    const size_t ix = slot(xs, std::get<0>(op), equal_x);
+    const size_t iy = slot(ys, std::get<1>(op), equal_y);
+    const size_t iz = slot(zs, std::get<2>(op), equal_z);
+    index.emplace_back(ix, iy, iz);
+  }
+  return {index, xs, ys, zs};
+}
+
+// Identity of referenced objects (reference ArrayHandler.h:100-106).
+template <typename T = int>
+struct RefEqual {
+  bool operator()(const std::reference_wrapper<T>& l, const std::reference_wrapper<T>& r) {
+    return std::addressof(l.get()) == std::addressof(r.get());
+  }
+};
 }  // namespace util
 
 // Element type of a container: mapped_type for maps (P space), value_type otherwise.
@@ -49,14 +111,13 @@ struct element_type<A, std::void_t<typename A::mapped_type>> {
 template <class A>
 using element_type_t = typename element_type<A>::type;
 
+// The abstract handler: the member names, signatures and protected customisation points of the
+// reference's ArrayHandler<AL, AR> (ArrayHandler.h:161-437), so that a handler written for one
+// base compiles against the other (include/itsolv_hbm/reference_handler.h builds the HBM handlers
+// on the reference's own header).
 template <class AL, class AR = AL>
 class ArrayHandler {
- public:
-  using value_type_L = element_type_t<AL>;
-  using value_type_R = element_type_t<AR>;
-  using value_type = decltype(value_type_L{} * value_type_R{});
-  using value_type_abs = decltype(std::abs(value_type{}));
-
+ protected:
   struct Counter {
     int scal = 0;
     int dot = 0;
@@ -65,8 +126,16 @@ class ArrayHandler {
     int gemm_inner = 0;
     int gemm_outer = 0;
   };
+  std::unique_ptr<Counter> m_counter;
 
-  virtual ~ArrayHandler() = default;
+  ArrayHandler() : m_counter(std::make_unique<Counter>()) {}
+  ArrayHandler(const ArrayHandler& o) : m_counter(std::make_unique<Counter>(*o.m_counter)) {}
+
+ public:
+  using value_type_L = element_type_t<AL>;
+  using value_type_R = element_type_t<AR>;
+  using value_type = decltype(value_type_L{} * value_type_R{});
+  using value_type_abs = decltype(std::abs(value_type{}));
 
   virtual AL copy(const AR& source) = 0;
   //! Copy content of y into x
@@ -83,7 +152,7 @@ class ArrayHandler {
   const Counter& counter() const { return *m_counter; }
   void clear_counter() { *m_counter = Counter{}; }
 
-  std::string counter_to_string(const std::string& L, const std::string& R) const {
+  std::string counter_to_string(std::string L, std::string R) {
     std::string s;
     const auto& c = *m_counter;
     if (c.scal > 0) s += std::to_string(c.scal) + " scaling operations of the " + L + " vectors, ";
@@ -97,71 +166,136 @@ class ArrayHandler {
     return s;
   }
 
-  // Deferred dot / axpy (reference ArrayHandler.h:298-432).  Only one kind of operation may be
-  // registered at a time; eval() runs them through fused_dot / fused_axpy and clears the register.
-  class LazyHandle {
-   public:
-    explicit LazyHandle(ArrayHandler& h) : m_handler(&h) {}
-    LazyHandle(const LazyHandle&) = delete;
-    ~LazyHandle() {
-      try {
-        eval();
-      } catch (...) {
-      }
-    }
-    void axpy(value_type a, const AR& x, AL& y) {
-      kind("axpy");
-      m_axpy.emplace_back(a, &x, &y);
-      if (m_off) eval();
-    }
-    void dot(const AL& x, const AR& y, value_type& out) {
-      kind("dot");
-      m_dot.emplace_back(&x, &y, &out);
-      if (m_off) eval();
-    }
-    void eval() {
-      if (!m_handler) return;
-      if (!m_axpy.empty()) m_handler->fused_axpy(m_axpy);
-      if (!m_dot.empty()) m_handler->fused_dot(m_dot);
-      m_axpy.clear();
-      m_dot.clear();
-      m_kind.clear();
-    }
-    void off() { m_off = true; }
-    void on() { m_off = false; }
-    bool is_off() const { return m_off; }
-    void invalidate() { m_handler = nullptr; }
-    bool invalid() const { return m_handler == nullptr; }
-
-   private:
-    void kind(const std::string& k) {
-      if (!m_kind.empty() && m_kind != k)
-        throw util::ArrayHandlerError("Failed to register operation type " + k + " with the current state of the LazyHandle");
-      m_kind = k;
-    }
-    ArrayHandler* m_handler;
-    bool m_off = false;
-    std::string m_kind;
-    std::vector<std::tuple<value_type, const AR*, AL*>> m_axpy;
-    std::vector<std::tuple<const AL*, const AR*, value_type*>> m_dot;
-  };
-  using ProxyHandle = std::shared_ptr<LazyHandle>;
-  ProxyHandle lazy_handle() { return std::make_shared<LazyHandle>(*this); }
+  //! Destroying the handler invalidates the lazy handles it made: they no longer evaluate.
+  virtual ~ArrayHandler() {
+    for (auto& w : m_lazy_handles)
+      if (auto h = w.lock()) h->invalidate();
+  }
 
  protected:
-  ArrayHandler() : m_counter(std::make_unique<Counter>()) {}
-  ArrayHandler(const ArrayHandler& o) : m_counter(std::make_unique<Counter>(*o.m_counter)) {}
   virtual void error(const std::string& message) { throw util::ArrayHandlerError{message}; }
 
-  // Default fusion: one call per registered operation, in registration order.
-  virtual void fused_axpy(const std::vector<std::tuple<value_type, const AR*, AL*>>& ops) {
-    for (auto& [a, x, y] : ops) axpy(a, *x, *y);
+  // Customisation points of lazy evaluation (reference :270-292): `reg` holds one (alpha, x, y)
+  // index triple per registered axpy, (x, y, out) per registered dot, over the distinct operands.
+  // The defaults evaluate one operation at a time in registration order; device handlers override
+  // them with one batched launch.
+  virtual void fused_axpy(const std::vector<std::tuple<size_t, size_t, size_t>>& reg,
+                          const std::vector<value_type>& alphas, const std::vector<std::reference_wrapper<const AR>>& xx,
+                          std::vector<std::reference_wrapper<AL>>& yy) {
+    for (const auto& [a, x, y] : reg) axpy(alphas[a], xx[x].get(), yy[y].get());
   }
-  virtual void fused_dot(const std::vector<std::tuple<const AL*, const AR*, value_type*>>& ops) {
-    for (auto& [x, y, out] : ops) *out = dot(*x, *y);
+  virtual void fused_dot(const std::vector<std::tuple<size_t, size_t, size_t>>& reg,
+                         const std::vector<std::reference_wrapper<const AL>>& xx,
+                         const std::vector<std::reference_wrapper<const AR>>& yy,
+                         std::vector<std::reference_wrapper<value_type>>& out) {
+    for (const auto& [x, y, z] : reg) out[z].get() = dot(xx[x].get(), yy[y].get());
   }
 
-  std::unique_ptr<Counter> m_counter;
+  // Deferred dot / axpy (reference :298-381): one kind of operation at a time; eval() (or the
+  // destructor) hands the de-duplicated register to fused_axpy / fused_dot and clears it.
+  class LazyHandle {
+   public:
+    using value_type = typename ArrayHandler<AL, AR>::value_type;
+    template <typename T>
+    using ref_wrap = std::reference_wrapper<T>;
+
+    explicit LazyHandle(ArrayHandler<AL, AR>& handler) : m_handler{handler} {}
+    virtual ~LazyHandle() { LazyHandle::eval(); }
+
+    virtual void axpy(value_type alpha, const AR& x, AL& y) {
+      if (!register_op_type("axpy"))
+        return error("Failed to register operation type axpy with the current state of the LazyHandle");
+      m_axpy.push(alpha, std::cref(x), std::ref(y));
+    }
+    virtual void dot(const AL& x, const AR& y, value_type& out) {
+      if (!register_op_type("dotLR"))
+        return error("Failed to register operation type dot with the current state of the LazyHandle");
+      m_dot.push(std::cref(x), std::cref(y), std::ref(out));
+    }
+    virtual void eval() {
+      if (m_invalid) return;
+      if (!m_axpy.empty()) {
+        auto [reg, alphas, xx, yy] =
+            util::remove_duplicates(m_axpy.m_register, std::equal_to<value_type>{}, util::RefEqual<const AR>{},
+                                    util::RefEqual<AL>{});
+        m_handler.fused_axpy(reg, alphas, xx, yy);
+      }
+      if (!m_dot.empty()) {
+        auto [reg, xx, yy, out] = util::remove_duplicates(m_dot.m_register, util::RefEqual<const AL>{},
+                                                          util::RefEqual<const AR>{}, util::RefEqual<value_type>{});
+        m_handler.fused_dot(reg, xx, yy, out);
+      }
+      clear();
+    }
+    void invalidate() { m_invalid = true; }
+    bool invalid() { return m_invalid; }
+
+   protected:
+    virtual bool register_op_type(const std::string& type) {
+      if (!m_op_types.empty() && m_op_types.count(type) == 0) return false;
+      m_op_types.insert(type);
+      return true;
+    }
+    void clear() {
+      m_op_types.clear();
+      m_axpy.clear();
+      m_dot.clear();
+    }
+    void error(std::string message) { m_handler.error(message); }
+
+    std::set<std::string> m_op_types;
+    util::OperationRegister<value_type, ref_wrap<const AR>, ref_wrap<AL>> m_axpy;
+    util::OperationRegister<ref_wrap<const AL>, ref_wrap<const AR>, ref_wrap<value_type>> m_dot;
+    ArrayHandler<AL, AR>& m_handler;
+    bool m_invalid = false;
+  };
+
+  // What lazy_handle() returns (reference :384-414): forwards to the LazyHandle; with off(), every
+  // registered operation is evaluated at once.
+  class ProxyHandle {
+   public:
+    ProxyHandle(std::shared_ptr<LazyHandle> handle) : m_lazy_handle{std::move(handle)} {}
+    template <typename... Args>
+    void axpy(Args&&... args) {
+      m_lazy_handle->axpy(std::forward<Args>(args)...);
+      if (m_off) eval();
+    }
+    template <typename... Args>
+    void dot(Args&&... args) {
+      m_lazy_handle->dot(std::forward<Args>(args)...);
+      if (m_off) eval();
+    }
+    void eval() { m_lazy_handle->eval(); }
+    void invalidate() { m_lazy_handle->invalidate(); }
+    bool invalid() { return m_lazy_handle->invalid(); }
+    void off() { m_off = true; }
+    void on() { m_off = false; }
+    bool is_off() { return m_off; }
+
+   protected:
+    std::shared_ptr<LazyHandle> m_lazy_handle;
+    bool m_off = false;
+  };
+
+  std::vector<std::weak_ptr<LazyHandle>> m_lazy_handles;
+
+  void save_handle(const std::shared_ptr<LazyHandle>& handle) {
+    for (auto& w : m_lazy_handles)
+      if (w.expired()) {
+        w = handle;
+        return;
+      }
+    m_lazy_handles.push_back(handle);
+  }
+  ProxyHandle lazy_handle(ArrayHandler<AL, AR>& handler) {
+    auto h = std::make_shared<LazyHandle>(handler);
+    save_handle(h);
+    return h;
+  }
+
+ public:
+  //! A lazy handle on this handler; implementations return lazy_handle(*this).
+  virtual ProxyHandle lazy_handle() = 0;
 };
 
 // Capabilities of a vector type's handlers beyond the reference interface.

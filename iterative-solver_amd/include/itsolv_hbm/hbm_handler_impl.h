@@ -1,0 +1,325 @@
+// The HBM ArrayHandlers, written once over whichever ArrayHandler base the translation unit has:
+//
+//   * itsolv_hbm/hbm_handlers.h includes this after the restated base (itsolv_hbm/array_handler.h):
+//     the handlers this package's solvers and C ABI run on;
+//   * itsolv_hbm/reference_handler.h includes it after the reference's own
+//     molpro/linalg/array/ArrayHandler.h: the same classes as a drop-in for the reference's
+//     ArrayHandlers<R, Q, P> injection (reference itsolv/ArrayHandlers.h:57-103).
+//
+// Both bases declare molpro::linalg::array::ArrayHandler<AL, AR>, ::util::ArrayHandlerError,
+// molpro::linalg::itsolv::subspace::Matrix and itsolv::{CVecRef, VecRef} with the reference's
+// signatures (reference ArrayHandler.h:161-437, subspace/Matrix.h, wrap.h), which is all this
+// header uses.  Every operation is one libsubspace_hip.so C-ABI call on HBM-resident shards:
+//
+//   copy / scal / fill / axpy / dot   ArrayHandlerIterable.h:46-82     ssp_copy/scal/fill/axpy/dot
+//   gemm_inner(xx, yy)                util/gemm.h:267-279 (+ :157-184)  ssp_gemm_inner (+ RCCL allreduce)
+//   gemm_outer(alphas, xx, yy)        util/gemm.h:257-265 (+ :186-203)  ssp_gemm_outer
+//   select / select_max_dot           util/select.h:28-55, DistrArray.cpp:170-276   ssp_select*
+//   lazy dot (fused_dot)              ArrayHandler.h:283-292           one ssp_gemm_inner over the
+//                                                                      distinct registered operands
+//   lazy axpy (fused_axpy)            ArrayHandler.h:271-280           one ssp_gemm_outer when every
+//                                     destination's sources arrive in first-appearance order (the
+//                                     kernel applies them in that order with one fma each: bit-for-
+//                                     bit the sequence of axpys); otherwise the sequence itself
+//   sparse R x P (ArrayHandlerHbmSparse)  ArrayHandlerIterableSparse.h:35-58, DistrArray.cpp:419-465
+//
+// Error behaviour: size mismatches call error() (util::ArrayHandlerError, as
+// ArrayHandlerIterable.h:68-69, :77-78 throw), alphas dimension mismatch -> std::out_of_range
+// (gemm.h:66-71), sparse copy-construction -> std::logic_error (ArrayHandlerDistrSparse.h:26-28).
+//
+// No include guard on purpose: it is included once per translation unit, by one of the two headers
+// above (each has #pragma once).
+#include <algorithm>
+#include <cmath>
+#include <functional>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "hbm_vec.h"
+
+namespace molpro::linalg::hbm {
+
+namespace detail {
+template <class Refs>
+std::vector<const double*> cptrs(const Refs& v) {
+  std::vector<const double*> p;
+  p.reserve(v.size());
+  for (auto& x : v) p.push_back(x.get().data());
+  return p;
+}
+template <class Refs>
+std::vector<double*> mptrs(const Refs& v) {
+  std::vector<double*> p;
+  p.reserve(v.size());
+  for (auto& x : v) p.push_back(x.get().data());
+  return p;
+}
+// (ptr, idx, val) CSR packing of sparse P vectors, indices ascending (std::map order).
+template <class PRefs>
+void pack(const PRefs& ps, std::vector<size_t>& ptr, std::vector<size_t>& idx, std::vector<double>& val) {
+  ptr.assign(1, 0);
+  for (auto& p : ps) {
+    for (auto& [i, v] : p.get()) {
+      idx.push_back(i);
+      val.push_back(v);
+    }
+    ptr.push_back(idx.size());
+  }
+}
+inline std::map<size_t, double> run_select(size_t n, const std::function<int(size_t*, double*, size_t*)>& f) {
+  std::vector<size_t> idx(std::max<size_t>(n, 1));
+  std::vector<double> val(std::max<size_t>(n, 1));
+  size_t cnt = 0;
+  check_status<array::util::ArrayHandlerError>(f(idx.data(), val.data(), &cnt), "ssp_select");
+  std::map<size_t, double> out;
+  for (size_t e = 0; e < cnt; ++e) out.emplace(idx[e], val[e]);
+  return out;
+}
+}  // namespace detail
+
+// Dense HBM x HBM handler (R x R, Q x Q, R x Q, Q x R).
+class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
+  using Base = array::ArrayHandler<Vec, Vec>;
+  static void check(int status, const char* what) { check_status<array::util::ArrayHandlerError>(status, what); }
+
+ public:
+  using typename Base::ProxyHandle;
+  using Base::lazy_handle;
+  ProxyHandle lazy_handle() override { return this->lazy_handle(*this); }
+
+  Vec copy(const Vec& source) override {
+    m_counter->copy++;
+    return Vec(source);
+  }
+  void copy(Vec& x, const Vec& y) override {
+    m_counter->copy++;
+    same(x, y, "copy");
+    check(ssp_copy(x.ctx(), x.data(), y.data(), x.local_size()), "ssp_copy");
+  }
+  void scal(double alpha, Vec& x) override {
+    m_counter->scal++;
+    check(ssp_scal(x.ctx(), alpha, x.data(), x.local_size()), "ssp_scal");
+  }
+  void fill(double alpha, Vec& x) override { check(ssp_fill(x.ctx(), alpha, x.data(), x.local_size()), "ssp_fill"); }
+  void axpy(double alpha, const Vec& x, Vec& y) override {
+    m_counter->axpy++;
+    if (x.size() < y.size()) error("ArrayHandlerHbm::axpy() incompatible x and y arrays, x.size() < y.size()");
+    same(x, y, "axpy");
+    check(ssp_axpy(y.ctx(), alpha, x.data(), y.data(), y.local_size()), "ssp_axpy");
+  }
+  double dot(const Vec& x, const Vec& y) override {
+    m_counter->dot++;
+    if (x.size() > y.size()) error("ArrayHandlerHbm::dot() incompatible x and y arrays, x.size() > y.size()");
+    same(x, y, "dot");
+    double out = 0;
+    check(ssp_dot(x.ctx(), x.data(), y.data(), x.local_size(), &out), "ssp_dot");
+    return out;
+  }
+  void gemm_outer(const itsolv::subspace::Matrix<double> alphas, const itsolv::CVecRef<Vec>& xx,
+                  const itsolv::VecRef<Vec>& yy) override {
+    m_counter->gemm_outer++;
+    if (yy.empty() || xx.empty()) return;
+    if (alphas.rows() != xx.size())
+      throw std::out_of_range("gemm_outer: dimensions of xx and alphas are different: " + std::to_string(alphas.rows()) +
+                              " " + std::to_string(xx.size()));
+    // As gemm_outer_default (util/gemm.h:257-265): alphas.cols() destinations, the first of yy
+    // (construct_solution fills a batch of roots into a larger parameter buffer).
+    if (alphas.cols() > yy.size())
+      throw std::out_of_range("gemm_outer: dimensions of yy and alphas are different: " + std::to_string(alphas.cols()) +
+                              " " + std::to_string(yy.size()));
+    for (auto& x : xx) same(x.get(), yy.front().get(), "gemm_outer");
+    auto xp = detail::cptrs(xx);
+    auto yp = detail::mptrs(yy);
+    const auto& y0 = yy.front().get();
+    check(ssp_gemm_outer(y0.ctx(), alphas.data().data(), xp.data(), int(xx.size()), yp.data(), int(alphas.cols()),
+                         y0.local_size()),
+          "ssp_gemm_outer");
+  }
+  itsolv::subspace::Matrix<double> gemm_inner(const itsolv::CVecRef<Vec>& xx, const itsolv::CVecRef<Vec>& yy) override {
+    m_counter->gemm_inner++;
+    std::vector<double> buf(xx.size() * yy.size(), 0.0);
+    if (!xx.empty() && !yy.empty()) {
+      for (auto& y : yy) same(xx.front().get(), y.get(), "gemm_inner");
+      auto xp = detail::cptrs(xx);
+      auto yp = detail::cptrs(yy);
+      const auto& x0 = xx.front().get();
+      check(ssp_gemm_inner(x0.ctx(), xp.data(), int(xx.size()), yp.data(), int(yy.size()), x0.local_size(),
+                           buf.data()),
+            "ssp_gemm_inner");
+    }
+    return itsolv::subspace::Matrix<double>(std::move(buf), {xx.size(), yy.size()});
+  }
+  std::map<size_t, double> select_max_dot(size_t n, const Vec& x, const Vec& y) override {
+    if (n > x.size() || n > y.size()) error("ArrayHandlerHbm::select_max_dot() n is too large");
+    same(x, y, "select_max_dot");
+    return detail::run_select(n, [&](size_t* i, double* v, size_t* c) {
+      return ssp_select_max_dot(x.ctx(), x.data(), y.data(), x.local_size(), x.offset(), n, i, v, c);
+    });
+  }
+  std::map<size_t, double> select(size_t n, const Vec& x, bool max = false, bool ignore_sign = false) override {
+    if (n > x.size()) error("ArrayHandlerHbm::select() n is too large");
+    return detail::run_select(n, [&](size_t* i, double* v, size_t* c) {
+      return ssp_select(x.ctx(), x.data(), x.local_size(), x.offset(), n, max, ignore_sign, i, v, c);
+    });
+  }
+
+ protected:
+  void same(const Vec& a, const Vec& b, const char* op) {
+    if (!a.compatible(b)) error(std::string("ArrayHandlerHbm::") + op + "() arrays have different distributions");
+  }
+
+  // Registered lazy dots: one gemm_inner over the distinct x and y (each vector read once).
+  void fused_dot(const std::vector<std::tuple<size_t, size_t, size_t>>& reg,
+                 const std::vector<std::reference_wrapper<const Vec>>& xx,
+                 const std::vector<std::reference_wrapper<const Vec>>& yy,
+                 std::vector<std::reference_wrapper<double>>& out) override {
+    const auto m = gemm_inner(itsolv::CVecRef<Vec>(xx.begin(), xx.end()), itsolv::CVecRef<Vec>(yy.begin(), yy.end()));
+    for (const auto& [x, y, z] : reg) out[z].get() = m(x, y);
+  }
+
+  // Registered lazy axpys: one gemm_outer (alphas(x, y) = the registered coefficient) when each
+  // (x, y) pair occurs once and every destination receives its sources in increasing x order --
+  // the order the kernel applies them -- so the result is the axpy sequence bit for bit.
+  void fused_axpy(const std::vector<std::tuple<size_t, size_t, size_t>>& reg, const std::vector<double>& alphas,
+                  const std::vector<std::reference_wrapper<const Vec>>& xx,
+                  std::vector<std::reference_wrapper<Vec>>& yy) override {
+    const size_t nx = xx.size(), ny = yy.size();
+    std::vector<double> coef(nx * ny, 0.0);
+    std::vector<char> seen(nx * ny, 0);
+    std::vector<long> last(ny, -1);
+    bool batched = nx > 0 && ny > 0;
+    for (const auto& [a, x, y] : reg) {
+      if (seen[x * ny + y] || long(x) < last[y]) {
+        batched = false;
+        break;
+      }
+      seen[x * ny + y] = 1;
+      last[y] = long(x);
+      coef[x * ny + y] = alphas[a];
+    }
+    if (!batched) {
+      for (const auto& [a, x, y] : reg) axpy(alphas[a], xx[x].get(), yy[y].get());
+      return;
+    }
+    for (size_t y = 1; y < ny; ++y) same(yy[y].get(), yy[0].get(), "fused_axpy");
+    for (size_t x = 0; x < nx; ++x) same(xx[x].get(), yy[0].get(), "fused_axpy");
+    m_counter->gemm_outer++;
+    auto xp = detail::cptrs(xx);
+    auto yp = detail::mptrs(yy);
+    const auto& y0 = yy.front().get();
+    check(ssp_gemm_outer(y0.ctx(), coef.data(), xp.data(), int(nx), yp.data(), int(ny), y0.local_size()),
+          "ssp_gemm_outer");
+  }
+};
+
+// HBM x sparse (R x P, Q x P) handler; P = std::map<size_t, double>.
+class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
+  using Base = array::ArrayHandler<Vec, SparseP>;
+  static void check(int status, const char* what) { check_status<array::util::ArrayHandlerError>(status, what); }
+
+ public:
+  using typename Base::ProxyHandle;
+  using Base::lazy_handle;
+  ProxyHandle lazy_handle() override { return this->lazy_handle(*this); }
+
+  Vec copy(const SparseP&) override {
+    throw std::logic_error("ArrayHandlerHbmSparse: cannot construct a distributed array from a sparse one");
+  }
+  void copy(Vec& x, const SparseP& y) override {
+    m_counter->copy++;
+    std::vector<size_t> idx;
+    std::vector<double> val;
+    for (auto& [i, v] : y) {
+      idx.push_back(i);
+      val.push_back(v);
+    }
+    check(ssp_sparse_copy(x.ctx(), x.data(), x.local_size(), x.offset(), idx.data(), val.data(), idx.size()),
+          "ssp_sparse_copy");
+  }
+  void scal(double, Vec&) override {}
+  void fill(double, Vec&) override {}
+  void axpy(double alpha, const SparseP& x, Vec& y) override {
+    m_counter->axpy++;
+    std::vector<size_t> idx;
+    std::vector<double> val;
+    for (auto& [i, v] : x)
+      if (i < y.size()) {
+        idx.push_back(i);
+        val.push_back(v);
+      }
+    check(ssp_sparse_axpy(y.ctx(), alpha, idx.data(), val.data(), idx.size(), y.data(), y.local_size(), y.offset()),
+          "ssp_sparse_axpy");
+  }
+  double dot(const Vec& x, const SparseP& y) override {
+    m_counter->dot++;
+    std::vector<size_t> idx;
+    std::vector<double> val;
+    for (auto& [i, v] : y)
+      if (i < x.size()) {
+        idx.push_back(i);
+        val.push_back(v);
+      }
+    double out = 0;
+    check(ssp_sparse_dot(x.ctx(), x.data(), x.local_size(), x.offset(), idx.data(), val.data(), idx.size(), &out),
+          "ssp_sparse_dot");
+    return out;
+  }
+  void gemm_outer(const itsolv::subspace::Matrix<double> alphas, const itsolv::CVecRef<SparseP>& xx,
+                  const itsolv::VecRef<Vec>& yy) override {
+    m_counter->gemm_outer++;
+    if (xx.empty() || yy.empty()) return;
+    if (alphas.rows() != xx.size() || alphas.cols() > yy.size())
+      throw std::out_of_range("gemm_outer (sparse): dimensions of alphas do not match xx, yy");
+    std::vector<size_t> ptr, idx;
+    std::vector<double> val;
+    detail::pack(xx, ptr, idx, val);
+    auto yp = detail::mptrs(yy);
+    const auto& y0 = yy.front().get();
+    check(ssp_gemm_outer_sparse(y0.ctx(), alphas.data().data(), ptr.data(), idx.data(), val.data(), int(xx.size()),
+                                yp.data(), int(alphas.cols()), y0.local_size(), y0.offset()),
+          "ssp_gemm_outer_sparse");
+  }
+  itsolv::subspace::Matrix<double> gemm_inner(const itsolv::CVecRef<Vec>& xx,
+                                              const itsolv::CVecRef<SparseP>& yy) override {
+    m_counter->gemm_inner++;
+    std::vector<double> buf(xx.size() * yy.size(), 0.0);
+    if (!xx.empty() && !yy.empty()) {
+      std::vector<size_t> ptr, idx;
+      std::vector<double> val;
+      detail::pack(yy, ptr, idx, val);
+      auto xp = detail::cptrs(xx);
+      const auto& x0 = xx.front().get();
+      check(ssp_gemm_inner_sparse(x0.ctx(), xp.data(), int(xx.size()), x0.local_size(), x0.offset(), ptr.data(),
+                                  idx.data(), val.data(), int(yy.size()), buf.data()),
+            "ssp_gemm_inner_sparse");
+    }
+    return itsolv::subspace::Matrix<double>(std::move(buf), {xx.size(), yy.size()});
+  }
+  // |x_i v_i| over the entries of y, reduced over ranks, then the reference's top-n rule.
+  std::map<size_t, double> select_max_dot(size_t n, const Vec& x, const SparseP& y) override {
+    if (n > x.size() || n > y.size()) error("ArrayHandlerHbmSparse::select_max_dot() n is too large");
+    std::vector<SparseP> storage;
+    for (auto& [i, v] : y)
+      if (i < x.size()) storage.push_back(SparseP{{i, v}});
+    itsolv::CVecRef<SparseP> singles(storage.begin(), storage.end());
+    const auto prod = gemm_inner(itsolv::CVecRef<Vec>{std::cref(x)}, singles);
+    std::vector<std::pair<double, size_t>> c;
+    for (size_t e = 0; e < storage.size(); ++e) c.emplace_back(std::abs(prod(0, e)), storage[e].begin()->first);
+    std::sort(c.begin(), c.end(), [](auto& a, auto& b) { return b < a; });
+    std::map<size_t, double> out;
+    for (size_t k = 0; k < std::min(n, c.size()); ++k) out.emplace(c[k].second, c[k].first);
+    return out;
+  }
+  std::map<size_t, double> select(size_t n, const Vec& x, bool max = false, bool ignore_sign = false) override {
+    if (n > x.size()) error("ArrayHandlerHbmSparse::select() n is too large");
+    return detail::run_select(n, [&](size_t* i, double* v, size_t* c) {
+      return ssp_select(x.ctx(), x.data(), x.local_size(), x.offset(), n, max, ignore_sign, i, v, c);
+    });
+  }
+};
+
+}  // namespace molpro::linalg::hbm

@@ -1,0 +1,138 @@
+// HBM-resident vectors: the R / Q container type of the MI355X handlers, on libsubspace_hip.so alone.
+//
+// This header depends on nothing but the C ABI (include/subspace_hip.h) and the standard library,
+// so it can be included beside either ArrayHandler base: the restated one
+// (itsolv_hbm/array_handler.h, used by this package's solvers) or the reference's own
+// molpro/linalg/array/ArrayHandler.h (itsolv_hbm/reference_handler.h, the drop-in).
+//
+// hbm::Vec is one rank's contiguous shard [offset, offset + local_size) of a global vector of length
+// size(), distributed as the reference's make_distribution_spread_remainder (reference
+// array/util/Distribution.h:99-109; DistrArraySpan.cpp:35-37).  It owns its HBM block (unlike
+// DistrArraySpan, whose copies alias, reference DistrArraySpan.cpp:47-51), is movable and
+// deep-copyable, and value_type is double (the reference's README.md:103 requirements on R and Q).
+#pragma once
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "subspace_hip.h"
+
+namespace molpro::linalg::hbm {
+
+//! The P-space vector type: the reference's sparse map of index -> coefficient.
+using SparseP = std::map<size_t, double>;
+
+// C-ABI status -> the reference's exception types: size mismatch -> SizeError (the handler's
+// util::ArrayHandlerError, reference ArrayHandler.h:25-27), alphas dimension mismatch ->
+// std::out_of_range (reference util/gemm.h:66-71), unsupported operation -> std::logic_error
+// (reference ArrayHandlerDistrSparse.h:26-28), anything else -> std::runtime_error.
+template <class SizeError = std::length_error>
+void check_status(int status, const char* what) {
+  if (status == SSP_OK) return;
+  std::string msg = std::string(what) + ": " + ssp_last_error();
+  switch (status) {
+    case SSP_ERR_SIZE: throw SizeError(msg);
+    case SSP_ERR_RANGE: throw std::out_of_range(msg);
+    case SSP_ERR_UNSUPPORTED: throw std::logic_error(msg);
+    default: throw std::runtime_error(msg);
+  }
+}
+
+// One process's device: the ssp context (HIP stream, HBM arena, optional RCCL communicator).
+class Device {
+ public:
+  explicit Device(int device) { check_status(ssp_ctx_create(device, &m_ctx), "ssp_ctx_create"); }
+  // Wraps a context owned by the caller (borrowed = true: not destroyed here).
+  Device(ssp_ctx* ctx, bool borrowed) : m_ctx(ctx), m_owned(!borrowed) {
+    if (!ctx) throw std::invalid_argument("hbm::Device: null ssp_ctx");
+  }
+  Device(const Device&) = delete;
+  Device& operator=(const Device&) = delete;
+  virtual ~Device() {
+    if (m_owned) ssp_ctx_destroy(m_ctx);
+  }
+  void attach_comm(int nranks, int rank, const char* unique_id) {
+    check_status(ssp_ctx_attach_comm(m_ctx, nranks, rank, unique_id), "ssp_ctx_attach_comm");
+  }
+  ssp_ctx* ctx() const { return m_ctx; }
+  int rank() const { return ssp_ctx_rank(m_ctx); }
+  int nranks() const { return ssp_ctx_nranks(m_ctx); }
+  // Shard of a global length n owned by this rank.
+  std::pair<size_t, size_t> shard(size_t n) const {
+    size_t offset = 0, length = 0;
+    check_status(ssp_shard_range(n, nranks(), rank(), &offset, &length), "ssp_shard_range");
+    return {offset, length};
+  }
+
+ private:
+  ssp_ctx* m_ctx = nullptr;
+  bool m_owned = true;
+};
+
+class Vec {
+ public:
+  using value_type = double;
+
+  Vec() = default;
+  Vec(std::shared_ptr<Device> dev, size_t n_global) : m_dev(std::move(dev)), m_size(n_global) {
+    auto [off, n] = m_dev->shard(n_global);
+    m_offset = off;
+    m_local = n;
+    check_status(ssp_alloc(m_dev->ctx(), m_local, &m_data), "ssp_alloc");
+  }
+  Vec(const Vec& o) : Vec(o.m_dev, o.m_size) {
+    check_status(ssp_copy(ctx(), m_data, o.m_data, m_local), "ssp_copy");
+  }
+  Vec(Vec&& o) noexcept { swap(o); }
+  Vec& operator=(const Vec& o) {
+    if (this != &o) {
+      Vec t(o);
+      swap(t);
+    }
+    return *this;
+  }
+  Vec& operator=(Vec&& o) noexcept {
+    Vec t(std::move(o));
+    swap(t);
+    return *this;
+  }
+  ~Vec() {
+    if (m_data) ssp_free(ctx(), m_data);
+  }
+  void swap(Vec& o) noexcept {
+    std::swap(m_dev, o.m_dev);
+    std::swap(m_data, o.m_data);
+    std::swap(m_size, o.m_size);
+    std::swap(m_local, o.m_local);
+    std::swap(m_offset, o.m_offset);
+  }
+
+  size_t size() const { return m_size; }
+  size_t local_size() const { return m_local; }
+  size_t offset() const { return m_offset; }
+  double* data() { return m_data; }
+  const double* data() const { return m_data; }
+  ssp_ctx* ctx() const { return m_dev->ctx(); }
+  const std::shared_ptr<Device>& device() const { return m_dev; }
+  bool compatible(const Vec& o) const { return m_size == o.m_size && m_offset == o.m_offset && m_local == o.m_local; }
+
+  std::vector<double> local_values() const {
+    std::vector<double> v(m_local);
+    check_status(ssp_download(ctx(), v.data(), m_data, m_local), "ssp_download");
+    return v;
+  }
+  void set_local_values(const std::vector<double>& v) {
+    if (v.size() != m_local) throw std::invalid_argument("Vec::set_local_values: wrong length");
+    check_status(ssp_upload(ctx(), m_data, v.data(), m_local), "ssp_upload");
+  }
+
+ private:
+  std::shared_ptr<Device> m_dev;
+  double* m_data = nullptr;
+  size_t m_size = 0, m_local = 0, m_offset = 0;
+};
+
+}  // namespace molpro::linalg::hbm

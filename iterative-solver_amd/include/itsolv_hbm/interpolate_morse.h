@@ -24,6 +24,9 @@ class MorseHandler : public array::ArrayHandler<MorseParameters, MorseParameters
   using V = MorseParameters;
 
  public:
+  using typename array::ArrayHandler<MorseParameters, MorseParameters>::ProxyHandle;
+  using array::ArrayHandler<MorseParameters, MorseParameters>::lazy_handle;
+  ProxyHandle lazy_handle() override { return this->lazy_handle(*this); }
   V copy(const V& s) override { return s; }
   void copy(V& x, const V& y) override { x = y; }
   void scal(double a, V& x) override {
@@ -64,6 +67,9 @@ class MorseNoP : public array::ArrayHandler<A, B> {
   [[noreturn]] static void no() { throw std::logic_error("Morse fit: no P space"); }
 
  public:
+  using typename array::ArrayHandler<A, B>::ProxyHandle;
+  using array::ArrayHandler<A, B>::lazy_handle;
+  ProxyHandle lazy_handle() override { return this->lazy_handle(*this); }
   A copy(const B&) override { no(); }
   void copy(A&, const B&) override { no(); }
   void scal(T, A&) override { no(); }

@@ -42,6 +42,23 @@ struct SyntheticSpec {
   double diagonal(size_t g) const { return 1.0 + double(g) + rank * rho; }
 };
 
+// One row of itsolv_result's per-iteration trace (called from solve()'s iteration_hook).
+template <class S>
+void record_trace(const S& solver, const std::vector<double>& eigenvalues, itsolv_result& out) {
+  const int it = out.n_eig_trace;
+  if (it >= ITSOLV_TRACE_ITER) return;
+  const auto& err = solver.errors();
+  out.trace_roots = int(std::min<size_t>(std::max(err.size(), eigenvalues.size()), ITSOLV_TRACE_ROOTS));
+  for (int r = 0; r < out.trace_roots; ++r) {
+    out.trace_eigenvalues[it * ITSOLV_TRACE_ROOTS + r] = size_t(r) < eigenvalues.size() ? eigenvalues[r] : 0.0;
+    out.trace_errors[it * ITSOLV_TRACE_ROOTS + r] = size_t(r) < err.size() ? err[r] : 0.0;
+  }
+  out.trace_nq[it] = int(solver.dimensions().nQ);
+  out.trace_nwork[it] = int(solver.working_set().size());
+  out.eig_trace[it] = eigenvalues.empty() ? 0.0 : eigenvalues.front();
+  out.n_eig_trace = it + 1;
+}
+
 inline void apply_options(const itsolv_options& o, Options& base) {
   base.n_roots = o.nroots;
   base.convergence_threshold = o.convergence_threshold;
@@ -73,10 +90,7 @@ void run_davidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Proble
     actions.push_back(make_vec());
   }
   out.n_eig_trace = 0;
-  solver.iteration_hook = [&] {
-    const auto ev = solver.eigenvalues();
-    if (!ev.empty() && out.n_eig_trace < 256) out.eig_trace[out.n_eig_trace++] = ev.front();
-  };
+  solver.iteration_hook = [&] { record_trace(solver, solver.eigenvalues(), out); };
   const auto t0 = std::chrono::steady_clock::now();
   out.converged = solver.solve(params, actions, problem, o.generate_initial_guess != 0);
   out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -126,6 +140,8 @@ void run_linear_equations(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, cons
     params.push_back(make_vec());
     actions.push_back(make_vec());
   }
+  out.n_eig_trace = 0;
+  solver.iteration_hook = [&] { record_trace(solver, std::vector<double>{}, out); };
   const auto t0 = std::chrono::steady_clock::now();
   out.converged = solver.solve(params, actions, problem, o.generate_initial_guess != 0);
   out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -134,7 +150,6 @@ void run_linear_equations(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, cons
   out.r_creations = st.r_creations;
   out.q_creations = st.q_creations;
   out.nroots = int(std::min<size_t>(nwork, ITSOLV_MAX_ROOTS));
-  out.n_eig_trace = 0;
   for (int i = 0; i < out.nroots; ++i) {
     out.eigenvalues[i] = 0;
     out.errors[i] = i < int(solver.errors().size()) ? solver.errors()[i] : 0.0;
@@ -173,6 +188,8 @@ void run_optimize(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Proble
   }
   R x = make_vec(), g = make_vec();
   init(x);
+  out.n_eig_trace = 0;
+  solver->iteration_hook = [&] { record_trace(*solver, std::vector<double>{solver->value()}, out); };
   const auto t0 = std::chrono::steady_clock::now();
   out.converged = solver->solve(x, g, problem);
   out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -183,7 +200,6 @@ void run_optimize(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Proble
   out.nroots = 1;
   out.errors[0] = solver->errors().empty() ? 0.0 : solver->errors().front();
   out.eigenvalues[0] = solver->value();
-  out.n_eig_trace = 0;
   R xs = make_vec(), gs = make_vec();
   solver->solution(xs, gs);
   problem.residual(xs, gs);
@@ -204,6 +220,8 @@ void run_diis(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R,
   solver.set_options(opt);
   R x = make_vec(), g = make_vec();
   init(x);
+  out.n_eig_trace = 0;
+  solver.iteration_hook = [&] { record_trace(solver, std::vector<double>{}, out); };
   const auto t0 = std::chrono::steady_clock::now();
   out.converged = solver.solve(x, g, problem);
   out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -214,7 +232,6 @@ void run_diis(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R,
   out.nroots = 1;
   out.errors[0] = solver.errors().empty() ? 0.0 : solver.errors().front();
   out.eigenvalues[0] = 0;
-  out.n_eig_trace = 0;
   R xs = make_vec(), gs = make_vec();
   solver.solution(xs, gs);
   problem.residual(xs, gs);

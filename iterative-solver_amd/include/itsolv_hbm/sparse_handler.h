@@ -19,6 +19,9 @@ using SparseP = std::map<size_t, double>;
 // P x P (sparse x sparse) handler on the host (reference ArrayHandlerSparse.h).
 class ArrayHandlerSparse : public array::ArrayHandler<SparseP, SparseP> {
  public:
+  using typename array::ArrayHandler<SparseP, SparseP>::ProxyHandle;
+  using array::ArrayHandler<SparseP, SparseP>::lazy_handle;
+  ProxyHandle lazy_handle() override { return this->lazy_handle(*this); }
   SparseP copy(const SparseP& s) override {
     m_counter->copy++;
     return s;

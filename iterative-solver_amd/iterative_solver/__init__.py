@@ -69,6 +69,8 @@ def _load():
             "IterativeSolverHbmSetThrow": (I, [I]),
             "IterativeSolverHbmStatistics": (I, [PI, PI, PI]),
             "IterativeSolverHbmLastError": (C.c_char_p, []),
+            "IterativeSolverHbmInstanceId": (C.c_uint64, []),
+            "IterativeSolverHbmFinalizeInstance": (I, [C.c_uint64]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -117,11 +119,27 @@ class IterativeSolver:
         self.n = n
         self.nroot = nroot
         self.value = None
+        self._id = 0
+
+    def _register(self):
+        """Called after the C layer pushed this object's instance: remember its id."""
+        self._id = int(_load().IterativeSolverHbmInstanceId())
+        self._active = self._id != 0
+
+    def _check_top(self):
+        # The C layer drives its top instance only (reference IterativeSolverCMPI.cpp); a call
+        # through an older object while a newer one is alive would silently drive the newer one.
+        if not getattr(self, "_active", False):
+            raise RuntimeError("this solver has been finalized")
+        if int(_load().IterativeSolverHbmInstanceId()) != self._id:
+            raise RuntimeError("another IterativeSolver instance is active (created later and not finalized)")
 
     def __del__(self):
+        # Removes this object's own instance wherever it is in the C layer's stack, never another's.
         try:
             if getattr(self, "_active", False):
-                _load().IterativeSolverFinalize()
+                _load().IterativeSolverHbmFinalizeInstance(self._id)
+                self._active = False
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
 
@@ -132,24 +150,28 @@ class IterativeSolver:
 
     def finalize(self):
         if getattr(self, "_active", False):
-            _call("IterativeSolverFinalize")
+            _load().IterativeSolverHbmFinalizeInstance(self._id)
             self._active = False
 
     def solution(self, roots, parameters, residual, sync=True):
+        self._check_top()
         roots_ = (C.c_int * max(1, len(roots)))(*roots)
         _call("IterativeSolverSolution", len(roots), roots_, _d(_flat(parameters)), _d(_flat(residual)), int(sync))
         return self.value
 
     def add_vector(self, parameters, action, sync=True):
+        self._check_top()
         nbuffer = parameters.shape[0] if parameters.ndim > 1 else 1
         return int(_call("IterativeSolverAddVector", nbuffer, _d(_flat(parameters)), _d(_flat(action)), int(sync)))
 
     def add_value(self, value, parameters, action, sync=True):
+        self._check_top()
         r = int(_call("IterativeSolverAddValue", value, _d(_flat(parameters)), _d(_flat(action)), int(sync)))
         self.value = value
         return r
 
     def end_iteration(self, parameters, residual, sync=True):
+        self._check_top()
         nbuffer = parameters.shape[0] if parameters.ndim > 1 else 1
         return int(_call("IterativeSolverEndIteration", nbuffer, _d(_flat(parameters)), _d(_flat(residual)),
                          int(sync)))
@@ -158,6 +180,7 @@ class IterativeSolver:
         """P space from sparse vectors [{index: coefficient}], the P-P action matrix `pp` (nP x nP)
         and a callback apply_p(p_coefficients (nvec x nP), actions_local, ranges) that adds the P
         contributions to this rank's range of the action rows (reference IterativeSolverAddP)."""
+        self._check_top()
         offsets = np.zeros(len(pvectors) + 1, dtype=np.uint64)
         idx, coef = [], []
         for k, p in enumerate(pvectors):
@@ -184,25 +207,30 @@ class IterativeSolver:
 
     @property
     def end_iteration_needed(self):
+        self._check_top()
         return _call("IterativeSolverEndIterationNeeded") != 0
 
     @property
     def errors(self):
+        self._check_top()
         e = np.zeros(self.nroot)
         _call("IterativeSolverErrors", _d(e))
         return e
 
     def working_set_eigenvalues(self, nwork):
+        self._check_top()
         ev = np.zeros(max(1, self.nroot))
         _call("IterativeSolverWorkingSetEigenvalues", _d(ev))
         return ev[:nwork]
 
     def statistics(self):
+        self._check_top()
         return statistics()
 
     def solve(self, parameters, actions, problem, generate_initial_guess=False, max_iter=None):
         """One-call driver over the reverse-communication API, the loop of the reference's
         IterativeSolver.solve (iterative_solver_extension.pyx:78-165)."""
+        self._check_top()
         if parameters.ndim < 2 or actions.ndim < 2:
             return self.solve(parameters.reshape([self.nroot, self.n]), actions.reshape([self.nroot, self.n]), problem,
                               generate_initial_guess, max_iter)
@@ -280,12 +308,13 @@ class LinearEigensystem(IterativeSolver):
         _call("IterativeSolverLinearEigensystemInitialize", n, nroot, C.byref(rb), C.byref(re), thresh, thresh_value,
               1 if hermitian else 0, verbosity, pname.encode(), int(mpicomm or 0), algorithm.encode(),
               options.encode())
-        self._active = True
+        self._register()
         if range is not None:
             range[0], range[1] = rb.value, re.value
 
     @property
     def eigenvalues(self):
+        self._check_top()
         e = np.zeros(self.nroot)
         _call("IterativeSolverEigenvalues", _d(e))
         return e
@@ -297,7 +326,7 @@ class NonLinearEquations(IterativeSolver):
         rb, re = _range_arrays(range)
         _call("IterativeSolverNonLinearEquationsInitialize", n, C.byref(rb), C.byref(re), thresh, verbosity,
               pname.encode(), int(mpicomm or 0), algorithm.encode(), options.encode())
-        self._active = True
+        self._register()
         if range is not None:
             range[0], range[1] = rb.value, re.value
 
@@ -313,7 +342,7 @@ class LinearEquations(IterativeSolver):
         _call("IterativeSolverLinearEquationsInitialize", n, nroot, C.byref(rb), C.byref(re), _d(r), aughes, thresh,
               thresh_value, 1 if hermitian else 0, verbosity, pname.encode(), int(mpicomm or 0), algorithm.encode(),
               options.encode())
-        self._active = True
+        self._register()
 
 
 class Optimize(IterativeSolver):
@@ -323,4 +352,4 @@ class Optimize(IterativeSolver):
         rb, re = _range_arrays(range)
         _call("IterativeSolverOptimizeInitialize", n, C.byref(rb), C.byref(re), thresh, thresh_value, verbosity,
               1 if minimize else 0, pname.encode(), int(mpicomm or 0), algorithm.encode(), options.encode())
-        self._active = True
+        self._register()

@@ -13,6 +13,7 @@ import subspace_hip as sh
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libitsolv_hbm.so")
 MAX_ROOTS = 64
+TRACE_ITER, TRACE_ROOTS = 256, 8
 
 EXPORTS = [
     "itsolv_last_error", "itsolv_default_options", "itsolv_davidson_synthetic", "itsolv_davidson_dense",
@@ -52,6 +53,11 @@ class Result(C.Structure):
         ("seconds", C.c_double),
         ("n_eig_trace", C.c_int),
         ("eig_trace", C.c_double * 256),
+        ("trace_roots", C.c_int),
+        ("trace_nq", C.c_int * TRACE_ITER),
+        ("trace_nwork", C.c_int * TRACE_ITER),
+        ("trace_eigenvalues", C.c_double * (TRACE_ITER * TRACE_ROOTS)),
+        ("trace_errors", C.c_double * (TRACE_ITER * TRACE_ROOTS)),
     ]
 
     def as_dict(self):
@@ -66,7 +72,16 @@ class Result(C.Structure):
             "residual_norms": np.array(self.residual_norms[:k]),
             "seconds": self.seconds,
             "eig_trace": np.array(self.eig_trace[: self.n_eig_trace]),
+            "trace": self.trace(),
         }
+
+    def trace(self):
+        """Per-iteration parity observables: one entry per solve() iteration."""
+        it, nr = self.n_eig_trace, self.trace_roots
+        ev = np.array(self.trace_eigenvalues[: it * TRACE_ROOTS]).reshape(it, TRACE_ROOTS)[:, :nr]
+        er = np.array(self.trace_errors[: it * TRACE_ROOTS]).reshape(it, TRACE_ROOTS)[:, :nr]
+        return {"eigenvalues": ev, "errors": er, "nq": np.array(self.trace_nq[:it]),
+                "nwork": np.array(self.trace_nwork[:it])}
 
 
 def make_options(**kw) -> Options:
@@ -121,12 +136,14 @@ def _call(fn, args, nout):
     return res.as_dict(), out
 
 
-def davidson_synthetic(ctx: sh.Context, n: int, rho: float, rank: int, seed: int, n_local: int | None = None, **opts):
+def davidson_synthetic(ctx: sh.Context, n: int, rho: float, rank: int, seed: int, n_local: int | None = None,
+                       solutions: bool = True, **opts):
     o = make_options(**opts)
     nl = n if n_local is None else n_local
     r, sol = _call(load_library().itsolv_davidson_synthetic, (ctx.handle, n, rho, rank, seed, C.byref(o)),
-                   o.nroots * nl)
-    r["solutions"] = sol[: o.nroots * nl].reshape(o.nroots, nl)
+                   o.nroots * nl if solutions else 0)
+    if solutions:
+        r["solutions"] = sol[: o.nroots * nl].reshape(o.nroots, nl)
     return r
 
 
@@ -140,11 +157,14 @@ def davidson_dense(ctx: sh.Context, h: np.ndarray, **opts):
     return r
 
 
-def diis_synthetic(ctx: sh.Context, n: int, rho: float, rank: int, seed: int, n_local: int | None = None, **opts):
+def diis_synthetic(ctx: sh.Context, n: int, rho: float, rank: int, seed: int, n_local: int | None = None,
+                   solutions: bool = True, **opts):
     o = make_options(**opts)
     nl = n if n_local is None else n_local
-    r, x = _call(load_library().itsolv_diis_synthetic, (ctx.handle, n, rho, rank, seed, C.byref(o)), nl)
-    r["x"] = x[:nl]
+    r, x = _call(load_library().itsolv_diis_synthetic, (ctx.handle, n, rho, rank, seed, C.byref(o)),
+                 nl if solutions else 0)
+    if solutions:
+        r["x"] = x[:nl]
     return r
 
 

@@ -41,6 +41,9 @@ void ok(int s, const char* what) {
 // reference ArrayHandlerIterable<std::vector<double>> (ArrayHandlerIterable.h:34-128)
 class IterableHandler : public ArrayHandler<V, V> {
  public:
+  using typename ArrayHandler<V, V>::ProxyHandle;
+  using ArrayHandler<V, V>::lazy_handle;
+  ProxyHandle lazy_handle() override { return this->lazy_handle(*this); }
   V copy(const V& s) override { return V(s); }
   void copy(V& x, const V& y) override { ok(or_copy(x.data(), x.size(), y.data(), y.size()), "copy"); }
   void scal(double a, V& x) override { or_scal(a, x.data(), x.size()); }
@@ -88,6 +91,9 @@ class IterableHandler : public ArrayHandler<V, V> {
 // reference ArrayHandlerIterableSparse<std::vector<double>, std::map<size_t,double>> (:151-217)
 class IterableSparseHandler : public ArrayHandler<V, SP> {
  public:
+  using typename ArrayHandler<V, SP>::ProxyHandle;
+  using ArrayHandler<V, SP>::lazy_handle;
+  ProxyHandle lazy_handle() override { return this->lazy_handle(*this); }
   V copy(const SP& s) override {
     V r;
     copy(r, s);

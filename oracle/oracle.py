@@ -356,22 +356,36 @@ class RcSolver:
                 "eigenvalues": ev[:self.nroot]}
 
 
+def set_sum_order(order):
+    """Summation order of the CPU path's dot / gemm_inner (oracle_ops.c or_set_sum_order): 0 = the
+    reference's sequential loop (default), 1 = 8 interleaved partial sums (a vectorised build of the
+    same loop).  Used only to measure the reference algorithm's own rounding sensitivity."""
+    L = itsolv_lib()
+    L.or_set_sum_order.argtypes = [C.c_int]
+    L.or_set_sum_order.restype = C.c_int
+    if L.or_set_sum_order(int(order)) != 0:
+        raise ValueError(order)
+
+
 def _solve(fn, args, nout):
+    """nout == 0: no solution copy-back (null pointer)."""
     from itsolv_hbm import Result
 
     res = Result()
     out = np.zeros(max(1, nout))
-    if fn(*args, C.byref(res), out.ctypes.data_as(PD)) != 0:
+    if fn(*args, C.byref(res), out.ctypes.data_as(PD) if nout > 0 else None) != 0:
         raise OracleError(itsolv_lib().oracle_itsolv_last_error().decode())
     return res.as_dict(), out
 
 
-def davidson_synthetic(n, rho, rank, seed, **opts):
+def davidson_synthetic(n, rho, rank, seed, solutions=True, **opts):
     from itsolv_hbm import make_options
 
     o = make_options(**opts)
-    r, sol = _solve(itsolv_lib().oracle_davidson_synthetic, (n, rho, rank, seed, C.byref(o)), o.nroots * n)
-    r["solutions"] = sol[: o.nroots * n].reshape(o.nroots, n)
+    r, sol = _solve(itsolv_lib().oracle_davidson_synthetic, (n, rho, rank, seed, C.byref(o)),
+                    o.nroots * n if solutions else 0)
+    if solutions:
+        r["solutions"] = sol[: o.nroots * n].reshape(o.nroots, n)
     return r
 
 
@@ -386,12 +400,13 @@ def davidson_dense(h, **opts):
     return r
 
 
-def diis_synthetic(n, rho, rank, seed, **opts):
+def diis_synthetic(n, rho, rank, seed, solutions=True, **opts):
     from itsolv_hbm import make_options
 
     o = make_options(**opts)
-    r, x = _solve(itsolv_lib().oracle_diis_synthetic, (n, rho, rank, seed, C.byref(o)), n)
-    r["x"] = x[:n]
+    r, x = _solve(itsolv_lib().oracle_diis_synthetic, (n, rho, rank, seed, C.byref(o)), n if solutions else 0)
+    if solutions:
+        r["x"] = x[:n]
     return r
 
 

@@ -28,8 +28,31 @@ int or_axpy(double alpha, const double* x, size_t nx, double* y, size_t ny) {
   return 0;
 }
 
+/* Summation order of dot / gemm_inner (a checker knob, never the product): 0 = the reference's
+ * sequential std::inner_product (ArrayHandlerIterable.h:76-82), the default and the only order the
+ * parity fixtures are generated with; 1 = 8 interleaved partial sums folded pairwise, the order a
+ * vectorising build of the same loop (-ffast-math / AVX-512) produces.  Order 1 exists to measure
+ * how sensitive the REFERENCE algorithm itself is to a valid change of summation order
+ * (tests/golden/make_traces.py: the "reordered" runs). */
+static int g_sum_order = 0;
+
+int or_set_sum_order(int order) {
+  if (order < 0 || order > 1) return 1;
+  g_sum_order = order;
+  return 0;
+}
+
 int or_dot(const double* x, size_t nx, const double* y, size_t ny, double* out) {
   if (nx > ny) return 1;
+  if (g_sum_order == 1) {
+    double p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    size_t i = 0;
+    for (; i + 8 <= nx; i += 8)
+      for (int l = 0; l < 8; ++l) p[l] = p[l] + x[i + l] * y[i + l];
+    for (int l = 0; i < nx; ++i, ++l) p[l] = p[l] + x[i] * y[i];
+    *out = ((p[0] + p[4]) + (p[2] + p[6])) + ((p[1] + p[5]) + (p[3] + p[7]));
+    return 0;
+  }
   double s = 0;
   for (size_t i = 0; i < nx; ++i) s = s + x[i] * y[i];
   *out = s;

@@ -31,6 +31,7 @@ int or_copy(double* x, size_t nx, const double* y, size_t ny);
 /* ArrayHandlerIterable.h:65-74  (error if x.size() < y.size()) */
 int or_axpy(double alpha, const double* x, size_t nx, double* y, size_t ny);
 /* ArrayHandlerIterable.h:76-82  (error if x.size() > y.size()), std::inner_product from 0 */
+int or_set_sum_order(int order); /* 0 = reference sequential (default), 1 = 8 interleaved sums */
 int or_dot(const double* x, size_t nx, const double* y, size_t ny, double* out);
 /* util/gemm.h:267-279 gemm_inner_default: out[i*k+j] = dot(xx[i], yy[j]) */
 int or_gemm_inner(const double* const* xx, int m, const double* const* yy, int k, size_t n, double* out);

@@ -1,0 +1,408 @@
+// The reference's array-handler tests, restated over the HBM handlers (built and run by
+// tests/test_handler_cpp.py; no gtest here, each case prints "PASS <name>" or "FAIL <name>: why").
+//
+// One source, two bases:
+//   default                -> itsolv_hbm/hbm_handlers.h: the restated ArrayHandler base the package's
+//                             solvers use (array_handler.h);
+//   -DWITH_REFERENCE_BASE  -> itsolv_hbm/reference_handler.h over the reference's own
+//                             molpro/linalg/array/ArrayHandler.h (-I<reference>/src): the drop-in.
+// and two device libraries: libsubspace_hip.so on an MI355X (tests -m gpu), or the host-memory
+// emulation of its ABI (oracle/build/libssp_emul.so, CPU tests).
+//
+// Cases (reference file:line):
+//   op_register_*, remove_duplicates_small      test/array/testArrayHandler.cpp:41-125
+//   lazy_dot, select_max_dot, lazy_axpy,
+//   lazy_axpy_lazy_off                          test/array/testArrayHandlerIterable.cpp:25-125
+//   lazy_* at n = 100003 against eager ops, invalidation on handler destruction, the one-kind rule,
+//   counters, error types, the sparse R x P handler (ArrayHandlerIterableSparse.h:35-58,
+//   testArrayHandlerIterableSparse.cpp:22-29).
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <list>
+#include <map>
+#include <memory>
+#include <numeric>
+#include <random>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#ifdef WITH_REFERENCE_BASE
+#include "itsolv_hbm/reference_handler.h"
+#else
+#include "itsolv_hbm/hbm_handlers.h"
+#endif
+
+namespace array = molpro::linalg::array;
+using molpro::linalg::hbm::ArrayHandlerHbm;
+using molpro::linalg::hbm::ArrayHandlerHbmSparse;
+using molpro::linalg::hbm::Device;
+using molpro::linalg::hbm::SparseP;
+using molpro::linalg::hbm::Vec;
+using molpro::linalg::itsolv::CVecRef;
+using molpro::linalg::itsolv::VecRef;
+using Mat = molpro::linalg::itsolv::subspace::Matrix<double>;
+
+namespace {
+
+int g_failures = 0;
+std::string g_filter;
+
+struct Failure {
+  std::string why;
+};
+void expect(bool ok, const std::string& why) {
+  if (!ok) throw Failure{why};
+}
+
+void run(const char* name, const std::function<void()>& f) {
+  if (!g_filter.empty() && g_filter != name) return;
+  try {
+    f();
+    std::printf("PASS %s\n", name);
+  } catch (const Failure& e) {
+    ++g_failures;
+    std::printf("FAIL %s: %s\n", name, e.why.c_str());
+  } catch (const std::exception& e) {
+    ++g_failures;
+    std::printf("FAIL %s: exception %s\n", name, e.what());
+  }
+  std::fflush(stdout);
+}
+
+std::shared_ptr<Device> g_dev;
+
+Vec make(const std::vector<double>& v) {
+  Vec x(g_dev, v.size());
+  x.set_local_values(v);
+  return x;
+}
+
+std::vector<double> random_values(size_t n, unsigned seed) {
+  std::mt19937_64 g(seed);
+  std::uniform_real_distribution<double> u(-1, 1);
+  std::vector<double> v(n);
+  for (auto& x : v) x = u(g);
+  return v;
+}
+
+template <class E, class F>
+bool throws(F f) {
+  try {
+    f();
+  } catch (const E&) {
+    return true;
+  } catch (...) {
+    return false;
+  }
+  return false;
+}
+
+// ---- test/array/testArrayHandler.cpp ----------------------------------------------------------
+void op_register_cases() {
+  using array::util::OperationRegister;
+  constexpr int size = 5;
+  std::vector<int> x(size);
+  std::vector<double> y(size, 0.0);
+  std::iota(x.begin(), x.end(), 1);
+  run("op_register_no_priority", [&] {
+    OperationRegister<int, double> reg;
+    std::list<std::tuple<int, double>> want;
+    for (int i = 0; i < size; ++i)
+      for (int j = 0; j < size; ++j) {
+        reg.push(x[i], y[i]);
+        want.emplace_back(x[i], y[i]);
+      }
+    expect(reg.m_register == want, "register order");
+  });
+  run("op_register_prioritize_first_element", [&] {
+    OperationRegister<int, double> reg;
+    std::list<std::tuple<int, double>> want;
+    for (int i = 0; i < size; ++i)
+      for (int j = 0; j < size; ++j) {
+        reg.push<0, std::equal_to<int>>(x[i], y[j], {});
+        want.emplace_back(x[i], y[i]);
+      }
+    expect(reg.m_register == want, "grouped by first element");
+  });
+  run("op_register_prioritize_second_element", [&] {
+    // distinct second elements, pushed interleaved, must come out grouped by them in arrival order
+    std::vector<double> z{0.5, 1.5, 2.5, 3.5, 4.5};
+    OperationRegister<int, double> reg;
+    for (int i = 0; i < size; ++i)
+      for (int j = 0; j < size; ++j) reg.push<1, std::equal_to<double>>(x[j], z[i], {});
+    std::list<std::tuple<int, double>> want;
+    for (int i = 0; i < size; ++i)
+      for (int j = 0; j < size; ++j) want.emplace_back(x[j], z[i]);
+    expect(reg.m_register == want, "grouped by second element");
+    OperationRegister<int, double> reg2;  // interleaved arrival: (1,a) (2,b) (3,a) -> (1,a) (3,a) (2,b)
+    reg2.push<1, std::equal_to<double>>(1, 0.5, {});
+    reg2.push<1, std::equal_to<double>>(2, 1.5, {});
+    reg2.push<1, std::equal_to<double>>(3, 0.5, {});
+    std::list<std::tuple<int, double>> want2{{1, 0.5}, {3, 0.5}, {2, 1.5}};
+    expect(reg2.m_register == want2, "group insertion");
+  });
+  run("remove_duplicates_small", [&] {
+    using array::util::RefEqual;
+    std::vector<double> xs{0, 1};
+    std::vector<int> ys{0, 1};
+    std::vector<size_t> ss{0, 1, 2, 3, 4};
+    using RX = std::reference_wrapper<double>;
+    using RY = std::reference_wrapper<int>;
+    using RS = std::reference_wrapper<size_t>;
+    std::list<std::tuple<RX, RY, RS>> reg{{xs[0], ys[0], ss[0]}, {xs[0], ys[1], ss[1]}, {xs[1], ys[1], ss[2]},
+                                          {xs[0], ys[0], ss[3]}, {xs[1], ys[0], ss[4]}, {xs[1], ys[0], ss[4]}};
+    auto res = array::util::remove_duplicates<RX, RY, RS, RefEqual<double>, RefEqual<int>, RefEqual<size_t>>(reg, {}, {},
+                                                                                                            {});
+    std::vector<std::tuple<size_t, size_t, size_t>> want{{0, 0, 0}, {0, 1, 1}, {1, 1, 2}, {0, 0, 3}, {1, 0, 4}, {1, 0, 4}};
+    expect(std::get<0>(res) == want, "index triples");
+    auto& ux = std::get<1>(res);
+    auto& uy = std::get<2>(res);
+    auto& us = std::get<3>(res);
+    expect(ux.size() == 2 && &ux[0].get() == &xs[0] && &ux[1].get() == &xs[1], "unique x");
+    expect(uy.size() == 2 && &uy[0].get() == &ys[0] && &uy[1].get() == &ys[1], "unique y");
+    expect(us.size() == 5, "unique s");
+    for (size_t i = 0; i < 5; ++i) expect(&us[i].get() == &ss[i], "unique s order");
+  });
+}
+
+// ---- test/array/testArrayHandlerIterable.cpp over the HBM handler ------------------------------
+void iterable_cases() {
+  run("constructor", [] {
+    ArrayHandlerHbm h;
+    array::ArrayHandler<Vec, Vec>& base = h;
+    (void)base;
+  });
+  run("lazy_dot", [] {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    constexpr int N = 3, dim = 5;
+    std::vector<Vec> xx, yy;
+    for (int i = 0; i < N; ++i) {
+      std::vector<double> a(dim), b(dim);
+      std::iota(a.begin(), a.end(), double(i));
+      std::iota(b.begin(), b.end(), 10.0 * i);
+      xx.push_back(make(a));
+      yy.push_back(make(b));
+    }
+    std::vector<double> result(N * N, 0.0), ref(N * N);
+    {
+      auto h = hb.lazy_handle();
+      for (int i = 0, ij = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j, ++ij) {
+          ref[ij] = hb.dot(xx[i], yy[j]);
+          h.dot(xx[i], yy[j], result[ij]);
+        }
+      expect(!h.invalid(), "handle valid");
+      for (double r : result) expect(r == 0, "evaluated before the handle's scope ended");
+    }
+    expect(result == ref, "lazy dot != eager dot");
+  });
+  run("select_max_dot", [] {
+    ArrayHandlerHbm handler;
+    auto x = make({1, -2, 1, 0, 3, 0, -4, 1});
+    auto y = make({1, 1, 1, 1, 1, 1, 1, 1});
+    std::map<size_t, double> want{{6, 4}, {4, 3}, {1, 2}};
+    expect(handler.select_max_dot(want.size(), x, y) == want, "selection");
+  });
+  auto lazy_axpy = [](bool off) {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    constexpr int N = 3, dim = 5;
+    const double alpha = 3, xval = 2, yval = 5;
+    std::vector<Vec> xx, yy;
+    for (int i = 0; i < N; ++i) {
+      xx.push_back(make(std::vector<double>(dim, xval)));
+      yy.push_back(make(std::vector<double>(dim, yval)));
+    }
+    {
+      auto h = hb.lazy_handle();
+      expect(!h.is_off(), "lazy evaluation on by default");
+      if (off) h.off();
+      for (int i = 0; i < N; ++i) h.axpy(alpha, xx[i], yy[i]);
+      expect(!h.invalid(), "handle valid");
+      expect(h.is_off() == off, "is_off");
+      for (auto& y : yy)
+        for (double v : y.local_values()) expect(v == (off ? alpha * xval + yval : yval), "state inside the scope");
+    }
+    for (auto& y : yy)
+      for (double v : y.local_values()) expect(v == alpha * xval + yval, "axpy result");
+  };
+  run("lazy_axpy", [&] { lazy_axpy(false); });
+  run("lazy_axpy_lazy_off", [&] { lazy_axpy(true); });
+}
+
+// ---- beyond the reference tests: the batched evaluation paths at size -------------------------
+void batched_cases() {
+  const size_t n = 100003;
+  run("lazy_dot_batched_n100003", [&] {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    std::vector<std::vector<double>> hx, hy;
+    std::vector<Vec> xx, yy;
+    for (int i = 0; i < 4; ++i) {
+      hx.push_back(random_values(n, 10 + i));
+      xx.push_back(make(hx.back()));
+    }
+    for (int j = 0; j < 6; ++j) {
+      hy.push_back(random_values(n, 100 + j));
+      yy.push_back(make(hy.back()));
+    }
+    // a sparse pattern of (x, y) pairs, one output registered twice (the later one wins)
+    std::vector<std::pair<int, int>> pairs{{0, 0}, {0, 3}, {1, 5}, {2, 2}, {3, 0}, {3, 4}, {1, 1}};
+    std::vector<double> out(pairs.size() + 1, 0.0);
+    {
+      auto h = hb.lazy_handle();
+      for (size_t p = 0; p < pairs.size(); ++p) h.dot(xx[pairs[p].first], yy[pairs[p].second], out[p]);
+      h.dot(xx[2], yy[5], out.back());
+      h.dot(xx[0], yy[1], out.back());
+    }
+    auto bound = [&](const std::vector<double>& a, const std::vector<double>& b) {
+      double s = 0;
+      for (size_t i = 0; i < n; ++i) s += std::abs(a[i] * b[i]);
+      return 64 * 2.220446049250313e-16 * s;
+    };
+    for (size_t p = 0; p < pairs.size(); ++p) {
+      const double eager = hb.dot(xx[pairs[p].first], yy[pairs[p].second]);
+      expect(std::abs(out[p] - eager) <= bound(hx[pairs[p].first], hy[pairs[p].second]), "lazy dot value");
+    }
+    expect(std::abs(out.back() - hb.dot(xx[0], yy[1])) <= bound(hx[0], hy[1]), "last registration wins");
+  });
+  auto lazy_axpy_vs_eager = [&](bool in_order) {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    std::vector<Vec> xx, ya, yb;
+    for (int i = 0; i < 3; ++i) xx.push_back(make(random_values(n, 20 + i)));
+    for (int j = 0; j < 2; ++j) {
+      ya.push_back(make(random_values(n, 200 + j)));
+      yb.push_back(make(random_values(n, 200 + j)));
+    }
+    const double c[3][2] = {{0.25, -1.5}, {3.0, 0.125}, {-0.75, 2.0}};
+    std::vector<std::pair<int, int>> order;
+    if (in_order) {  // sources in first-appearance order for every destination: one gemm_outer
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 2; ++j) order.emplace_back(i, j);
+    } else {  // destination 0 receives x2 before x0: evaluated as the axpy sequence
+      order = {{0, 1}, {2, 0}, {0, 0}, {1, 1}, {1, 0}, {2, 1}};
+    }
+    {
+      auto h = hb.lazy_handle();
+      for (auto [i, j] : order) h.axpy(c[i][j], xx[i], ya[j]);
+    }
+    for (auto [i, j] : order) hb.axpy(c[i][j], xx[i], yb[j]);
+    for (int j = 0; j < 2; ++j) expect(ya[j].local_values() == yb[j].local_values(), "lazy axpy != axpy sequence");
+  };
+  run("lazy_axpy_batched_bit_exact", [&] { lazy_axpy_vs_eager(true); });
+  run("lazy_axpy_unordered_bit_exact", [&] { lazy_axpy_vs_eager(false); });
+  run("lazy_one_kind_at_a_time", [] {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    auto x = make({1, 2, 3});
+    auto y = make({4, 5, 6});
+    double out = 0;
+    auto h = hb.lazy_handle();
+    h.dot(x, y, out);
+    expect(throws<array::util::ArrayHandlerError>([&] { h.axpy(1.0, x, y); }), "axpy after dot must throw");
+    h.eval();
+    expect(out == 32, "dot evaluated");
+    h.axpy(2.0, x, y);  // the register is empty again: any kind
+    h.eval();
+    expect(y.local_values() == std::vector<double>({6, 9, 12}), "axpy after eval");
+  });
+  run("lazy_invalidated_with_handler", [] {
+    auto x = make({1, 2, 3});
+    auto y = make({4, 5, 6});
+    double out = -1;
+    auto handler = std::make_unique<ArrayHandlerHbm>();
+    auto h = static_cast<array::ArrayHandler<Vec, Vec>&>(*handler).lazy_handle();
+    h.dot(x, y, out);
+    handler.reset();
+    expect(h.invalid(), "handle invalid once its handler is gone");
+    h.eval();
+    expect(out == -1, "an invalid handle evaluates nothing");
+  });
+}
+
+void op_cases() {
+  run("ops_through_base_and_counters", [] {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    auto x = make({1, 2, 3, 4});
+    auto y = make({0.5, 0.5, 0.5, 0.5});
+    auto z = hb.copy(x);
+    expect(z.local_values() == x.local_values(), "copy-construct");
+    hb.scal(2, z);
+    hb.axpy(-1, x, z);
+    expect(z.local_values() == x.local_values(), "scal + axpy");
+    hb.fill(0.25, y);
+    expect(hb.dot(x, y) == 2.5, "fill + dot");
+    hb.copy(y, x);
+    expect(y.local_values() == x.local_values(), "copy");
+    Mat m = hb.gemm_inner(CVecRef<Vec>{std::cref(x), std::cref(z)}, CVecRef<Vec>{std::cref(y)});
+    expect(m.rows() == 2 && m.cols() == 1 && m(0, 0) == 30 && m(1, 0) == 30, "gemm_inner");
+    Mat a(std::vector<double>{1, -1}, {2, 1});
+    hb.gemm_outer(a, CVecRef<Vec>{std::cref(x), std::cref(z)}, VecRef<Vec>{std::ref(y)});
+    expect(y.local_values() == x.local_values(), "gemm_outer");
+    const auto& c = hb.counter();
+    expect(c.copy == 2 && c.scal == 1 && c.axpy == 1 && c.dot == 1 && c.gemm_inner == 1 && c.gemm_outer == 1,
+           "counters");
+    const auto s = hb.counter_to_string("R", "Q");
+    expect(s.find("1 gemm_inner operations between the R and Q vectors") != std::string::npos, "counter_to_string");
+    hb.clear_counter();
+    expect(hb.counter().copy == 0, "clear_counter");
+    auto sel = hb.select(2, x, true);
+    expect(sel == std::map<size_t, double>({{2, 3}, {3, 4}}), "select max");
+  });
+  run("error_types", [] {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    auto x = make({1, 2, 3});
+    auto y = make({1, 2, 3, 4});
+    expect(throws<array::util::ArrayHandlerError>([&] { hb.axpy(1, x, y); }), "axpy size mismatch");
+    expect(throws<array::util::ArrayHandlerError>([&] { hb.dot(y, x); }), "dot size mismatch");
+    Mat a({3, 1});
+    expect(throws<std::out_of_range>([&] { hb.gemm_outer(a, CVecRef<Vec>{std::cref(x)}, VecRef<Vec>{std::ref(x)}); }),
+           "gemm_outer alphas rows");
+    expect(throws<array::util::ArrayHandlerError>([&] { hb.select(4, x); }), "select n too large");
+  });
+  run("sparse_handler", [] {
+    ArrayHandlerHbmSparse handler;
+    array::ArrayHandler<Vec, SparseP>& hb = handler;
+    auto x = make({1, -2, 1, 0, 3, 0, -4, 1});
+    SparseP p{{1, 2.0}, {4, -1.0}, {6, 0.5}, {100, 7.0}};  // index 100 is outside x: ignored
+    expect(hb.dot(x, p) == -9.0, "sparse dot");
+    auto y = make(std::vector<double>(8, 1.0));
+    hb.axpy(2.0, p, y);
+    expect(y.local_values() == std::vector<double>({1, 5, 1, 1, -1, 1, 2, 1}), "sparse axpy");
+    SparseP q{{0, 1.0}, {7, 2.0}};
+    hb.copy(y, q);
+    expect(y.local_values() == std::vector<double>({1, 0, 0, 0, 0, 0, 0, 2}), "sparse copy zero-fills");
+    expect(throws<std::logic_error>([&] { hb.copy(q); }), "copy-construct from sparse");
+    Mat m = hb.gemm_inner(CVecRef<Vec>{std::cref(x)}, CVecRef<SparseP>{std::cref(p), std::cref(q)});
+    expect(m(0, 0) == -9.0 && m(0, 1) == 3.0, "sparse gemm_inner");
+    // testArrayHandlerIterableSparse.cpp:22-29 analogue: largest |x_i p_i|
+    auto sel = hb.select_max_dot(2, x, p);
+    expect(sel == std::map<size_t, double>({{1, 4.0}, {4, 3.0}}), "sparse select_max_dot");
+  });
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc > 1) g_filter = argv[1];
+#ifdef WITH_REFERENCE_BASE
+  std::printf("base: reference molpro/linalg/array/ArrayHandler.h\n");
+#else
+  std::printf("base: restated itsolv_hbm/array_handler.h\n");
+#endif
+  g_dev = std::make_shared<Device>(0);
+  op_register_cases();
+  iterable_cases();
+  batched_cases();
+  op_cases();
+  g_dev.reset();
+  std::printf("%s %d failure(s)\n", g_failures ? "FAILED" : "OK", g_failures);
+  return g_failures ? 1 : 0;
+}

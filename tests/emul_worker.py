@@ -63,9 +63,11 @@ def case_api():
     tg.test_optimize("SD")
     # method dispatch of the C API through the SolverFactory restatement (SolverFactory.h:114-185):
     # unknown methods raise "Unimplemented method <m>", the named methods construct
-    from test_python_api_gpu import check_factory_dispatch
+    from test_python_api_gpu import check_factory_dispatch, check_instance_lifecycle, check_minimize_flag_ignored
 
     check_factory_dispatch()
+    check_instance_lifecycle()
+    check_minimize_flag_ignored()
     # RSPT (test_RSPT.cpp:191-196) through the product host code: the reference path's steps
     import rc_problems as rp
 

@@ -1,0 +1,145 @@
+"""Generates tests/golden/traces.json — per-iteration traces of the reference CPU path at the BASELINE
+configurations, the fixtures the GPU solver must reproduce step for step (tests/test_traces_gpu.py).
+
+The CPU path is the oracle: the restated solver stack over the restated ArrayHandlerIterable
+(sequential std::inner_product / std::transform loops and pairwise gemm_*_default,
+oracle/oracle_ops.c, built with -ffp-contract=off), i.e. the reference's CPU algorithm.  Each trace
+records what the reference's driver exposes as parity observables (IterativeSolverTemplate.h:322-408,
+LinearEigensystemDavidson.h:79): the iteration count, R/Q creations, convergence, and after every
+iteration the eigenvalues and errors of every root, the Q-space size and the working-set size.
+Each case is also run with the CPU path's dots summed in another valid order ("reordered": 8
+interleaved partial sums, what a vectorising build of the same loops does): that measures the
+reference algorithm's own sensitivity to rounding, which is what a GPU (whose reductions also sum in
+another order) can be held to -- same steps where the reordered CPU path takes the same steps, and
+per-iteration errors within a few times the reordered CPU path's own deviation.
+
+Problem: H = diag(1 + i) + rho * sum_{l<rank} u_l u_l^T (rank 1 with u = 1 is the
+reference's test_rayleigh_quotient.cpp:37-42 matrix at large n), options of §8d
+(convergence_threshold 1e-8, max_size_qspace 6 * nroots, reset_D 8, max_p 16 for C3).
+
+  C1  Davidson  1 root              N = 1e4   (rank 1 and rank 8)
+  C2  Davidson  4 roots             N = 1e7   (rank 1 and the rank-8 perf problem)
+  C3  Davidson  8 roots + P 16      N = 1e7   (C3's shape at a tenth of its length: the CPU path
+                                               at N = 1e8 needs > 64 GB with 112 vectors)
+  C3  Davidson  8 roots + P 16      N = 1e8   rank 1 (Q stays small: fits this container)
+  C5  DIIS      max_size_qspace 6   N = 1e7   fixed 12-iteration trajectory (the descent to
+                                              the 1e-6 plateau) (threshold 1e-14) and the
+                                              converged run (threshold 1e-8)
+
+Run (about 5 minutes on 8 cores, < 48 GB):  python tests/golden/make_traces.py [--only NAME ...]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ProcessPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(ROOT, "iterative-solver_amd"), os.path.join(ROOT, "oracle")]
+
+RHO, SEED = 0.1, 1
+
+CASES = {
+    "C1_rank1": dict(kind="davidson", n=10_000, rho=RHO, rank=1, seed=SEED, nroots=1, max_p=0),
+    "C1_rank8": dict(kind="davidson", n=10_000, rho=RHO, rank=8, seed=SEED, nroots=1, max_p=0),
+    "C2_rank1": dict(kind="davidson", n=10_000_000, rho=RHO, rank=1, seed=SEED, nroots=4, max_p=0),
+    "C2_rank8": dict(kind="davidson", n=10_000_000, rho=RHO, rank=8, seed=SEED, nroots=4, max_p=0),
+    "C3_n1e7_rank1": dict(kind="davidson", n=10_000_000, rho=RHO, rank=1, seed=SEED, nroots=8, max_p=16),
+    "C3_n1e7_rank8": dict(kind="davidson", n=10_000_000, rho=RHO, rank=8, seed=SEED, nroots=8, max_p=16),
+    "C3_n1e8_rank1": dict(kind="davidson", n=100_000_000, rho=RHO, rank=1, seed=SEED, nroots=8, max_p=16),
+    # C5: the DIIS problem of profiles/r1/solver_ledger_v10.json (rho 0.01, rank 3, seed 3)
+    "C5_n1e7_traj12": dict(kind="diis", n=10_000_000, rho=0.01, rank=3, seed=3, max_iter=12,
+                           convergence_threshold=1e-14),
+    "C5_n1e7": dict(kind="diis", n=10_000_000, rho=0.01, rank=3, seed=3, convergence_threshold=1e-8),
+}
+
+
+def options(c):
+    if c["kind"] == "davidson":
+        return dict(nroots=c["nroots"], max_p=c["max_p"], convergence_threshold=1e-8,
+                    max_size_qspace=6 * c["nroots"], reset_D=8)
+    o = dict(max_size_qspace=6, convergence_threshold=c["convergence_threshold"])
+    if "max_iter" in c:
+        o["max_iter"] = c["max_iter"]
+    return o
+
+
+def run(name):
+    import numpy as np
+    import oracle
+
+    c = CASES[name]
+    t0 = time.time()
+    fn = oracle.davidson_synthetic if c["kind"] == "davidson" else oracle.diis_synthetic
+    # the same CPU path with its dots summed in another valid order (8 interleaved partial sums):
+    # how far the REFERENCE algorithm itself moves under a change of rounding
+    oracle.set_sum_order(1)
+    v = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **options(c))
+    oracle.set_sum_order(0)
+    r = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **options(c))
+    tr, tv = r["trace"], v["trace"]
+    k = min(len(tr["nq"]), len(tv["nq"]))
+    reordered = {
+        "iterations": v["iterations"],
+        "r_creations": v["r_creations"],
+        "q_creations": v["q_creations"],
+        "converged": v["converged"],
+        "same_steps": bool(v["iterations"] == r["iterations"] and v["r_creations"] == r["r_creations"]
+                           and tv["nq"].tolist() == tr["nq"].tolist()
+                           and tv["nwork"].tolist() == tr["nwork"].tolist()),
+        # per iteration (over the common prefix): max |error_reordered - error_reference| over roots
+        "error_abs_dev": np.max(np.abs(tv["errors"][:k] - tr["errors"][:k]), axis=1).tolist(),
+        "eigenvalue_rel_dev": (np.max(np.abs(tv["eigenvalues"][:k] - tr["eigenvalues"][:k])
+                                      / np.maximum(np.abs(tr["eigenvalues"][:k]), 1.0), axis=1).tolist()
+                               if c["kind"] == "davidson" else []),
+    }
+    out = {
+        "case": c,
+        "options": options(c),
+        "converged": r["converged"],
+        "iterations": r["iterations"],
+        "r_creations": r["r_creations"],
+        "q_creations": r["q_creations"],
+        "eigenvalues": [float(x) for x in r["eigenvalues"]] if c["kind"] == "davidson" else [],
+        "errors": [float(x) for x in r["errors"]],
+        "trace": {
+            "eigenvalues": tr["eigenvalues"].tolist() if c["kind"] == "davidson" else [],
+            "errors": tr["errors"].tolist(),
+            "nq": tr["nq"].tolist(),
+            "nwork": tr["nwork"].tolist(),
+        },
+        "reordered": reordered,
+        "cpu_seconds": round(time.time() - t0, 1),
+    }
+    return name, out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*")
+    ap.add_argument("--jobs", type=int, default=3)
+    ap.add_argument("--out", default=os.path.join(HERE, "traces.json"))
+    a = ap.parse_args()
+    names = a.only or list(CASES)
+    old = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    old = {k: v for k, v in old.items() if k in CASES}
+    # the N = 1e8 case alone holds ~40 GB: run it by itself
+    big = [n for n in names if CASES[n]["n"] >= 100_000_000]
+    small = [n for n in names if n not in big]
+    with ProcessPoolExecutor(a.jobs) as ex:
+        for name, out in ex.map(run, small):
+            old[name] = out
+            print(name, out["iterations"], out["converged"], out["cpu_seconds"], "s", flush=True)
+    for n in big:
+        name, out = run(n)
+        old[name] = out
+        print(name, out["iterations"], out["converged"], out["cpu_seconds"], "s", flush=True)
+    old["_generator"] = ("tests/golden/make_traces.py: oracle (reference CPU path restated over "
+                         "ArrayHandlerIterable loops, -ffp-contract=off)")
+    json.dump(dict(sorted(old.items())), open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -77,9 +77,54 @@ def test_optimize(algorithm):
     solver.finalize()
 
 
-def test_maximize_is_rejected():
-    with pytest.raises(RuntimeError, match="maximisation"):
-        iterative_solver.Optimize(4, minimize=False)
+def check_minimize_flag_ignored():
+    # The reference ignores `minimize` (IterativeSolverCMPI.cpp:250-268; its Fortran wrapper may pass
+    # an uninitialised value, IterativeSolverF.F90:321, :362-364): minimize=False still minimises.
+    problem = RayleighQuotient(4, 0.01)
+    parameters = np.full(problem.size, 10.0)
+    residual = np.zeros(problem.size)
+    solver = iterative_solver.Optimize(problem.size, minimize=False)
+    solver.solve(parameters, residual, problem)
+    assert solver.solution([0], parameters, residual) == pytest.approx(problem.eigenvalues[0], abs=1e-7)
+    solver.finalize()
+
+
+def test_minimize_flag_ignored():
+    check_minimize_flag_ignored()
+
+
+def check_instance_lifecycle():
+    """Each Python solver finalizes its OWN C-layer instance: reassigning a variable in a
+    loop creates the new instance before the old object is collected, and the old object's __del__
+    must not pop the new one."""
+    import gc
+
+    ids = []
+    s = None
+    for n in (8, 5, 11):
+        problem = RayleighQuotient(n, 0.1)
+        s = iterative_solver.LinearEigensystem(n, 1)  # the previous s dies here, after the new push
+        gc.collect()
+        ids.append(s._id)
+        x, g = np.zeros([1, n]), np.zeros([1, n])
+        s.solve(x, g, problem, generate_initial_guess=True)
+        assert s.eigenvalues[0] == pytest.approx(problem.eigenvalues[0], abs=1e-7)
+    assert len(set(ids)) == 3
+    # an older live object must not drive the newer instance
+    t = iterative_solver.LinearEigensystem(6, 1)
+    with pytest.raises(RuntimeError, match="another IterativeSolver instance is active"):
+        s.errors
+    t.finalize()
+    assert s.errors.size == 1  # s is the top again
+    s.finalize()
+    with pytest.raises(RuntimeError, match="finalized"):
+        s.errors
+    del s, t
+    gc.collect()
+
+
+def test_instance_lifecycle():
+    check_instance_lifecycle()
 
 
 def test_linear_equations():

@@ -1,0 +1,44 @@
+"""The committed per-iteration traces of the reference CPU path (tests/golden/traces.json,
+tests/golden/make_traces.py): C1 (N = 1e4, 1 root -- BASELINE config 1, the CPU
+ArrayHandlerIterable plumbing case) is re-run here and must reproduce its trace bit for bit (the CPU
+path is deterministic), and every rank-1 trace must end on the exact eigenvalues of
+diag(1 + i) + rho 11^T (secular equation), which pins the fixtures independently of the oracle."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+T = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "traces.json")))
+
+
+@pytest.mark.parametrize("name", ["C1_rank1", "C1_rank8"])
+def test_c1_cpu_path_reproduces_trace(name):
+    ref = T[name]
+    c = ref["case"]
+    r = oracle.davidson_synthetic(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **ref["options"])
+    assert r["converged"] and r["iterations"] == ref["iterations"] and r["r_creations"] == ref["r_creations"]
+    assert r["trace"]["eigenvalues"].tolist() == ref["trace"]["eigenvalues"]
+    assert r["trace"]["errors"].tolist() == ref["trace"]["errors"]
+    assert r["trace"]["nq"].tolist() == ref["trace"]["nq"]
+
+
+@pytest.mark.parametrize("name", sorted(k for k, v in T.items() if not k.startswith("_")
+                                        and v["case"]["kind"] == "davidson" and v["case"]["rank"] == 1))
+def test_rank_one_traces_end_on_exact_eigenvalues(name):
+    ref = T[name]
+    c = ref["case"]
+    assert ref["converged"]
+    exact = oracle.rank_one_eigenvalues(c["n"], c["rho"], c["nroots"])
+    np.testing.assert_allclose(ref["eigenvalues"], exact, rtol=1e-10, atol=0)
+    assert max(ref["errors"]) <= 1e-8
+
+
+def test_traces_cover_the_baseline_configs():
+    # C1, C2, C3 (shape at 1e7 and the real size at 1e8, rank 1), C5 (trajectory + converged run)
+    for k in ("C1_rank1", "C2_rank1", "C2_rank8", "C3_n1e7_rank8", "C3_n1e8_rank1", "C5_n1e7_traj12", "C5_n1e7"):
+        assert k in T
+    assert T["C3_n1e8_rank1"]["case"]["n"] == 100_000_000 and T["C3_n1e8_rank1"]["options"]["max_p"] == 16
+    assert T["C2_rank8"]["options"]["nroots"] == 4 and T["C2_rank8"]["case"]["n"] == 10_000_000

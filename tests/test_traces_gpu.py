@@ -1,0 +1,132 @@
+"""North-star parity at the BASELINE sizes: the GPU solver (libitsolv_hbm.so over libsubspace_hip.so,
+every vector in HBM) against committed per-iteration traces of the reference CPU path
+(tests/golden/traces.json, written by tests/golden/make_traces.py from the oracle).
+
+Bar (BASELINE.json north_star; IterativeSolverTemplate.h:322-408, LinearEigensystemDavidson.h:79):
+  * identical iteration count and convergence flag;
+  * identical R and Q creations and, after EVERY iteration, identical Q-space and working-set
+    sizes -- wherever the reference CPU path itself keeps them under a valid reordering of its sums
+    (the fixture's "reordered" run, make_traces.py).  Where it does not (C3 rank 1: the redundancy
+    screen of propose_rspace.h:481-512 meets near-dependent residuals of a rank-one problem, and the
+    CPU path's own R-creation count moves 11 -> 10 at N = 1e7 and 8 -> 11 at N = 1e8 when only its
+    summation order changes), the creation counts are not a parity observable and are not compared;
+  * after every iteration, eigenvalues of every root within 1e-10 relative;
+  * after every iteration, errors within 1e-6 relative plus 10x the reference CPU path's own
+    deviation under reordering at that point of the trajectory (max over the iteration and its
+    neighbours): a residual norm is a difference of O(|H x|) quantities, so its rounding floor
+    (~1e-10 at N = 1e7) is a property of the problem, measured, not assumed;
+  * final eigenvalues within 1e-10 relative; for rank 1 also the exact eigenvalues of
+    diag(1 + i) + rho 11^T (secular equation, oracle.rank_one_eigenvalues).
+
+C1 runs here as well (CPU, the oracle against its committed trace: test_traces.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import itsolv_hbm as ih
+import oracle
+
+pytestmark = pytest.mark.gpu
+T = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "traces.json")))
+DAVIDSON = sorted(k for k, v in T.items() if not k.startswith("_") and v["case"]["kind"] == "davidson")
+EIG_REL, ERR_REL, ERR_ABS, DEV_FACTOR = 1e-10, 1e-6, 1e-13, 10.0
+
+
+def error_tolerance(ref):
+    """Per-iteration absolute tolerance on the errors: ERR_REL * e + DEV_FACTOR * (the reference CPU
+    path's own deviation under reordering, max over the iteration and its two neighbours)."""
+    e = np.array(ref["trace"]["errors"])
+    dev = np.array(ref["reordered"]["error_abs_dev"] + [0.0] * (len(e) - len(ref["reordered"]["error_abs_dev"])))
+    win = np.maximum.reduce([dev, np.r_[dev[1:], 0.0], np.r_[0.0, dev[:-1]]])
+    return ERR_REL * e + DEV_FACTOR * win[:, None] + ERR_ABS
+
+
+def assert_trace(gpu, ref, name):
+    assert gpu["converged"] == ref["converged"], name
+    assert gpu["iterations"] == ref["iterations"], (name, gpu["iterations"], ref["iterations"])
+    g, r = gpu["trace"], ref["trace"]
+    if ref["reordered"]["same_steps"]:
+        assert gpu["r_creations"] == ref["r_creations"], (name, gpu["r_creations"], ref["r_creations"])
+        assert gpu["q_creations"] == ref["q_creations"], name
+        assert list(g["nq"]) == r["nq"], (name, list(g["nq"]), r["nq"])
+        assert list(g["nwork"]) == r["nwork"], name
+    if r["eigenvalues"]:
+        re = np.array(r["eigenvalues"])
+        de = np.abs(g["eigenvalues"] - re)
+        assert np.all(de <= EIG_REL * np.maximum(np.abs(re), 1.0)), (name, de.max())
+    rr = np.array(r["errors"])
+    dr = np.abs(g["errors"] - rr)
+    tol = error_tolerance(ref)
+    assert np.all(dr <= tol), (name, np.max(dr / tol))
+    # the reported run ends where the reference's does: converged errors below the threshold
+    if ref["converged"]:
+        assert np.max(g["errors"][-1]) <= ref["options"]["convergence_threshold"], name
+
+
+@pytest.mark.parametrize("name", DAVIDSON)
+def test_davidson_trace_matches_reference_path(ctx, name):
+    ref = T[name]
+    c = ref["case"]
+    gpu = ih.davidson_synthetic(ctx, c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **ref["options"])
+    assert_trace(gpu, ref, name)
+    ev = np.array(ref["eigenvalues"])
+    np.testing.assert_allclose(gpu["eigenvalues"], ev, rtol=EIG_REL, atol=0)
+    if c["rank"] == 1:
+        exact = oracle.rank_one_eigenvalues(c["n"], c["rho"], c["nroots"])
+        np.testing.assert_allclose(gpu["eigenvalues"], exact, rtol=EIG_REL, atol=0)
+    assert np.all(gpu["residual_norms"] <= 1e-7)
+
+
+# block Gram-Schmidt (off by default) under the same bar except the per-
+# iteration error tolerance: its projection is the same in exact arithmetic, rounded differently.
+@pytest.mark.parametrize("name", [n for n in DAVIDSON if T[n]["case"]["n"] >= 10_000_000])
+def test_block_gram_schmidt_trace(ctx, name):
+    ref = T[name]
+    c = ref["case"]
+    gpu = ih.davidson_synthetic(ctx, c["n"], c["rho"], c["rank"], c["seed"], solutions=False, block_gram_schmidt=1,
+                                **ref["options"])
+    assert gpu["converged"] and gpu["iterations"] == ref["iterations"]
+    if ref["reordered"]["same_steps"]:
+        assert gpu["r_creations"] == ref["r_creations"]
+        assert list(gpu["trace"]["nq"]) == ref["trace"]["nq"]
+    np.testing.assert_allclose(gpu["eigenvalues"], ref["eigenvalues"], rtol=EIG_REL, atol=0)
+
+
+def test_c5_diis_trajectory_n1e7(ctx):
+    # C5's DIIS problem (NonLinearEquationsDIIS.h:83-119) at N = 1e7: the fixed 12-iteration descent
+    # from |r| = 1.9e10 to the 1e-6 plateau, step for step with the reference CPU path.
+    ref = T["C5_n1e7_traj12"]
+    c = ref["case"]
+    gpu = ih.diis_synthetic(ctx, c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **ref["options"])
+    assert_trace(gpu, ref, "C5_n1e7_traj12")
+
+
+def test_c5_diis_converges_n1e8(ctx):
+    # BASELINE config C5 (DIIS, N = 1e8) on one MI355X: converges to the solution x = 1 at the
+    # threshold.  Past the 1e-6 plateau the reference algorithm itself is rounding-chaotic (the CPU
+    # path at N = 1e7 wanders 25 iterations there, traces.json C5_n1e7), so the count is reported,
+    # not compared.
+    n = 100_000_000
+    r = ih.diis_synthetic(ctx, n, 0.01, 3, 3, convergence_threshold=1e-8, max_size_qspace=6)
+    assert r["converged"], r["iterations"]
+    assert r["errors"][0] < 1e-8
+    assert r["residual_norms"][0] < 1e-8
+    # |x - 1| <= |H (x - 1)| / lambda_min(H), lambda_min >= 1
+    assert np.max(np.abs(r["x"] - 1.0)) <= 1e-8
+    print(f"C5 N=1e8: {r['iterations']} iterations, {r['seconds']:.3f} s")
+
+
+def test_c5_diis_converges_n1e7_like_reference(ctx):
+    ref = T["C5_n1e7"]
+    c = ref["case"]
+    r = ih.diis_synthetic(ctx, c["n"], c["rho"], c["rank"], c["seed"], **ref["options"])
+    assert r["converged"] and ref["converged"]
+    assert np.max(np.abs(r["x"] - 1.0)) <= 1e-8
+    # past the plateau the iteration count is not a parity observable: the reference CPU path
+    # itself takes 36 iterations with sequential sums and 27 with reordered ones (traces.json)
+    assert ref["reordered"]["iterations"] != ref["iterations"]
+    print(f"C5 N=1e7: GPU {r['iterations']} iterations, CPU path {ref['iterations']} "
+          f"(reordered CPU path {ref['reordered']['iterations']})")
