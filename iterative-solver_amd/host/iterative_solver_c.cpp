@@ -175,10 +175,8 @@ void IterativeSolverLinearEigensystemInitialize(size_t nQ, size_t nroot, size_t*
     // method dispatch and option parsing as the reference's create_LinearEigensystem (SolverFactory.h:114-125)
     auto solver = it::create_LinearEigensystem(algorithm ? algorithm : "", options ? options : "",
                                                molpro::linalg::hbm::make_handlers());
-    if (auto* d = dynamic_cast<Davidson*>(solver.get())) {
-      d->set_n_roots(nroot);
-      d->set_hermiticity(hermitian != 0);
-    }
+    solver->set_n_roots(nroot);  // every method (reference IterativeSolverCMPI.cpp:176)
+    if (auto* d = dynamic_cast<Davidson*>(solver.get())) d->set_hermiticity(hermitian != 0);
     solver->set_verbosity(verbosity_of(verbosity));
     solver->set_convergence_threshold(thresh);
     solver->set_convergence_threshold_value(thresh_value);

@@ -117,6 +117,11 @@ class Matrix {
   coord_type dimensions() const { return {rows_, cols_}; }
   void fill(T v) { std::fill(buf_.begin(), buf_.end(), v); }
   void clear() { resize({0, 0}); }
+  //! Row-major index -> (row, column) (reference Matrix.h:80-86).
+  coord_type to_coord(size_t ind) const {
+    if (ind >= size()) throw std::out_of_range("Matrix::to_coord: index is larger than size");
+    return {ind / cols_, ind % cols_};
+  }
 
   Slice slice(coord_type ul, coord_type br) { return Slice(*this, ul, br); }
   Slice slice() { return slice({0, 0}, dimensions()); }

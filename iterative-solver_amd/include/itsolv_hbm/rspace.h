@@ -368,11 +368,7 @@ inline std::vector<int> redundant_parameters(const Matrix<double>& ov, size_t oR
   return red;
 }
 
-template <class Container>
-void delete_parameters(std::vector<int> indices, Container& params) {
-  std::sort(indices.begin(), indices.end(), std::greater<int>());
-  for (int i : indices) params.erase(params.begin() + i);
-}
+using util::delete_parameters;
 
 // Roots from `working_set` whose residual survived into `wparams` (reference :515-523).
 template <class R>
@@ -396,6 +392,16 @@ void construct_solutions(const VecRef<R>& params, const std::vector<int>& roots,
     for (size_t j = 0; j < qp.size(); ++j) hrq.axpy(sol(root, oQ + j), qp.at(j), params.at(i));
     for (size_t j = 0; j < dp.size(); ++j) hrq.axpy(sol(root, oD + j), dp.at(j), params.at(i));
   }
+}
+
+// Removes the Q parameters contributing least to any solution until nQ <= max_q (reference
+// DSpaceResetter.h:13-23); XS: anything with dimensions() and eraseq(i).
+template <class XS>
+void resize_qspace(XS& xs, const Matrix<double>& solutions, size_t max_q, Logger& log) {
+  log.msg("resize_qspace()", Logger::Trace);
+  auto del = limit_qspace_size(xs.dimensions(), max_q, solutions, log);
+  std::sort(del.begin(), del.end(), std::greater<int>());
+  for (int i : del) xs.eraseq(size_t(i));
 }
 
 // Q indices with the largest overlap with each R parameter, descending (reference DSpaceResetter.h:32-54).
@@ -463,12 +469,8 @@ class DSpaceResetter {
     }
     const auto wparams = cwrap(rparams.begin(), rparams.begin() + nR);
     for (int i : max_overlap_with_R(wparams, xs.cparamsq(), h.rq())) xs.eraseq(size_t(i));
-    if (xs.dimensions().nQ + nR > size_t(m_max_q)) {
-      const size_t lim = size_t(m_max_q) > nR ? size_t(m_max_q) - nR : 0;
-      auto del = limit_qspace_size(xs.dimensions(), lim, sol, log);
-      std::sort(del.begin(), del.end(), std::greater<int>());
-      for (int i : del) xs.eraseq(size_t(i));
-    }
+    if (xs.dimensions().nQ + nR > size_t(m_max_q))
+      resize_qspace(xs, sol, size_t(m_max_q) > nR ? size_t(m_max_q) - nR : 0, log);
     std::vector<int> ws(nR);
     std::iota(ws.begin(), ws.end(), 0);
     return ws;

@@ -23,18 +23,6 @@
 
 namespace molpro::linalg::itsolv {
 
-// The option sets of the two methods whose reference options add nothing to Options
-// (LinearEigensystemRSPTOptions.h, OptimizeSDOptions.h).
-struct LinearEigensystemRSPTOptions : Options {
-  LinearEigensystemRSPTOptions() = default;
-  explicit LinearEigensystemRSPTOptions(const options_map& opt) : Options(opt) {}
-};
-
-struct OptimizeSDOptions : Options {
-  OptimizeSDOptions() = default;
-  explicit OptimizeSDOptions(const options_map& opt) : Options(opt) {}
-};
-
 template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>
 class SolverFactory {
  public:

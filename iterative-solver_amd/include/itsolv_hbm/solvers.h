@@ -427,6 +427,14 @@ class IterativeSolverTemplate {
   std::shared_ptr<Logger> logger() const { return m_logger; }
   subspace::XSpace<R, Q, P>& xspace() { return *m_xspace; }
 
+  //! The current settings (reference IterativeSolverTemplate.h:262-267; derived solvers add theirs).
+  virtual std::shared_ptr<Options> get_options() const {
+    auto o = std::make_shared<Options>();
+    o->n_roots = int(n_roots());
+    o->convergence_threshold = convergence_threshold();
+    return o;
+  }
+
   virtual void set_options(const Options& o) {
     if (o.n_roots) set_n_roots(size_t(*o.n_roots));
     if (o.convergence_threshold) set_convergence_threshold(*o.convergence_threshold);
@@ -647,6 +655,20 @@ class DavidsonSolver : public IterativeSolverTemplate<R, Q, P> {
   SubspaceSolverLinEig& subspace_solver() { return static_cast<SubspaceSolverLinEig&>(*this->m_subspace_solver); }
 
   template <class O>
+  std::shared_ptr<O> davidson_options() const {
+    auto o = std::make_shared<O>();
+    o->copy(*Base::get_options());
+    o->reset_D = get_reset_D();
+    o->reset_D_max_Q_size = get_reset_D_maxQ_size();
+    o->max_size_qspace = get_max_size_qspace();
+    o->norm_thresh = norm_thresh;
+    o->svd_thresh = svd_thresh;
+    o->hermiticity = get_hermiticity();
+    o->block_gram_schmidt = m_block_gram_schmidt;
+    return o;
+  }
+
+  template <class O>
   void set_davidson_options(const O& d) {
     if (d.reset_D) set_reset_D(size_t(*d.reset_D));
     if (d.reset_D_max_Q_size) set_reset_D_maxQ_size(size_t(*d.reset_D_max_Q_size));
@@ -729,6 +751,10 @@ class LinearEigensystemDavidson : public DavidsonSolver<R, Q, P> {
     Base::set_options(o);
     if (auto* d = dynamic_cast<const LinearEigensystemDavidsonOptions*>(&o)) this->set_davidson_options(*d);
   }
+  //! reference LinearEigensystemDavidson.h:168-178
+  std::shared_ptr<Options> get_options() const override {
+    return this->template davidson_options<LinearEigensystemDavidsonOptions>();
+  }
 
  protected:
   void set_value_errors() override {
@@ -796,6 +822,24 @@ class LinearEigensystemRSPT : public IterativeSolverTemplate<R, Q, P> {
   }
   bool get_hermiticity() const { return true; }
 
+  //! reference LinearEigensystemRSPT.h:139-151 (options norm_thresh / svd_thresh)
+  void set_options(const Options& o) override {
+    Base::set_options(o);
+    if (auto* r = dynamic_cast<const LinearEigensystemRSPTOptions*>(&o)) {
+      if (r->norm_thresh) propose_rspace_norm_thresh = *r->norm_thresh;
+      if (r->svd_thresh) propose_rspace_svd_thresh = *r->svd_thresh;
+    }
+  }
+  std::shared_ptr<Options> get_options() const override {
+    auto o = std::make_shared<LinearEigensystemRSPTOptions>();
+    o->copy(*Base::get_options());
+    o->norm_thresh = propose_rspace_norm_thresh;
+    o->svd_thresh = propose_rspace_svd_thresh;
+    return o;
+  }
+  double propose_rspace_norm_thresh = 1e-10;
+  double propose_rspace_svd_thresh = 1e-12;
+
   void report(std::ostream& o = std::cout) const override {
     o << "Perturbed energies " << std::fixed << std::setprecision(8);
     for (double e : m_rspt_values) o << e << ", ";
@@ -850,6 +894,12 @@ class LinearEquationsDavidson : public DavidsonSolver<R, Q, P> {
       this->set_davidson_options(*d);
       if (d->augmented_hessian) set_augmented_hessian(*d->augmented_hessian);
     }
+  }
+  //! reference LinearEquationsDavidson.h:147-158
+  std::shared_ptr<Options> get_options() const override {
+    auto o = this->template davidson_options<LinearEquationsDavidsonOptions>();
+    o->augmented_hessian = const_cast<LinearEquationsDavidson*>(this)->get_augmented_hessian();
+    return o;
   }
 
  protected:
@@ -923,6 +973,15 @@ class NonLinearEquationsDIIS : public IterativeSolverTemplate<R, Q, P> {
       if (d->norm_thresh) set_norm_thresh(*d->norm_thresh);
       if (d->svd_thresh) set_svd_thresh(*d->svd_thresh);
     }
+  }
+  //! reference NonLinearEquationsDIIS.h:150-157
+  std::shared_ptr<Options> get_options() const override {
+    auto o = std::make_shared<NonLinearEquationsDIISOptions>();
+    o->copy(*Base::get_options());
+    o->max_size_qspace = m_max_size_qspace;
+    o->norm_thresh = m_norm_thresh;
+    o->svd_thresh = m_svd_thresh;
+    return o;
   }
 
  protected:
@@ -1024,6 +1083,13 @@ class OptimizeSD : public OptimizeSolver<R, Q, P> {
     return 1;
   }
   using Base::end_iteration;
+
+  //! reference OptimizeSD.h:70-74
+  std::shared_ptr<Options> get_options() const override {
+    auto o = std::make_shared<OptimizeSDOptions>();
+    o->copy(*IterativeSolverTemplate<R, Q, P>::get_options());
+    return o;
+  }
 };
 
 // Limited-memory quasi-Newton (BFGS two-loop recursion over the Q space) with a cubic line search
@@ -1115,6 +1181,18 @@ class OptimizeBFGS : public OptimizeSolver<R, Q, P> {
 
   void set_max_size_qspace(int n) { m_max_size_qspace = n; }
   int get_max_size_qspace() const { return m_max_size_qspace; }
+  //! reference OptimizeBFGS.h:229-239 (which reports Wolfe_1 as the strong_Wolfe flag; the value here)
+  std::shared_ptr<Options> get_options() const override {
+    auto o = std::make_shared<OptimizeBFGSOptions>();
+    o->copy(*IterativeSolverTemplate<R, Q, P>::get_options());
+    o->max_size_qspace = m_max_size_qspace;
+    o->strong_Wolfe = m_strong_Wolfe;
+    o->Wolfe_1 = m_Wolfe_1;
+    o->Wolfe_2 = m_Wolfe_2;
+    o->linesearch_tolerance = m_linesearch_tolerance;
+    o->linesearch_grow_factor = m_linesearch_grow_factor;
+    return o;
+  }
   void set_options(const Options& o) override {
     Base::set_options(o);
     if (auto* b = dynamic_cast<const OptimizeBFGSOptions*>(&o)) {
