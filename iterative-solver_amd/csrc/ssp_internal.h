@@ -172,11 +172,16 @@ __device__ inline double block_sum256(double v) {
 // results in device memory (`out`, for a following allreduce) or publishes them straight into
 // coherent host memory followed by the sequence flag (one rank: no second kernel, no D2H copy).
 //
-// Hand-off (cdna_hip_programming.md Guideline 16, write-through form): every partial is stored by
-// wave 0 of its workgroup with an agent-scope write-through store (store_partial, sc1); wave 0 waits
-// for its stores (vmcnt(0)) before lane 0 adds to the arrival counters (agent-scope atomics, two
-// levels); the last arriver reads every partial with sc1 loads.  No __threadfence(): its L2 write-back + invalidate in
-// every workgroup costs more than the launch it saves.
+// Hand-off: the write-through form of /opt/skills/guides/cdna_hip_programming.md §6 Guideline 16
+// (R1; "equally valid" to release/acquire in the split-K recipe of §5): every partial is stored by
+// wave 0 of its workgroup with an agent-scope relaxed atomic store, which is a write-through sc1
+// store (store_partial); wave 0 drains it (s_waitcnt vmcnt(0)) before lane 0 adds to the arrival
+// counters (agent-scope atomics, two levels); the last arriver reads EVERY partial with sc1 loads
+// (agent-scope relaxed atomic loads), so its acquire reduces to fence(acquire, "wavefront"), which
+// only keeps the compiler from hoisting those loads.  Guideline 16's conditions (1)-(4) for this form
+// are checked in the emitted gfx950 assembly of every kernel with the tail by
+// tests/test_fold_tail_isa.py.  A release fence per workgroup (buffer_wbl2) and an L1 invalidate
+// would add cost for no visibility the sc1 accesses do not already give.
 constexpr unsigned kFoldShards = 8;  // arrival-counter shards (one per XCD's worth of workgroups)
 constexpr unsigned kFoldLine = 32;   // unsigned per 128-B line
 struct FoldTail {
