@@ -14,6 +14,17 @@ Global N is fixed and sharded by index range over the ranks (strong scaling, con
 rank runs the identical SPMD sequence and the reductions are RCCL allreduces.
 
 value = algorithmic bytes of all ranks per step x steps / (max over ranks of the timed wall time).
+
+Beside the headline the JSON line carries (none of them inside the timed region):
+  product_step  the same update as the product's solver runs it: construct_solution as ONE
+                write-only pass per space (ssp_gemm_outer_set, IterativeSolverTemplate.h:33-65 fused,
+                8N(k + m) B) and the 8 root norms as one lazy-handle batch (ArrayHandler.h:298-437:
+                one gemm_inner launch, one reduction);
+  in_solver     whole LinearEigensystemDavidson solves (C3 at N = 1: 8 roots + P 16, rank-8 problem,
+                N = 1e8; at N > 1 the same solve sharded, BASELINE config C4): iterations, wall time,
+                kernel time and algorithmic bytes from the HIP-event ledger, reductions per iteration;
+  startup       context creation and the first (cold) solve against the warm one;
+  cpu_baseline.dram_resident  one call each of the reference loops on DRAM-resident operands.
 """
 from __future__ import annotations
 
@@ -56,6 +67,13 @@ def step_bytes(n, m, k):
             + m * 8 * n)             # norm dots (x == y: one vector read)
 
 
+def product_step_bytes(n, m, k):
+    return (2 * 8 * n * (m + k)      # two gemm_inner
+            + 2 * 8 * n * (k + m)    # two write-only construct_solution passes (gemm_outer_set)
+            + m * 24 * n             # residual axpy
+            + m * 8 * n)             # norms: one batched gemm_inner over the m residuals (x == y)
+
+
 class Workload:
     def __init__(self, ctx, n_local, offset, m, k):
         self.ctx, self.m, self.k = ctx, m, k
@@ -86,6 +104,23 @@ class Workload:
         for i in range(self.m):
             err = max(err, c.dot(self.ra[i], self.ra[i]))
         return err
+
+    def free(self):
+        for v in self.rp + self.ra + self.qp + self.qa:
+            v.free()
+        self.ctx.synchronize()
+
+    def product_step(self):
+        """The same update as the product's solver issues it (see the module docstring)."""
+        c = self.ctx
+        c.gemm_inner(self.rp, self.qp)
+        c.gemm_inner(self.rp, self.qa)
+        c.gemm_outer_set(self.coef, self.qp, self.rp)
+        c.gemm_outer_set(self.coef, self.qa, self.ra)
+        for i in range(self.m):
+            c.axpy(-self.lam[i], self.rp[i], self.ra[i])
+        g = c.gemm_inner(self.ra, self.ra)
+        return float(np.max(np.diag(g)))
 
 
 OP_KERNELS = {"gemm_inner": ("k_gemm_inner",), "gemm_outer": ("k_gemm_outer",), "axpy": ("k_axpy",),
@@ -170,6 +205,8 @@ def cpu_baseline(m, k, seconds):
     except OSError:
         pass
     hp = host_parallel(m, k, max(1.0, seconds / 3))
+    dram = {op: {kk: (round(v, 4) if isinstance(v, float) else v) for kk, v in d.items()}
+            for op, d in oracle.dram_resident_sample(SEED).items()}
     return {
         "value": step_bytes(n, m, k) * steps / dt / 1e9,
         "unit": "GB/s",
@@ -178,6 +215,8 @@ def cpu_baseline(m, k, seconds):
         "sample": f"{steps} step(s) of the same op sequence at N=1e6 (m={m}, k={k}) on 1 core of "
                   f"{cpu} (nproc={os.cpu_count()}), {dt:.1f} s, oracle/oracle_ops.c (reference loops)",
         "host_parallel": hp,
+        "dram_resident": dict(dram, note="one call each on 1 core, operands far beyond the host caches "
+                                         "(the N=1e6 step above is partly cache-resident)"),
     }
 
 
@@ -204,11 +243,62 @@ def host_parallel(m, k, seconds):
                       "oracle/host_parallel.c (blocked gemm, not the reference's pairwise loops)"}
 
 
+C3 = dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48, reset_D=8, convergence_threshold=1e-8)
+REDUCING_OPS = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "select", "sparse")
+
+
+def in_solver(ctx, n_global, world, barrier, repeat=2):
+    """Whole Davidson solves (C3 options; sharded over the ranks = C4 at N > 1) with the ledger on.
+    Returns the last (warm) solve's numbers and the first (cold) solve's wall time."""
+    import itsolv_hbm as ih
+
+    def allmax(x):
+        if world == 1:
+            return x
+        return max(struct.unpack("<d", b)[0] for b in ctx.allgather_bytes(struct.pack("<d", x)))
+
+    walls = []
+    for rep in range(repeat):
+        ctx.ledger_reset()
+        ctx.ledger_enable(rep == repeat - 1)
+        barrier()
+        t0 = time.perf_counter()
+        r = ih.davidson_synthetic(ctx, n_global, n_local=0, **C3)
+        ctx.synchronize()
+        walls.append(allmax(time.perf_counter() - t0))
+        ctx.ledger_enable(False)
+    led = ctx.ledger()
+    ms = sum(v["ms"] for v in led.values())
+    nb = sum(v["bytes"] for v in led.values())
+    red = sum(v["calls"] for op, v in led.items() if op.split("(")[0] in REDUCING_OPS or op.startswith("select"))
+    it = max(1, r["iterations"])
+    top = sorted(led.items(), key=lambda kv: -kv[1]["ms"])[:6]
+    return {
+        "config": "LinearEigensystemDavidson " + ("C3" if world == 1 else "C4") + ": 8 roots + P 16, rank-8 "
+                  "H = diag(1+i) + 0.1 sum u u^T, max_size_qspace 48, reset_D 8, threshold 1e-8",
+        "n_global": n_global,
+        "converged": bool(r["converged"]),
+        "iterations": r["iterations"],
+        "r_creations": r["r_creations"],
+        "wall_s": round(walls[-1], 4),
+        "wall_s_cold": round(walls[0], 4),
+        "kernel_ms_rank0": round(ms, 3),
+        "algorithmic_GB_rank0": round(nb / 1e9, 2),
+        "kernel_GBs_rank0": round(nb / (ms / 1e3) / 1e9, 1) if ms else None,
+        "wall_GBs_all_ranks": round(world * nb / walls[-1] / 1e9, 1),
+        "reductions_per_iteration": round(red / it, 1),
+        "top_ops": {op: {"calls": v["calls"], "ms": round(v["ms"], 2),
+                         "GBs": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] else None}
+                    for op, v in top},
+        "eigenvalues": [round(float(e), 12) for e in r["eigenvalues"][:8]],
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
     # not "--n": torch.distributed.run would take it as an abbreviation of its own --nnodes/--nproc-per-node
     ap.add_argument("--n-global", type=float, default=1e8, help="global vector length")
     ap.add_argument("--roots", type=int, default=8)
@@ -216,6 +306,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ledger-steps", type=int, default=3)
+    ap.add_argument("--no-in-solver", action="store_true", help="skip the whole-solve block")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
                     help="rank transport at N > 1: RCCL (the product path) or the host socket hub, which "
                          "lets tests run several ranks on ONE device (RCCL refuses duplicate GPUs)")
@@ -231,6 +322,7 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
+    t_ctx = time.perf_counter()
     if args.comm == "host":
         ctx = sh.Context(local_rank % max(1, sh.device_count()))
         if world > 1:
@@ -245,6 +337,8 @@ def main():
             if uid_path:
                 os.remove(uid_path)
 
+    ctx.synchronize()
+    ctx_create_s = time.perf_counter() - t_ctx
     n_global = int(args.n_global)
     m, k = args.roots, args.qsize
     borders = distribution(n_global, world)
@@ -277,6 +371,37 @@ def main():
         wl.step()
     ctx.ledger_enable(False)
     led = ctx.ledger()
+
+    # The product's own form of the same update (not the headline; see the module docstring).
+    for _ in range(2):
+        wl.product_step()
+    ctx.synchronize()
+    barrier()
+    tp = time.perf_counter()
+    p_steps = max(5, args.steps // 4)
+    for _ in range(p_steps):
+        wl.product_step()
+    ctx.synchronize()
+    tp = time.perf_counter() - tp
+    if world > 1:
+        tp = max(struct.unpack("<d", b)[0] for b in ctx.allgather_bytes(struct.pack("<d", tp)))
+    ctx.ledger_reset()
+    ctx.ledger_enable(True)
+    wl.product_step()
+    ctx.ledger_enable(False)
+    pled = ctx.ledger()
+    product = {
+        "ms_per_step": round(1e3 * tp / p_steps, 4),
+        "bytes_per_step": product_step_bytes(n_global, m, k),
+        "GBs": round(product_step_bytes(n_global, m, k) * p_steps / tp / 1e9, 2),
+        "vs_headline_step_time": None,
+        "ops": {op: {"calls_per_step": v["calls"], "avg_us": round(1e3 * v["ms"] / v["calls"], 2),
+                     "GBs": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)} for op, v in pled.items()},
+    }
+    wl.free()  # back to the arena before the whole solves
+    solve = None
+    if not args.no_in_solver:
+        solve = in_solver(ctx, n_global, world, barrier)
 
     total_bytes = step_bytes(n_global, m, k) * args.steps
     value = total_bytes / elapsed / 1e9
@@ -326,7 +451,13 @@ def main():
                 "bytes_per_launch": e["bytes"] / e["calls"],
             },
             "ops": ops,
+            "product_step": product,
+            "in_solver": solve,
+            "startup": {"ctx_create_s": round(ctx_create_s, 3),
+                        "first_solve_wall_s": solve["wall_s_cold"] if solve else None,
+                        "warm_solve_wall_s": solve["wall_s"] if solve else None},
         }
+        product["vs_headline_step_time"] = round(product["ms_per_step"] / (1e3 * elapsed / args.steps), 4)
         if "gemm_inner" in led and world == 1:
             # gemm_inner runs on the f64 matrix cores: live MFMA rate from the ledger (2 m k N flops
             # per call) against the dense f64 MFMA peak, and the PMC-measured MfmaUtil beside it.

@@ -479,6 +479,40 @@ class CpuUpdateStep:
             _c(L.or_dot(_d(self.ra[i]), n, _d(self.ra[i]), n, C.byref(out)))
 
 
+def dram_resident_sample(seed=20251015):
+    """One call each of the reference CPU loops on DRAM-resident operands (vectors far larger than
+    the host caches): dot and axpy at N = 1e8, gemm_inner 8 x 48 (pairwise, gemm_inner_default) at
+    N = 1e7.  Returns {op: {"n", "seconds", "bytes", "GBs"}} with the algorithmic bytes of SURVEY.md
+    §8d (dot 16N, axpy 24N, gemm_inner 8N(m+k); the pairwise loop itself streams 2mk N 8 B)."""
+    import time as _t
+
+    L = lib()
+    r = np.random.default_rng(seed)
+    out = {}
+    n = 100_000_000
+    x, y = r.uniform(-1, 1, n), r.uniform(-1, 1, n)
+    res = C.c_double()
+    t0 = _t.perf_counter()
+    _c(L.or_dot(_d(x), n, _d(y), n, C.byref(res)))
+    dt = _t.perf_counter() - t0
+    out["dot"] = {"n": n, "seconds": dt, "bytes": 16 * n, "GBs": 16 * n / dt / 1e9}
+    t0 = _t.perf_counter()
+    _c(L.or_axpy(0.5, _d(x), n, _d(y), n))
+    dt = _t.perf_counter() - t0
+    out["axpy"] = {"n": n, "seconds": dt, "bytes": 24 * n, "GBs": 24 * n / dt / 1e9}
+    del x, y
+    n, m, k = 10_000_000, 8, 48
+    xs = [r.uniform(-1, 1, n) for _ in range(m)]
+    ys = [r.uniform(-1, 1, n) for _ in range(k)]
+    prod = np.zeros(m * k)
+    t0 = _t.perf_counter()
+    _c(L.or_gemm_inner(_ptrs(xs), m, _ptrs(ys), k, n, _d(prod)))
+    dt = _t.perf_counter() - t0
+    out["gemm_inner_8x48"] = {"n": n, "seconds": dt, "bytes": 8 * n * (m + k), "GBs": 8 * n * (m + k) / dt / 1e9,
+                              "streamed_bytes": 16 * m * k * n}
+    return out
+
+
 class HostParallelStep:
     """bench.py's host-parallel baseline: the same op sequence with OpenMP over
     all host threads and cache-blocked gemm (oracle/host_parallel.c); not the reference's loops."""

@@ -226,11 +226,20 @@ int ssp_construct_solution(ssp_ctx* c, const double* palphas, const size_t* ptr,
   if (kp > 0) ssp_gemm_outer_sparse(c, palphas, ptr, idx, val, kp, yy, m, n, offset);
   return ssp_gemm_outer(c, alphas, xx, k, yy, m, n);
 }
+static int gemm_outer_body(const double* al, const double* const* xx, int k, double* const* yy, int m, size_t n) {
+  for (int j = 0; j < m; ++j)
+    for (int i = 0; i < k; ++i) {
+      const double a = al[size_t(i) * m + j];
+      for (size_t e = 0; e < n; ++e) yy[j][e] += a * xx[i][e];
+    }
+  return SSP_OK;
+}
 int ssp_gemm_outer_set(ssp_ctx* c, const double* al, const double* const* xx, int k, double* const* yy, int m,
                        size_t n) {
+  Led l(c, "gemm_outer_set", 8.0 * n * (k + 1.0 * m));
   for (int j = 0; j < m; ++j)
     for (size_t e = 0; e < n; ++e) yy[j][e] = 0;
-  return ssp_gemm_outer(c, al, xx, k, yy, m, n);
+  return gemm_outer_body(al, xx, k, yy, m, n);
 }
 int ssp_gemm_outer(ssp_ctx* c, const double* al, const double* const* xx, int k, double* const* yy, int m, size_t n) {
   Led l(c, "gemm_outer", 8.0 * n * (k + 2.0 * m));

@@ -17,6 +17,9 @@ for p in (ROOT, os.path.join(ROOT, "iterative-solver_amd")):
 import subspace_hip as sh  # noqa: E402
 
 sh.LIB_PATH = os.path.join(ROOT, "oracle", "build", "libssp_emul.so")
+import itsolv_hbm as ih  # noqa: E402
+
+ih.LIB_PATH = os.path.join(ROOT, "oracle", "build", "libitsolv_emul.so")
 
 import bench  # noqa: E402
 
