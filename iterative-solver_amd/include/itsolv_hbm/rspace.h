@@ -15,6 +15,7 @@
 #include <cmath>
 #include <list>
 #include <numeric>
+#include <set>
 #include <sstream>
 #include <tuple>
 #include <vector>
@@ -28,12 +29,28 @@ using subspace::Dimensions;
 using subspace::EqnData;
 using subspace::Matrix;
 
+// <x_i, x_i> for every x in xs, registered on the handler's lazy handle (reference
+// ArrayHandler.h:298-437) and evaluated together: device handlers fold the batch into one
+// gemm_inner launch and one reduction (fused_dot); the reference's CPU handler evaluates the same
+// dots one by one in order.
+template <class R, class Refs>
+std::vector<double> self_dots(const Refs& xs, array::ArrayHandler<R, R>& handler) {
+  std::vector<double> d(xs.size(), 0.0);
+  auto lazy = handler.lazy_handle();
+  for (size_t i = 0; i < xs.size(); ++i) lazy.dot(xs[i].get(), xs[i].get(), d[i]);
+  lazy.eval();
+  return d;
+}
+
+// reference propose_rspace.h:17-28 (the norms first, as one batch: scaling one vector does not
+// change another's norm)
 template <class R>
 void normalise(VecRef<R>& params, array::ArrayHandler<R, R>& handler, Logger& logger, double thresh = 1.0e-14) {
-  for (auto& p : params) {
-    const double nrm = std::sqrt(std::abs(handler.dot(p, p)));
+  const auto dots = self_dots(params, handler);
+  for (size_t i = 0; i < params.size(); ++i) {
+    const double nrm = std::sqrt(std::abs(dots[i]));
     if (nrm > thresh)
-      handler.scal(1. / nrm, p);
+      handler.scal(1. / nrm, params[i]);
     else
       logger.msg("parameter's length is too small for normalisation, dot = " + Logger::scientific(nrm), Logger::Warn);
   }
@@ -224,18 +241,28 @@ std::tuple<std::vector<Q>, std::vector<Q>> construct_dspace(const Matrix<double>
       h.fill(0, newp.back());
       h.fill(0, newa.back());
     }
-  for (size_t i = 0; i < nD; ++i) {
-    for (size_t j = 0; j < nqd; ++j) {
-      h.axpy(proj(i, j), qp.at(qdel[j]), newp.at(i));
-      h.axpy(proj(i, j), qa.at(qdel[j]), newa.at(i));
+  // The reference's axpy loops, registered per destination set on a lazy handle: every destination
+  // receives its sources in increasing order, so a device handler applies each set as one
+  // gemm_outer, bit for bit the axpy sequence (fused_axpy); params and actions are disjoint sets.
+  {
+    auto lp = h.lazy_handle();
+    auto la = h.lazy_handle();
+    for (size_t i = 0; i < nD; ++i) {
+      for (size_t j = 0; j < nqd; ++j) {
+        lp.axpy(proj(i, j), qp.at(qdel[j]).get(), newp.at(i));
+        la.axpy(proj(i, j), qa.at(qdel[j]).get(), newa.at(i));
+      }
+      for (size_t j = 0; j < d.nD; ++j) {
+        lp.axpy(proj(i, nqd + j), dp.at(j).get(), newp.at(i));
+        la.axpy(proj(i, nqd + j), da.at(j).get(), newa.at(i));
+      }
     }
-    for (size_t j = 0; j < d.nD; ++j) {
-      h.axpy(proj(i, nqd + j), dp.at(j), newp.at(i));
-      h.axpy(proj(i, nqd + j), da.at(j), newa.at(i));
-    }
+    lp.eval();
+    la.eval();
   }
+  const auto dots = self_dots(wrap(newp), h);
   for (size_t i = 0; i < nD; ++i) {
-    const double nrm = std::sqrt(std::abs(h.dot(newp.at(i), newp.at(i))));
+    const double nrm = std::sqrt(std::abs(dots[i]));
     h.scal(1. / nrm, newp[i]);
     h.scal(1. / nrm, newa[i]);
   }
@@ -281,7 +308,26 @@ std::vector<int> modified_gram_schmidt(const VecRef<R>& rparams, const Matrix<do
       handler.gemm_outer(coeff, cwrap_arg(xparams.at(i).get()), rparams);
     }
   };
-  orthogonalise(pp, h.rp(), d.oP, pp.size());
+  // P vectors with pairwise disjoint supports (solve()'s P space is unit vectors on distinct
+  // indices): <R_j, p_i> reads R_j only where no earlier p_l updated it, and each element of R_j is
+  // updated by at most one p_i, so one gemm_inner over all of P followed by one gemm_outer is the
+  // sequential sweep bit for bit -- two sparse launches (one reduction) instead of two per p_i.
+  auto disjoint = [&] {
+    std::set<size_t> seen;
+    for (const auto& p : pp)
+      for (const auto& e : p.get())
+        if (!seen.insert(e.first).second) return false;
+    return true;
+  };
+  if (nR > 0 && pp.size() > 1 && disjoint()) {
+    auto dots = h.rp().gemm_inner(cwrap(rparams), pp);
+    Matrix<double> coeff({pp.size(), nR});
+    for (size_t i = 0; i < pp.size(); ++i)
+      for (size_t j = 0; j < nR; ++j) coeff(i, j) = -dots(j, i) / std::abs(S(d.oP + i, d.oP + i));
+    h.rp().gemm_outer(coeff, pp, rparams);
+  } else {
+    orthogonalise(pp, h.rp(), d.oP, pp.size());
+  }
   // Q then D: the same handler and the same call sequence as two orthogonalise() sweeps, except
   // that a handler with a fused form (array::fused_axpy_inner) merges each step's gemm_outer with
   // the next step's gemm_inner into one pass over R: R is read once per

@@ -127,8 +127,9 @@ inline std::vector<std::vector<double>> construct_vectorP(const std::vector<int>
 template <class R>
 void normalise_pairs(size_t n, const VecRef<R>& params, const VecRef<R>& actions, array::ArrayHandler<R, R>& h,
                      Logger& log) {
+  const auto dots = self_dots(VecRef<R>(params.begin(), params.begin() + long(n)), h);
   for (size_t i = 0; i < n; ++i) {
-    const double d = std::sqrt(std::abs(h.dot(params.at(i), params.at(i))));
+    const double d = std::sqrt(std::abs(dots[i]));
     if (d > 1.0e-14) {
       h.scal(1. / d, params.at(i));
       h.scal(1. / d, actions.at(i));
@@ -138,9 +139,11 @@ void normalise_pairs(size_t n, const VecRef<R>& params, const VecRef<R>& actions
   }
 }
 
+// reference IterativeSolverTemplate.h:95-102, the root norms as one lazy batch (detail::self_dots)
 template <class R>
 void update_errors(std::vector<double>& errors, const CVecRef<R>& residual, array::ArrayHandler<R, R>& h) {
-  for (size_t i = 0; i < errors.size(); ++i) errors[i] = std::sqrt(std::abs(h.dot(residual[i], residual[i])));
+  const auto dots = self_dots(CVecRef<R>(residual.begin(), residual.begin() + long(errors.size())), h);
+  for (size_t i = 0; i < errors.size(); ++i) errors[i] = std::sqrt(std::abs(dots[i]));
 }
 
 // The nw roots with the largest errors above threshold, in ascending root order (reference :104-117).
