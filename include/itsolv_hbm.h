@@ -38,7 +38,8 @@ typedef struct {
   int generate_initial_guess;  /* 1: initial guess from the n smallest diagonals           */
   int verbosity;               /* 0 none .. 3 detailed                                     */
   double augmented_hessian;    /* LinearEquationsDavidson augmented-Hessian parameter (0: off) */
-  int block_gram_schmidt;      /* extension (0: off, the reference's MGS): orthogonalise the new
+  int block_gram_schmidt;      /* extension (-1: the vector type's default, 0: the reference's MGS,
+                                  1: on): orthogonalise the new
                                   R vectors against P, Q, D with coefficients from the overlaps
                                   already computed for redundancy screening (forward substitution
                                   through the stored S) and one gemm_outer per space; same result

@@ -306,6 +306,11 @@ class ArrayHandler {
 template <class T>
 struct batched_symmetric_overlap : std::false_type {};
 
+//  * block_gram_schmidt_default: whether Davidson solvers over this R type orthogonalise new R
+//    vectors by block Gram-Schmidt (rspace.h block_gram_schmidt) unless the option says otherwise.
+template <class T>
+struct block_gram_schmidt_default : std::false_type {};
+
 // Fused MGS step hook: y_j += c_j x for all j, then dots_j = <y_j, z>, in one pass; returns false
 // when the handler has no fused form (the caller then issues gemm_outer + gemm_inner).  Found by
 // argument-dependent lookup; the HBM overload lives in namespace molpro::linalg::hbm.

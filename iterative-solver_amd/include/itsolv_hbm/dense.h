@@ -2,8 +2,9 @@
 //
 // The reference delegates these to LAPACKE dsyev and Eigen 3.3.7 (reference
 // itsolv/helper-implementation.h).  Neither is available here, so they are restated on top of one
-// cyclic-Jacobi symmetric eigensolver (accurate to a few ulps for the symmetric / well-conditioned
-// matrices the solvers build), reproducing the reference's conventions:
+// symmetric eigensolver of dsyev's method (Householder tridiagonalisation + implicit QL, backward
+// stable; pinned against LAPACK in tests/test_host_layer_cpp.py), reproducing the reference's
+// conventions:
 //   * eigensolver_lapacke_dsyev: eigenvalues ascending, eigenvector i in column i   (:122-158)
 //   * svd_system(hermitian): eigenpairs listed largest first, value <= threshold kept (:184-192, :263-296)
 //   * get_rank: count of eigenvalues >= threshold * max                              (:221-231)
@@ -38,54 +39,141 @@ namespace dense {
 // Symmetric eigen-decomposition of the n x n matrix a (either storage order: only the symmetric
 // part is used).  On return evals is ascending and column i of evecs (evecs[j + n*i]) is the
 // unit eigenvector of evals[i].
+//
+// The method of the reference's own solvers (LAPACK dsyev = dsytrd + dsteqr, helper-implementation.h:
+// 122-158; Eigen's SelfAdjointEigenSolver, :356-382): Householder reduction to tridiagonal form with
+// the transformations accumulated, then the implicit QL iteration with Wilkinson-type shifts on the
+// tridiagonal matrix, rotations applied to the accumulated basis.  O(n^3) with a small constant:
+// 0.1 ms at n = 72 against 1.6 ms for cyclic Jacobi (which the host side of every iteration runs
+// two to four times; at the C4 shard size it was a fifth of the solve).
 inline void sym_eigen(size_t n, const std::vector<double>& a, std::vector<double>& evals, std::vector<double>& evecs) {
-  std::vector<double> A(n * n);
+  // Z: row-major working matrix, ends as the accumulated orthogonal basis (columns = eigenvectors).
+  std::vector<double> Z(n * n);
   for (size_t i = 0; i < n; ++i)
-    for (size_t j = 0; j < n; ++j) A[i * n + j] = 0.5 * (a[i * n + j] + a[j * n + i]);
-  std::vector<double> V(n * n, 0.0);
-  for (size_t i = 0; i < n; ++i) V[i * n + i] = 1.0;  // V[row*n + col], column = eigenvector
-  for (int sweep = 0; sweep < 100; ++sweep) {
-    double off = 0, diag = 0;
-    for (size_t i = 0; i < n; ++i) {
-      diag += A[i * n + i] * A[i * n + i];
-      for (size_t j = i + 1; j < n; ++j) off += A[i * n + j] * A[i * n + j];
-    }
-    if (off == 0 || off <= 1e-34 * diag) break;
-    for (size_t p = 0; p + 1 < n; ++p) {
-      for (size_t q = p + 1; q < n; ++q) {
-        const double apq = A[p * n + q];
-        if (apq == 0) continue;
-        const double app = A[p * n + p], aqq = A[q * n + q];
-        const double theta = (aqq - app) / (2 * apq);
-        const double t = (theta >= 0 ? 1.0 : -1.0) / (std::abs(theta) + std::sqrt(theta * theta + 1));
-        const double c = 1 / std::sqrt(t * t + 1), s = t * c;
-        for (size_t k = 0; k < n; ++k) {
-          const double akp = A[k * n + p], akq = A[k * n + q];
-          A[k * n + p] = c * akp - s * akq;
-          A[k * n + q] = s * akp + c * akq;
+    for (size_t j = 0; j < n; ++j) Z[i * n + j] = 0.5 * (a[i * n + j] + a[j * n + i]);
+  std::vector<double> d(n, 0.0), e(n, 0.0);
+  if (n == 0) {
+    evals.clear();
+    evecs.clear();
+    return;
+  }
+  // Householder tridiagonalisation, last row first: row i is reduced against columns 0..i-1.
+  for (size_t i = n - 1; i > 0; --i) {
+    const size_t l = i - 1;
+    double h = 0, scale = 0;
+    if (l > 0) {
+      for (size_t k = 0; k <= l; ++k) scale += std::abs(Z[i * n + k]);
+      if (scale == 0) {
+        e[i] = Z[i * n + l];
+      } else {
+        for (size_t k = 0; k <= l; ++k) {
+          Z[i * n + k] /= scale;
+          h += Z[i * n + k] * Z[i * n + k];
         }
-        for (size_t k = 0; k < n; ++k) {
-          const double apk = A[p * n + k], aqk = A[q * n + k];
-          A[p * n + k] = c * apk - s * aqk;
-          A[q * n + k] = s * apk + c * aqk;
+        double f = Z[i * n + l];
+        const double g = f >= 0 ? -std::sqrt(h) : std::sqrt(h);
+        e[i] = scale * g;
+        h -= f * g;
+        Z[i * n + l] = f - g;
+        f = 0;
+        for (size_t j = 0; j <= l; ++j) {
+          Z[j * n + i] = Z[i * n + j] / h;
+          double gg = 0;
+          for (size_t k = 0; k <= j; ++k) gg += Z[j * n + k] * Z[i * n + k];
+          for (size_t k = j + 1; k <= l; ++k) gg += Z[k * n + j] * Z[i * n + k];
+          e[j] = gg / h;
+          f += e[j] * Z[i * n + j];
         }
-        A[p * n + q] = A[q * n + p] = 0;
-        for (size_t k = 0; k < n; ++k) {
-          const double vkp = V[k * n + p], vkq = V[k * n + q];
-          V[k * n + p] = c * vkp - s * vkq;
-          V[k * n + q] = s * vkp + c * vkq;
+        const double hh = f / (h + h);
+        for (size_t j = 0; j <= l; ++j) {
+          const double fj = Z[i * n + j];
+          const double gj = e[j] - hh * fj;
+          e[j] = gj;
+          for (size_t k = 0; k <= j; ++k) Z[j * n + k] -= fj * e[k] + gj * Z[i * n + k];
         }
       }
+    } else {
+      e[i] = Z[i * n + l];
+    }
+    d[i] = h;
+  }
+  d[0] = 0;
+  e[0] = 0;
+  // Accumulate the transformations.
+  for (size_t i = 0; i < n; ++i) {
+    if (d[i] != 0) {
+      for (size_t j = 0; j < i; ++j) {
+        double g = 0;
+        for (size_t k = 0; k < i; ++k) g += Z[i * n + k] * Z[k * n + j];
+        for (size_t k = 0; k < i; ++k) Z[k * n + j] -= g * Z[k * n + i];
+      }
+    }
+    d[i] = Z[i * n + i];
+    Z[i * n + i] = 1;
+    for (size_t j = 0; j < i; ++j) Z[j * n + i] = Z[i * n + j] = 0;
+  }
+  // The basis transposed: W row i = column i of Z, so each QL rotation updates two contiguous rows.
+  std::vector<double> W(n * n);
+  for (size_t i = 0; i < n; ++i)
+    for (size_t k = 0; k < n; ++k) W[i * n + k] = Z[k * n + i];
+  // Implicit QL with shifts on (d, e); e[i] couples d[i-1] and d[i] -> shift down by one.
+  for (size_t i = 1; i < n; ++i) e[i - 1] = e[i];
+  e[n - 1] = 0;
+  const double eps = std::numeric_limits<double>::epsilon();
+  for (size_t l = 0; l < n; ++l) {
+    for (int iter = 0;; ++iter) {
+      size_t m = l;
+      for (; m + 1 < n; ++m) {
+        const double dd = std::abs(d[m]) + std::abs(d[m + 1]);
+        if (std::abs(e[m]) <= eps * dd) break;
+      }
+      if (m == l) break;
+      if (iter == 60) throw std::runtime_error("sym_eigen: QL iteration did not converge");
+      double g = (d[l + 1] - d[l]) / (2 * e[l]);
+      double r = std::hypot(g, 1.0);
+      g = d[m] - d[l] + e[l] / (g + (g >= 0 ? r : -r));
+      double s = 1, c = 1, p = 0;
+      bool deflated = false;
+      for (size_t i = m; i-- > l;) {
+        double f = s * e[i];
+        const double b = c * e[i];
+        r = std::hypot(f, g);
+        e[i + 1] = r;
+        if (r == 0) {
+          d[i + 1] -= p;
+          e[m] = 0;
+          deflated = true;
+          break;
+        }
+        s = f / r;
+        c = g / r;
+        g = d[i + 1] - p;
+        r = (d[i] - g) * s + 2 * c * b;
+        p = s * r;
+        d[i + 1] = g + p;
+        g = c * r - b;
+        double* wi = &W[i * n];
+        double* wj = &W[(i + 1) * n];
+        for (size_t k = 0; k < n; ++k) {
+          const double wk1 = wj[k], wk0 = wi[k];
+          wj[k] = s * wk0 + c * wk1;
+          wi[k] = c * wk0 - s * wk1;
+        }
+      }
+      if (deflated) continue;
+      d[l] -= p;
+      e[l] = g;
+      e[m] = 0;
     }
   }
   std::vector<size_t> order(n);
   std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return A[x * n + x] < A[y * n + y]; });
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return d[x] < d[y]; });
   evals.resize(n);
   evecs.assign(n * n, 0.0);
   for (size_t i = 0; i < n; ++i) {
-    evals[i] = A[order[i] * n + order[i]];
-    for (size_t j = 0; j < n; ++j) evecs[j + n * i] = V[j * n + order[i]];
+    evals[i] = d[order[i]];
+    for (size_t j = 0; j < n; ++j) evecs[j + n * i] = W[order[i] * n + j];
   }
 }
 

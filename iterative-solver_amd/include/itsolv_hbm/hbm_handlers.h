@@ -128,4 +128,12 @@ namespace molpro::linalg::array {
 // HBM handlers form symmetric overlaps with one gemm_inner (reads each vector once).
 template <>
 struct batched_symmetric_overlap<hbm::Vec> : std::true_type {};
+// Davidson over HBM vectors orthogonalises new R vectors by block Gram-Schmidt (rspace.h) unless the
+// option BLOCK_GRAM_SCHMIDT=false selects the reference's sequential MGS: it passes the same parity
+// bar as the sequential sweep on every GPU test (traces at the BASELINE sizes step for step, the
+// reference's reverse-communication loops, fixtures, linear equations), removes one
+// gemm_inner + gemm_outer per Q / D vector and iteration (C3: 0.85 -> 0.59 s) and a third of the
+// reductions (C3: 57 -> 39 per iteration, the latency that bounds the sharded C4 solve).
+template <>
+struct block_gram_schmidt_default<hbm::Vec> : std::true_type {};
 }  // namespace molpro::linalg::array

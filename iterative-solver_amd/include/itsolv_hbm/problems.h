@@ -81,7 +81,7 @@ void run_davidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Proble
   if (o.reset_D > 0) opt.reset_D = o.reset_D;
   if (o.reset_D_max_Q_size > 0) opt.reset_D_max_Q_size = o.reset_D_max_Q_size;
   opt.hermiticity = o.hermitian != 0;
-  if (o.block_gram_schmidt) opt.block_gram_schmidt = true;
+  if (o.block_gram_schmidt >= 0) opt.block_gram_schmidt = o.block_gram_schmidt != 0;
   solver.set_options(opt);
   const size_t nwork = size_t(o.nwork > 0 ? o.nwork : o.nroots);
   std::vector<R> params, actions;
@@ -132,7 +132,7 @@ void run_linear_equations(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, cons
   if (o.reset_D_max_Q_size > 0) opt.reset_D_max_Q_size = o.reset_D_max_Q_size;
   opt.hermiticity = o.hermitian != 0;
   if (o.augmented_hessian > 0) opt.augmented_hessian = o.augmented_hessian;
-  if (o.block_gram_schmidt) opt.block_gram_schmidt = true;
+  if (o.block_gram_schmidt >= 0) opt.block_gram_schmidt = o.block_gram_schmidt != 0;
   solver.set_options(opt);
   const size_t nwork = rhs.size();
   std::vector<R> params, actions;
@@ -247,7 +247,7 @@ inline void default_options(itsolv_options* o) {
   o->reset_D = 0;
   o->reset_D_max_Q_size = 0;
   o->augmented_hessian = 0;
-  o->block_gram_schmidt = 0;
+  o->block_gram_schmidt = -1;
   o->max_p = 0;
   o->p_threshold = 0;
   o->convergence_threshold = 1e-8;

@@ -729,7 +729,7 @@ class DavidsonSolver : public IterativeSolverTemplate<R, Q, P> {
   detail::DSpaceResetter<Q> m_resetter;
   bool m_hermiticity = false;
   bool m_resetting = false;
-  bool m_block_gram_schmidt = false;
+  bool m_block_gram_schmidt = array::block_gram_schmidt_default<R>::value;
 };
 
 template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>

@@ -87,7 +87,7 @@ class Result(C.Structure):
 def make_options(**kw) -> Options:
     o = Options(nroots=1, nwork=0, max_iter=100, max_size_qspace=0, reset_D=0, reset_D_max_Q_size=0, max_p=0,
                 p_threshold=0.0, convergence_threshold=1e-8, hermitian=1, generate_initial_guess=1, verbosity=0,
-                augmented_hessian=0.0, block_gram_schmidt=0)
+                augmented_hessian=0.0, block_gram_schmidt=-1)
     for k, v in kw.items():
         if not hasattr(o, k):
             raise KeyError(k)

@@ -381,11 +381,27 @@ void svd_dump() {
 }
 }  // namespace
 
+// "sym_eigen" mode: reads n and an n x n row-major matrix from stdin, prints the restated
+// dense::sym_eigen result (eigenvalues ascending, then the eigenvector columns) for the Python side.
+int sym_eigen_io() {
+  size_t n = 0;
+  if (std::scanf("%zu", &n) != 1) return 2;
+  std::vector<double> a(n * n);
+  for (auto& x : a)
+    if (std::scanf("%lf", &x) != 1) return 2;
+  std::vector<double> ev, vec;
+  it::dense::sym_eigen(n, a, ev, vec);
+  for (double x : ev) std::printf("%.17g\n", x);
+  for (double x : vec) std::printf("%.17g\n", x);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && std::string(argv[1]) == "svd") {
     svd_dump();
     return 0;
   }
+  if (argc > 1 && std::string(argv[1]) == "sym_eigen") return sym_eigen_io();
   subspace_util_cases();
   dspace_resetter_cases();
   itsolv_util_cases();

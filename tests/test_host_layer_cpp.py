@@ -83,3 +83,48 @@ def test_svd_system_against_lapack(host_exe):
     np.testing.assert_allclose(d["svd_values"], np.sort(np.linalg.svd(m, compute_uv=False))[::-1], rtol=1e-12)
     sv = np.array(d["svd_vectors"]).reshape(n, n)
     np.testing.assert_allclose(np.abs(sv), np.abs(v[:, ::-1].T), atol=1e-10)
+
+
+def sym_eigen(exe, a):
+    n = a.shape[0]
+    inp = f"{n}\n" + "\n".join(repr(float(x)) for x in a.ravel()) + "\n"
+    r = subprocess.run([exe, "sym_eigen"], input=inp, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    v = np.array(r.stdout.split(), dtype=float)
+    return v[:n], v[n:].reshape(n, n).T  # eigenvector i in column i
+
+
+def sym_cases():
+    r = np.random.default_rng(3)
+    for n in (1, 2, 3, 7, 24, 48, 72, 100):
+        m = r.standard_normal((n, n))
+        yield f"random{n}", m + m.T
+    yield "identity", np.eye(9)
+    yield "zero", np.zeros((5, 5))
+    yield "repeated", np.diag([1.0, 2.0, 2.0, 2.0, 5.0, 5.0])
+    u = r.standard_normal(20)
+    yield "rank_one", np.outer(u, u)
+    w = np.diag(np.abs(np.arange(-10, 11)).astype(float)) + np.diag(np.ones(20), 1) + np.diag(np.ones(20), -1)
+    yield "wilkinson21", w
+    q, _ = np.linalg.qr(r.standard_normal((30, 30)))
+    yield "clustered", q @ np.diag(1 + 1e-12 * np.arange(30)) @ q.T
+    yield "graded", q @ np.diag(10.0 ** np.linspace(-10, 10, 30)) @ q.T
+    x = r.standard_normal((60, 12))
+    yield "overlap_rank12", x.T @ x  # a Davidson overlap matrix shape (full rank)
+    y = r.standard_normal((40, 8))
+    yield "overlap_rank_deficient", np.hstack([y, y[:, :3]]).T @ np.hstack([y, y[:, :3]])
+
+
+@pytest.mark.parametrize("name,a", list(sym_cases()), ids=[c[0] for c in sym_cases()])
+def test_sym_eigen_tridiagonal_ql_against_lapack(host_exe, name, a):
+    # dense::sym_eigen (Householder + implicit QL, as dsyev / Eigen's SelfAdjointEigenSolver) against
+    # LAPACK through numpy: eigenvalues, residuals and orthonormality to backward-stable accuracy.
+    n = a.shape[0]
+    ev, vec = sym_eigen(host_exe, a)
+    w = np.linalg.eigvalsh(a)
+    scale = max(np.linalg.norm(a, 2), 1e-300)
+    tol = 1e-14 * max(n, 4) * scale
+    assert np.all(np.diff(ev) >= 0), "ascending"
+    np.testing.assert_allclose(ev, w, rtol=0, atol=tol)
+    assert np.max(np.abs(a @ vec - vec * ev)) <= 10 * tol
+    assert np.max(np.abs(vec.T @ vec - np.eye(n))) <= 1e-14 * max(n, 4) * 10

@@ -178,30 +178,30 @@ def test_optimize_gpu_vs_cpu(ctx, n, alg, thresh):
     assert abs(gpu["eigenvalues"][0] - cpu["eigenvalues"][0]) < 1e-12
 
 
-# block_gram_schmidt on the HIP handlers against the reference CPU path (sequential MGS): the bar of
-# the default path (same iterations and R creations, eigenvalues within 1e-10).
+# The HIP handlers' default is block Gram-Schmidt (hbm_handlers.h); these run the reference's
+# sequential MGS on the GPU (block_gram_schmidt=0) under the same bar against the CPU path.
 @pytest.mark.parametrize("name,split,nroot,np_", [("hf", 1e-8, 1, 0), ("hf", 1e-8, 3, 0), ("bh", 1e-8, 3, 0),
                                                   ("bh", 1e-8, 3, 6)])
-def test_block_gram_schmidt_fixture_gpu_vs_reference(ctx, name, split, nroot, np_):
+def test_sequential_mgs_fixture_gpu_vs_reference(ctx, name, split, nroot, np_):
     h = hamiltonian(name, split)
     kw = dict(nroots=nroot, max_p=np_, convergence_threshold=1e-8, max_size_qspace=6 * nroot, reset_D=8)
-    assert_same_run(ih.davidson_dense(ctx, h, block_gram_schmidt=1, **kw), oracle.davidson_dense(h, **kw))
+    assert_same_run(ih.davidson_dense(ctx, h, block_gram_schmidt=0, **kw), oracle.davidson_dense(h, **kw))
 
 
 @pytest.mark.parametrize("rank,nroot,np_", [(1, 4, 0), (4, 8, 0), (4, 8, 16)])
-def test_block_gram_schmidt_synthetic_gpu_vs_reference(ctx, rank, nroot, np_):
+def test_sequential_mgs_synthetic_gpu_vs_reference(ctx, rank, nroot, np_):
     n, rho, seed = 100_003, 0.1, 20251015
     kw = dict(nroots=nroot, max_p=np_, convergence_threshold=1e-8, max_size_qspace=6 * nroot, reset_D=8)
-    gpu = ih.davidson_synthetic(ctx, n, rho, rank, seed, block_gram_schmidt=1, **kw)
+    gpu = ih.davidson_synthetic(ctx, n, rho, rank, seed, block_gram_schmidt=0, **kw)
     assert_same_run(gpu, oracle.davidson_synthetic(n, rho, rank, seed, **kw))
     assert np.all(gpu["residual_norms"] <= 1e-7)
 
 
-def test_block_gram_schmidt_config_c3(ctx):
+def test_sequential_mgs_config_c3(ctx):
     n, rho = 100_000_000, 0.1
     kw = dict(nroots=8, max_p=16, convergence_threshold=1e-8, max_size_qspace=48, reset_D=8)
-    seq = ih.davidson_synthetic(ctx, n, rho, 1, 1, **kw)
-    blk = ih.davidson_synthetic(ctx, n, rho, 1, 1, block_gram_schmidt=1, **kw)
-    assert blk["converged"] and blk["iterations"] == seq["iterations"]
-    np.testing.assert_allclose(blk["eigenvalues"], oracle.rank_one_eigenvalues(n, rho, 8), rtol=1e-10, atol=0)
-    assert np.all(blk["residual_norms"] <= 1e-7)
+    default = ih.davidson_synthetic(ctx, n, rho, 1, 1, **kw)
+    seq = ih.davidson_synthetic(ctx, n, rho, 1, 1, block_gram_schmidt=0, **kw)
+    assert seq["converged"] and seq["iterations"] == default["iterations"]
+    np.testing.assert_allclose(seq["eigenvalues"], oracle.rank_one_eigenvalues(n, rho, 8), rtol=1e-10, atol=0)
+    assert np.all(seq["residual_norms"] <= 1e-7)

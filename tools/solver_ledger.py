@@ -4,7 +4,7 @@ ledger enabled and report, per handler operation, calls, kernel time, algorithmi
 plus the solve's wall time.  Complements bench.py (a fixed subspace-update step) with the op mix
 of real Davidson / DIIS iterations.
 
-usage: python tools/solver_ledger.py [--configs C2,C2-bgs,C3,C3-bgs,C5] [--out profiles/r1/solver_ledger.json]
+usage: python tools/solver_ledger.py [--configs C2,C2-mgs,C3,C3-mgs,C5,C4-shard] [--out profiles/r1/solver_ledger.json]
 """
 import argparse
 import json
@@ -24,13 +24,19 @@ CONFIGS = {
                                          convergence_threshold=1e-8)),
     "C3": ("davidson", 100_000_000, dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48,
                                           reset_D=8, convergence_threshold=1e-8)),
-    # C3 with the block Gram-Schmidt option (itsolv_options.block_gram_schmidt)
-    "C3-bgs": ("davidson", 100_000_000, dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48,
-                                              reset_D=8, convergence_threshold=1e-8, block_gram_schmidt=1)),
-    "C2-bgs": ("davidson", 10_000_000, dict(rho=0.1, rank=8, seed=1, nroots=4, max_size_qspace=24, reset_D=8,
-                                             convergence_threshold=1e-8, block_gram_schmidt=1)),
+    # the same with the reference's sequential MGS (itsolv_options.block_gram_schmidt = 0; the HBM
+    # handlers' default is block Gram-Schmidt)
+    "C3-mgs": ("davidson", 100_000_000, dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48,
+                                              reset_D=8, convergence_threshold=1e-8, block_gram_schmidt=0)),
+    "C2-mgs": ("davidson", 10_000_000, dict(rho=0.1, rank=8, seed=1, nroots=4, max_size_qspace=24, reset_D=8,
+                                             convergence_threshold=1e-8, block_gram_schmidt=0)),
     "C5": ("diis", 100_000_000, dict(rho=0.01, rank=3, seed=3, max_size_qspace=6, convergence_threshold=1e-8)),
+    # one rank's shard of C4 (N = 1e8 over 8 GPUs): the C3 problem at N = 1.25e7 (run with --rccl for
+    # the multi-rank reduction path: fold -> ncclAllReduce -> publish)
+    "C4-shard": ("davidson", 12_500_000, dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48,
+                                              reset_D=8, convergence_threshold=1e-8)),
 }
+REDUCING = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "select", "sparse")
 
 
 def run(ctx, name, repeat=2):
@@ -41,7 +47,7 @@ def run(ctx, name, repeat=2):
         cold = run_once(ctx, name)["wall_s"]
     out = run_once(ctx, name)
     out["wall_s_cold"] = cold
-    print(json.dumps({k: out[k] for k in ("config", "iterations", "wall_s", "wall_s_cold", "kernel_ms", "kernel_GBs",
+    print(json.dumps({k: out[k] for k in ("config", "iterations", "wall_s", "wall_s_cold", "kernel_ms", "kernel_GBs", "reductions_per_iteration", "host_overhead_ms",
                                             "wall_GBs")}), flush=True)
     return out
 
@@ -69,7 +75,11 @@ def run_once(ctx, name):
     out = {"config": name, "solver": solver, "n": n, "options": CONFIGS[name][2], "converged": r["converged"],
            "iterations": r["iterations"], "wall_s": round(wall, 3), "kernel_ms": round(ms, 3),
            "algorithmic_GB": round(nb / 1e9, 3), "kernel_GBs": round(nb / (ms / 1e3) / 1e9, 1) if ms else None,
-           "wall_GBs": round(nb / wall / 1e9, 1), "ops": ops}
+           "wall_GBs": round(nb / wall / 1e9, 1), "ops": ops,
+           "reductions_per_iteration": round(sum(v["calls"] for op, v in led.items() if op.split("(")[0] in REDUCING)
+                                             / max(1, r["iterations"]), 1),
+           "launches_per_iteration": round(sum(v["calls"] for v in led.values()) / max(1, r["iterations"]), 1),
+           "host_overhead_ms": round(1e3 * wall - ms, 2)}
     if solver == "davidson":
         out["eigenvalues"] = [float(e) for e in r["eigenvalues"]]
     return out
@@ -77,10 +87,13 @@ def run_once(ctx, name):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="C2,C2-bgs,C3,C3-bgs,C5")
+    ap.add_argument("--configs", default="C2,C2-mgs,C3,C3-mgs,C5")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "solver_ledger.json"))
+    ap.add_argument("--rccl", action="store_true", help="attach a one-rank RCCL communicator (multi-rank path)")
     a = ap.parse_args()
     ctx = sh.Context(0)
+    if a.rccl:
+        ctx.attach_comm(1, 0, sh.Context.unique_id())
     res = [run(ctx, c) for c in a.configs.split(",")]
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
