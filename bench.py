@@ -444,7 +444,7 @@ def main():
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "frac": float(f"{achieved / HBM_PEAK_GBS:.4g}"),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "avg_launch_us": round(1e3 * e["ms"] / e["calls"], 2),
