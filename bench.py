@@ -34,6 +34,7 @@ import os
 import struct
 import sys
 import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -123,8 +124,13 @@ class Workload:
         return float(np.max(np.diag(g)))
 
 
-OP_KERNELS = {"gemm_inner": ("k_gemm_inner",), "gemm_outer": ("k_gemm_outer",), "axpy": ("k_axpy",),
-              "fill": ("k_fill",), "dot": ("k_dot_partial",)}
+def op_kernels(op, m):
+    """rocprofv3 kernel-name prefixes of `op`'s main kernel for m destinations / rows (the template
+    instance the launcher picks; older summaries predate the SET parameter)."""
+    mt = next(v for v in (1, 2, 4, 8, 16) if m <= v or v == 16)
+    return {"gemm_inner": ("k_gemm_inner<",), "gemm_outer": (f"k_gemm_outer<{mt}, false, false>", f"k_gemm_outer<{mt}, false>"),
+            "gemm_outer_set": (f"k_gemm_outer<{mt}, false, true>",), "axpy": ("k_axpy",), "fill": ("k_fill(",),
+            "dot": ("k_dot_partial",)}.get(op, ())
 
 
 def pmc_traffic(path, op, n_global, m, k, world):
@@ -137,11 +143,10 @@ def pmc_traffic(path, op, n_global, m, k, world):
     w = d.get("workload") or {}
     if (w.get("n_global"), w.get("roots"), w.get("qspace"), w.get("n_gpus")) != (n_global, m, k, world):
         return None, None
-    prefixes = OP_KERNELS.get(op, ())
-    for name, v in d["kernels"].items():
-        base = name.split("<")[0]
-        if base in prefixes:
-            return v["hbm_bytes_per_dispatch"], os.path.relpath(path, ROOT) + ":" + name
+    for prefix in op_kernels(op, m):
+        for name, v in d["kernels"].items():
+            if name == prefix.rstrip("(<") or name.startswith(prefix):
+                return v["hbm_bytes_per_dispatch"], os.path.relpath(path, ROOT) + ":" + name
     return None, None
 
 
@@ -182,7 +187,14 @@ def rendezvous_uid(rank, world, timeout=300.0):
 
 def cpu_baseline(m, k, seconds):
     """The oracle (CPU restatement of ArrayHandlerIterable: pairwise gemm, sequential loops) on one
-    host core, same op sequence, bounded sample."""
+    host core, same op sequence, bounded sample; then the host-parallel and DRAM-resident figures."""
+    cb = cpu_baseline_core(m, k, seconds)
+    cpu_baseline_extras(cb, m, k, seconds)
+    return cb
+
+
+def cpu_baseline_core(m, k, seconds):
+    """The 1-core leg of cpu_baseline (bench.py runs it beside the GPU's sustained phase)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
 
@@ -204,9 +216,6 @@ def cpu_baseline(m, k, seconds):
                 break
     except OSError:
         pass
-    hp = host_parallel(m, k, max(1.0, seconds / 3))
-    dram = {op: {kk: (round(v, 4) if isinstance(v, float) else v) for kk, v in d.items()}
-            for op, d in oracle.dram_resident_sample(SEED).items()}
     return {
         "value": step_bytes(n, m, k) * steps / dt / 1e9,
         "unit": "GB/s",
@@ -214,10 +223,19 @@ def cpu_baseline(m, k, seconds):
         "kind": "port",
         "sample": f"{steps} step(s) of the same op sequence at N=1e6 (m={m}, k={k}) on 1 core of "
                   f"{cpu} (nproc={os.cpu_count()}), {dt:.1f} s, oracle/oracle_ops.c (reference loops)",
-        "host_parallel": hp,
-        "dram_resident": dict(dram, note="one call each on 1 core, operands far beyond the host caches "
-                                         "(the N=1e6 step above is partly cache-resident)"),
     }
+
+
+def cpu_baseline_extras(cb, m, k, seconds):
+    """host-parallel (every host thread) and the DRAM-resident single calls, run with the GPU idle."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg only
+
+    cb["host_parallel"] = host_parallel(m, k, max(1.0, seconds / 3))
+    dram = {op: {kk: (round(v, 4) if isinstance(v, float) else v) for kk, v in d.items()}
+            for op, d in oracle.dram_resident_sample(SEED).items()}
+    cb["dram_resident"] = dict(dram, note="one call each on 1 core, operands far beyond the host caches "
+                                          "(the N=1e6 step above is partly cache-resident)")
 
 
 def host_parallel(m, k, seconds):
@@ -305,7 +323,11 @@ def main():
     ap.add_argument("--qsize", type=int, default=48)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--ledger-steps", type=int, default=3)
+    ap.add_argument("--ledger-steps", type=int, default=3,
+                    help="with --no-timed-ledger: extra steps under the HIP-event ledger after the timed region")
+    ap.add_argument("--no-timed-ledger", action="store_true",
+                    help="time the K steps without HIP events (the roofline ledger then runs on --ledger-steps "
+                         "extra steps); for measuring the events' cost")
     ap.add_argument("--no-in-solver", action="store_true", help="skip the whole-solve block")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
                     help="rank transport at N > 1: RCCL (the product path) or the host socket hub, which "
@@ -353,23 +375,38 @@ def main():
     for _ in range(args.warmup):
         wl.step()
     ctx.synchronize()
+    # The roofline ledger is the timed region itself: a HIP event pair on the context stream around
+    # every op of the K steps (the kernels' own stream; resolved after the region).
+    timed_ledger = not args.no_timed_ledger
+    if timed_ledger:  # one counted step sizes the event pool: no event is created inside the region
+        ctx.ledger_reset()
+        ctx.ledger_enable(True)
+        wl.step()
+        ctx.ledger_enable(False)
+        ctx.ledger_reserve(2 * sum(v["calls"] for v in ctx.ledger().values()) * args.steps)
+        ctx.synchronize()
+    ctx.ledger_reset()
+    ctx.ledger_enable(timed_ledger)
     barrier()
     t0 = time.perf_counter()
     for s in range(args.steps):
         wl.step()
     ctx.synchronize()
     t1 = time.perf_counter()
+    ctx.ledger_enable(False)
     barrier()
     elapsed = t1 - t0
     if world > 1:  # max over ranks
         elapsed = max(struct.unpack("<d", b)[0] for b in ctx.allgather_bytes(struct.pack("<d", elapsed)))
-
-    # Per-kernel HIP-event ledger over a few extra steps (not part of the timed region).
-    ctx.ledger_reset()
-    ctx.ledger_enable(True)
-    for _ in range(args.ledger_steps):
-        wl.step()
-    ctx.ledger_enable(False)
+    ledger_steps = args.steps
+    if not timed_ledger:
+        # Per-kernel HIP-event ledger over a few extra steps (not part of the timed region).
+        ctx.ledger_reset()
+        ctx.ledger_enable(True)
+        for _ in range(args.ledger_steps):
+            wl.step()
+        ctx.ledger_enable(False)
+        ledger_steps = args.ledger_steps
     led = ctx.ledger()
 
     # The product's own form of the same update (not the headline; see the module docstring).
@@ -398,6 +435,30 @@ def main():
         "ops": {op: {"calls_per_step": v["calls"], "avg_us": round(1e3 * v["ms"] / v["calls"], 2),
                      "GBs": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)} for op, v in pled.items()},
     }
+    # Sustained phase (rank 0 of a 1-GPU run): the headline step repeated on the GPU for as long as
+    # the 1-core CPU baseline runs on another host core -- the GPU's long-run rate over ~15 s beside the
+    # 0.8-8 s timed region.  The GPU thread only enqueues kernels and waits on reductions; the CPU leg
+    # streams host DRAM on its own core.  host-parallel (all host threads) runs later, GPU idle.
+    sustained, cb = None, None
+    run_cpu = world == 1 and not args.no_cpu_baseline
+    if run_cpu:
+        log("timing CPU baseline (oracle, 1 core) beside the GPU's sustained phase...")
+        box = {}
+        th = threading.Thread(target=lambda: box.update(cb=cpu_baseline_core(m, k, args.cpu_seconds)))
+        ctx.synchronize()
+        ts = time.perf_counter()
+        th.start()
+        n_sus = 0
+        while th.is_alive() or n_sus < 5:
+            wl.step()
+            n_sus += 1
+        ctx.synchronize()
+        ts = time.perf_counter() - ts
+        th.join()
+        cb = box["cb"]
+        sustained = {"steps": n_sus, "seconds": round(ts, 2), "ms_per_step": round(1e3 * ts / n_sus, 4),
+                     "GBs": round(step_bytes(n_global, m, k) * n_sus / ts / 1e9, 2),
+                     "note": "headline step repeated while the 1-core CPU baseline runs on another core"}
     wl.free()  # back to the arena before the whole solves
     solve = None
     if not args.no_in_solver:
@@ -411,7 +472,7 @@ def main():
         e = led[dom]
         achieved = (e["bytes"] / e["calls"]) / (e["ms"] / e["calls"] / 1e3) / 1e9
         traffic, traffic_src = pmc_traffic(args.pmc_json, dom, n_global, m, k, world)
-        ops = {op: {"calls_per_step": v["calls"] / args.ledger_steps,
+        ops = {op: {"calls_per_step": v["calls"] / ledger_steps,
                     "avg_us": 1e3 * v["ms"] / v["calls"],
                     "GBs": v["bytes"] / (v["ms"] / 1e3) / 1e9} for op, v in led.items()}
         result = {
@@ -451,6 +512,8 @@ def main():
                 "bytes_per_launch": e["bytes"] / e["calls"],
             },
             "ops": ops,
+            "ledger": "HIP events around every op of the timed steps" if timed_ledger
+                      else f"HIP events over {ledger_steps} extra steps after the timed region",
             "product_step": product,
             "in_solver": solve,
             "startup": {"ctx_create_s": round(ctx_create_s, 3),
@@ -467,11 +530,10 @@ def main():
             result["mfma"] = {"kernel": "gemm_inner", "achieved_tflops": round(tflops, 2),
                               "peak_tflops": MFMA_F64_PEAK_TFLOPS, "frac": round(tflops / MFMA_F64_PEAK_TFLOPS, 4),
                               "mfma_util_pct": util, "util_source": util_src}
-        if world == 1 and not args.no_cpu_baseline:
-            log("timing CPU baseline (oracle, 1 core)...")
-            result["cpu_baseline"] = cpu_baseline(m, k, args.cpu_seconds)
-        else:
-            result["cpu_baseline"] = None
+        if cb is not None:
+            cpu_baseline_extras(cb, m, k, args.cpu_seconds)
+        result["cpu_baseline"] = cb
+        result["sustained"] = sustained
         print(json.dumps(result), flush=True)
     barrier()
     ctx.close()

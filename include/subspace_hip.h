@@ -89,6 +89,8 @@ int ssp_shard_range(size_t n, int nranks, int rank, size_t* offset, size_t* leng
 int ssp_ledger_enable(ssp_ctx* ctx, int enable);
 int ssp_ledger_reset(ssp_ctx* ctx);
 int ssp_ledger_count(ssp_ctx* ctx);
+/* Pre-create n ledger events (2 per recorded op), so that a ledger over a timed region creates none. */
+int ssp_ledger_reserve(ssp_ctx* ctx, int n);
 int ssp_ledger_entry(ssp_ctx* ctx, int i, const char** name, long long* calls, double* kernel_ms, double* bytes);
 
 /* ---- dense (R x R, Q x Q, R x Q) operations: reference ArrayHandlerIterable.h:46-90,

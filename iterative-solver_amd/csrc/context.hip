@@ -284,6 +284,17 @@ int ssp_ledger_reset(ssp_ctx* ctx) {
   return SSP_OK;
 }
 
+int ssp_ledger_reserve(ssp_ctx* ctx, int n) {
+  SSP_CHECK_CTX(ctx);
+  SSP_TRY(ssp::use_device(ctx));
+  while (int(ctx->event_pool.size()) < n) {
+    hipEvent_t e = nullptr;
+    SSP_TRY_HIP(hipEventCreate(&e));
+    ctx->event_pool.push_back(e);
+  }
+  return SSP_OK;
+}
+
 int ssp_ledger_count(ssp_ctx* ctx) {
   if (!ctx) return -1;
   if (ssp::use_device(ctx) != SSP_OK || ssp::ledger_resolve(ctx) != SSP_OK) return -1;

@@ -33,7 +33,7 @@ EXPORTS = [
     "ssp_synchronize", "ssp_alloc", "ssp_free", "ssp_release_cached", "ssp_memory_stats", "ssp_upload",
     "ssp_download", "ssp_comm_unique_id", "ssp_ctx_attach_comm", "ssp_ctx_rank", "ssp_ctx_nranks",
     "ssp_allreduce_sum", "ssp_allgather_host", "ssp_ctx_attach_host_comm", "ssp_shard_range", "ssp_select_merge",
-    "ssp_ledger_enable", "ssp_ledger_reset", "ssp_ledger_count",
+    "ssp_ledger_enable", "ssp_ledger_reset", "ssp_ledger_count", "ssp_ledger_reserve",
     "ssp_ledger_entry", "ssp_fill", "ssp_scal", "ssp_copy", "ssp_axpy", "ssp_dot",
     "ssp_gemm_inner", "ssp_gemm_outer", "ssp_gemm_outer_set", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_precondition", "ssp_select", "ssp_select_max_dot",
     "ssp_sparse_copy", "ssp_sparse_axpy", "ssp_sparse_dot", "ssp_gemm_inner_sparse", "ssp_gemm_outer_sparse",
@@ -100,6 +100,7 @@ def _declare(lib):
         "ssp_ledger_enable": (I, [P, I]),
         "ssp_ledger_reset": (I, [P]),
         "ssp_ledger_count": (I, [P]),
+        "ssp_ledger_reserve": (I, [P, I]),
         "ssp_ledger_entry": (I, [P, I, C.POINTER(C.c_char_p), C.POINTER(C.c_longlong), PD, PD]),
         "ssp_fill": (I, [P, D, P, Z]),
         "ssp_scal": (I, [P, D, P, Z]),
@@ -438,6 +439,10 @@ class Context:
 
     def ledger_reset(self):
         _check(self.lib.ssp_ledger_reset(self.handle))
+
+    def ledger_reserve(self, n_events: int):
+        """Pre-create HIP events for a ledger of n_events / 2 ops (none created while it records)."""
+        _check(self.lib.ssp_ledger_reserve(self.handle, int(n_events)))
 
     def ledger(self) -> dict:
         """{op: {"calls": c, "ms": kernel milliseconds, "bytes": algorithmic bytes}}"""

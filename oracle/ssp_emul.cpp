@@ -166,6 +166,7 @@ int ssp_ledger_reset(ssp_ctx* c) {
   return SSP_OK;
 }
 int ssp_ledger_count(ssp_ctx* c) { return int(c->ledger.size()); }
+int ssp_ledger_reserve(ssp_ctx*, int) { return SSP_OK; }
 int ssp_ledger_entry(ssp_ctx* c, int i, const char** name, long long* calls, double* ms, double* bytes) {
   if (i < 0 || i >= int(c->ledger.size())) return fail(SSP_ERR_ARG, "ssp_ledger_entry: index out of range");
   const auto& e = c->ledger[size_t(i)];

@@ -82,6 +82,9 @@ def test_bench_single_gpu():
     d = parse(r.stdout)
     assert d["n_gpus"] == 1 and d["steps"] == 3 and d["cpu_baseline"]["value"] > 0
     assert d["config"]["n_global"] == 4_000_000
+    # the roofline ledger is the timed region: every op of the 3 steps carries its event pair
+    assert d["ledger"].startswith("HIP events around every op") and d["ops"]["gemm_outer"]["calls_per_step"] == 2
+    assert d["sustained"]["steps"] >= 5 and d["sustained"]["GBs"] > 0
 
 
 @pytest.mark.gpu
