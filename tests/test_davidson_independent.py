@@ -1,0 +1,166 @@
+"""The restated solver stack pinned by an INDEPENDENT restatement (oracle/davidson_np.py).
+
+The product's host layer (solvers.h / rspace.h / subspace.h / dense.h) is compiled both into the GPU
+library and, over CPU handlers, into the C++ oracle (oracle/itsolv_oracle.cpp), so the GPU-vs-oracle
+traces (test_traces_gpu.py) vary only the handlers.  oracle/davidson_np.py is a second reading of the
+reference's LinearEigensystemDavidson (IterativeSolverTemplate.h, propose_rspace.h, XSpace.h,
+QSpace.h, DSpaceResetter.h, helper-implementation.h eigenproblem), in numpy, sharing no code with
+those headers.  Agreement between the two, step for step, is what pins the host restatement.
+
+Bar (parity observables of IterativeSolverTemplate.h:322-408 and LinearEigensystemDavidson.h:79):
+identical iteration and R-creation counts, convergence flag, and after every iteration identical
+Q-space and working-set sizes; eigenvalues within 1e-10 relative after every iteration.  The cases
+cover P spaces (add_p, apply_p), Q-space limits with D-space construction (propose_rspace.h:568-588),
+D-space resets (DSpaceResetter.h:84-144), rank-8 and rank-16 synthetic problems and the reference's
+own matrices (examples/{he,bh,hf}.hamiltonian, test_simplified.cpp:24, test_LinearEigensystem.cpp
+n_eigen).  Slowly converging runs (~100 iterations at the smallest Q-space limits) are
+rounding-chaotic in the reference algorithm itself: there the CPU path's trajectory under a valid
+reordering of its own sums is the yardstick (test_slow_runs_agree_as_long_as_the_reference_agrees_with_itself).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import davidson_np as dn
+import oracle
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+EIG_REL = 1e-10
+
+
+def fixture_matrix(name):
+    txt = open(os.path.join(HERE, "golden", name + ".hamiltonian")).read().split()
+    n = int(txt[0])
+    return np.array([float(x) for x in txt[1:1 + n * n]]).reshape(n, n)
+
+
+def simplified(n=100):
+    # test_simplified.cpp:24
+    i = np.arange(n)
+    h = 0.001 * (i[:, None] + i[None, :])
+    h[i, i] = i + 1.0
+    return h
+
+
+def n_eigen(n=100):
+    # test_LinearEigensystem.cpp n_eigen family: H = 1 + diag(i)
+    return np.ones((n, n)) + np.diag(np.arange(n, dtype=np.float64))
+
+
+def assert_same_steps(ref, ind, name):
+    assert ref["converged"] == ind["converged"], name
+    assert ref["iterations"] == ind["iterations"], (name, ref["iterations"], ind["iterations"])
+    assert ref["r_creations"] == ind["r_creations"], (name, ref["r_creations"], ind["r_creations"])
+    tr, ti = ref["trace"], ind["trace"]
+    assert [int(x) for x in tr["nq"]] == ti["nq"], name
+    assert [int(x) for x in tr["nwork"]] == ti["nwork"], name
+    for it, (er, ei) in enumerate(zip(tr["eigenvalues"], ti["eigenvalues"])):
+        er = np.asarray(er)[: len(ei)]
+        ei = np.asarray(ei)
+        assert np.all(np.abs(er - ei) <= EIG_REL * np.maximum(np.abs(ei), 1.0)), (name, it, np.max(np.abs(er - ei)))
+    ef = np.asarray(ref["eigenvalues"])[: len(ind["eigenvalues"])]
+    assert np.all(np.abs(ef - ind["eigenvalues"]) <= EIG_REL * np.maximum(np.abs(ef), 1.0)), name
+
+
+# (n, rank, rho, nroots, max_p, max_size_qspace, reset_D); 0 = the reference's default
+SYNTHETIC = [
+    (2000, 1, 0.1, 1, 0, 6, 8),      # C1 shape, rank 1
+    (2000, 8, 0.1, 1, 0, 6, 8),      # C1 shape, rank 8: Q limit, D space, two resets
+    (5000, 8, 0.1, 4, 0, 24, 8),     # C2 shape
+    (5000, 8, 0.1, 8, 16, 48, 8),    # C3 shape
+    (20000, 8, 0.1, 8, 16, 48, 8),   # C3 shape, longer vectors
+    (3000, 1, 0.1, 8, 16, 48, 8),    # rank 1 with P: near-dependent residuals
+    (4000, 8, 0.3, 4, 8, 12, 4),     # P space + Q limit + resets
+    (8000, 8, 0.1, 8, 16, 16, 3),
+    (3000, 16, 0.5, 3, 6, 6, 5),     # 47 iterations through many resets
+]
+
+
+def options(nroots, max_p, q, rd):
+    o = dict(nroots=nroots, max_p=max_p, convergence_threshold=1e-8)
+    kw = dict(max_p=max_p)
+    if q:
+        o.update(max_size_qspace=q)
+        kw.update(max_size_qspace=q)
+    if rd:
+        o.update(reset_D=rd)
+        kw.update(reset_D=rd)
+    return o, kw
+
+
+@pytest.mark.parametrize("case", SYNTHETIC, ids=lambda c: "n{}_r{}_rho{}_roots{}_P{}_Q{}_D{}".format(*c))
+def test_synthetic_same_steps(case):
+    n, rank, rho, nroots, max_p, q, rd = case
+    o, kw = options(nroots, max_p, q, rd)
+    ref = oracle.davidson_synthetic(n, rho, rank, 1, solutions=False, **o)
+    ind = dn.Davidson(nroots, 1e-8, **kw).solve(dn.SyntheticProblem(n, rho, rank, 1))
+    assert_same_steps(ref, ind, str(case))
+
+
+DENSE = ([(f"{m}_roots{r}_P{p}", m, r, p, 0, 0) for m in ("he", "bh", "hf") for r in (1, 2, 3, 4)
+          for p in (0, r, 2 * r) if (m != "he" or 2 * r + p <= 4)]
+         + [(f"simplified_roots{r}_P{p}", "simplified", r, p, 0, 0) for r in (1, 3, 6) for p in (0, 10)]
+         + [(f"simplified_roots{r}_Q{q}", "simplified", r, 0, q, 4) for r in (1, 3, 6) for q in (3 * r,)]
+         + [(f"n_eigen_roots{r}", "n_eigen", r, 0, 0, 0) for r in (1, 2, 4)])
+
+
+@pytest.mark.parametrize("case", DENSE, ids=lambda c: c[0])
+def test_dense_same_steps(case):
+    name, mat, nroots, max_p, q, rd = case
+    h = {"simplified": simplified, "n_eigen": n_eigen}.get(mat, lambda: fixture_matrix(mat))()
+    o, kw = options(nroots, max_p, q, rd)
+    ref = oracle.davidson_dense(h, **o)
+    ind = dn.Davidson(nroots, 1e-8, **kw).solve(dn.DenseProblem(h))
+    assert_same_steps(ref, ind, name)
+
+
+def first_divergence(a, b):
+    for i, (x, y) in enumerate(zip(zip(a["nq"], a["nwork"]), zip(b["nq"], b["nwork"]))):
+        if (int(x[0]), int(x[1])) != (int(y[0]), int(y[1])):
+            return i
+    return min(len(a["nq"]), len(b["nq"]))
+
+
+def test_slow_runs_agree_as_long_as_the_reference_agrees_with_itself():
+    # rank 8, rho 0.3, 4 roots, Q limit 8, resets every 3: ~60-100 slowly converging iterations.  The CPU
+    # path leaves its own trajectory at iteration 47 when only its dot products are summed in another
+    # valid order (oracle.set_sum_order(1)); the independent restatement leaves it at 48.
+    n, rank, rho, nroots, q, rd = 4000, 8, 0.3, 4, 8, 3
+    o, kw = options(nroots, 0, q, rd)
+    try:
+        oracle.set_sum_order(1)
+        reordered = oracle.davidson_synthetic(n, rho, rank, 1, solutions=False, **o)
+    finally:
+        oracle.set_sum_order(0)
+    ref = oracle.davidson_synthetic(n, rho, rank, 1, solutions=False, **o)
+    ind = dn.Davidson(nroots, 1e-8, **kw).solve(dn.SyntheticProblem(n, rho, rank, 1))
+    self_div = first_divergence(ref["trace"], reordered["trace"])
+    ind_div = first_divergence(ref["trace"], ind["trace"])
+    assert self_div < ref["iterations"]  # the case is chaotic in the reference algorithm itself
+    assert ind_div >= 0.75 * self_div, (ind_div, self_div)
+    k = ind_div
+    er, ei = np.asarray(ref["trace"]["eigenvalues"][:k]), np.asarray(ind["trace"]["eigenvalues"][:k])
+    assert np.max(np.abs(er - ei)) <= EIG_REL * np.max(np.abs(er))
+
+
+def test_independent_restatement_reaches_the_exact_eigenvalues():
+    # the restatement is itself pinned by the exact answer (secular equation of diag(1+i) + rho 11^T)
+    n, rho = 3000, 0.1
+    ind = dn.Davidson(4, 1e-10).solve(dn.SyntheticProblem(n, rho, 1, 1))
+    exact = oracle.rank_one_eigenvalues(n, rho, 4)
+    np.testing.assert_allclose(ind["eigenvalues"], exact, rtol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [c for c in SYNTHETIC if c[0] <= 8000][:6],
+                         ids=lambda c: "n{}_r{}_rho{}_roots{}_P{}_Q{}_D{}".format(*c))
+def test_gpu_solver_same_steps_as_independent_restatement(ctx, case):
+    import itsolv_hbm as ih
+
+    n, rank, rho, nroots, max_p, q, rd = case
+    o, kw = options(nroots, max_p, q, rd)
+    gpu = ih.davidson_synthetic(ctx, n, rho, rank, 1, solutions=False, **o)
+    ind = dn.Davidson(nroots, 1e-8, **kw).solve(dn.SyntheticProblem(n, rho, rank, 1))
+    gpu["trace"] = {k: np.asarray(v).tolist() for k, v in gpu["trace"].items()}
+    assert_same_steps(gpu, ind, str(case))
