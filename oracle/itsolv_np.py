@@ -1,4 +1,4 @@
-"""Independent numpy restatement of the reference's LinearEigensystemDavidson solver stack.
+"""Independent numpy restatement of the reference's LinearEigensystemDavidson and NonLinearEquationsDIIS.
 
 TEST INFRASTRUCTURE (only tests/ import it).  It shares no code with the product's host layer
 (iterative-solver_amd/include/itsolv_hbm/{solvers,rspace,subspace,dense}.h) or with the C++ oracle
@@ -25,6 +25,9 @@ Followed, file:line under /root/reference/src/molpro/linalg/itsolv/:
   subspace/SubspaceSolverLinEig.h:32-57 solve_eigenvalue
   helper-implementation.h:221-231 get_rank, :263-296 svd_system (hermitian), :318-543 eigenproblem
   util.h:70-100 construct_solutions / delete_parameters; array/util/select.h:28-55 select
+  NonLinearEquationsDIIS.h:52-83 least_important_vector, :86-102 add_vector, :103-119 end_iteration;
+      subspace/SubspaceSolverDIIS.h:27-66; helper-implementation.h:619-669 solve_DIIS;
+      XSpace.h:45-50 (action . action H for DIIS)
 """
 from __future__ import annotations
 
@@ -123,6 +126,9 @@ class DenseProblem:
     def p_column(self, i):
         return self.h[:, i].copy()
 
+    def residual(self, x):
+        return self.h @ (x - 1.0)
+
 
 def splitmix64(z):
     z = (z + np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
@@ -164,6 +170,9 @@ class SyntheticProblem:
         c[i] += self.d0[i]
         return c
 
+    def residual(self, x):
+        return self.action(x - 1.0)
+
 
 # ---- the solver ----------------------------------------------------------------------------------
 class Davidson:
@@ -195,6 +204,7 @@ class Davidson:
         self.iterations = 0
         self.r_creations = 0
         self.solution_params = []  # DSpaceResetter's pending solutions
+        self.action_dot_action = False
         self.trace = {"eigenvalues": [], "errors": [], "nq": [], "nwork": []}
 
     # -- dimensions
@@ -232,10 +242,11 @@ class Davidson:
         k = len(params)
         qq_s = sym_overlap(params)
         qx_s = np.hstack([cross(params, pv), cross(params, qp), cross(params, dp)]) if nX else np.zeros((k, 0))
-        qq_h = cross(params, actions)
+        left = actions if self.action_dot_action else params  # XSpace.h:45-50
+        qq_h = sym_overlap(actions) if self.action_dot_action else cross(params, actions)
         qx_h = np.zeros((k, nX))
-        qx_h[:, nP:nP + nQ] = cross(params, qa)
-        qx_h[:, nP + nQ:] = cross(params, da)
+        qx_h[:, nP:nP + nQ] = cross(left, qa)
+        qx_h[:, nP + nQ:] = cross(left, da)
         xq_h = np.zeros((nX, k))
         xq_h[:nP, :] = cross(pv, actions)  # hermitian (XSpace.h:52-60)
         xq_h[nP:nP + nQ, :] = qx_h[:, nP:nP + nQ].T
@@ -594,3 +605,128 @@ class Davidson:
         converged = nwork == 0 and max(self.errors) <= self.thresh
         return {"converged": converged, "iterations": self.iterations, "r_creations": self.r_creations,
                 "eigenvalues": list(self.eigvals), "errors": list(self.errors), "trace": self.trace}
+
+
+def solve_diis(h):
+    """helper-implementation.h:619-669: the augmented B matrix [[H, -1], [-1, 0]] solved for
+    rhs (0, ..., 0, -1) by a JacobiSVD with threshold 0 (a full-rank solve); the first dim entries."""
+    dim = h.shape[0]
+    b = np.zeros((dim + 1, dim + 1))
+    b[:dim, :dim] = h
+    b[dim, :dim] = b[:dim, dim] = -1.0
+    rhs = np.zeros(dim + 1)
+    rhs[dim] = -1.0
+    u, sv, vt = np.linalg.svd(b)
+    coeffs = vt.T @ (np.where(sv > 0, 1.0 / np.where(sv > 0, sv, 1.0), 0.0) * (u.T @ rhs))
+    if np.any(np.isnan(coeffs)):
+        raise OverflowError("NaN detected in DIIS submatrix solution")
+    return coeffs[:dim]
+
+
+class DIIS(Davidson):
+    """NonLinearEquationsDIIS (hermitian X space, H = action . action) over the shared X-space code."""
+
+    def __init__(self, convergence_threshold=1e-8, max_size_qspace=INT_MAX, max_iter=100):
+        super().__init__(1, convergence_threshold, max_iter=max_iter)
+        self.diis_max_q = max_size_qspace
+        self.action_dot_action = True
+        self.converged_flag = False
+
+    def least_important_vector(self):
+        h = self.H
+        result = (0, DBL_MAX)
+        if h.shape[1] < 2:
+            return result
+        w, v = sym_eig_ascending(h)
+        evmax, second, first = 0.0, DBL_MAX, 0
+        for i in range(len(w)):
+            evmax = max(evmax, w[i])
+            if w[i] < second:
+                second, first = w[i], 1
+                for j in range(1, h.shape[0]):
+                    if abs(v[j, i]) > abs(v[first, i]):
+                        first = j
+        second /= evmax
+        if second > self.svd_thresh:
+            return h.shape[1] - 1, DBL_MAX
+        return first, second
+
+    def subspace_solve(self, nroots_max):
+        dim = self.H.shape[0]
+        self.solutions = np.zeros((1, dim))
+        if self.converged_flag:
+            self.solutions[0, 0] = 1.0
+            return  # errors kept (SubspaceSolverDIIS.h:40-44)
+        self.solutions[0] = solve_diis(self.H)
+        self.sub_errors = [self.H[0, 0]]
+
+    def solve_and_generate_working_set(self, params, actions):
+        self.subspace_solve(1)
+        self.solution([0], params, actions)
+        if not self.sub_errors:
+            self.sub_errors = [0.0]
+        self.sub_errors[0] = float(np.sqrt(abs(actions[0] @ actions[0])))
+        self.errors = list(self.sub_errors)  # set_value_errors is the base no-op: no value errors
+        ws = [0] if self.errors[0] > self.thresh else []
+        self.working_set = ws
+        return len(ws)
+
+    def solution(self, roots, params, actions):
+        xs = self.construct_solution(roots)
+        gs = self.construct_solution(roots, with_p=False, actions=True)  # residual: no construct_residual
+        for k in range(len(roots)):
+            params[k] = xs[k]
+            actions[k] = gs[k]
+
+    def add_vector(self, params, actions):
+        x, r = params[0], actions[0]
+        error = float(np.sqrt(r @ r))
+        self.converged_flag = error < self.thresh
+        d = self.least_important_vector()
+        while self.nX >= self.diis_max_q or d[1] < self.svd_thresh:
+            self.eraseq(d[0])
+            d = self.least_important_vector()
+        nw = min(len(self.working_set), 1)
+        self.r_creations += nw
+        self.update_qspace([x][:nw], [r][:nw])
+        nwork = self.solve_and_generate_working_set(params, actions)
+        self.errors[0] = error
+        return nwork
+
+    def end_iteration(self, params, actions):
+        if self.working_set:
+            params[0] = self.construct_solution(self.working_set)[0]
+        if self.errors[0] < self.thresh:
+            self.working_set = []
+            return 0
+        self.working_set = [0]
+        params[0] = params[0] - actions[0]
+        self.iterations += 1
+        return 1
+
+    def solve(self, problem, generate_initial_guess=False):
+        """IterativeSolverTemplate::solve for a nonlinear solver: x starts at e_0 (the product's DIIS
+        driver), r = residual(x), preconditioner shift 0 (IterativeSolver.h:320-322)."""
+        self.problem, self.n = problem, problem.n
+        x = np.zeros(self.n)
+        x[0] = 1.0
+        params, actions = [x], [np.zeros(self.n)]
+        diag = problem.diagonals()
+        nwork = 1
+        for it in range(self.max_iter):
+            if nwork <= 0:
+                break
+            actions[0] = problem.residual(params[0])
+            nwork = self.add_vector(params, actions)
+            end_needed = True
+            while end_needed:
+                if nwork > 0:
+                    actions[0] = actions[0] / (diag - 0.0 + 1e-15)
+                nwork = self.end_iteration(params, actions)
+                end_needed = False
+            self.trace["errors"].append(list(self.errors))
+            self.trace["nq"].append(self.nQ)
+            self.trace["nwork"].append(len(self.working_set))
+        converged = nwork == 0 and max(self.errors) <= self.thresh
+        return {"converged": converged, "iterations": self.iterations, "r_creations": self.r_creations,
+                "errors": list(self.errors), "x": params[0], "trace": self.trace}
