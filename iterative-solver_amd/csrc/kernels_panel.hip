@@ -124,10 +124,13 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
 
 // Panels of 1 x 1 and 1 x 2 (or 2 x 1) vectors: with only one or two MFMA operand rows live, the
 // 4x4x4 layout leaves 3/4 of the lanes idle on loads (tools/shapes_bench.py: 1 x 1 at 3.4 TB/s),
-// so these run on the VALU with every lane streaming 16 B per vector, 4 positions in flight.  (The
-// window shape of the other streaming kernels changes this kernel's summation order, which moved
-// DIIS (n = 1e5, rank 2, rho = 0.01) from the reference's 15 iterations to 30: the stride shape,
-// whose order matches the CPU path's trajectory there, stays.)
+// so these run on the VALU with every lane streaming 16 B per vector, 4 positions in flight.  This
+// kernel keeps the grid-stride shape (the other streaming kernels moved to windows): with the window
+// order DIIS on (n = 1e5, rank 2, rho = 0.01) took 30 iterations instead of 15.  That case is not a
+// parity guarantee either way -- from its sixth step DIIS's residual-overlap matrix is singular to
+// rounding, and an independent restatement with LAPACK subspace solves takes 14
+// (tests/test_davidson_independent.py) -- the stride shape is kept because it converges there in the
+// reference's count, not because any summation order is exact.
 template <int K>
 __global__ __launch_bounds__(kBlock) void k_gemm_inner_row(const InnerArgs a) {
   using ssp::ld2nt;

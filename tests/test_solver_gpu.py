@@ -84,13 +84,23 @@ def test_synthetic_davidson_gpu_vs_cpu(ctx, rank, nroot, np_):
 
 @pytest.mark.parametrize("n,rank,rho", [(1000, 3, 0.01), (3000, 3, 0.01), (100_000, 2, 0.01)])
 def test_diis_synthetic_converges_gpu_vs_cpu(ctx, n, rank, rho):
-    # Well-conditioned cases (<= 15 iterations).  With rho = 0.1 the reference DIIS trajectory is
-    # sensitive to rounding (see the two tests below).
+    # Cases of <= 15 iterations.  With rho = 0.1 the reference DIIS trajectory is sensitive to rounding
+    # (see the two tests below).  (100_000, 2, 0.01) is sensitive to the DENSE solver: the reference
+    # CPU path takes 15 iterations with sequential or reordered sums, the independent restatement
+    # (oracle/itsolv_np.py, LAPACK for the subspace solves) 14, because from the sixth step DIIS's
+    # residual-overlap matrix is singular to rounding (tests/test_davidson_independent.py); there the
+    # count is checked within that spread and the first five steps to rounding.
     kw = dict(convergence_threshold=1e-8, max_size_qspace=6)
     gpu, cpu = ih.diis_synthetic(ctx, n, rho, rank, 3, **kw), oracle.diis_synthetic(n, rho, rank, 3, **kw)
     assert gpu["converged"] and cpu["converged"]
-    assert gpu["iterations"] == cpu["iterations"]
     np.testing.assert_allclose(gpu["x"], np.ones(n), atol=1e-8)
+    if n < 100_000:
+        assert gpu["iterations"] == cpu["iterations"]
+        return
+    assert abs(gpu["iterations"] - cpu["iterations"]) <= 1, (gpu["iterations"], cpu["iterations"])
+    e_g = [x[0] for x in gpu["trace"]["errors"][:5]]
+    e_c = [x[0] for x in cpu["trace"]["errors"][:5]]
+    np.testing.assert_allclose(e_g, e_c, rtol=1e-6)
 
 
 def test_diis_synthetic_rounding_sensitive_case(ctx):
