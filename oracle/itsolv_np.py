@@ -25,6 +25,9 @@ Followed, file:line under /root/reference/src/molpro/linalg/itsolv/:
   subspace/SubspaceSolverLinEig.h:32-57 solve_eigenvalue
   helper-implementation.h:221-231 get_rank, :263-296 svd_system (hermitian), :318-543 eigenproblem
   util.h:70-100 construct_solutions / delete_parameters; array/util/select.h:28-55 select
+  LinearEquationsDavidson.h:46-60 end_iteration, :170-181 construct_residual; XSpace.h:218-230
+      add_rhs_equations, :273-276 update_rhs_with_pspace; SubspaceSolverLinEig.h:59-79
+      solve_linear_equations; helper-implementation.h:555-614 solve_LinearEquations (incl. augmented Hessian)
   NonLinearEquationsDIIS.h:52-83 least_important_vector, :86-102 add_vector, :103-119 end_iteration;
       subspace/SubspaceSolverDIIS.h:27-66; helper-implementation.h:619-669 solve_DIIS;
       XSpace.h:45-50 (action . action H for DIIS)
@@ -205,6 +208,7 @@ class Davidson:
         self.r_creations = 0
         self.solution_params = []  # DSpaceResetter's pending solutions
         self.action_dot_action = False
+        self.record_eigenvalues = True
         self.trace = {"eigenvalues": [], "errors": [], "nq": [], "nwork": []}
 
     # -- dimensions
@@ -354,11 +358,28 @@ class Davidson:
         for k, r in enumerate(roots):  # apply_p: the P-space part of the action (:210-211)
             for j, i in enumerate(self.P):
                 gs[k] = gs[k] + self.problem.p_column(i) * self.solutions[r, j]
-        for k, r in enumerate(roots):  # construct_residual (LinearEigensystemDavidson.h:186-192)
-            gs[k] = gs[k] - self.eigvals[r] * xs[k]
+        for k, r in enumerate(roots):
+            gs[k] = self.construct_residual(r, xs[k], gs[k])
         for k in range(len(roots)):
             params[k] = xs[k]
             actions[k] = gs[k]
+
+    def construct_residual(self, root, x, g):
+        """LinearEigensystemDavidson.h:186-192: g -= lambda x."""
+        return g - self.eigvals[root] * x
+
+    def set_value_errors(self):
+        """LinearEigensystemDavidson.h:106-113."""
+        cur = list(self.eigvals)
+        self.value_errors = [DBL_MAX] * len(cur)
+        for i in range(min(len(self.last_values), len(cur))):
+            self.value_errors[i] = abs(cur[i] - self.last_values[i])
+        if not self.resetting:
+            self.last_values = cur
+
+    def shifts(self):
+        """working_set_eigenvalues (LinearEigensystemDavidson.h:98-104)."""
+        return [self.eigvals[i] for i in self.working_set]
 
     def solve_and_generate_working_set(self, params, actions):
         self.subspace_solve(self.nroots)
@@ -371,16 +392,11 @@ class Davidson:
             self.solution(roots, params, actions)
             for k, r in enumerate(roots):
                 self.sub_errors[r] = float(np.sqrt(abs(actions[k] @ actions[k])))
-        # set_value_errors (LinearEigensystemDavidson.h:106-113)
-        cur = list(self.eigvals)
-        self.value_errors = [DBL_MAX] * len(cur)
-        for i in range(min(len(self.last_values), len(cur))):
-            self.value_errors[i] = abs(cur[i] - self.last_values[i])
-        if not self.resetting:
-            self.last_values = cur
+        self.set_value_errors()
         self.errors = list(self.sub_errors)
         # select_working_set (:104-117): value threshold is DBL_MAX, so only errors decide
-        cand = [i for i, e in enumerate(self.errors) if e > self.thresh or self.value_errors[i] > DBL_MAX]
+        cand = [i for i, e in enumerate(self.errors)
+                if e > self.thresh or (i < len(self.value_errors) and self.value_errors[i] > DBL_MAX)]
         cand.sort(key=lambda i: -self.errors[i])  # multimap<greater>: equal keys keep insertion order
         ws = sorted(cand[:nbuf])
         self.working_set = ws
@@ -593,12 +609,13 @@ class Davidson:
                 end_needed = True
             while end_needed:
                 if nwork > 0:
-                    shifts = [self.eigvals[i] for i in self.working_set]
+                    shifts = self.shifts()
                     for k in range(nwork):
                         actions[k] = actions[k] / (diag - shifts[k] + 1e-15)
                 nwork = self.end_iteration(params, actions)
                 end_needed = False
-            self.trace["eigenvalues"].append(list(self.eigvals))
+            if self.record_eigenvalues:
+                self.trace["eigenvalues"].append(list(self.eigvals))
             self.trace["errors"].append(list(self.errors))
             self.trace["nq"].append(self.nQ)
             self.trace["nwork"].append(len(self.working_set))
@@ -730,3 +747,93 @@ class DIIS(Davidson):
         converged = nwork == 0 and max(self.errors) <= self.thresh
         return {"converged": converged, "iterations": self.iterations, "r_creations": self.r_creations,
                 "errors": list(self.errors), "x": params[0], "trace": self.trace}
+
+
+class LinearEquations(Davidson):
+    """LinearEquationsDavidson (hermitian by default): A x_r = b_r for the given right-hand sides."""
+
+    def __init__(self, rhs, convergence_threshold=1e-8, max_size_qspace=INT_MAX, reset_D=INT_MAX,
+                 reset_D_max_Q_size=INT_MAX, augmented_hessian=0.0, max_p=0, max_iter=100):
+        super().__init__(len(rhs), convergence_threshold, max_size_qspace, reset_D, reset_D_max_Q_size, max_p,
+                         max_iter=max_iter)
+        self.b = [np.array(r, dtype=np.float64) for r in rhs]
+        self.b_norm = []
+        for r in self.b:  # XSpace::add_rhs_equations
+            d = abs(r @ r)
+            if d == 0:
+                raise RuntimeError("RHS vector cannot be zero")
+            self.b_norm.append(np.sqrt(d))
+        self.ah = augmented_hessian
+        self.RHS = np.zeros((0, len(self.b)))  # data[rhs]: nX x nRHS
+        self.record_eigenvalues = False
+
+    # the rhs block follows every change of the X space
+    def update_qspace(self, params, actions):
+        nP, k = self.nP, len(params)
+        rows = cross(params, self.b)  # XSpace.h:65
+        self.RHS = np.vstack([self.RHS[:nP], rows, self.RHS[nP:]])
+        super().update_qspace(params, actions)
+
+    def update_dspace(self, dparams, dactions):
+        super().update_dspace(dparams, dactions)
+        keep = self.RHS[: self.nP + self.nQ]
+        self.RHS = np.vstack([keep, cross([p for p, _ in self.d], self.b)]) if self.nD else keep.copy()
+
+    def update_pspace(self, pidx, pp_action):
+        super().update_pspace(pidx, pp_action)
+        self.RHS = cross([self._p_vec(i) for i in range(self.nP)], self.b)
+
+    def eraseq(self, i):
+        self.RHS = np.delete(self.RHS, self.nP + i, axis=0)
+        super().eraseq(i)
+
+    def subspace_solve(self, nroots_max):
+        """SubspaceSolverLinEig::solve_linear_equations -> solve_LinearEquations."""
+        nx, nr = self.H.shape[0], len(self.b)
+        self.eigvals = np.zeros(nr)
+        sol = np.zeros((nr, nx))
+        if self.ah > 0:
+            import scipy.linalg
+
+            flat = self.RHS.reshape(-1)  # rhs[i + nX * root] of the row-major nX x nRHS block
+            for root in range(nr):
+                a = np.zeros((nx + 1, nx + 1))
+                b = np.zeros((nx + 1, nx + 1))
+                a[:nx, :nx] = self.H.T  # column-major Map of the row-major H (helper-implementation.h:571)
+                b[:nx, :nx] = self.S.T
+                col = -self.ah * flat[np.arange(nx) + nx * root]
+                a[:nx, nx] = a[nx, :nx] = col
+                b[nx, nx] = 1.0
+                w, v = scipy.linalg.eig(a, b)
+                imax = 0
+                for i in range(nx + 1):
+                    if w[i].real < w[imax].real:
+                        imax = i
+                self.eigvals[root] = w[imax].real
+                sol[root] = v[:nx, imax].real / (self.ah * v[nx, imax].real)
+        else:
+            sol = np.linalg.solve(self.H, self.RHS).T
+        self.solutions = sol
+        self.sub_errors = [DBL_MAX] * nr
+
+    def construct_residual(self, root, x, g):
+        """LinearEquationsDavidson.h:170-181: g = (g - b_root) / |b_root|."""
+        g = g - self.b[root]
+        if self.b_norm[root] != 0:
+            g = g * (1.0 / self.b_norm[root])
+        return g
+
+    def set_value_errors(self):
+        self.value_errors = []  # the base no-op: LinearEquationsDavidson has no value errors
+
+    def shifts(self):
+        return [0.0] * len(self.working_set)  # IterativeSolver.h:320-322
+
+    def end_iteration(self, params, actions):
+        do_reset = ((self.iterations + 1) % self.reset_D == 0 and self.nD > 0) or bool(self.solution_params)
+        if do_reset:
+            self.working_set = self.dspace_reset_run(params)
+        else:
+            self.working_set = self.propose_rspace(params, actions)
+        self.iterations += 1
+        return len(self.working_set)
