@@ -374,6 +374,7 @@ int ssp_ctx_destroy(ssp_ctx* ctx) {
   if (ctx->result_host) (void)hipHostFree(ctx->result_host);
   if (ctx->pub_flag) (void)hipHostFree(ctx->pub_flag);
   if (ctx->fold_counter) (void)hipFree(ctx->fold_counter);
+  if (ctx->synth_mask) (void)hipFree(ctx->synth_mask);
   if (ctx->ring_dev) (void)hipFree(ctx->ring_dev);
   if (ctx->ring_host) (void)hipHostFree(ctx->ring_host);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -59,6 +59,13 @@ struct ssp_ctx {
   size_t ring_cap = 0;
   size_t ring_head = 0;
 
+  // Synthetic test problem (synthetic.hip): the per-element sign masks of u_1..u_{rank-1}, computed
+  // once per (seed, rank, shard) and reused by every action of a solve.
+  unsigned short* synth_mask = nullptr;
+  size_t synth_mask_n = 0, synth_mask_offset = 0;
+  unsigned long long synth_mask_seed = 0;
+  int synth_mask_rank = 0;
+
   // Communicator (RCCL over xGMI, one process per GPU).
   ncclComm_t comm = nullptr;
   // Host-callback communicator (ssp_ctx_attach_host_comm), used instead of RCCL when set.

@@ -4,6 +4,7 @@
 // reference test/itsolv/test_rayleigh_quotient.cpp:37-42 for rank 1) and u_l(g) = +/-1 from
 // splitmix64 for l > 0.  Applying H costs one rank x nvec reduction (+ allreduce) and one stream.
 #include <algorithm>
+#include <cstdint>
 #include <vector>
 
 #include "ssp_internal.h"
@@ -26,8 +27,11 @@ inline unsigned long long stream_key(unsigned long long seed, unsigned long long
   return splitmix64(seed ^ (stream * 0xD1B54A32D192ED03ull));
 }
 
-// Bit l of the mask is set when u_l(g) = -1 (u_0 = 1 always): the R - 1 hashes of an element are
-// computed once and shared by every vector of the launch.
+// Bit l of the mask is set when u_l(g) = -1 (u_0 = 1 always).  The masks are computed once per
+// (seed, rank, shard) into a 2-byte-per-element table (sspx_synthetic_action's cache in the context),
+// so the action kernels stream x, y and the table instead of evaluating rank - 1 splitmix64 hashes
+// (two 64-bit multiplies each) per element and pass: 3.3 TB/s with the hashes inline, the table adds
+// 2 B per element to the 16-24 B per element and vector the kernels move.
 template <int R>
 __device__ __forceinline__ unsigned sign_mask(const unsigned long long (&key)[16], unsigned long long g) {
   unsigned m = 0;
@@ -42,6 +46,7 @@ struct SynthArgs {
   const double* x[kMaxVec];
   double* y[kMaxVec];
   unsigned long long key[kMaxRank];
+  const unsigned short* mask;  // [n] sign masks of this shard
   int nvec;
   int rank;
   size_t n;
@@ -50,6 +55,13 @@ struct SynthArgs {
   double* partial;      // [grid][nvec*rank]
   const double* coeff;  // [nvec*rank] global u_l . x_v
 };
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_synth_mask(const SynthArgs a, unsigned short* mask) {
+  const size_t stride = size_t(gridDim.x) * kBlock;
+  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
+    mask[i] = (unsigned short)sign_mask<R>(a.key, a.offset + i);
+}
 
 __device__ __forceinline__ double block_sum(double v, double* wsum) {
 #pragma unroll
@@ -64,27 +76,40 @@ __device__ __forceinline__ double block_sum(double v, double* wsum) {
   return s;
 }
 
+// Element pairs: 16 B of each vector and 4 B of the mask table per lane and visit (the tail element
+// of an odd-length shard is folded in by the thread that owns pair n/2).
+__device__ __forceinline__ double2 ld2nt(const double* p) { return ssp::ld2nt(p); }
+
 // Per-block partial sums of u_l . x_v, vectors in groups of G (R x G accumulators per thread).
 template <int R, int G>
 __global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a) {
   __shared__ double wsum[kBlock / 64];
-  const size_t stride = size_t(gridDim.x) * kBlock;
+  const size_t stride = size_t(gridDim.x) * kBlock, n2 = a.n >> 1;
+  const unsigned* mask2 = reinterpret_cast<const unsigned*>(a.mask);
   for (int v0 = 0; v0 < a.nvec; v0 += G) {
     double s[G][R];
 #pragma unroll
     for (int v = 0; v < G; ++v)
 #pragma unroll
       for (int l = 0; l < R; ++l) s[v][l] = 0;
-    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
-      const unsigned mask = sign_mask<R>(a.key, a.offset + i);
+    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += stride) {
+      const unsigned mm = mask2[i];
 #pragma unroll
       for (int v = 0; v < G; ++v) {
         if (v0 + v < a.nvec) {
-          const double xv = __builtin_nontemporal_load(a.x[v0 + v] + i);
+          const double2 xv = ld2nt(a.x[v0 + v] + 2 * i);
 #pragma unroll
-          for (int l = 0; l < R; ++l) s[v][l] += flip(mask, l, xv);
+          for (int l = 0; l < R; ++l) s[v][l] += flip(mm, l, xv.x) + flip(mm >> 16, l, xv.y);
         }
       }
+    }
+    if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+      const unsigned mm = a.mask[a.n - 1];
+#pragma unroll
+      for (int v = 0; v < G; ++v)
+        if (v0 + v < a.nvec)
+#pragma unroll
+          for (int l = 0; l < R; ++l) s[v][l] += flip(mm, l, a.x[v0 + v][a.n - 1]);
     }
 #pragma unroll
     for (int v = 0; v < G; ++v) {
@@ -99,23 +124,44 @@ __global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a) {
   }
 }
 
+template <int R>
+__device__ __forceinline__ double lowrank(unsigned mm, const double* c) {
+  double s = 0;
+#pragma unroll
+  for (int l = 0; l < R; ++l) s += flip(mm, l, c[l]);
+  return s;
+}
+
 // y_v = d x_v + rho sum_l u_l coeff[v][l]   (ADD = false)
 // y_v += rho sum_l u_l coeff[v][l]          (ADD = true, the P-space low-rank term)
 template <int R, bool ADD>
 __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
-  const size_t stride = size_t(gridDim.x) * kBlock;
-  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
-    const unsigned long long g = a.offset + i;
-    const unsigned mask = sign_mask<R>(a.key, g);
-    const double d = 1.0 + double(g);
+  const size_t stride = size_t(gridDim.x) * kBlock, n2 = a.n >> 1;
+  const unsigned* mask2 = reinterpret_cast<const unsigned*>(a.mask);
+  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += stride) {
+    const unsigned mm = mask2[i];
+    const size_t g = a.offset + 2 * i;
+    const double d0 = 1.0 + double(g), d1 = 1.0 + double(g + 1);
     for (int v = 0; v < a.nvec; ++v) {
-      double s = 0;
-#pragma unroll
-      for (int l = 0; l < R; ++l) s += flip(mask, l, a.coeff[v * R + l]);
-      if (ADD)
-        a.y[v][i] = fma(a.rho, s, a.y[v][i]);
-      else
-        a.y[v][i] = fma(d, __builtin_nontemporal_load(a.x[v] + i), a.rho * s);
+      const double s0 = lowrank<R>(mm, a.coeff + v * R), s1 = lowrank<R>(mm >> 16, a.coeff + v * R);
+      double2 out;
+      if (ADD) {
+        const double2 y = *reinterpret_cast<const double2*>(a.y[v] + 2 * i);
+        out = make_double2(fma(a.rho, s0, y.x), fma(a.rho, s1, y.y));
+      } else {
+        const double2 x = ld2nt(a.x[v] + 2 * i);
+        out = make_double2(fma(d0, x.x, a.rho * s0), fma(d1, x.y, a.rho * s1));
+      }
+      ssp::st2nt(a.y[v] + 2 * i, out);
+    }
+  }
+  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const size_t e = a.n - 1;
+    const unsigned mm = a.mask[e];
+    const double d = 1.0 + double(a.offset + e);
+    for (int v = 0; v < a.nvec; ++v) {
+      const double s = lowrank<R>(mm, a.coeff + v * R);
+      a.y[v][e] = ADD ? fma(a.rho, s, a.y[v][e]) : fma(d, a.x[v][e], a.rho * s);
     }
   }
 }
@@ -152,6 +198,45 @@ void synth_apply(unsigned grid, hipStream_t st, const SynthArgs& a) {
     SSP_RANK_CASES(F)
 #undef F
   }
+}
+
+void synth_mask_kernel(unsigned grid, hipStream_t st, const SynthArgs& a, unsigned short* mask) {
+  switch (a.rank) {
+#define F(r)                                                                                \
+  case r:                                                                                   \
+    hipLaunchKernelGGL((k_synth_mask<r>), dim3(grid), dim3(kBlock), 0, st, a, mask); \
+    break;
+    SSP_RANK_CASES(F)
+#undef F
+  }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// The shard's sign-mask table for (seed, rank, offset, n), built on first use (one hash pass).
+int ensure_mask(ssp_ctx* ctx, SynthArgs& a, unsigned long long seed) {
+  if (ctx->synth_mask && ctx->synth_mask_n == a.n && ctx->synth_mask_offset == a.offset &&
+      ctx->synth_mask_seed == seed && ctx->synth_mask_rank == a.rank) {
+    a.mask = ctx->synth_mask;
+    return SSP_OK;
+  }
+  if (ctx->synth_mask) {
+    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    SSP_TRY_HIP(hipFree(ctx->synth_mask));
+    ctx->synth_mask = nullptr;
+  }
+  // +1 element: the pair loads of an odd-length shard stay inside the table
+  SSP_TRY_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->synth_mask), (a.n + 2) * sizeof(unsigned short)));
+  ctx->synth_mask_n = a.n;
+  ctx->synth_mask_offset = a.offset;
+  ctx->synth_mask_seed = seed;
+  ctx->synth_mask_rank = a.rank;
+  if (a.n > 0) {
+    synth_mask_kernel(ssp::stream_grid(ctx, a.n, 1), ctx->stream, a, ctx->synth_mask);
+    SSP_TRY_HIP(hipGetLastError());
+  }
+  a.mask = ctx->synth_mask;
+  return SSP_OK;
 }
 
 __global__ __launch_bounds__(kBlock) void k_synth_diag(double* d, size_t n, size_t offset, double rho, int rank) {
@@ -198,7 +283,11 @@ int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* 
   SSP_CHECK_CTX(ctx);
   if (rank < 1 || rank > kMaxRank) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_action: rank out of [1,16]");
   if (nvec < 0) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_action: nvec < 0");
-  // x read twice (coefficients, then apply) and y written: 24 N per vector.
+  for (int v = 0; v < nvec; ++v)
+    if (!aligned16(xx[v]) || !aligned16(yy[v]))
+      return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_action: vectors must be 16-byte aligned");
+  // x read twice (coefficients, then apply) and y written: 24 N per vector (the 2 B per element
+  // sign table is not counted).
   ssp::LedgerScope ls(ctx, "action(synthetic)", 24.0 * n * nvec);
   for (int v0 = 0; v0 < nvec; v0 += kMaxVec) {
     SynthArgs a{};
@@ -212,6 +301,7 @@ int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* 
       a.y[v] = yy[v0 + v];
     }
     for (int l = 0; l < rank; ++l) a.key[l] = stream_key(seed, 1000 + l);
+    SSP_TRY(ensure_mask(ctx, a, seed));
     const int nc = a.nvec * rank;
     const unsigned grid = std::min<unsigned>(ssp::stream_grid(ctx, n, 4), 1024);
     SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * nc));
@@ -245,6 +335,8 @@ int sspx_synthetic_add_lowrank(ssp_ctx* ctx, double* const* yy, int nvec, size_t
   SSP_CHECK_CTX(ctx);
   if (rank < 1 || rank > kMaxRank) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_add_lowrank: rank out of [1,16]");
   if (n == 0 || nvec <= 0) return SSP_OK;
+  for (int v = 0; v < nvec; ++v)
+    if (!aligned16(yy[v])) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_add_lowrank: vectors must be 16-byte aligned");
   ssp::LedgerScope ls(ctx, "p_action(synthetic)", 16.0 * n * nvec);
   for (int v0 = 0; v0 < nvec; v0 += kMaxVec) {
     SynthArgs a{};
@@ -255,6 +347,7 @@ int sspx_synthetic_add_lowrank(ssp_ctx* ctx, double* const* yy, int nvec, size_t
     a.rho = rho;
     for (int v = 0; v < a.nvec; ++v) a.y[v] = yy[v0 + v];
     for (int l = 0; l < rank; ++l) a.key[l] = stream_key(seed, 1000 + l);
+    SSP_TRY(ensure_mask(ctx, a, seed));
     void* coeff;
     SSP_TRY(ssp::upload_small(ctx, w + size_t(v0) * rank, size_t(a.nvec) * rank * sizeof(double), &coeff));
     a.coeff = static_cast<const double*>(coeff);
