@@ -28,6 +28,9 @@ Followed, file:line under /root/reference/src/molpro/linalg/itsolv/:
   LinearEquationsDavidson.h:46-60 end_iteration, :170-181 construct_residual; XSpace.h:218-230
       add_rhs_equations, :273-276 update_rhs_with_pspace; SubspaceSolverLinEig.h:59-79
       solve_linear_equations; helper-implementation.h:555-614 solve_LinearEquations (incl. augmented Hessian)
+  OptimizeBFGS.h:40-185 (Wolfe tests, cubic line search, two-loop BFGS update), OptimizeSD.h:37-95,
+      subspace/SubspaceSolverOptBFGS.h / SubspaceSolverOptSD.h, Interpolate.cpp:51-66 cubic, :115-134
+      minimize_cubic (Interpolate.h:46: analytic by default)
   NonLinearEquationsDIIS.h:52-83 least_important_vector, :86-102 add_vector, :103-119 end_iteration;
       subspace/SubspaceSolverDIIS.h:27-66; helper-implementation.h:619-669 solve_DIIS;
       XSpace.h:45-50 (action . action H for DIIS)
@@ -208,6 +211,7 @@ class Davidson:
         self.r_creations = 0
         self.solution_params = []  # DSpaceResetter's pending solutions
         self.action_dot_action = False
+        self.hermitian = True
         self.record_eigenvalues = True
         self.trace = {"eigenvalues": [], "errors": [], "nq": [], "nwork": []}
 
@@ -252,10 +256,14 @@ class Davidson:
         qx_h[:, nP:nP + nQ] = cross(left, qa)
         qx_h[:, nP + nQ:] = cross(left, da)
         xq_h = np.zeros((nX, k))
-        xq_h[:nP, :] = cross(pv, actions)  # hermitian (XSpace.h:52-60)
-        xq_h[nP:nP + nQ, :] = qx_h[:, nP:nP + nQ].T
-        xq_h[nP + nQ:, :] = qx_h[:, nP + nQ:].T
-        qx_h[:, :nP] = xq_h[:nP, :].T
+        if self.hermitian:  # XSpace.h:52-60
+            xq_h[:nP, :] = cross(pv, actions)
+            xq_h[nP:nP + nQ, :] = qx_h[:, nP:nP + nQ].T
+            xq_h[nP + nQ:, :] = qx_h[:, nP + nQ:].T
+            qx_h[:, :nP] = xq_h[:nP, :].T
+        else:  # XSpace.h:61-64: <x_old, action_new>
+            xq_h[nP:nP + nQ, :] = cross(qp, actions)
+            xq_h[nP + nQ:, :] = cross(dp, actions)
         xq_s = qx_s.T
         for name, qq, qx, xq in (("S", qq_s, qx_s, xq_s), ("H", qq_h, qx_h, xq_h)):
             old = getattr(self, name)
@@ -837,3 +845,204 @@ class LinearEquations(Davidson):
             self.working_set = self.propose_rspace(params, actions)
         self.iterations += 1
         return len(self.working_set)
+
+
+class Cubic:
+    """Interpolate(p0, p1, "cubic") and its analytic minimum (Interpolate.cpp:56-66, :101-134);
+    points are (x, f, f1)."""
+
+    def __init__(self, p0, p1):
+        self.x0, self.x1 = p0[0], p1[0]
+        x1mx0 = p1[0] - p0[0]
+        f1pf0, f1mf0 = p1[1] + p0[1], p1[1] - p0[1]
+        g1pg0, g1mg0 = p1[2] + p0[2], p1[2] - p0[2]
+        self.c = [0.5 * f1pf0 - 0.125 * g1mg0 * x1mx0, -0.25 * g1pg0 + 1.5 * f1mf0 / x1mx0, 0.5 * g1mg0 / x1mx0,
+                  (-2 * f1mf0 + g1pg0 * x1mx0) / x1mx0 ** 3]
+
+    def __call__(self, x):
+        c, xb = self.c, 0.5 * (self.x1 + self.x0)
+        t = x - xb
+        return x, c[0] + t * (c[1] + t * (c[2] + t * c[3])), c[1] + t * (2 * c[2] + 3 * t * c[3])
+
+    def minimize_cubic(self):
+        cc, b, a = self.c[1], 2 * self.c[2], 3 * self.c[3]
+        with np.errstate(all="ignore"):
+            disc = b * b / (4 * a * a) - cc / a
+        if np.isnan(disc) or disc < 0:
+            return float("nan")
+        xb = 0.5 * (self.x1 + self.x0)
+        pm = self(xb - (b / (2 * a)) + np.sqrt(disc))
+        pp = self(xb - (b / (2 * a)) - np.sqrt(disc))
+        return pm[0] if pm[1] < pp[1] else pp[0]
+
+
+class Optimize(Davidson):
+    """OptimizeBFGS (bfgs = True) / OptimizeSD over a non-hermitian X space; value data as the reference
+    keeps it (BFGS shifts it with the Q space, SD overwrites its first row)."""
+
+    def __init__(self, bfgs=True, convergence_threshold=1e-8, max_size_qspace=INT_MAX, max_iter=100):
+        super().__init__(1, convergence_threshold, max_iter=max_iter)
+        self.bfgs = bfgs
+        self.hermitian = False
+        self.opt_max_q = max_size_qspace
+        self.value = np.zeros(0)
+        self.alpha = []
+        self.linesearch = False
+        self.last_linesearching = False
+        self.strong_wolfe, self.wolfe1, self.wolfe2 = True, 1e-4, 0.9
+        self.ls_tol, self.ls_grow = 0.2, 2.0
+        self.record_eigenvalues = False
+        self.line_searches = 0
+
+    def eraseq(self, i):
+        self.value = np.delete(self.value, self.nP + i)
+        super().eraseq(i)
+
+    def subspace_solve(self, nroots_max):
+        dim = self.H.shape[0]
+        self.solutions = np.zeros((1, dim))
+        self.solutions[0, 0] = 1.0
+        self.sub_errors = [self.H[0, 0]]
+
+    def set_value_errors(self):
+        self.value_errors = [DBL_MAX]
+        if self.nX > 1 and self.value[0] < self.value[1]:
+            self.value_errors[0] = self.value[1] - self.value[0]
+
+    def solution(self, roots, params, actions):
+        xs = self.construct_solution(roots)
+        gs = self.construct_solution(roots, with_p=False, actions=True)
+        for k in range(len(roots)):
+            params[k] = xs[k]
+            actions[k] = gs[k]
+
+    def solve_and_generate_working_set(self, params, actions):
+        self.subspace_solve(1)
+        self.solution([0], params, actions)
+        self.sub_errors[0] = float(np.sqrt(abs(actions[0] @ actions[0])))
+        self.set_value_errors()
+        self.errors = list(self.sub_errors)
+        ws = [0] if (self.errors[0] > self.thresh or self.value_errors[0] > DBL_MAX) else []
+        self.working_set = ws
+        return len(ws)
+
+    def base_add_vector(self, params, actions):
+        nw = min(len(self.working_set), 1)
+        self.r_creations += nw
+        self.update_qspace(params[:nw], actions[:nw])
+        return self.solve_and_generate_working_set(params, actions)
+
+    def _h4(self, a):
+        h = self.H
+        return h[a, a] - h[a, a + 1] - h[a + 1, a] + h[a + 1, a + 1]
+
+    def add_vector(self, params, actions, value):
+        if not self.bfgs:  # OptimizeSD.h:79-87
+            v = np.zeros(self.nX + 1)
+            v[: len(self.value)] = self.value[: self.nX + 1]
+            v[0] = value
+            self.value = v
+            return self.base_add_vector(params, actions)
+        while self.nX >= self.opt_max_q:
+            self.eraseq(self.nX - 1)
+        self.value = np.r_[value, self.value]
+        nwork = self.base_add_vector(params, actions)
+        if self.nX > 1:
+            fprev, fcur = self.value[1], self.value[0]
+            gprev, gcur = self.H[0, 1] - self.H[1, 1], self.H[0, 0] - self.H[1, 0]
+            w1 = fcur <= fprev + self.wolfe1 * gprev
+            w2 = gcur >= self.wolfe2 * gprev if self.strong_wolfe else abs(gcur) <= self.wolfe2 * abs(gprev)
+            if not (w1 and w2):
+                x = Cubic((-1.0, fprev, gprev), (0.0, fcur, gcur)).minimize_cubic()
+                if abs(x) > self.ls_tol:
+                    params[0] = params[0] * (1 + x)
+                    params[0] = params[0] + (-x) * self.q[1][0]
+                    self.eraseq(0 if fprev < fcur else 1)
+                    self.linesearch = True
+                    return -1
+        self.linesearch = False
+        while True:  # accept: drop a Q pair that makes a BFGS denominator vanish
+            # (the reference indexes past the shrunken H when an erase leaves fewer pairs than alphas;
+            # the loop stops at the last pair, as the product's restatement does)
+            for a in range(min(len(self.alpha), self.nX - 1)):
+                if abs(self._h4(a)) < max(5e-14 * abs(self.H[a, a]), 1e-15):
+                    self.eraseq(a + 1)
+                    break
+            else:
+                break
+        g = actions[0]  # BFGS_update_1 (OptimizeBFGS.h:135-146)
+        self.alpha = [0.0] * (self.nX - 1)
+        for a in range(len(self.alpha)):
+            qa, qb = self.q[a][0], self.q[a + 1][0]
+            self.alpha[a] = ((g @ qa) - (g @ qb)) / self._h4(a)
+            g = g + (-self.alpha[a]) * self.q[a][1]
+            g = g + self.alpha[a] * self.q[a + 1][1]
+        actions[0] = g
+        return nwork
+
+    def end_iteration(self, params, actions):
+        if not self.bfgs:  # OptimizeSD.h:37-47
+            if self.working_set:
+                params[0] = self.construct_solution(self.working_set)[0]
+            if self.errors[0] < self.thresh:
+                self.working_set = []
+                return 0
+            self.working_set = [0]
+            params[0] = params[0] - actions[0]
+            self.iterations += 1
+            return 1
+        self.working_set = [0]
+        if not self.linesearch:
+            self.last_linesearching = False
+            params[0] = self.construct_solution([0])[0]
+            if self.errors[0] < self.thresh:
+                self.working_set = []
+                return 0
+            z = actions[0]  # BFGS_update_2 (:148-157)
+            for a in range(len(self.alpha) - 1, -1, -1):
+                beta = ((z @ self.q[a][1]) - (z @ self.q[a + 1][1])) / self._h4(a)
+                z = z + (self.alpha[a] - beta) * self.q[a][0]
+                z = z + (-self.alpha[a] + beta) * self.q[a + 1][0]
+            params[0] = params[0] - z
+        else:
+            if not self.last_linesearching:
+                self.line_searches += 1
+            self.last_linesearching = True
+        self.iterations += 1
+        return 0 if self.errors[0] < self.thresh else 1
+
+    def solve(self, problem, generate_initial_guess=False):
+        """IterativeSolverTemplate::solve, nonlinear branch: value = residual(x, g); add_vector; the
+        diagonal preconditioner with shift 0 when nwork > 0; end_iteration.  x starts at e_0."""
+        self.problem, self.n = problem, problem.n
+        x = np.zeros(self.n)
+        x[0] = 1.0
+        params, actions = [x], [np.zeros(self.n)]
+        diag = problem.diagonals()
+        nwork = 1
+        for it in range(self.max_iter):
+            if nwork <= 0 and it > 0:
+                break
+            f, actions[0] = problem.value_gradient(params[0])
+            nwork = self.add_vector(params, actions, f)
+            if nwork > 0:
+                actions[0] = actions[0] / (diag - 0.0 + 1e-15)
+            nwork = self.end_iteration(params, actions)
+            self.trace["eigenvalues"].append([self.value[0]])
+            self.trace["errors"].append(list(self.errors))
+            self.trace["nq"].append(self.nQ)
+            self.trace["nwork"].append(len(self.working_set))
+        converged = nwork == 0 and max(self.errors) <= self.thresh
+        return {"converged": converged, "iterations": self.iterations, "r_creations": self.r_creations,
+                "errors": list(self.errors), "x": params[0], "value": self.value[0], "trace": self.trace}
+
+
+class RayleighProblem(DenseProblem):
+    """f(x) = x.Hx / x.x, g = 2 (Hx - f x) / x.x (the product's optimize_dense problem,
+    test_Optimize.cpp's Rayleigh-quotient form)."""
+
+    def value_gradient(self, x):
+        g = self.h @ x
+        xx, xg = x @ x, x @ g
+        f = xg / xx
+        return f, (g - f * x) * (2 / xx)

@@ -299,3 +299,94 @@ def test_gpu_linear_equations_same_steps_as_independent_restatement(ctx, case):
     assert gpu["converged"] == ind["converged"] and gpu["iterations"] == ind["iterations"], name
     assert [int(x) for x in gpu["trace"]["nq"]] == ind["trace"]["nq"], name
     assert [int(x) for x in gpu["trace"]["nwork"]] == ind["trace"]["nwork"], name
+
+
+# ---- OptimizeBFGS / OptimizeSD (§8f row 4) on the Rayleigh quotient f = x.Hx / x.x from e_0 ----------------
+def _opt_matrices():
+    rng = np.random.default_rng(1)
+    a = rng.standard_normal((60, 60)) * 0.05
+    return {"he": fixture_matrix("he"), "bh": fixture_matrix("bh"), "hf": fixture_matrix("hf"),
+            "simplified": simplified(), "random60": np.diag(np.linspace(1, 3, 60)) + a + a.T}
+
+
+OPT_M = _opt_matrices()
+
+
+def _run_opt(mat, alg, q):
+    kw = dict(convergence_threshold=1e-8)
+    if q:
+        kw["max_size_qspace"] = q
+    ref = oracle.optimize_dense(OPT_M[mat], alg, **kw)
+    ind = dn.Optimize(alg == "BFGS", 1e-8, max_size_qspace=q or dn.INT_MAX).solve(dn.RayleighProblem(OPT_M[mat]))
+    return kw, ref, ind
+
+
+def _assert_opt_prefix(ref, ind, k, name):
+    assert [int(x) for x in ref["trace"]["nq"][:k]] == ind["trace"]["nq"][:k], name
+    assert [int(x) for x in ref["trace"]["nwork"][:k]] == ind["trace"]["nwork"][:k], name
+    v = np.array([x[0] for x in ref["trace"]["eigenvalues"][:k]])
+    vi = np.array([x[0] for x in ind["trace"]["eigenvalues"][:k]])
+    assert np.all(np.abs(v - vi) <= 1e-12 * np.abs(v) + 1e-14), (name, np.max(np.abs(v - vi)))
+
+
+@pytest.mark.parametrize("mat", ["he", "bh", "hf", "simplified", "random60"])
+@pytest.mark.parametrize("q", [0, 4])
+def test_optimize_sd_same_steps(mat, q):
+    # OptimizeSD.h:37-95: 41-100 iterations, every step identical (values within 6e-14 measured)
+    kw, ref, ind = _run_opt(mat, "SD", q)
+    assert ref["converged"] == ind["converged"] and ref["iterations"] == ind["iterations"]
+    _assert_opt_prefix(ref, ind, len(ref["trace"]["nq"]), (mat, q))
+
+
+@pytest.mark.parametrize("mat,q", [("he", 0), ("he", 4), ("simplified", 0), ("simplified", 4), ("random60", 4)])
+def test_optimize_bfgs_same_steps(mat, q):
+    # OptimizeBFGS.h:40-185: Wolfe tests, cubic line searches and the two-loop update, step for step
+    kw, ref, ind = _run_opt(mat, "BFGS", q)
+    assert ref["converged"] == ind["converged"] and ref["iterations"] == ind["iterations"]
+    _assert_opt_prefix(ref, ind, len(ref["trace"]["nq"]), (mat, q))
+
+
+def test_optimize_bfgs_convergence_step_is_a_knife_edge():
+    # random60, unlimited Q: 53 identical steps; at the converged point the Wolfe test compares values
+    # equal to rounding, so the CPU path takes one extra line-search step (54 iterations) where the
+    # restatement takes the quasi-Newton step (53); both converge with the same final error.
+    kw, ref, ind = _run_opt("random60", "BFGS", 0)
+    assert ref["converged"] and ind["converged"] and abs(ref["iterations"] - ind["iterations"]) <= 1
+    k = min(ref["iterations"], ind["iterations"])
+    _assert_opt_prefix(ref, ind, k, "random60")
+    assert abs(ref["trace"]["errors"][k][0] - ind["trace"]["errors"][k][0]) <= 1e-6 * ref["trace"]["errors"][k][0]
+
+
+def first_divergence_opt(a, b):
+    return first_divergence(a["trace"], b["trace"])
+
+
+@pytest.mark.parametrize("mat,q", [("bh", 0), ("bh", 4), ("hf", 0), ("hf", 4)])
+def test_optimize_bfgs_chaotic_cases_agree_as_long_as_the_reference_agrees_with_itself(mat, q):
+    # bh / hf: the CPU path leaves its own step sequence after 31-67 steps when only its sums are
+    # reordered (oracle.set_sum_order(1)); the restatement leaves it after 39-67.
+    kw, ref, ind = _run_opt(mat, "BFGS", q)
+    try:
+        oracle.set_sum_order(1)
+        reordered = oracle.optimize_dense(OPT_M[mat], "BFGS", **kw)
+    finally:
+        oracle.set_sum_order(0)
+    self_div = first_divergence_opt(ref, reordered)
+    ind_div = first_divergence_opt(ref, ind)
+    assert ind_div >= 0.75 * self_div, (ind_div, self_div)
+    v = np.array([x[0] for x in ref["trace"]["eigenvalues"][:ind_div]])
+    vi = np.array([x[0] for x in ind["trace"]["eigenvalues"][:ind_div]])
+    assert np.max(np.abs(v - vi)) <= 1e-2 * abs(v[-1] - v[0]) + 1e-10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mat,alg,q", [("he", "BFGS", 0), ("simplified", "BFGS", 4), ("random60", "BFGS", 4),
+                                       ("simplified", "SD", 0)])
+def test_gpu_optimize_same_steps_as_independent_restatement(ctx, mat, alg, q):
+    import itsolv_hbm as ih
+
+    kw, _, ind = _run_opt(mat, alg, q)
+    gpu = ih.optimize_dense(ctx, OPT_M[mat], alg, **kw)
+    assert gpu["converged"] == ind["converged"] and gpu["iterations"] == ind["iterations"], (mat, alg, q)
+    gpu["trace"] = {k: np.asarray(v).tolist() for k, v in gpu["trace"].items()}
+    _assert_opt_prefix(gpu, ind, len(ind["trace"]["nq"]), (mat, alg, q))
