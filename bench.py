@@ -23,6 +23,8 @@ Beside the headline the JSON line carries (none of them inside the timed region)
   in_solver     whole LinearEigensystemDavidson solves (C3 at N = 1: 8 roots + P 16, rank-8 problem,
                 N = 1e8; at N > 1 the same solve sharded, BASELINE config C4): iterations, wall time,
                 kernel time and algorithmic bytes from the HIP-event ledger, reductions per iteration;
+  in_solver_diis  the same for NonLinearEquationsDIIS on BASELINE config C5's problem (N = 1e8, sharded
+                at N > 1);
   startup       context creation and the first (cold) solve against the warm one;
   cpu_baseline.dram_resident  one call each of the reference loops on DRAM-resident operands.
 """
@@ -262,12 +264,16 @@ def host_parallel(m, k, seconds):
 
 
 C3 = dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48, reset_D=8, convergence_threshold=1e-8)
+# BASELINE config C5 (NonLinearEquationsDIIS, N = 1e8): the DIIS problem of tools/solver_ledger.py and
+# tests/golden/traces.json (r = H (x - 1), x from e_0, test_NonLinearEquations.cpp:25-49)
+C5 = dict(rho=0.01, rank=3, seed=3, max_size_qspace=6, convergence_threshold=1e-8)
 REDUCING_OPS = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "select", "sparse")
 
 
-def in_solver(ctx, n_global, world, barrier, repeat=2):
-    """Whole Davidson solves (C3 options; sharded over the ranks = C4 at N > 1) with the ledger on.
-    Returns the last (warm) solve's numbers and the first (cold) solve's wall time."""
+def in_solver(ctx, n_global, world, barrier, repeat=2, kind="davidson"):
+    """Whole solves with the ledger on: Davidson with C3's options (sharded over the ranks = C4 at
+    N > 1) or, kind = "diis", NonLinearEquationsDIIS with C5's.  Returns the last (warm) solve's
+    numbers and the first (cold) solve's wall time."""
     import itsolv_hbm as ih
 
     def allmax(x):
@@ -281,7 +287,10 @@ def in_solver(ctx, n_global, world, barrier, repeat=2):
         ctx.ledger_enable(rep == repeat - 1)
         barrier()
         t0 = time.perf_counter()
-        r = ih.davidson_synthetic(ctx, n_global, n_local=0, **C3)
+        if kind == "diis":
+            r = ih.diis_synthetic(ctx, n_global, n_local=0, **C5)
+        else:
+            r = ih.davidson_synthetic(ctx, n_global, n_local=0, **C3)
         ctx.synchronize()
         walls.append(allmax(time.perf_counter() - t0))
         ctx.ledger_enable(False)
@@ -291,9 +300,14 @@ def in_solver(ctx, n_global, world, barrier, repeat=2):
     red = sum(v["calls"] for op, v in led.items() if op.split("(")[0] in REDUCING_OPS or op.startswith("select"))
     it = max(1, r["iterations"])
     top = sorted(led.items(), key=lambda kv: -kv[1]["ms"])[:6]
+    if kind == "diis":
+        config = ("NonLinearEquationsDIIS C5: r = H (x - 1), H = diag(1+i) + 0.01 sum_{l<3} u u^T, x from e_0, "
+                  "max_size_qspace 6, threshold 1e-8" + (f", sharded over {world} ranks" if world > 1 else ""))
+    else:
+        config = ("LinearEigensystemDavidson " + ("C3" if world == 1 else "C4") + ": 8 roots + P 16, rank-8 "
+                  "H = diag(1+i) + 0.1 sum u u^T, max_size_qspace 48, reset_D 8, threshold 1e-8")
     return {
-        "config": "LinearEigensystemDavidson " + ("C3" if world == 1 else "C4") + ": 8 roots + P 16, rank-8 "
-                  "H = diag(1+i) + 0.1 sum u u^T, max_size_qspace 48, reset_D 8, threshold 1e-8",
+        "config": config,
         "n_global": n_global,
         "converged": bool(r["converged"]),
         "iterations": r["iterations"],
@@ -308,7 +322,8 @@ def in_solver(ctx, n_global, world, barrier, repeat=2):
         "top_ops": {op: {"calls": v["calls"], "ms": round(v["ms"], 2),
                          "GBs": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] else None}
                     for op, v in top},
-        "eigenvalues": [round(float(e), 12) for e in r["eigenvalues"][:8]],
+        "eigenvalues": [round(float(e), 12) for e in r["eigenvalues"][:8]] if kind != "diis" else None,
+        "final_error": float(r["errors"][0]) if kind == "diis" else None,
     }
 
 
@@ -460,9 +475,10 @@ def main():
                      "GBs": round(step_bytes(n_global, m, k) * n_sus / ts / 1e9, 2),
                      "note": "headline step repeated while the 1-core CPU baseline runs on another core"}
     wl.free()  # back to the arena before the whole solves
-    solve = None
+    solve = solve_diis = None
     if not args.no_in_solver:
         solve = in_solver(ctx, n_global, world, barrier)
+        solve_diis = in_solver(ctx, n_global, world, barrier, kind="diis")
 
     total_bytes = step_bytes(n_global, m, k) * args.steps
     value = total_bytes / elapsed / 1e9
@@ -516,6 +532,7 @@ def main():
                       else f"HIP events over {ledger_steps} extra steps after the timed region",
             "product_step": product,
             "in_solver": solve,
+            "in_solver_diis": solve_diis,
             "startup": {"ctx_create_s": round(ctx_create_s, 3),
                         "first_solve_wall_s": solve["wall_s_cold"] if solve else None,
                         "warm_solve_wall_s": solve["wall_s"] if solve else None},
