@@ -45,6 +45,15 @@ def test_pmc_traffic_lookup():
     assert bench.pmc_traffic("/nonexistent.json", "dot", 1, 1, 1, 1) == (None, None)
 
 
+def test_pmc_traffic_lookup_r2_names_the_rmw_instance():
+    # r2's summary holds both gemm_outer instances; the roofline kernel is the read-modify-write one
+    path = os.path.join(ROOT, "profiles", "r2", "pmc_traffic_n1e8.json")
+    t, src = bench.pmc_traffic(path, "gemm_outer", 10**8, 8, 48, 1)
+    assert src.endswith("k_gemm_outer<8, false, false>") and abs(t - 8 * 10**8 * (48 + 16)) / t < 0.02
+    t, src = bench.pmc_traffic(path, "gemm_outer_set", 10**8, 8, 48, 1)
+    assert src.endswith("k_gemm_outer<8, false, true>") and abs(t - 8 * 10**8 * (48 + 8)) / t < 0.02
+
+
 def test_mfma_util_lookup():
     path = os.path.join(ROOT, "profiles", "r1", "mfma_util_n1e8.json")
     util, src = bench.mfma_util(path)
