@@ -153,6 +153,46 @@ def case_spmd(gloo=False):
         comm.close()
 
 
+def case_c4(gloo=False):
+    """BASELINE configs C4 / C5 at world size 8 (socket host communicator): the sharded Davidson with
+    C3/C4's options and the sharded DIIS with C5's, at N = 16_003 (shards 2000-2001 long), against the
+    independent restatement (oracle/itsolv_np.py) and the unsharded CPU path (rank 0 checks): same
+    steps."""
+    import itsolv_np
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    comm = sh.HubComm(rank, world, "127.0.0.1", int(os.environ["SSP_HUB_PORT"]))
+    ctx = sh.Context(0)
+    ctx.attach_host_comm(comm)
+    n = 16_003
+    _, nl = sh.shard_range(n, world, rank)
+    kw = dict(nroots=8, max_p=16, convergence_threshold=1e-8, max_size_qspace=48, reset_D=8)
+    got = ih.davidson_synthetic(ctx, n, 0.1, 8, 1, n_local=nl, **kw)
+    c5 = dict(convergence_threshold=1e-8, max_size_qspace=6)
+    got5 = ih.diis_synthetic(ctx, n, 0.01, 3, 3, n_local=nl, **c5)
+    comm.barrier()
+    comm.close()
+    if rank:
+        return
+    ind = itsolv_np.Davidson(8, 1e-8, max_size_qspace=48, reset_D=8, max_p=16).solve(
+        itsolv_np.SyntheticProblem(n, 0.1, 8, 1))
+    ref = oracle.davidson_synthetic(n, 0.1, 8, 1, solutions=False, **kw)
+    print("c4: sharded", got["iterations"], "iterations; independent", ind["iterations"], "; cpu", ref["iterations"],
+          "; c5 sharded", got5["iterations"], flush=True)
+    for other in (ind, ref):
+        assert got["converged"] == other["converged"] and got["iterations"] == other["iterations"]
+        assert got["r_creations"] == other["r_creations"]
+        assert [int(x) for x in got["trace"]["nq"]] == [int(x) for x in other["trace"]["nq"]]
+        assert [int(x) for x in got["trace"]["nwork"]] == [int(x) for x in other["trace"]["nwork"]]
+        assert np.max(np.abs(got["eigenvalues"] - np.asarray(other["eigenvalues"])[:8])) <= 1e-10 * 9
+    got = got5
+    ind = itsolv_np.DIIS(1e-8, max_size_qspace=6).solve(itsolv_np.SyntheticProblem(n, 0.01, 3, 3))
+    assert got["converged"] and ind["converged"] and got["iterations"] == ind["iterations"]
+    e = [x[0] for x in got["trace"]["errors"][:5]]
+    ei = [x[0] for x in ind["trace"]["errors"][:5]]
+    assert np.allclose(e, ei, rtol=1e-4, atol=0), (e, ei)
+
+
 if __name__ == "__main__":
-    {"api": case_api, "spmd": case_spmd, "spmd-gloo": lambda: case_spmd(gloo=True)}[sys.argv[1]]()
+    {"api": case_api, "spmd": case_spmd, "spmd-gloo": lambda: case_spmd(gloo=True), "c4": case_c4}[sys.argv[1]]()
     print(f"{sys.argv[1]} OK", flush=True)

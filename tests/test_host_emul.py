@@ -6,7 +6,8 @@ C API and its Python binding -- on CPU, over the host-memory emulation of the de
   loop taking the same iterations as the CPU reference path on the fixtures;
 * world size 2 (socket host communicator, and gloo): Davidson with and without a P space, DIIS
   and the C API with shard ranges + sync, each rank holding its index range of every vector,
-  against the unsharded CPU reference path (same iterations, eigenvalues within 1e-10).
+  against the unsharded CPU reference path (same iterations, eigenvalues within 1e-10);
+* world size 8: C4's sharded Davidson and C5's sharded DIIS against the independent restatement.
 
 The same host code over the real HIP library is tests/test_python_api_gpu.py,
 tests/test_solver_gpu.py and tests/test_distributed_gpu.py.
@@ -41,3 +42,17 @@ def test_world2_sharded_solvers_gloo():
            "127.0.0.1", "--master-port", str(free_port()), WORKER, "spmd-gloo"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.count("OK") == 2, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_world8_c4_c5_sharded_against_independent_restatement():
+    # the driver's 8-GPU configuration (C4: 8 roots + P 16 sharded over 8 ranks; C5: DIIS sharded) on
+    # the host emulation, each rank holding its index range: the same steps as the independent
+    # numpy restatement and the unsharded CPU path
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, WORKER, "c4"],
+                              env=dict(os.environ, RANK=str(r), WORLD_SIZE="8", SSP_HUB_PORT=str(port),
+                                       OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1"),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(8)]
+    outs = [p.communicate(timeout=900)[0] for p in procs]
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0 and "c4 OK" in out, out[-3000:]
