@@ -19,7 +19,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-for p in (ROOT, os.path.join(ROOT, "iterative-solver_amd"), os.path.join(ROOT, "oracle")):
+for p in (ROOT, os.path.join(ROOT, "iterative-solver_amd"), os.path.join(ROOT, "oracle"), HERE):
     sys.path.insert(0, p)
 
 EPS = 2.220446049250313e-16
@@ -156,13 +156,25 @@ def case_gpu_solver(comm):
     ctx.close()
 
 
+def case_gpu_distr(comm):
+    """The reference's distributed-array known answers (tests/distr_cases.py) on HBM shards."""
+    import distr_cases
+    import subspace_hip as sh
+
+    ctx = sh.Context(0)
+    ctx.attach_host_comm(comm)
+    distr_cases.check(ctx, sh, comm.rank, comm.nranks)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--comm", choices=["gloo", "hub"], required=True)
-    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver"], required=True)
+    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver", "gpu_distr"], required=True)
     a = ap.parse_args()
     comm = make_comm(a.comm)
-    {"reductions": case_reductions, "gpu_ops": case_gpu_ops, "gpu_solver": case_gpu_solver}[a.case](comm)
+    {"reductions": case_reductions, "gpu_ops": case_gpu_ops, "gpu_solver": case_gpu_solver,
+     "gpu_distr": case_gpu_distr}[a.case](comm)
     if a.comm == "gloo":
         import torch.distributed as dist
 

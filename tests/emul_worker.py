@@ -193,6 +193,19 @@ def case_c4(gloo=False):
     assert np.allclose(e, ei, rtol=1e-4, atol=0), (e, ei)
 
 
+def case_distr():
+    """The reference's distributed-array known answers (tests/distr_cases.py) at this world size."""
+    import distr_cases
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    comm = sh.HubComm(rank, world, "127.0.0.1", int(os.environ["SSP_HUB_PORT"]))
+    ctx = sh.Context(0)
+    ctx.attach_host_comm(comm)
+    distr_cases.check(ctx, sh, rank, world)
+    comm.barrier()
+    comm.close()
+
+
 if __name__ == "__main__":
-    {"api": case_api, "spmd": case_spmd, "spmd-gloo": lambda: case_spmd(gloo=True), "c4": case_c4}[sys.argv[1]]()
+    {"api": case_api, "spmd": case_spmd, "spmd-gloo": lambda: case_spmd(gloo=True), "c4": case_c4, "distr": case_distr}[sys.argv[1]]()
     print(f"{sys.argv[1]} OK", flush=True)

@@ -22,3 +22,8 @@ def test_world2_ops_on_shards():
 
 def test_world2_davidson_and_diis_on_shards():
     run_hub("gpu_solver", timeout=900)
+
+
+def test_world2_reference_distributed_array_known_answers():
+    # testDistrArray.h / testArrayHandlerDistrSparse.cpp known answers on HBM shards (tests/distr_cases.py)
+    run_hub("gpu_distr", timeout=300)

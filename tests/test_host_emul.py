@@ -16,6 +16,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from test_distributed import free_port
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -56,3 +58,17 @@ def test_world8_c4_c5_sharded_against_independent_restatement():
     outs = [p.communicate(timeout=900)[0] for p in procs]
     for p, out in zip(procs, outs):
         assert p.returncode == 0 and "c4 OK" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_reference_distributed_array_known_answers(world):
+    # testDistrArray.h / testArrayHandlerDistrSparse.cpp / testDistribution.cpp known answers on the
+    # sharded ops at world sizes 1-4 (tests/distr_cases.py)
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, WORKER, "distr"],
+                              env=dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), SSP_HUB_PORT=str(port),
+                                       OMP_NUM_THREADS="1"),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    outs = [p.communicate(timeout=300)[0] for p in procs]
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0 and "distr OK" in out, out[-3000:]
