@@ -11,6 +11,10 @@ the one device through the host communicator).
   testArrayHandlerDistrSparse.cpp:23-62   sparse axpy and dot over dim 20 with
                                {1: 1, 3: 2, 6: 3, 11: 4}: dot = 0.5 (1 + 2 + 3 + 4) = 5
   testDistribution.cpp:58-62   make_distribution_spread_remainder(11, 3) = {0, 4, 8, 11}
+  testGemm.cpp:228-257, :290-326, :463-497   distrsparse_inner, distr_outer, distrsparse_outer: the
+                               gemm forms equal the handler's pairwise dot / axpy loops (x_i = iota
+                               from i + 0.5, sparse {1: i+1, 3: i+2, 6: i+3, 9: i+4}, alpha = iota
+                               from 1, n = dim = 10)
 """
 import numpy as np
 
@@ -84,3 +88,39 @@ def check(ctx, sh, rank, world):
     assert np.array_equal(y20.numpy(), ref[o:o + ln])
     x20, _ = upload_range(np.full(d20, 0.5))
     assert ctx.sparse_dot(x20, i20, v20, offset=off20) == 0.5 + 0.5 * 2.0 + 0.5 * 3.0 + 0.5 * 4.0
+
+    # testGemm.cpp distrsparse_inner / distr_outer / distrsparse_outer (n = dim = 10)
+    n = dim = 10
+    vx = [np.arange(dim) + i + 0.5 for i in range(n)]
+    my = [{1: i + 1.0, 3: i + 2.0, 6: i + 3.0, 9: i + 4.0} for i in range(n)]
+    cx = [upload_range(v)[0] for v in vx]
+    off = shard(dim)[0]
+    g = ctx.gemm_inner_sparse(cx, my, offset=off)
+    ref = np.array([[sum(vx[i][k] * v for k, v in my[j].items()) for j in range(n)] for i in range(n)])
+    pair = np.array([[ctx.sparse_dot(cx[i], list(my[j]), list(my[j].values()), offset=off) for j in range(n)]
+                     for i in range(n)])
+    assert np.all(np.abs(g - pair) <= 4 * np.finfo(float).eps * np.abs(ref)), np.max(np.abs(g - pair))
+    assert np.all(np.abs(g - ref) <= 4 * np.finfo(float).eps * np.abs(ref))
+    alpha = np.arange(1, n * n + 1, dtype=np.float64).reshape(n, n)
+    cy = [upload_range(v)[0] for v in vx]
+    cz = [upload_range(v)[0] for v in vx]
+    ctx.gemm_outer(alpha, cx, cy)  # cy[j] += sum_i alpha(i, j) cx[i]
+    for i in range(n):
+        for j in range(n):
+            ctx.axpy(alpha[i, j], cx[i], cz[j])
+    for j in range(n):
+        assert np.array_equal(cy[j].numpy(), cz[j].numpy())  # the reference's summation order per destination
+    cx = [upload_range(v)[0] for v in vx]
+    cy = [upload_range(v)[0] for v in vx]
+    ctx.gemm_outer_sparse(alpha, my, cx, offset=off)  # cx[j] += sum_i alpha(i, j) my[i]
+    for i in range(n):
+        for j in range(n):
+            ctx.sparse_axpy(alpha[j, i], list(my[j]), list(my[j].values()), cy[i], offset=off)
+    o, ln = shard(dim)
+    for i in range(n):
+        full = vx[i].copy()
+        for j in range(n):
+            for k, v in my[j].items():
+                full[k] += alpha[j, i] * v
+        assert np.allclose(cx[i].numpy(), cy[i].numpy(), rtol=4 * np.finfo(float).eps, atol=0)
+        assert np.allclose(cx[i].numpy(), full[o:o + ln], rtol=8 * np.finfo(float).eps, atol=0)
