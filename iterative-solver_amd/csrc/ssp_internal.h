@@ -187,8 +187,12 @@ __device__ inline double block_sum256(double v) {
 // (agent-scope relaxed atomic loads), so its acquire reduces to fence(acquire, "wavefront"), which
 // only keeps the compiler from hoisting those loads.  Guideline 16's conditions (1)-(4) for this form
 // are checked in the emitted gfx950 assembly of every kernel with the tail by
-// tests/test_fold_tail_isa.py.  A release fence per workgroup (buffer_wbl2) and an L1 invalidate
-// would add cost for no visibility the sc1 accesses do not already give.
+// tests/test_fold_tail_isa.py.  The C++ memory-model form (release / acq_rel arrivals, agent-scope
+// acquire fence; build with -DSSP_FOLD_RELACQ) was measured against it in one process on the same
+// vectors (tools/ab_fold.py, profiles/r2/ab_fold_relacq.txt): bit-identical results, 5 % lower call
+// latency at n = 1e3 (11.7 vs 12.3 us, within the host-timing noise), but dot at n = 1e8 28 % slower
+// (320 vs 250 us: every one of the ~2000 workgroups writes back its L2 before arriving), so the
+// write-through form stays.
 constexpr unsigned kFoldShards = 8;  // arrival-counter shards (one per XCD's worth of workgroups)
 constexpr unsigned kFoldLine = 32;   // unsigned per 128-B line
 struct FoldTail {
@@ -218,17 +222,28 @@ __device__ inline void fold_tail(const double* partial, const FoldTail& t) {
       const unsigned nsh = G < kFoldShards ? G : kFoldShards, in_sh = (G - sh + kFoldShards - 1) / kFoldShards;
       unsigned last = 0;
       unsigned* c = t.counter + kFoldLine * sh;
-      if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_sh - 1) {
+#ifdef SSP_FOLD_RELACQ
+      // A/B variant (tools/ab_fold.py): the C++ memory-model form -- release on the shard arrival,
+      // acquire-release on the top arrival, agent-scope acquire fence in the last arriver.
+      constexpr int kArrive = __ATOMIC_RELEASE, kTop = __ATOMIC_ACQ_REL;
+#else
+      constexpr int kArrive = __ATOMIC_RELAXED, kTop = __ATOMIC_RELAXED;
+#endif
+      if (__hip_atomic_fetch_add(c, 1u, kArrive, __HIP_MEMORY_SCOPE_AGENT) == in_sh - 1) {
         __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = __hip_atomic_fetch_add(t.counter + kFoldLine * kFoldShards, 1u, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+        last = __hip_atomic_fetch_add(t.counter + kFoldLine * kFoldShards, 1u, kTop, __HIP_MEMORY_SCOPE_AGENT) ==
+               nsh - 1;
       }
       s_last = last;
     }
   }
   __syncthreads();
   if (!s_last) return;
+#ifdef SSP_FOLD_RELACQ
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#else
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the loads are sc1
+#endif
   const int G = int(gridDim.x);
   for (int o = 0; o < t.nout; ++o) {
     // Thread t adds workgroups t, t + 256, ... in that order; the loads are issued 8 at a time so
