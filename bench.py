@@ -25,6 +25,7 @@ Beside the headline the JSON line carries (none of them inside the timed region)
                 kernel time and algorithmic bytes from the HIP-event ledger, reductions per iteration;
   in_solver_diis  the same for NonLinearEquationsDIIS on BASELINE config C5's problem (N = 1e8, sharded
                 at N > 1);
+  headline_step_at_n_div_10   the headline step at N / 10 (C2's length at N = 1e8);
   startup       context creation and the first (cold) solve against the warm one;
   cpu_baseline.dram_resident  one call each of the reference loops on DRAM-resident operands.
 """
@@ -344,6 +345,7 @@ def main():
                     help="time the K steps without HIP events (the roofline ledger then runs on --ledger-steps "
                          "extra steps); for measuring the events' cost")
     ap.add_argument("--no-in-solver", action="store_true", help="skip the whole-solve block")
+    ap.add_argument("--no-small", action="store_true", help="skip the headline step at N / 10")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
                     help="rank transport at N > 1: RCCL (the product path) or the host socket hub, which "
                          "lets tests run several ranks on ONE device (RCCL refuses duplicate GPUs)")
@@ -475,6 +477,28 @@ def main():
                      "GBs": round(step_bytes(n_global, m, k) * n_sus / ts / 1e9, 2),
                      "note": "headline step repeated while the 1-core CPU baseline runs on another core"}
     wl.free()  # back to the arena before the whole solves
+    # The same headline step at a tenth of the length (BASELINE config C2's N = 1e7 sharded alike):
+    # the rate where launch and reduction latencies weigh ten times more.
+    small = None
+    if not args.no_small and n_global >= 10:
+        ns_global = n_global // 10
+        sb = distribution(ns_global, world)
+        wls = Workload(ctx, sb[rank + 1] - sb[rank], sb[rank], m, k)
+        for _ in range(3):
+            wls.step()
+        ctx.synchronize()
+        barrier()
+        t_s = time.perf_counter()
+        s_steps = max(10, args.steps)
+        for _ in range(s_steps):
+            wls.step()
+        ctx.synchronize()
+        t_s = time.perf_counter() - t_s
+        if world > 1:
+            t_s = max(struct.unpack("<d", b)[0] for b in ctx.allgather_bytes(struct.pack("<d", t_s)))
+        wls.free()
+        small = {"n_global": ns_global, "steps": s_steps, "ms_per_step": round(1e3 * t_s / s_steps, 4),
+                 "GBs": round(step_bytes(ns_global, m, k) * s_steps / t_s / 1e9, 2)}
     solve = solve_diis = None
     if not args.no_in_solver:
         solve = in_solver(ctx, n_global, world, barrier)
@@ -531,6 +555,7 @@ def main():
             "ledger": "HIP events around every op of the timed steps" if timed_ledger
                       else f"HIP events over {ledger_steps} extra steps after the timed region",
             "product_step": product,
+            "headline_step_at_n_div_10": small,
             "in_solver": solve,
             "in_solver_diis": solve_diis,
             "startup": {"ctx_create_s": round(ctx_create_s, 3),

@@ -6,5 +6,5 @@ timeout -k 10 300 python bench.py > $OUT/b_timed.json 2> $OUT/b_timed.err || exi
 timeout -k 10 300 python bench.py --no-timed-ledger --no-cpu-baseline --no-in-solver > $OUT/b_untimed.json 2> $OUT/b_untimed.err || exit 1
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-in-solver > $OUT/b_timed2.json 2> $OUT/b_timed2.err || exit 1
 rm -rf $OUT/prof2
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof2 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-in-solver > $OUT/b_rocprof.json 2> $OUT/b_rocprof.err || exit 1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof2 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-in-solver --no-small > $OUT/b_rocprof.json 2> $OUT/b_rocprof.err || exit 1
 echo done

@@ -40,7 +40,7 @@ fi
 if [ "$what" = prof ] || [ "$what" = all ]; then
   rm -rf "$OUT/prof"
   step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-in-solver "$@"
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-in-solver --no-small "$@"
   rc=$?
   if [ $rc -ne 0 ]; then exit $rc; fi
   # The bench line of the profiled process itself: its HIP-event ledger and the kernel statistics
@@ -53,7 +53,7 @@ if [ "$what" = pmc ] || [ "$what" = all ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     rm -rf "$OUT/pmc_$c"
     step "pmc_$c" 600 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- \
-      python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 --no-cpu-baseline --no-in-solver "$@"
+      python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 --no-cpu-baseline --no-in-solver --no-small "$@"
     rc=$?
     if [ $rc -ne 0 ]; then exit $rc; fi
   done
@@ -63,7 +63,7 @@ if [ "$what" = mfma ] || [ "$what" = all ]; then
   # (gemm_inner 16x64 is the densest panel), one --pmc pass each.
   rm -rf "$OUT/pmc_mfma" "$OUT/pmc_mfma_shapes"
   step pmc_mfma 600 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 --kernel-trace -d "$OUT/pmc_mfma" \
-    -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 --no-cpu-baseline --no-in-solver "$@"
+    -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 --no-cpu-baseline --no-in-solver --no-small "$@"
   rc=$?
   if [ $rc -ne 0 ]; then exit $rc; fi
   step pmc_mfma_shapes 600 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 --kernel-trace \
