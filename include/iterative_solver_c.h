@@ -79,6 +79,15 @@ int64_t mpicomm_self(void);
 int64_t mpicomm_global(void);
 int64_t IterativeSolver_mpicomm_global(void);
 int64_t IterativeSolver_mpicomm_self(void);
+/* IterativeSolverCMPI.cpp:516-534; size and rank of the context set by IterativeSolverHbmSetContext
+ * (1 and 0 without one); init/finalize return 0.  The _mpi_size_/_mpi_rank_ spellings are the
+ * names the reference's Fortran module binds (IterativeSolverF.F90:50-57). */
+int64_t IterativeSolver_mpisize_global(void);
+int64_t IterativeSolver_mpirank_global(void);
+int64_t IterativeSolver_mpi_size_global(void);
+int64_t IterativeSolver_mpi_rank_global(void);
+int IterativeSolver_mpi_init(void);
+int IterativeSolver_mpi_finalize(void);
 
 /* ---- extension: device / communicator selection ----------------------------------------- */
 /* Use `ctx` (not owned) for the instances initialised after this call; NULL restores the
@@ -97,6 +106,9 @@ uint64_t IterativeSolverHbmInstanceId(void);
  * is destroyed after a newer one was created must not pop the newer one, which
  * IterativeSolverFinalize would).  Returns 0, or 1 when no instance has that id. */
 int IterativeSolverHbmFinalizeInstance(uint64_t id);
+/* Number of roots of the top instance (0 when there is none): the length of the arrays
+ * IterativeSolverErrors / IterativeSolverEigenvalues fill (used by the Fortran module). */
+size_t IterativeSolverHbmNRoots(void);
 
 #ifdef __cplusplus
 }

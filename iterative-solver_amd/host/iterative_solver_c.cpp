@@ -497,10 +497,26 @@ void IterativeSolverSetMaxIter(int max_iter) {
   guarded([&] { top().solver->set_max_iter(max_iter); });
 }
 
+size_t IterativeSolverHbmNRoots(void) {
+  return instances.empty() ? 0 : instances.back()->solver->n_roots();
+}
+
 // No MPI on this back end: ranks come from the ssp_ctx communicator (IterativeSolverHbmSetContext).
 int64_t mpicomm_self(void) { return 0; }
 int64_t mpicomm_global(void) { return 0; }
 int64_t IterativeSolver_mpicomm_global(void) { return 0; }
 int64_t IterativeSolver_mpicomm_self(void) { return 0; }
+// reference IterativeSolverCMPI.cpp:516-534 (mpi::size_global / rank_global / init / finalize), for
+// the Fortran module.  Size and rank are those of the context the next instance will use; init
+// and finalize have nothing to start or stop (the launcher owns the processes, the caller the
+// communicator) and return 0 as MPI_SUCCESS.  The reference's Fortran module binds the size/rank
+// functions as IterativeSolver_mpi_size_global / _mpi_rank_global (IterativeSolverF.F90:50-57)
+// while its C++ defines IterativeSolver_mpisize_global / _mpirank_global: both spellings exist here.
+int64_t IterativeSolver_mpisize_global(void) { return g_user_ctx ? ssp_ctx_nranks(g_user_ctx) : 1; }
+int64_t IterativeSolver_mpirank_global(void) { return g_user_ctx ? ssp_ctx_rank(g_user_ctx) : 0; }
+int64_t IterativeSolver_mpi_size_global(void) { return IterativeSolver_mpisize_global(); }
+int64_t IterativeSolver_mpi_rank_global(void) { return IterativeSolver_mpirank_global(); }
+int IterativeSolver_mpi_init(void) { return 0; }
+int IterativeSolver_mpi_finalize(void) { return 0; }
 
 }  // extern "C"

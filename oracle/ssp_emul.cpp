@@ -38,6 +38,33 @@ struct ssp_ctx {
 };
 
 namespace {
+
+// Arithmetic variants of the CPU path (checker knobs, never the product; ssp_emul_set_arith).  Both
+// are valid builds of the reference's loops: 0/0 is the sequential, uncontracted arithmetic of an
+// x86-64 build without FMA (the default, and what every parity fixture is generated with);
+// sum order 1 = 8 interleaved partial sums folded pairwise (a vectorising build of
+// std::inner_product), fma 1 = y + a*x contracted to fma(a, x, y) (-ffp-contract=fast on a CPU with
+// FMA, as the GPU kernels do).  They measure which steps the reference algorithm itself decides by
+// rounding (tests/fortran_cases.py).
+int g_sum_order = 0;
+int g_fma = 0;
+
+inline double madd(double a, double x, double y) { return g_fma ? std::fma(a, x, y) : y + a * x; }
+
+double dot_n(const double* x, const double* y, size_t n) {
+  if (g_sum_order == 1) {
+    double p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8)
+      for (int l = 0; l < 8; ++l) p[l] = madd(x[i + l], y[i + l], p[l]);
+    for (int l = 0; i < n; ++i, ++l) p[l] = madd(x[i], y[i], p[l]);
+    return ((p[0] + p[4]) + (p[2] + p[6])) + ((p[1] + p[5]) + (p[3] + p[7]));
+  }
+  double s = 0;
+  for (size_t i = 0; i < n; ++i) s = madd(x[i], y[i], s);
+  return s;
+}
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string& m) {
@@ -192,16 +219,20 @@ int ssp_copy(ssp_ctx* c, double* x, const double* y, size_t n) {
   if (n && x != y) std::memmove(x, y, n * sizeof(double));
   return SSP_OK;
 }
+int ssp_emul_set_arith(int sum_order, int fma) {
+  if (sum_order < 0 || sum_order > 1 || fma < 0 || fma > 1) return SSP_ERR_ARG;
+  g_sum_order = sum_order;
+  g_fma = fma;
+  return SSP_OK;
+}
 int ssp_axpy(ssp_ctx* c, double a, const double* x, double* y, size_t n) {
   Led l(c, "axpy", 24.0 * n);
-  for (size_t i = 0; i < n; ++i) y[i] += a * x[i];
+  for (size_t i = 0; i < n; ++i) y[i] = madd(a, x[i], y[i]);
   return SSP_OK;
 }
 int ssp_dot(ssp_ctx* c, const double* x, const double* y, size_t n, double* out) {
   Led l(c, "dot", (x == y ? 8.0 : 16.0) * n);
-  double s = 0;
-  for (size_t i = 0; i < n; ++i) s += x[i] * y[i];
-  *out = s;
+  *out = dot_n(x, y, n);
   return reduce(c, out, 1);
 }
 int ssp_gemm_inner(ssp_ctx* c, const double* const* xx, int m, const double* const* yy, int k, size_t n, double* out) {
@@ -210,11 +241,7 @@ int ssp_gemm_inner(ssp_ctx* c, const double* const* xx, int m, const double* con
   std::sort(distinct.begin(), distinct.end());
   Led l(c, "gemm_inner", 8.0 * n * double(std::unique(distinct.begin(), distinct.end()) - distinct.begin()));
   for (int i = 0; i < m; ++i)
-    for (int j = 0; j < k; ++j) {
-      double s = 0;
-      for (size_t e = 0; e < n; ++e) s += xx[i][e] * yy[j][e];
-      out[size_t(i) * k + j] = s;
-    }
+    for (int j = 0; j < k; ++j) out[size_t(i) * k + j] = dot_n(xx[i], yy[j], n);
   return reduce(c, out, size_t(m) * k);
 }
 int ssp_gemm_outer_sparse(ssp_ctx*, const double* alphas, const size_t* ptr, const size_t* idx, const double* val,
@@ -231,7 +258,7 @@ static int gemm_outer_body(const double* al, const double* const* xx, int k, dou
   for (int j = 0; j < m; ++j)
     for (int i = 0; i < k; ++i) {
       const double a = al[size_t(i) * m + j];
-      for (size_t e = 0; e < n; ++e) yy[j][e] += a * xx[i][e];
+      for (size_t e = 0; e < n; ++e) yy[j][e] = madd(a, xx[i][e], yy[j][e]);
     }
   return SSP_OK;
 }
@@ -244,40 +271,25 @@ int ssp_gemm_outer_set(ssp_ctx* c, const double* al, const double* const* xx, in
 }
 int ssp_gemm_outer(ssp_ctx* c, const double* al, const double* const* xx, int k, double* const* yy, int m, size_t n) {
   Led l(c, "gemm_outer", 8.0 * n * (k + 2.0 * m));
-  for (int j = 0; j < m; ++j)
-    for (int i = 0; i < k; ++i) {
-      const double a = al[size_t(i) * m + j];
-      for (size_t e = 0; e < n; ++e) yy[j][e] += a * xx[i][e];
-    }
-  return SSP_OK;
+  return gemm_outer_body(al, xx, k, yy, m, n);
 }
 int ssp_axpy_inner(ssp_ctx* c, const double* cc, const double* x, double* const* yy, int m, const double* z, size_t n,
                    double* out) {
   for (int j = 0; j < m; ++j) {
-    double s = 0;
-    for (size_t e = 0; e < n; ++e) {
-      yy[j][e] += cc[j] * x[e];
-      s += yy[j][e] * z[e];
-    }
-    out[j] = s;
+    for (size_t e = 0; e < n; ++e) yy[j][e] = madd(cc[j], x[e], yy[j][e]);
+    out[j] = dot_n(yy[j], z, n);
   }
   return reduce(c, out, size_t(m));
 }
 int ssp_scal_inner(ssp_ctx* c, double alpha, double* x, const double* const* yy, int m, size_t n, double* out) {
   for (size_t e = 0; e < n; ++e) x[e] *= alpha;
-  for (int j = 0; j < m; ++j) {
-    double s = 0;
-    for (size_t e = 0; e < n; ++e) s += x[e] * yy[j][e];
-    out[j] = s;
-  }
+  for (int j = 0; j < m; ++j) out[j] = dot_n(x, yy[j], n);
   return reduce(c, out, size_t(m));
 }
 int ssp_axpy_norm(ssp_ctx* c, const double* cc, const double* x, double* const* yy, int m, size_t n, double* out) {
   for (int j = 0; j < m; ++j)
-    for (size_t e = 0; e < n; ++e) yy[j][e] += cc[j] * x[e];
-  double s = 0;
-  for (size_t e = 0; e < n; ++e) s += yy[0][e] * yy[0][e];
-  *out = s;
+    for (size_t e = 0; e < n; ++e) yy[j][e] = madd(cc[j], x[e], yy[j][e]);
+  *out = dot_n(yy[0], yy[0], n);
   return reduce(c, out, 1);
 }
 int ssp_precondition(ssp_ctx*, double* const* a, int nvec, const double* d, const double* shift, size_t n) {

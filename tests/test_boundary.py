@@ -26,6 +26,9 @@ REFERENCE_C_API = [
     "IterativeSolverSetDiagonals", "IterativeSolverDiagonals", "IterativeSolverValue", "IterativeSolverVerbosity",
     "IterativeSolverMaxIter", "IterativeSolverSetMaxIter", "mpicomm_self", "mpicomm_global",
     "IterativeSolver_mpicomm_global", "IterativeSolver_mpicomm_self",
+    # IterativeSolverCMPI.cpp:516-534, and the spellings IterativeSolverF.F90:46-57 binds
+    "IterativeSolver_mpisize_global", "IterativeSolver_mpirank_global", "IterativeSolver_mpi_init",
+    "IterativeSolver_mpi_finalize", "IterativeSolver_mpi_size_global", "IterativeSolver_mpi_rank_global",
 ]
 
 
