@@ -178,6 +178,32 @@ print('FAILS', fails)
     assert "FAILS []" in out.stdout, out.stdout[-2000:]
 
 
+@pytest.mark.skipif(not os.path.isdir(REF_TESTS), reason="reference tree not present")
+def test_reference_fortran_examples_build_and_run(tmp_path):
+    """The reference's Fortran example programs that build without MPI / the profiler
+    (examples/*F*.F90), compiled unchanged against the module and run over the C API's host
+    emulation.  (The others need mpif.h or ProfilerF, or declare their own mpi_init beside the
+    module's, or test Add_Vector as LOGICAL -- defects of the examples, not of the binding.)"""
+    ex = os.path.normpath(os.path.join(REF_TESTS, "..", "..", "examples"))
+    outputs = {}
+    for name in ("LinearEigensystemExampleF-Pspace", "LinearEigensystemExampleF-problem", "LinearEquationsExampleF",
+                 "OptimizeExampleF", "OptimizeExampleF-problem"):
+        obj, exe = tmp_path / f"{name}.o", tmp_path / f"{name}.x"
+        subprocess.run([FLANG, "-O1", "-I", os.path.join(PKG, "lib", "fmod"), "-module-dir", str(tmp_path), "-c",
+                        os.path.join(ex, f"{name}.F90"), "-o", str(obj)], check=True)
+        subprocess.run([FLANG, "-o", str(exe), str(obj), os.path.join(PKG, "lib", "obj", "f_iterative_solver_problem.o"),
+                        os.path.join(PKG, "lib", "obj", "f_iterative_solver.o"), "-L" + EMUL, "-litsolv_emul",
+                        "-Wl,-rpath," + EMUL, "-lstdc++"], check=True)
+        run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+        assert run.returncode == 0, (name, run.stdout[-1000:], run.stderr[-1000:])
+        outputs[name] = run.stdout
+    # P-space example: n = 200, m = 1 + (3i - 1) delta, 3 roots
+    m = np.ones((200, 200))
+    m[np.diag_indices(200)] = 3.0 * np.arange(1, 201)
+    last = [ln for ln in outputs["LinearEigensystemExampleF-Pspace"].splitlines() if "eigenvalues=" in ln][-1]
+    np.testing.assert_allclose([float(t) for t in last.split("=")[1].split()], np.linalg.eigvalsh(m)[:3], rtol=1e-12)
+
+
 # ---- GPU -----------------------------------------------------------------------------------------
 @pytest.mark.gpu
 def test_fortran_cases_gpu(ctx, tmp_path):
