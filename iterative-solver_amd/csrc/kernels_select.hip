@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kTileBlock) void k_select_tile(const SelectArgs a) 
   for (int k = 2; k <= kTile; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int t = threadIdx.x; t < kTile / 2; t += kTileBlock) {
-        const int i = 2 * j * (t / j) + (t % j);
+        const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));  // 2 j (t / j) + t % j, j a power of two
         const int l = i + j;
         const bool desc = ((i & k) == 0);
         Cand ci = tile[i], cl = tile[l];
@@ -112,54 +112,37 @@ struct RadixArgs {
   const double* x;
   const double* y;
   size_t n;
-  int mode;
-  int max;
-  int ignore_sign;
-  int bits;   // composite bits fixed so far (0..128): key bits 63.., then local index bits 63..
-  int width;  // digit width (<= 12), bits + width <= 64 or bits >= 64
+  int neg;  // mode 0: v' = (abs ? |x| : x), negated when neg (select's max = false)
+  int abs;
+  // Digit extraction at the current composite position: the element matches the fixed prefix when
+  // ((key ^ tkey) & pmask) == 0 (key phase) or key == tkey && ((i ^ tidx) & pmask) == 0 (index
+  // phase); its digit is ((key or i) >> dshift) & dmask.
+  unsigned long long pmask;
+  int dshift;
+  unsigned dmask;
   unsigned long long tkey, tidx;  // threshold composite (fixed bits, zeros below)
-  unsigned* hist;                 // [gridDim.x][kBins]
+  unsigned* hist;                 // [kBins], zeroed before each pass
   Cand* cand;                     // compaction output
   unsigned long long* counter;
 };
 
-__device__ __forceinline__ unsigned long long value_key(const RadixArgs& a, double xv, double yv) {
-  double v;
-  if (a.mode == 1)
-    v = fabs(xv * yv);
-  else
-    v = a.max ? (a.ignore_sign ? fabs(xv) : xv) : (a.ignore_sign ? -fabs(xv) : -xv);
-  return order_key(v);
+// Branch-free order_key of one element's v': mode 1 |x*y|; mode 0 the select transform (sign flips
+// and absolute values as bit operations, so every input's bits map exactly as order_key maps them),
+// -0 as +0, then the order-preserving image.
+template <int MODE>
+__device__ __forceinline__ unsigned long long elem_key(const RadixArgs& a, double xv, double yv) {
+  double v = MODE == 1 ? fabs(xv * yv) : (a.abs ? fabs(xv) : xv);
+  if (MODE == 0) v = a.neg ? -v : v;
+  long long b = __double_as_longlong(v);
+  b = (b << 1) != 0 ? b : 0;
+  return (unsigned long long)(b ^ ((b >> 63) | (long long)0x8000000000000000ull));
 }
 
-// Keys of elements 2p and 2p+1 (16-byte loads; a missing second element gets valid = false).
-constexpr int kRadixU = 4;  // double2 slots per thread per iteration
-__device__ __forceinline__ void load_pair(const RadixArgs& a, size_t p, unsigned long long (&k)[2], bool (&ok)[2]) {
-  const size_t i = 2 * p;
-  ok[0] = i < a.n;
-  ok[1] = i + 1 < a.n;
-  double2 xv = make_double2(0, 0), yv = make_double2(0, 0);
-  if (ok[1]) {
-    xv = ssp::ld2nt(a.x + i);
-    if (a.mode == 1) yv = ssp::ld2nt(a.y + i);
-  } else if (ok[0]) {
-    xv.x = a.x[i];
-    if (a.mode == 1) yv.x = a.y[i];
-  }
-  k[0] = value_key(a, xv.x, yv.x);
-  k[1] = value_key(a, xv.y, yv.y);
-}
-
-// Digit of (key, i) at composite bit position a.bits, or -1 when the fixed prefix differs.
+template <bool IDX>
 __device__ __forceinline__ int elem_digit(const RadixArgs& a, unsigned long long key, unsigned long long i) {
-  const unsigned mask = (1u << a.width) - 1u;
-  if (a.bits < 64) {
-    if (a.bits > 0 && (key >> (64 - a.bits)) != (a.tkey >> (64 - a.bits))) return -1;
-    return int((key >> (64 - a.bits - a.width)) & mask);
-  }
-  const int ib = a.bits - 64;
-  if (key != a.tkey || (ib > 0 && (i >> (64 - ib)) != (a.tidx >> (64 - ib)))) return -1;
-  return int((i >> (64 - ib - a.width)) & mask);
+  const unsigned long long w = IDX ? i : key;
+  const bool match = IDX ? (key == a.tkey && ((i ^ a.tidx) & a.pmask) == 0) : (((key ^ a.tkey) & a.pmask) == 0);
+  return match ? int((w >> a.dshift) & a.dmask) : -1;
 }
 
 __device__ __forceinline__ void hist_add(unsigned* h, int d) {
@@ -173,127 +156,168 @@ __device__ __forceinline__ void hist_add(unsigned* h, int d) {
   }
 }
 
+// Streams the shard in iterations of kRadixU double2 slots per lane, unguarded while every slot is
+// a whole pair, then one guarded tail; f(key, local index, valid) for each element, the same number
+// of calls on every lane of a wave (the ballots in f need the whole wave).
+constexpr int kRadixU = 4;
+template <int MODE, typename F>
+__device__ __forceinline__ void radix_stream(const RadixArgs& a, F&& f) {
+  const size_t stride = size_t(gridDim.x) * kBlock, npair = a.n / 2, n2 = (a.n + 1) / 2;
+  size_t p0 = size_t(blockIdx.x) * kBlock;
+  for (; p0 + (kRadixU - 1) * stride + kBlock <= npair; p0 += kRadixU * stride) {
+    double2 xv[kRadixU], yv[kRadixU];
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) {
+      const size_t i = 2 * (p0 + threadIdx.x + u * stride);
+      xv[u] = ssp::ld2nt(a.x + i);
+      if (MODE == 1) yv[u] = ssp::ld2nt(a.y + i);
+    }
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) {
+      const unsigned long long i = 2 * (p0 + threadIdx.x + u * stride);
+      f(elem_key<MODE>(a, xv[u].x, MODE == 1 ? yv[u].x : 0.0), i, true);
+      f(elem_key<MODE>(a, xv[u].y, MODE == 1 ? yv[u].y : 0.0), i + 1, true);
+    }
+  }
+  for (; p0 < n2; p0 += kRadixU * stride) {
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) {
+      const size_t i = 2 * (p0 + threadIdx.x + u * stride);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const bool ok = i + e < a.n;
+        const double xe = ok ? a.x[i + e] : 0.0;
+        const double ye = (MODE == 1 && ok) ? a.y[i + e] : 0.0;
+        f(elem_key<MODE>(a, xe, ye), i + e, ok);
+      }
+    }
+  }
+}
+
+template <int MODE, bool IDX>
 __global__ __launch_bounds__(kBlock) void k_radix_hist(const RadixArgs a) {
   __shared__ unsigned h[kBins];
   for (int s = threadIdx.x; s < kBins; s += kBlock) h[s] = 0;
   __syncthreads();
-  const size_t stride = size_t(gridDim.x) * kBlock, n2 = (a.n + 1) / 2;
-  // Every lane of a wave makes the same trips (the ballots in hist_add need the whole wave).
-  for (size_t p0 = size_t(blockIdx.x) * kBlock; p0 < n2; p0 += kRadixU * stride) {
-    unsigned long long k[kRadixU][2];
-    bool ok[kRadixU][2];
-#pragma unroll
-    for (int u = 0; u < kRadixU; ++u) load_pair(a, p0 + threadIdx.x + u * stride, k[u], ok[u]);
-#pragma unroll
-    for (int u = 0; u < kRadixU; ++u)
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const unsigned long long i = 2 * (p0 + threadIdx.x + u * stride) + e;
-        hist_add(h, ok[u][e] ? elem_digit(a, k[u][e], i) : -1);
-      }
-  }
+  radix_stream<MODE>(a, [&](unsigned long long key, unsigned long long i, bool ok) {
+    hist_add(h, ok ? elem_digit<IDX>(a, key, i) : -1);
+  });
   __syncthreads();
-  for (int s = threadIdx.x; s < kBins; s += kBlock) a.hist[size_t(blockIdx.x) * kBins + s] = h[s];
+  // Block histograms meet in one global histogram through integer atomics (order-free, so the
+  // counts are exact and reproducible); only the bins this block touched are sent.  Replaces a
+  // per-block table summed by a second kernel (131 us per pass at N = 1e8, latency-bound).
+  for (int s = threadIdx.x; s < kBins; s += kBlock)
+    if (h[s]) atomicAdd(&a.hist[s], h[s]);
 }
 
-// out[b] = sum over blocks of hist[block][b] (fixed order).
-__global__ __launch_bounds__(kBlock) void k_radix_hist_sum(const unsigned* hist, int nblocks, unsigned* out) {
-  const int b = blockIdx.x * kBlock + threadIdx.x;
-  if (b >= kBins) return;
-  unsigned s = 0;
-  for (int k = 0; k < nblocks; ++k) s += hist[size_t(k) * kBins + b];
-  out[b] = s;
-}
-
-// Every element whose composite is >= (tkey, tidx).
+// Every element whose composite is >= (tkey, tidx).  Slots are claimed once per wave (ballot, one
+// atomic for the wave's survivors, lane prefix counts).  The slot order is arbitrary; the tile sort
+// that follows orders the candidates completely, so the selection does not depend on it.
+template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_radix_compact(const RadixArgs a, size_t offset) {
-  const size_t stride = size_t(gridDim.x) * kBlock, n2 = (a.n + 1) / 2;
-  for (size_t p0 = size_t(blockIdx.x) * kBlock + threadIdx.x; p0 < n2; p0 += kRadixU * stride) {
-    unsigned long long k[kRadixU][2];
-    bool ok[kRadixU][2];
-#pragma unroll
-    for (int u = 0; u < kRadixU; ++u) load_pair(a, p0 + u * stride, k[u], ok[u]);
-#pragma unroll
-    for (int u = 0; u < kRadixU; ++u)
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const unsigned long long i = 2 * (p0 + u * stride) + e;
-        if (ok[u][e] && (k[u][e] > a.tkey || (k[u][e] == a.tkey && i >= a.tidx))) {
-          const unsigned long long slot = atomicAdd(a.counter, 1ull);
-          if (slot < kRadixCap) a.cand[slot] = Cand{k[u][e], offset + i};
-        }
-      }
-  }
+  const unsigned long long lt = (1ull << __lane_id()) - 1ull;
+  radix_stream<MODE>(a, [&](unsigned long long key, unsigned long long i, bool ok) {
+    const bool take = ok && (key > a.tkey || (key == a.tkey && i >= a.tidx));
+    const unsigned long long mask = __ballot(take);
+    if (mask) {
+      const int leader = __ffsll((long long)mask) - 1;
+      unsigned long long base = 0;
+      if (__lane_id() == leader) base = atomicAdd(a.counter, (unsigned long long)__popcll(mask));
+      base = __shfl(base, leader, 64);
+      const unsigned long long slot = base + __popcll(mask & lt);
+      if (take && slot < kRadixCap) a.cand[slot] = Cand{key, offset + i};
+    }
+  });
 }
 
 // Fixes digits of the composite threshold until at most kRadixCap elements lie at or above it,
 // then compacts them into `cand`; returns their number in *count.
 int radix_candidates(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t n, size_t offset,
-                     size_t nsel, int max, int ignore_sign, Cand* cand, unsigned* hist, unsigned* hsum,
+                     size_t nsel, int max, int ignore_sign, Cand* cand, unsigned* hist,
                      unsigned long long* counter, unsigned grid, size_t* count) {
   RadixArgs a{};
   a.x = x;
   a.y = y;
   a.n = n;
-  a.mode = mode;
-  a.max = max;
-  a.ignore_sign = ignore_sign;
+  a.neg = !max;
+  a.abs = ignore_sign;
   a.hist = hist;
   int idx_bits = 1;
   while (idx_bits < 64 && ((n - 1) >> idx_bits) != 0) ++idx_bits;
   size_t need = nsel, above = 0;
   std::vector<unsigned> h(kBins);
+  int bits = 0;  // composite bits fixed so far (0..128): key bits 63.., then local index bits 63..
   for (;;) {
-    a.width = a.bits < 64 ? std::min(kDigitBits, 64 - a.bits) : std::min(kDigitBits, 128 - a.bits);
-    hipLaunchKernelGGL(k_radix_hist, dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    const int width = bits < 64 ? std::min(kDigitBits, 64 - bits) : std::min(kDigitBits, 128 - bits);
+    const bool idx_phase = bits >= 64;
+    const int fixed = idx_phase ? bits - 64 : bits;  // bits fixed within the current word
+    a.pmask = fixed ? ~0ull << (64 - fixed) : 0ull;
+    a.dshift = 64 - fixed - width;
+    a.dmask = (1u << width) - 1u;
+    SSP_TRY_HIP(hipMemsetAsync(hist, 0, sizeof(unsigned) * kBins, ctx->stream));
+    if (mode == 1 && idx_phase)
+      hipLaunchKernelGGL((k_radix_hist<1, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else if (mode == 1)
+      hipLaunchKernelGGL((k_radix_hist<1, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else if (idx_phase)
+      hipLaunchKernelGGL((k_radix_hist<0, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else
+      hipLaunchKernelGGL((k_radix_hist<0, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_radix_hist_sum, dim3((kBins + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, hist,
-                       int(grid), hsum);
-    SSP_TRY_HIP(hipGetLastError());
-    SSP_TRY_HIP(hipMemcpyAsync(h.data(), hsum, sizeof(unsigned) * kBins, hipMemcpyDeviceToHost, ctx->stream));
-    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
-    const int nb = 1 << a.width;
+    // hist is the context's result staging buffer: published to coherent host memory and polled
+    // (ssp::fetch_result), not a D2H copy + stream synchronisation.
+    SSP_TRY(ssp::fetch_result(ctx, reinterpret_cast<double*>(h.data()), kBins / 2));
+    const int nb = 1 << width;
     size_t cum = 0;
     int b = nb - 1;
     for (; b > 0; --b) {
       if (cum + h[b] >= need) break;
       cum += h[b];
     }
-    if (a.bits < 64)
-      a.tkey |= (unsigned long long)b << (64 - a.bits - a.width);
+    if (!idx_phase)
+      a.tkey |= (unsigned long long)b << a.dshift;
     else
-      a.tidx |= (unsigned long long)b << (64 - (a.bits - 64) - a.width);
+      a.tidx |= (unsigned long long)b << a.dshift;
     above += cum;
     need -= cum;
-    a.bits += a.width;
-    if (above + h[b] <= kRadixCap || a.bits >= 128) {
+    bits += width;
+    if (above + h[b] <= kRadixCap || bits >= 128) {
       *count = above + h[b];
       break;
     }
-    if (a.bits == 64) a.bits = 128 - idx_bits;  // local indices have no bits above idx_bits
+    if (bits == 64) bits = 128 - idx_bits;  // local indices have no bits above idx_bits
   }
   if (*count > kRadixCap) return ssp::set_error(SSP_ERR_UNSUPPORTED, "ssp_select: radix threshold did not converge");
   a.cand = cand;
   a.counter = counter;
   SSP_TRY_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), ctx->stream));
-  hipLaunchKernelGGL(k_radix_compact, dim3(grid), dim3(kBlock), 0, ctx->stream, a, offset);
+  if (mode == 1)
+    hipLaunchKernelGGL(k_radix_compact<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, a, offset);
+  else
+    hipLaunchKernelGGL(k_radix_compact<0>, dim3(grid), dim3(kBlock), 0, ctx->stream, a, offset);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
 
 // Returned values recomputed from the selected elements as the reference returns them
-// (select.h:52: max ? v' : -v', so the sign of a zero is the element's, not the key's).
-__global__ void k_select_values(const double* x, const double* y, const unsigned long long* li, int cnt, int mode,
+// (select.h:52: max ? v' : -v', so the sign of a zero is the element's, not the key's), written
+// beside their global indices (bit patterns) for one publication to the host.
+__global__ void k_select_values(const Cand* best, int cnt, const double* x, const double* y, size_t offset, int mode,
                                 int max, int ignore_sign, double* out) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= cnt) return;
-  const double xv = x[li[e]];
+  const unsigned long long gi = best[e].idx;
+  const size_t li = size_t(gi - offset);
+  const double xv = x[li];
+  double r;
   if (mode == 1) {
-    out[e] = fabs(xv * y[li[e]]);
+    r = fabs(xv * y[li]);
   } else {
     const double v = max ? (ignore_sign ? fabs(xv) : xv) : (ignore_sign ? -fabs(xv) : -xv);
-    out[e] = max ? v : -v;
+    r = max ? v : -v;
   }
+  out[2 * e] = __longlong_as_double((long long)gi);
+  out[2 * e + 1] = r;
 }
 
 int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t n, size_t offset, size_t nsel,
@@ -305,7 +329,8 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
     return ssp::set_error(SSP_ERR_UNSUPPORTED, "ssp_select: n > 1024 not supported by the tile selection");
   if (n > 0 && (!x || (mode == 1 && !y))) return ssp::set_error(SSP_ERR_ARG, "ssp_select: null vector");
   const int keep = int(nsel);
-  std::vector<Cand> local;
+  std::vector<size_t> sel_idx;  // this rank's best (global index, returned value)
+  std::vector<double> sel_val;
   if (keep > 0 && n > 0) {
     ssp::LedgerScope ls(ctx, mode == 1 ? "select_max_dot" : "select", (mode == 1 ? 16.0 : 8.0) * n);
     // Level 0 reads the shard (short shards) or the radix candidates; later levels read the
@@ -315,23 +340,21 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
     size_t tiles = (count + kTile - 1) / kTile;
     const size_t cap = tiles * size_t(keep);  // Cands per level buffer
     const unsigned grid = radix ? std::min<unsigned>(ssp::stream_grid(ctx, n, 4), unsigned(ctx->num_cus) * 4) : 0;
-    // Workspace (doubles): two level buffers, radix candidates, per-block and summed histograms,
-    // the compaction counter.
+    // Workspace (doubles): two level buffers, radix candidates, the compaction counter; the
+    // histogram lives in the result staging buffer (published to the host after each pass).
     const size_t w_lvl = 2 * cap * 2, w_cand = radix ? 2 * kRadixCap : 0;
-    const size_t w_hist = radix ? (size_t(grid) + 1) * kBins / 2 : 0;
-    SSP_TRY(ssp::ensure_partial(ctx, w_lvl + w_cand + w_hist + 2));
+    SSP_TRY(ssp::ensure_partial(ctx, w_lvl + w_cand + 2));
+    SSP_TRY(ssp::ensure_result(ctx, kBins / 2));
     Cand* buf0 = reinterpret_cast<Cand*>(ctx->partial);
     Cand* buf1 = buf0 + cap;
     Cand* cand = buf1 + cap;
-    unsigned* hist = reinterpret_cast<unsigned*>(ctx->partial + w_lvl + w_cand);
-    unsigned* hsum = hist + size_t(grid) * kBins;
-    auto* counter = reinterpret_cast<unsigned long long*>(ctx->partial + w_lvl + w_cand + w_hist);
+    unsigned* hist = reinterpret_cast<unsigned*>(ctx->result_dev);
+    auto* counter = reinterpret_cast<unsigned long long*>(ctx->partial + w_lvl + w_cand);
     SelectArgs a{};
     a.keep = keep;
     a.out = buf0;
     if (radix) {
-      SSP_TRY(radix_candidates(ctx, mode, x, y, n, offset, nsel, max, ignore_sign, cand, hist, hsum, counter, grid,
-                               &count));
+      SSP_TRY(radix_candidates(ctx, mode, x, y, n, offset, nsel, max, ignore_sign, cand, hist, counter, grid, &count));
       tiles = (count + kTile - 1) / kTile;
       a.in = cand;
       a.count = count;
@@ -363,34 +386,31 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
       count = tiles * size_t(keep);
       std::swap(cur, nxt);
     }
-    local.resize(keep);
-    SSP_TRY_HIP(hipMemcpyAsync(local.data(), cur, sizeof(Cand) * keep, hipMemcpyDeviceToHost, ctx->stream));
-    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    // The best `real` candidates of this rank (padding sorts after them when n < nsel): indices and
+    // returned values in one published block.
     const size_t real = std::min(n, nsel);
-    local.resize(real);
+    SSP_TRY(ssp::ensure_result(ctx, 2 * real));
+    hipLaunchKernelGGL(k_select_values, dim3(unsigned((real + 255) / 256)), dim3(256), 0, ctx->stream, cur, int(real), x,
+                       y, offset, mode, max, ignore_sign, ctx->result_dev);
+    SSP_TRY_HIP(hipGetLastError());
+    std::vector<double> pub(2 * real);
+    SSP_TRY(ssp::fetch_result(ctx, pub.data(), 2 * real));
+    for (size_t e = 0; e < real; ++e) {
+      unsigned long long gi;
+      std::memcpy(&gi, &pub[2 * e], sizeof(gi));
+      sel_idx.push_back(size_t(gi));
+      sel_val.push_back(pub[2 * e + 1]);
+    }
   }
   // This rank's best n as (global index, returned value), then the fixed-size exchange: nsel
   // slots per rank plus the real count, and the same host merge on every rank.
   std::vector<size_t> lidx(nsel, 0);
   std::vector<double> lval(nsel, 0.0);
-  if (!local.empty()) {
-    std::vector<unsigned long long> li(local.size());
-    for (size_t e = 0; e < local.size(); ++e) {
-      lidx[e] = size_t(local[e].idx);
-      li[e] = local[e].idx - offset;
-    }
-    void* dli;
-    SSP_TRY(ssp::upload_small(ctx, li.data(), li.size() * sizeof(unsigned long long), &dli));
-    SSP_TRY(ssp::ensure_result(ctx, li.size()));
-    hipLaunchKernelGGL(k_select_values, dim3(unsigned((li.size() + 255) / 256)), dim3(256), 0, ctx->stream, x, y,
-                       static_cast<const unsigned long long*>(dli), int(li.size()), mode, max, ignore_sign,
-                       ctx->result_dev);
-    SSP_TRY_HIP(hipGetLastError());
-    SSP_TRY(ssp::fetch_result(ctx, lval.data(), li.size()));
-  }
+  std::copy(sel_idx.begin(), sel_idx.end(), lidx.begin());
+  std::copy(sel_val.begin(), sel_val.end(), lval.begin());
   const int nr = ctx->nranks;
   std::vector<size_t> counts(nr), gidx(nsel * size_t(nr)), gval_bits(nsel * size_t(nr));
-  const size_t my_count = local.size();
+  const size_t my_count = sel_idx.size();
   SSP_TRY(ssp_allgather_host(ctx, &my_count, counts.data(), sizeof(size_t)));
   if (nsel) {
     SSP_TRY(ssp_allgather_host(ctx, lidx.data(), gidx.data(), sizeof(size_t) * nsel));
