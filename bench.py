@@ -268,7 +268,7 @@ C3 = dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48, reset
 # BASELINE config C5 (NonLinearEquationsDIIS, N = 1e8): the DIIS problem of tools/solver_ledger.py and
 # tests/golden/traces.json (r = H (x - 1), x from e_0, test_NonLinearEquations.cpp:25-49)
 C5 = dict(rho=0.01, rank=3, seed=3, max_size_qspace=6, convergence_threshold=1e-8)
-REDUCING_OPS = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "select", "sparse")
+REDUCING_OPS = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "select", "gemm_inner_sparse")
 
 
 def in_solver(ctx, n_global, world, barrier, repeat=2, kind="davidson"):

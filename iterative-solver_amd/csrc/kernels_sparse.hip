@@ -151,7 +151,7 @@ int ssp_sparse_copy(ssp_ctx* ctx, double* x, size_t n, size_t offset, const size
   unsigned long long *dptr, *dli;
   double* dv;
   SSP_TRY(upload_entries(ctx, ptr, li, lv, &dptr, &dli, &dv));
-  ssp::LedgerScope ls(ctx, "sparse", 16.0 * li.size());
+  ssp::LedgerScope ls(ctx, "sparse_copy", 16.0 * li.size());
   const unsigned grid = unsigned(std::min<size_t>((li.size() + kBlock - 1) / kBlock, 1024));
   hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), 1.0, 0);
   SSP_TRY_HIP(hipGetLastError());
@@ -171,7 +171,7 @@ int ssp_sparse_axpy(ssp_ctx* ctx, double alpha, const size_t* idx, const double*
   unsigned long long *dptr, *dli;
   double* dv;
   SSP_TRY(upload_entries(ctx, ptr, li, lv, &dptr, &dli, &dv));
-  ssp::LedgerScope ls(ctx, "sparse", 24.0 * li.size());
+  ssp::LedgerScope ls(ctx, "sparse_axpy", 24.0 * li.size());
   // Distinct map keys never collide, so entries can be applied in parallel.
   const unsigned grid = unsigned(std::min<size_t>((li.size() + kBlock - 1) / kBlock, 1024));
   hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), alpha, 1);
@@ -197,7 +197,7 @@ int ssp_gemm_inner_sparse(ssp_ctx* ctx, const double* const* xx, int m, size_t n
   unsigned long long *dptr, *dli;
   double* dv;
   SSP_TRY(upload_entries(ctx, lptr, li, lv, &dptr, &dli, &dv));
-  ssp::LedgerScope ls(ctx, "sparse", 16.0 * li.size() * m);
+  ssp::LedgerScope ls(ctx, "gemm_inner_sparse", 16.0 * li.size() * m);
   for (int i0 = 0; i0 < m; i0 += 64) {
     SparseInnerArgs a{};
     a.m = std::min(64, m - i0);
@@ -239,7 +239,7 @@ int ssp_gemm_outer_sparse(ssp_ctx* ctx, const double* alphas, const size_t* ptr,
   unsigned long long *dptr, *dli;
   double* dv;
   SSP_TRY(upload_entries(ctx, lptr, li, lv, &dptr, &dli, &dv));
-  ssp::LedgerScope ls(ctx, "sparse", 24.0 * li.size() * m);
+  ssp::LedgerScope ls(ctx, "gemm_outer_sparse", 24.0 * li.size() * m);
   for (int j0 = 0; j0 < m; j0 += 64) {
     SparseOuterArgs a{};
     a.m = std::min(64, m - j0);
@@ -304,7 +304,7 @@ int ssp_construct_solution(ssp_ctx* ctx, const double* palphas, const size_t* pt
   a.m = m;
   a.kp = kp;
   a.k = k;
-  ssp::LedgerScope ls(ctx, "sparse", 8.0 * a.nu * m * (2.0 + k));
+  ssp::LedgerScope ls(ctx, "construct_solution_sparse", 8.0 * a.nu * m * (2.0 + k));
   const size_t threads = a.nu * size_t(m);
   hipLaunchKernelGGL(k_construct_fixup, dim3(unsigned((threads + 255) / 256)), dim3(256), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());
