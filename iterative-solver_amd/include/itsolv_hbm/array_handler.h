@@ -329,6 +329,16 @@ bool fused_construct_solution(HP&, const Matrix<double>&, const RefP&, const Mat
   return false;
 }
 
+// Hook for new Q vectors that are linear combinations of existing ones (construct_dspace,
+// reference propose_rspace.h:380-394: a copy of a prototype, fill(0), then the axpy loops):
+// out[i] = sum_j coeff(i, j) src[j], sources applied in order j = 0..; returns false when the
+// handler has no form that writes the new vectors without copying, zeroing and re-reading them.
+// Found by argument-dependent lookup.
+template <class H, class Q>
+bool fused_new_combinations(H&, const Matrix<double>&, const std::vector<const Q*>&, std::vector<Q>&) {
+  return false;
+}
+
 // Hook for a fused sequential self-orthonormalisation of R (reference propose_rspace.h:450-465):
 // returns false when the handler has no fused form (the caller then runs the reference loop of
 // dot / scal / dot / axpy calls).  Found by argument-dependent lookup.

@@ -73,6 +73,29 @@ inline bool fused_construct_solution(array::ArrayHandler<Vec, SparseP>&, const i
   return true;
 }
 
+// New vectors as linear combinations (array::fused_new_combinations hook): allocated without a
+// copy and written by one ssp_gemm_outer_set, bit-identical to copy + fill(0) + the axpy sequence
+// (sources in order), without the copy, the fill and the destination reads (64N bytes per new
+// vector).
+inline bool fused_new_combinations(array::ArrayHandler<Vec, Vec>&, const itsolv::subspace::Matrix<double>& coeff,
+                                   const std::vector<const Vec*>& src, std::vector<Vec>& out) {
+  const size_t nout = coeff.rows(), k = src.size();
+  if (k == 0 || coeff.cols() != k) return false;
+  std::vector<const double*> xp;
+  for (auto* v : src) xp.push_back(v->data());
+  std::vector<double> alphas(k * nout);  // alphas[i * m + j]: source i, destination j
+  for (size_t j = 0; j < nout; ++j)
+    for (size_t i = 0; i < k; ++i) alphas[i * nout + j] = coeff(j, i);
+  const size_t first = out.size();
+  for (size_t j = 0; j < nout; ++j) out.push_back(src.front()->alloc_like());
+  std::vector<double*> yp;
+  for (size_t j = first; j < out.size(); ++j) yp.push_back(out[j].data());
+  const Vec& v0 = *src.front();
+  check(ssp_gemm_outer_set(v0.ctx(), alphas.data(), xp.data(), int(k), yp.data(), int(nout), v0.local_size()),
+        "ssp_gemm_outer_set");
+  return true;
+}
+
 // Sequential self-orthonormalisation of R (reference propose_rspace.h:450-465) in two passes per
 // vector: ssp_scal_inner (r_i *= 1/|r_i|, then <r_i, r_j> for j > i) and ssp_axpy_norm
 // (r_j -= <r_i, r_j> r_i for j > i, then |r_{i+1}|^2).  The vector updates are the reference loop's

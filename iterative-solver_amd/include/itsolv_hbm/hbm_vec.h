@@ -87,6 +87,9 @@ class Vec {
     check_status(ssp_copy(ctx(), m_data, o.m_data, m_local), "ssp_copy");
   }
   Vec(Vec&& o) noexcept { swap(o); }
+  // A vector of the same length and distribution whose contents are not initialised (for
+  // destinations that a kernel writes without reading).
+  Vec alloc_like() const { return Vec(m_dev, m_size); }
   Vec& operator=(const Vec& o) {
     if (this != &o) {
       Vec t(o);

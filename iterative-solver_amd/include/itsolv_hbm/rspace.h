@@ -233,8 +233,21 @@ std::tuple<std::vector<Q>, std::vector<Q>> construct_dspace(const Matrix<double>
   const size_t nD = proj.rows(), nqd = qdel.size();
   const auto qp = xs.cparamsq(), qa = xs.cactionsq(), dp = xs.cparamsd(), da = xs.cactionsd();
   std::vector<Q> newp, newa;
+  // The reference's copy + fill(0) + axpy loops, or one write-only pass when the handler has it
+  // (sources in the same order: Q vectors being deleted, then D).
+  std::vector<const Q*> srcp, srca;
+  for (size_t j = 0; j < nqd; ++j) srcp.push_back(&qp.at(qdel[j]).get()), srca.push_back(&qa.at(qdel[j]).get());
+  for (size_t j = 0; j < d.nD; ++j) srcp.push_back(&dp.at(j).get()), srca.push_back(&da.at(j).get());
+  using array::fused_new_combinations;
+  bool fused = false;
+  if (nD > 0 && !srcp.empty()) {
+    Matrix<double> c(std::make_pair(nD, srcp.size()));
+    for (size_t i = 0; i < nD; ++i)
+      for (size_t j = 0; j < srcp.size(); ++j) c(i, j) = proj(i, j);
+    fused = fused_new_combinations(h, c, srcp, newp) && fused_new_combinations(h, c, srca, newa);
+  }
   const Q* proto = !qp.empty() ? &qp.front().get() : (!dp.empty() ? &dp.front().get() : nullptr);
-  if (proto)
+  if (proto && !fused)
     for (size_t i = 0; i < nD; ++i) {
       newp.emplace_back(h.copy(*proto));
       newa.emplace_back(h.copy(*proto));
@@ -244,7 +257,7 @@ std::tuple<std::vector<Q>, std::vector<Q>> construct_dspace(const Matrix<double>
   // The reference's axpy loops, registered per destination set on a lazy handle: every destination
   // receives its sources in increasing order, so a device handler applies each set as one
   // gemm_outer, bit for bit the axpy sequence (fused_axpy); params and actions are disjoint sets.
-  {
+  if (!fused) {
     auto lp = h.lazy_handle();
     auto la = h.lazy_handle();
     for (size_t i = 0; i < nD; ++i) {
