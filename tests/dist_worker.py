@@ -10,6 +10,7 @@ Cases:
   reductions  (CPU) oracle shard pieces + the product's host exchange + ssp_select_merge
   gpu_ops     (GPU) every reducing op of libsubspace_hip.so on shards, host communicator attached
   gpu_solver  (GPU) Davidson / DIIS on sharded HBM vectors vs the single-rank CPU reference path
+  gpu_traces  (GPU) the committed BASELINE-size traces (C4 shape, C2, C5 descent) on shards
 
 Exit status 0 = every assertion held on this rank.
 """
@@ -156,6 +157,32 @@ def case_gpu_solver(comm):
     ctx.close()
 
 
+def case_gpu_traces(comm):
+    """North-star traces on shards: the C4 shape (8 roots + P 16, rank-8 H, N = 1e7), C2 and C5's
+    fixed-length DIIS descent, sharded over this world on HBM, against the committed per-iteration
+    traces of the single-rank reference CPU path (tests/golden/traces.json) under the same bar as the
+    single-GPU runs (trace_check.assert_trace)."""
+    import numpy as np
+
+    import itsolv_hbm as ih
+    import subspace_hip as sh
+    from trace_check import EIG_REL, T, assert_trace
+
+    rank, world = comm.rank, comm.nranks
+    ctx = sh.Context(0)
+    ctx.attach_host_comm(comm)
+    for name in ("C3_n1e7_rank8", "C2_rank8", "C5_n1e7_traj12"):
+        ref = T[name]
+        c = ref["case"]
+        nl = sh.shard_range(c["n"], world, rank)[1]
+        run = ih.diis_synthetic if c["kind"] == "diis" else ih.davidson_synthetic
+        g = run(ctx, c["n"], c["rho"], c["rank"], c["seed"], n_local=nl, solutions=False, **ref["options"])
+        assert_trace(g, ref, f"{name} on {world} shards")
+        if c["kind"] == "davidson":
+            np.testing.assert_allclose(g["eigenvalues"], ref["eigenvalues"], rtol=EIG_REL, atol=0)
+    ctx.close()
+
+
 def case_gpu_distr(comm):
     """The reference's distributed-array known answers (tests/distr_cases.py) on HBM shards."""
     import distr_cases
@@ -170,11 +197,12 @@ def case_gpu_distr(comm):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--comm", choices=["gloo", "hub"], required=True)
-    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver", "gpu_distr"], required=True)
+    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver", "gpu_distr", "gpu_traces"],
+                    required=True)
     a = ap.parse_args()
     comm = make_comm(a.comm)
     {"reductions": case_reductions, "gpu_ops": case_gpu_ops, "gpu_solver": case_gpu_solver,
-     "gpu_distr": case_gpu_distr}[a.case](comm)
+     "gpu_distr": case_gpu_distr, "gpu_traces": case_gpu_traces}[a.case](comm)
     if a.comm == "gloo":
         import torch.distributed as dist
 

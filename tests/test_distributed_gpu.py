@@ -27,3 +27,10 @@ def test_world2_davidson_and_diis_on_shards():
 def test_world2_reference_distributed_array_known_answers():
     # testDistrArray.h / testArrayHandlerDistrSparse.cpp known answers on HBM shards (tests/distr_cases.py)
     run_hub("gpu_distr", timeout=300)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_traces_match_reference_path(world):
+    # C4's shape (8 roots + P 16, rank-8 H) at N = 1e7, C2 and C5's DIIS descent, sharded over 2 and 4
+    # ranks on HBM: step for step with the single-rank reference CPU path's committed traces
+    run_hub("gpu_traces", world=world, timeout=600)

@@ -1,0 +1,43 @@
+"""The north-star trace bar shared by the single-GPU trace tests (test_traces_gpu.py) and the sharded
+ones (dist_worker.py gpu_traces): a solver run against a committed per-iteration trace of the
+reference CPU path (tests/golden/traces.json, tests/golden/make_traces.py).  The bar itself is
+described in test_traces_gpu.py's docstring."""
+import json
+import os
+
+import numpy as np
+
+T = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "traces.json")))
+DAVIDSON = sorted(k for k, v in T.items() if not k.startswith("_") and v["case"]["kind"] == "davidson")
+EIG_REL, ERR_REL, ERR_ABS, DEV_FACTOR = 1e-10, 1e-6, 1e-13, 10.0
+
+
+def error_tolerance(ref):
+    """Per-iteration absolute tolerance on the errors: ERR_REL * e + DEV_FACTOR * (the reference CPU
+    path's own deviation under reordering, max over the iteration and its two neighbours)."""
+    e = np.array(ref["trace"]["errors"])
+    dev = np.array(ref["reordered"]["error_abs_dev"] + [0.0] * (len(e) - len(ref["reordered"]["error_abs_dev"])))
+    win = np.maximum.reduce([dev, np.r_[dev[1:], 0.0], np.r_[0.0, dev[:-1]]])
+    return ERR_REL * e + DEV_FACTOR * win[:, None] + ERR_ABS
+
+
+def assert_trace(gpu, ref, name):
+    assert gpu["converged"] == ref["converged"], name
+    assert gpu["iterations"] == ref["iterations"], (name, gpu["iterations"], ref["iterations"])
+    g, r = gpu["trace"], ref["trace"]
+    if ref["reordered"]["same_steps"]:
+        assert gpu["r_creations"] == ref["r_creations"], (name, gpu["r_creations"], ref["r_creations"])
+        assert gpu["q_creations"] == ref["q_creations"], name
+        assert list(g["nq"]) == r["nq"], (name, list(g["nq"]), r["nq"])
+        assert list(g["nwork"]) == r["nwork"], name
+    if r["eigenvalues"]:
+        re = np.array(r["eigenvalues"])
+        de = np.abs(g["eigenvalues"] - re)
+        assert np.all(de <= EIG_REL * np.maximum(np.abs(re), 1.0)), (name, de.max())
+    rr = np.array(r["errors"])
+    dr = np.abs(g["errors"] - rr)
+    tol = error_tolerance(ref)
+    assert np.all(dr <= tol), (name, np.max(dr / tol))
+    # the reported run ends where the reference's does: converged errors below the threshold
+    if ref["converged"]:
+        assert np.max(g["errors"][-1]) <= ref["options"]["convergence_threshold"], name
