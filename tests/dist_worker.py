@@ -171,13 +171,19 @@ def case_gpu_traces(comm):
     rank, world = comm.rank, comm.nranks
     ctx = sh.Context(0)
     ctx.attach_host_comm(comm)
-    for name in ("C3_n1e7_rank8", "C2_rank8", "C5_n1e7_traj12"):
+    names = ("C3_n1e7_rank8", "C2_rank8", "C5_n1e7_traj12")
+    if os.environ.get("SSP_TRACES_FULL"):  # BASELINE C4 itself: N = 1e8, 8 roots + P 16
+        names = ("C3_n1e8_rank1",)
+    for name in names:
         ref = T[name]
         c = ref["case"]
         nl = sh.shard_range(c["n"], world, rank)[1]
         run = ih.diis_synthetic if c["kind"] == "diis" else ih.davidson_synthetic
         g = run(ctx, c["n"], c["rho"], c["rank"], c["seed"], n_local=nl, solutions=False, **ref["options"])
         assert_trace(g, ref, f"{name} on {world} shards")
+        if rank == 0:
+            print(f"{name} on {world} shards: {g['iterations']} iterations (CPU path {ref['iterations']}), "
+                  f"{g['seconds']:.3f} s", flush=True)
         if c["kind"] == "davidson":
             np.testing.assert_allclose(g["eigenvalues"], ref["eigenvalues"], rtol=EIG_REL, atol=0)
     ctx.close()

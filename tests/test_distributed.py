@@ -62,6 +62,7 @@ def run_hub(case, world=WORLD, timeout=600):
     for rank, (p, out) in enumerate(zip(procs, outs)):
         assert p.returncode == 0, f"rank {rank} failed:\n{out[-4000:]}"
         assert f"{case} OK" in out
+    return outs
 
 
 @pytest.mark.parametrize("n", [0, 1, 7, 8, 1000, 10**8 + 3])

@@ -33,4 +33,13 @@ def test_world2_reference_distributed_array_known_answers():
 def test_sharded_traces_match_reference_path(world):
     # C4's shape (8 roots + P 16, rank-8 H) at N = 1e7, C2 and C5's DIIS descent, sharded over 2, 4 and 8
     # ranks on HBM: step for step with the single-rank reference CPU path's committed traces
-    run_hub("gpu_traces", world=world, timeout=600)
+    print(run_hub("gpu_traces", world=world, timeout=600)[0])
+
+
+def test_c4_full_size_on_8_shards(monkeypatch):
+    # BASELINE config C4 at full size: N = 1e8, 8 roots + P 16, sharded over 8 ranks (12.5e6 elements,
+    # 100 MB per vector per rank, 90 GB in all) -- here 8 processes on one MI355X with the host
+    # communicator in place of RCCL -- against the committed single-rank CPU-path trace (traces.json
+    # C3_n1e8_rank1) under the same bar as the one-GPU run.
+    monkeypatch.setenv("SSP_TRACES_FULL", "1")
+    print(run_hub("gpu_traces", world=8, timeout=600)[0])
