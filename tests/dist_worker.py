@@ -189,6 +189,29 @@ def case_gpu_traces(comm):
     ctx.close()
 
 
+def case_gpu_c5_full(comm):
+    """BASELINE C5 at full size (NonLinearEquationsDIIS, N = 1e8) sharded over this world: converges
+    to x = 1 at the threshold on every shard (past the 1e-6 plateau the reference algorithm itself
+    is rounding-chaotic, so the iteration count is reported, not compared; test_traces_gpu.py)."""
+    import numpy as np
+
+    import itsolv_hbm as ih
+    import subspace_hip as sh
+
+    rank, world = comm.rank, comm.nranks
+    ctx = sh.Context(0)
+    ctx.attach_host_comm(comm)
+    n = 100_000_000
+    nl = sh.shard_range(n, world, rank)[1]
+    r = ih.diis_synthetic(ctx, n, 0.01, 3, 3, n_local=nl, convergence_threshold=1e-8, max_size_qspace=6)
+    assert r["converged"], r["iterations"]
+    assert r["errors"][0] < 1e-8 and r["residual_norms"][0] < 1e-8
+    assert np.max(np.abs(r["x"] - 1.0)) <= 1e-8  # |x - 1| <= |H (x - 1)| / lambda_min(H), lambda_min >= 1
+    if rank == 0:
+        print(f"C5 N=1e8 on {world} shards: {r['iterations']} iterations, {r['seconds']:.3f} s", flush=True)
+    ctx.close()
+
+
 def case_gpu_distr(comm):
     """The reference's distributed-array known answers (tests/distr_cases.py) on HBM shards."""
     import distr_cases
@@ -203,12 +226,12 @@ def case_gpu_distr(comm):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--comm", choices=["gloo", "hub"], required=True)
-    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver", "gpu_distr", "gpu_traces"],
+    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver", "gpu_distr", "gpu_traces", "gpu_c5_full"],
                     required=True)
     a = ap.parse_args()
     comm = make_comm(a.comm)
     {"reductions": case_reductions, "gpu_ops": case_gpu_ops, "gpu_solver": case_gpu_solver,
-     "gpu_distr": case_gpu_distr, "gpu_traces": case_gpu_traces}[a.case](comm)
+     "gpu_distr": case_gpu_distr, "gpu_traces": case_gpu_traces, "gpu_c5_full": case_gpu_c5_full}[a.case](comm)
     if a.comm == "gloo":
         import torch.distributed as dist
 

@@ -43,3 +43,9 @@ def test_c4_full_size_on_8_shards(monkeypatch):
     # C3_n1e8_rank1) under the same bar as the one-GPU run.
     monkeypatch.setenv("SSP_TRACES_FULL", "1")
     print(run_hub("gpu_traces", world=8, timeout=600)[0])
+
+
+def test_c5_full_size_on_8_shards():
+    # BASELINE config C5 at full size (DIIS, N = 1e8) over 8 ranks (8 processes on one MI355X, host
+    # communicator): converges to x = 1 on every shard
+    print(run_hub("gpu_c5_full", world=8, timeout=600)[0])
