@@ -4,6 +4,7 @@
 #include "iterative_solver_c.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <limits>
@@ -66,9 +67,22 @@ void push(Instance&& in) {
   instances.push_back(std::make_unique<Instance>(std::move(in)));
 }
 
+// Without IterativeSolverHbmSetContext the node-local rank a launcher exports (torchrun, Open MPI,
+// MPICH, Slurm) picks the device, so independent processes on one node spread over its GPUs
+// instead of all landing on device 0.
+int default_device() {
+  for (const char* var : {"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "SLURM_LOCALID"}) {
+    const char* s = std::getenv(var);
+    if (!s || !*s) continue;
+    const int r = std::atoi(s), n = ssp_device_count();
+    return (r >= 0 && n > 0) ? r % n : 0;
+  }
+  return 0;
+}
+
 std::shared_ptr<Device> make_device() {
   if (g_user_ctx) return std::make_shared<Device>(g_user_ctx, true);
-  return std::make_shared<Device>(0);
+  return std::make_shared<Device>(default_device());
 }
 
 void setup(Instance& in, size_t n, size_t* range_begin, size_t* range_end) {
