@@ -29,9 +29,9 @@ def test_world2_reference_distributed_array_known_answers():
     run_hub("gpu_distr", timeout=300)
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_sharded_traces_match_reference_path(world):
-    # C4's shape (8 roots + P 16, rank-8 H) at N = 1e7, C2 and C5's DIIS descent, sharded over 2, 4 and 8
+    # C4's shape (8 roots + P 16, rank-8 H) at N = 1e7, C2 and C5's DIIS descent, sharded over 2, 3 (ragged), 4 and 8
     # ranks on HBM: step for step with the single-rank reference CPU path's committed traces
     print(run_hub("gpu_traces", world=world, timeout=600)[0])
 
