@@ -265,9 +265,26 @@ def host_parallel(m, k, seconds):
 
 
 C3 = dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48, reset_D=8, convergence_threshold=1e-8)
-# BASELINE config C5 (NonLinearEquationsDIIS, N = 1e8): the DIIS problem of tools/solver_ledger.py and
-# tests/golden/traces.json (r = H (x - 1), x from e_0, test_NonLinearEquations.cpp:25-49)
-C5 = dict(rho=0.01, rank=3, seed=3, max_size_qspace=6, convergence_threshold=1e-8)
+# BASELINE config C5 (NonLinearEquationsDIIS, N = 1e8): the well-posed instance of tests/golden/traces.json
+# C5_n1e7 / C5_n1e8 (itsolv_hbm.c5_spec: r = H (x - 1), x from e_0, the reference test's 1 1^T + diag
+# form of test_NonLinearEquations.cpp:25-49 with the coupling scaled by 1/N and a bounded diagonal)
+C5_OPTIONS = dict(max_size_qspace=6, convergence_threshold=1e-8)
+TRACES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "traces.json")
+
+
+def cpu_trace(kind, n_global):
+    """The committed reference-CPU-path trace of this solve, if there is one (parity evidence only)."""
+    name = {("diis", 10**7): "C5_n1e7", ("diis", 10**8): "C5_n1e8",
+            ("davidson", 10**8): "C3_n1e8_rank8", ("davidson", 10**7): "C3_n1e7_rank8"}.get((kind, int(n_global)))
+    try:
+        with open(TRACES) as f:
+            t = json.load(f)
+    except OSError:
+        return None, None
+    ref = t.get(name) if name else None
+    if ref and kind == "davidson" and ref["options"].get("max_size_qspace") != C3["max_size_qspace"]:
+        return None, None
+    return name, ref
 REDUCING_OPS = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "select", "gemm_inner_sparse")
 
 
@@ -289,7 +306,7 @@ def in_solver(ctx, n_global, world, barrier, repeat=2, kind="davidson"):
         barrier()
         t0 = time.perf_counter()
         if kind == "diis":
-            r = ih.diis_synthetic(ctx, n_global, n_local=0, **C5)
+            r = ih.diis_synthetic(ctx, n_global, n_local=0, solutions=False, **ih.c5_spec(n_global), **C5_OPTIONS)
         else:
             r = ih.davidson_synthetic(ctx, n_global, n_local=0, **C3)
         ctx.synchronize()
@@ -301,9 +318,17 @@ def in_solver(ctx, n_global, world, barrier, repeat=2, kind="davidson"):
     red = sum(v["calls"] for op, v in led.items() if op.split("(")[0] in REDUCING_OPS or op.startswith("select"))
     it = max(1, r["iterations"])
     top = sorted(led.items(), key=lambda kv: -kv[1]["ms"])[:6]
+    tname, ref = cpu_trace(kind, n_global)
+    parity = {}
+    if ref is not None:
+        same = (r["iterations"] == ref["iterations"] and r["r_creations"] == ref["r_creations"]
+                and list(r["trace"]["nq"]) == ref["trace"]["nq"] and list(r["trace"]["nwork"]) == ref["trace"]["nwork"])
+        parity = {"cpu_path_trace": f"tests/golden/traces.json:{tname}", "cpu_path_iterations": ref["iterations"],
+                  "same_steps_as_cpu_path": bool(same)}
     if kind == "diis":
-        config = ("NonLinearEquationsDIIS C5: r = H (x - 1), H = diag(1+i) + 0.01 sum_{l<3} u u^T, x from e_0, "
-                  "max_size_qspace 6, threshold 1e-8" + (f", sharded over {world} ranks" if world > 1 else ""))
+        config = ("NonLinearEquationsDIIS C5: r = H (x - 1), H = diag(1 + 2 frac(i phi)) + (1/N) 1 1^T, x from e_0, "
+                  "approximate preconditioner diagonal (alpha 0.5), max_size_qspace 6, threshold 1e-8"
+                  + (f", sharded over {world} ranks" if world > 1 else ""))
     else:
         config = ("LinearEigensystemDavidson " + ("C3" if world == 1 else "C4") + ": 8 roots + P 16, rank-8 "
                   "H = diag(1+i) + 0.1 sum u u^T, max_size_qspace 48, reset_D 8, threshold 1e-8")
@@ -325,6 +350,7 @@ def in_solver(ctx, n_global, world, barrier, repeat=2, kind="davidson"):
                     for op, v in top},
         "eigenvalues": [round(float(e), 12) for e in r["eigenvalues"][:8]] if kind != "diis" else None,
         "final_error": float(r["errors"][0]) if kind == "diis" else None,
+        **parity,
     }
 
 

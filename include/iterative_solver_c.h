@@ -15,10 +15,17 @@
  * Differences:
  *  - `fcomm` (a Fortran MPI communicator) is ignored: ranks and the device are taken from the
  *    context set by IterativeSolverHbmSetContext (an ssp_ctx with an RCCL or host communicator
- *    attached), or a single-rank context on device 0 is created.
+ *    attached), or a single-rank context is created on the device of the node-local rank the
+ *    launcher exports (LOCAL_RANK, OMPI_COMM_WORLD_LOCAL_RANK, MPI_LOCALRANKID or SLURM_LOCALID,
+ *    first one set, modulo the visible device count; device 0 without any of them).
  *  - Supported algorithms: LinearEigensystem and LinearEquations "Davidson" (or ""),
  *    NonLinearEquations "DIIS" (or ""), Optimize "BFGS" (or "") and "SD"; `minimize` is ignored,
  *    as in the reference (IterativeSolverCMPI.cpp:250-268).
+ *  - Davidson instances (LinearEigensystem, LinearEquations) orthogonalise new R vectors by block
+ *    Gram-Schmidt (coefficients by forward substitution through the stored overlaps, one gemm_outer
+ *    per space): the same projection as the reference's sequential MGS in exact
+ *    arithmetic, not bit-identical.  "BLOCK_GRAM_SCHMIDT=false" in the options string restores
+ *    the reference's MGS.
  *  - IterativeSolverAddVector on a non-linear solver (DIIS) passes the vector through the solver's
  *    own add_vector (residual norm, convergence flag, least-important-vector deletion), as the
  *    reference's solve() driver does; the reference's C layer reaches the generic vector-list
@@ -91,7 +98,7 @@ int IterativeSolver_mpi_finalize(void);
 
 /* ---- extension: device / communicator selection ----------------------------------------- */
 /* Use `ctx` (not owned) for the instances initialised after this call; NULL restores the
- * default (a private single-rank context on device 0).  Returns 0. */
+ * default (a private single-rank context on the node-local rank's device, see above).  Returns 0. */
 int IterativeSolverHbmSetContext(ssp_ctx* ctx);
 /* enable = 0: errors are recorded (IterativeSolverHbmLastError, cleared by every call) instead of
  * thrown, and the failing call returns 0 -- for callers that cannot unwind C++ exceptions

@@ -85,6 +85,14 @@ int itsolv_davidson_dense(ssp_ctx* ctx, const double* h, size_t n, const itsolv_
 int itsolv_diis_synthetic(ssp_ctx* ctx, size_t n, double rho, int rank, unsigned long long seed,
                           const itsolv_options* opt, itsolv_result* out, double* x_out);
 
+/* The same two solves on any synthetic family (subspace_hip.h sspx_synth), e.g. BASELINE config
+ * C5's well-posed DIIS instance: diag_kind SSPX_DIAG_BOUNDED, rho = 1/n, rank 1, alpha 0.5
+ * (itsolv_hbm/problems.h c5_spec). */
+int itsolv_davidson_synth(ssp_ctx* ctx, size_t n, const sspx_synth* spec, const itsolv_options* opt,
+                          itsolv_result* out, double* solutions_out);
+int itsolv_diis_synth(ssp_ctx* ctx, size_t n, const sspx_synth* spec, const itsolv_options* opt, itsolv_result* out,
+                      double* x_out);
+
 /* DIIS on r(x) = H (x - 1) for a dense row-major H (reference test_NonLinearEquations.cpp:38-49). */
 /* LinearEquationsDavidson (reference itsolv/LinearEquationsDavidson.h): A x_r = b_r for nrhs
  * right-hand sides b (row-major nrhs x n, host), dense row-major A resident in HBM (single rank).

@@ -180,9 +180,29 @@ int ssp_construct_solution(ssp_ctx* ctx, const double* palphas, const size_t* pt
                            double* const* yy, int m, size_t n, size_t offset);
 
 /* ---- synthetic problem (harness only; not a reference operation) ----------------------------
- * H = diag(1 + g) + rho * sum_{l<rank} u_l u_l^T, g = global index, u_0 = 1 and for l > 0
+ * H = diag(d) + rho * sum_{l<rank} u_l u_l^T, g = global index, u_0 = 1 and for l > 0
  * u_l(g) = +/-1 from a splitmix64 hash of (seed, l, g).  The rank-one (rank=1) case is the
- * matrix of reference test/itsolv/test_rayleigh_quotient.cpp:37-42.  yy[v] = H xx[v]. */
+ * matrix of reference test/itsolv/test_rayleigh_quotient.cpp:37-42.  yy[v] = H xx[v].
+ * Diagonal families (itsolv_hbm/problems.h SyntheticSpec):
+ *   SSPX_DIAG_LINEAR   d_g = 1 + g; sspx_synth_diagonal reports H_gg = 1 + g + rank*rho
+ *   SSPX_DIAG_BOUNDED  d_g = 1 + 2 frac(g phi1); sspx_synth_diagonal reports the approximate
+ *                      diagonal d_g (1 + alpha (2 frac(g phi2) - 1)) (C5's DIIS preconditioner) */
+#define SSPX_DIAG_LINEAR 0
+#define SSPX_DIAG_BOUNDED 1
+typedef struct {
+  double rho;
+  int rank;                /* 1..16 */
+  unsigned long long seed;
+  int diag_kind;           /* SSPX_DIAG_* */
+  double alpha;            /* SSPX_DIAG_BOUNDED: preconditioner mismatch */
+} sspx_synth;
+int sspx_synth_action(ssp_ctx* ctx, const sspx_synth* spec, const double* const* xx, double* const* yy, int nvec,
+                      size_t n, size_t offset);
+/* yy[v] += rho * sum_l w[v*rank + l] u_l */
+int sspx_synth_add_lowrank(ssp_ctx* ctx, const sspx_synth* spec, double* const* yy, int nvec, size_t n,
+                           size_t offset, const double* w);
+int sspx_synth_diagonal(ssp_ctx* ctx, const sspx_synth* spec, double* d, size_t n, size_t offset);
+/* The SSPX_DIAG_LINEAR forms of the three calls above. */
 int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* yy, int nvec, size_t n,
                           size_t offset, double rho, int rank, unsigned long long seed);
 /* yy[v] += rho * sum_l w[v*rank + l] u_l  (the low-rank part of H applied to P-space vectors) */

@@ -1,8 +1,11 @@
 // Synthetic problem generator for tests and benchmarks (not a reference hot-path operation).
 //
-// H = diag(1 + g) + rho * sum_{l < rank} u_l u_l^T, g = global index; u_0 = 1 (the matrix of
+// H = diag(d) + rho * sum_{l < rank} u_l u_l^T, g = global index; u_0 = 1 (the matrix of
 // reference test/itsolv/test_rayleigh_quotient.cpp:37-42 for rank 1) and u_l(g) = +/-1 from
-// splitmix64 for l > 0.  Applying H costs one rank x nvec reduction (+ allreduce) and one stream.
+// splitmix64 for l > 0.  d_g = 1 + g (SSPX_DIAG_LINEAR, the Davidson configurations) or
+// d_g = 1 + 2 frac(g phi1) (SSPX_DIAG_BOUNDED, the C5 DIIS instance; its preconditioner diagonal is
+// d_g (1 + alpha (2 frac(g phi2) - 1)), itsolv_hbm/problems.h).  Applying H costs one rank x nvec
+// reduction (+ allreduce) and one stream.
 #include <algorithm>
 #include <cstdint>
 #include <vector>
@@ -42,6 +45,20 @@ __device__ __forceinline__ unsigned sign_mask(const unsigned long long (&key)[16
 
 __device__ __forceinline__ double flip(unsigned mask, int l, double v) { return ((mask >> l) & 1u) ? -v : v; }
 
+// The diagonal families, bit-identical to itsolv_hbm/problems.h SyntheticSpec::d / ::diagonal (the
+// same IEEE operations in the same order, contraction off).
+constexpr double kPhi1 = 0x1.3c6ef372fe950p-1;
+constexpr double kPhi2 = 0x1.827f5352054c6p-1;
+__device__ __forceinline__ double frac_phi(unsigned long long g, double phi) {
+#pragma clang fp contract(off)
+  const double f = double(g) * phi;
+  return f - floor(f);
+}
+__device__ __forceinline__ double synth_d(int kind, unsigned long long g) {
+#pragma clang fp contract(off)
+  return kind == SSPX_DIAG_BOUNDED ? 1.0 + 2.0 * frac_phi(g, kPhi1) : 1.0 + double(g);
+}
+
 struct SynthArgs {
   const double* x[kMaxVec];
   double* y[kMaxVec];
@@ -49,6 +66,7 @@ struct SynthArgs {
   const unsigned short* mask;  // [n] sign masks of this shard
   int nvec;
   int rank;
+  int diag_kind;
   size_t n;
   size_t offset;
   double rho;
@@ -141,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
   for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += stride) {
     const unsigned mm = mask2[i];
     const size_t g = a.offset + 2 * i;
-    const double d0 = 1.0 + double(g), d1 = 1.0 + double(g + 1);
+    const double d0 = synth_d(a.diag_kind, g), d1 = synth_d(a.diag_kind, g + 1);
     for (int v = 0; v < a.nvec; ++v) {
       const double s0 = lowrank<R>(mm, a.coeff + v * R), s1 = lowrank<R>(mm >> 16, a.coeff + v * R);
       double2 out;
@@ -158,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
   if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
     const size_t e = a.n - 1;
     const unsigned mm = a.mask[e];
-    const double d = 1.0 + double(a.offset + e);
+    const double d = synth_d(a.diag_kind, a.offset + e);
     for (int v = 0; v < a.nvec; ++v) {
       const double s = lowrank<R>(mm, a.coeff + v * R);
       a.y[v][e] = ADD ? fma(a.rho, s, a.y[v][e]) : fma(d, a.x[v][e], a.rho * s);
@@ -239,10 +257,20 @@ int ensure_mask(ssp_ctx* ctx, SynthArgs& a, unsigned long long seed) {
   return SSP_OK;
 }
 
-__global__ __launch_bounds__(kBlock) void k_synth_diag(double* d, size_t n, size_t offset, double rho, int rank) {
+__global__ __launch_bounds__(kBlock) void k_synth_diag(double* d, size_t n, size_t offset, double rho, int rank,
+                                                      int kind, double alpha) {
+#pragma clang fp contract(off)
   const size_t stride = size_t(gridDim.x) * kBlock;
-  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
-    d[i] = 1.0 + double(offset + i) + rank * rho;
+  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+    const unsigned long long g = offset + i;
+    if (kind == SSPX_DIAG_BOUNDED) {
+      const double t = 2.0 * frac_phi(g, kPhi2) - 1.0;
+      const double s = alpha * t;
+      d[i] = synth_d(kind, g) * (1.0 + s);
+    } else {
+      d[i] = 1.0 + double(g) + rank * rho;
+    }
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_fill_random(double* x, size_t n, size_t offset, unsigned long long key) {
@@ -278,14 +306,19 @@ __global__ void k_dense_action(const DenseArgs p) {
 
 extern "C" {
 
-int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* yy, int nvec, size_t n, size_t offset,
-                          double rho, int rank, unsigned long long seed) {
+int sspx_synth_action(ssp_ctx* ctx, const sspx_synth* spec, const double* const* xx, double* const* yy, int nvec,
+                      size_t n, size_t offset) {
   SSP_CHECK_CTX(ctx);
-  if (rank < 1 || rank > kMaxRank) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_action: rank out of [1,16]");
-  if (nvec < 0) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_action: nvec < 0");
+  if (!spec) return ssp::set_error(SSP_ERR_ARG, "sspx_synth_action: null spec");
+  const int rank = spec->rank;
+  const unsigned long long seed = spec->seed;
+  if (rank < 1 || rank > kMaxRank) return ssp::set_error(SSP_ERR_ARG, "sspx_synth_action: rank out of [1,16]");
+  if (spec->diag_kind != SSPX_DIAG_LINEAR && spec->diag_kind != SSPX_DIAG_BOUNDED)
+    return ssp::set_error(SSP_ERR_ARG, "sspx_synth_action: unknown diag_kind");
+  if (nvec < 0) return ssp::set_error(SSP_ERR_ARG, "sspx_synth_action: nvec < 0");
   for (int v = 0; v < nvec; ++v)
     if (!aligned16(xx[v]) || !aligned16(yy[v]))
-      return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_action: vectors must be 16-byte aligned");
+      return ssp::set_error(SSP_ERR_ARG, "sspx_synth_action: vectors must be 16-byte aligned");
   // x read twice (coefficients, then apply) and y written: 24 N per vector (the 2 B per element
   // sign table is not counted).
   ssp::LedgerScope ls(ctx, "action(synthetic)", 24.0 * n * nvec);
@@ -293,9 +326,10 @@ int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* 
     SynthArgs a{};
     a.nvec = std::min(kMaxVec, nvec - v0);
     a.rank = rank;
+    a.diag_kind = spec->diag_kind;
     a.n = n;
     a.offset = offset;
-    a.rho = rho;
+    a.rho = spec->rho;
     for (int v = 0; v < a.nvec; ++v) {
       a.x[v] = xx[v0 + v];
       a.y[v] = yy[v0 + v];
@@ -330,24 +364,27 @@ int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* 
   return SSP_OK;
 }
 
-int sspx_synthetic_add_lowrank(ssp_ctx* ctx, double* const* yy, int nvec, size_t n, size_t offset, double rho,
-                               int rank, unsigned long long seed, const double* w) {
+int sspx_synth_add_lowrank(ssp_ctx* ctx, const sspx_synth* spec, double* const* yy, int nvec, size_t n,
+                           size_t offset, const double* w) {
   SSP_CHECK_CTX(ctx);
-  if (rank < 1 || rank > kMaxRank) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_add_lowrank: rank out of [1,16]");
+  if (!spec) return ssp::set_error(SSP_ERR_ARG, "sspx_synth_add_lowrank: null spec");
+  const int rank = spec->rank;
+  if (rank < 1 || rank > kMaxRank) return ssp::set_error(SSP_ERR_ARG, "sspx_synth_add_lowrank: rank out of [1,16]");
   if (n == 0 || nvec <= 0) return SSP_OK;
   for (int v = 0; v < nvec; ++v)
-    if (!aligned16(yy[v])) return ssp::set_error(SSP_ERR_ARG, "sspx_synthetic_add_lowrank: vectors must be 16-byte aligned");
+    if (!aligned16(yy[v])) return ssp::set_error(SSP_ERR_ARG, "sspx_synth_add_lowrank: vectors must be 16-byte aligned");
   ssp::LedgerScope ls(ctx, "p_action(synthetic)", 16.0 * n * nvec);
   for (int v0 = 0; v0 < nvec; v0 += kMaxVec) {
     SynthArgs a{};
     a.nvec = std::min(kMaxVec, nvec - v0);
     a.rank = rank;
+    a.diag_kind = spec->diag_kind;
     a.n = n;
     a.offset = offset;
-    a.rho = rho;
+    a.rho = spec->rho;
     for (int v = 0; v < a.nvec; ++v) a.y[v] = yy[v0 + v];
-    for (int l = 0; l < rank; ++l) a.key[l] = stream_key(seed, 1000 + l);
-    SSP_TRY(ensure_mask(ctx, a, seed));
+    for (int l = 0; l < rank; ++l) a.key[l] = stream_key(spec->seed, 1000 + l);
+    SSP_TRY(ensure_mask(ctx, a, spec->seed));
     void* coeff;
     SSP_TRY(ssp::upload_small(ctx, w + size_t(v0) * rank, size_t(a.nvec) * rank * sizeof(double), &coeff));
     a.coeff = static_cast<const double*>(coeff);
@@ -357,13 +394,32 @@ int sspx_synthetic_add_lowrank(ssp_ctx* ctx, double* const* yy, int nvec, size_t
   return SSP_OK;
 }
 
-int sspx_synthetic_diagonal(ssp_ctx* ctx, double* d, size_t n, size_t offset, double rho, int rank) {
+int sspx_synth_diagonal(ssp_ctx* ctx, const sspx_synth* spec, double* d, size_t n, size_t offset) {
   SSP_CHECK_CTX(ctx);
+  if (!spec) return ssp::set_error(SSP_ERR_ARG, "sspx_synth_diagonal: null spec");
   if (n == 0) return SSP_OK;
-  hipLaunchKernelGGL(k_synth_diag, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, d, n, offset, rho,
-                     rank);
+  hipLaunchKernelGGL(k_synth_diag, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, d, n, offset,
+                     spec->rho, spec->rank, spec->diag_kind, spec->alpha);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
+}
+
+// The SSPX_DIAG_LINEAR entry points of round 1 (d_g = 1 + g).
+int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* yy, int nvec, size_t n, size_t offset,
+                          double rho, int rank, unsigned long long seed) {
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  return sspx_synth_action(ctx, &s, xx, yy, nvec, n, offset);
+}
+
+int sspx_synthetic_add_lowrank(ssp_ctx* ctx, double* const* yy, int nvec, size_t n, size_t offset, double rho,
+                               int rank, unsigned long long seed, const double* w) {
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  return sspx_synth_add_lowrank(ctx, &s, yy, nvec, n, offset, w);
+}
+
+int sspx_synthetic_diagonal(ssp_ctx* ctx, double* d, size_t n, size_t offset, double rho, int rank) {
+  const sspx_synth s{rho, rank, 0, SSPX_DIAG_LINEAR, 0.0};
+  return sspx_synth_diagonal(ctx, &s, d, n, offset);
 }
 
 int sspx_fill_random(ssp_ctx* ctx, double* x, size_t n, size_t offset, unsigned long long seed,

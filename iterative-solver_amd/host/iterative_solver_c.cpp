@@ -103,7 +103,7 @@ void ensure_r(Instance& in, size_t nvec) {
 // This rank's range of host vectors [k*dimension + offset, +local) <-> HBM.
 void upload(Instance& in, std::vector<Vec>& v, size_t nvec, const double* host) {
   for (size_t k = 0; k < nvec; ++k)
-    check(ssp_upload(in.dev->ctx(), v[k].data(), host + k * in.dimension + in.offset, in.local), "ssp_upload");
+    check(ssp_upload(in.dev->ctx(), v[k].data_wo(), host + k * in.dimension + in.offset, in.local), "ssp_upload");
 }
 void download(Instance& in, std::vector<Vec>& v, size_t nvec, double* host) {
   for (size_t k = 0; k < nvec; ++k)
@@ -218,7 +218,7 @@ void IterativeSolverLinearEquationsInitialize(size_t n, size_t nroot, size_t* ra
     std::vector<Vec> b;
     for (size_t r = 0; r < nroot; ++r) {
       b.emplace_back(in.dev, n);
-      check(ssp_upload(in.dev->ctx(), b.back().data(), rhs + r * n + in.offset, in.local), "ssp_upload");
+      check(ssp_upload(in.dev->ctx(), b.back().data_wo(), rhs + r * n + in.offset, in.local), "ssp_upload");
     }
     solver->set_hermiticity(hermitian != 0);
     solver->set_n_roots(nroot);
@@ -407,7 +407,7 @@ size_t IterativeSolverAddP(size_t buffer_size, size_t nP, const size_t* offsets,
               "ssp_download");
       I.apply_on_p_fort(flat.data(), host.data() + I.offset, nu, ranges.data());
       for (size_t k = 0; k < nu; ++k)
-        check(ssp_upload(I.dev->ctx(), act[k].get().data(), host.data() + k * I.dimension + I.offset, I.local),
+        check(ssp_upload(I.dev->ctx(), act[k].get().data_wo(), host.data() + k * I.dimension + I.offset, I.local),
               "ssp_upload");
     };
     const size_t nwork =
@@ -474,7 +474,7 @@ void IterativeSolverSetDiagonals(const double* diagonals) {
   guarded([&] {
     auto& in = top();
     in.diagonals = std::make_unique<Vec>(in.dev, in.dimension);
-    check(ssp_upload(in.dev->ctx(), in.diagonals->data(), diagonals + in.offset, in.local), "ssp_upload");
+    check(ssp_upload(in.dev->ctx(), in.diagonals->data_wo(), diagonals + in.offset, in.local), "ssp_upload");
   });
 }
 

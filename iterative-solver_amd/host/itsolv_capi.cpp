@@ -31,13 +31,14 @@ std::shared_ptr<Device> borrow(ssp_ctx* ctx) {
 
 Vec zero_vec(const std::shared_ptr<Device>& dev, size_t n) {
   Vec v(dev, n);
-  check(ssp_fill(dev->ctx(), 0.0, v.data(), v.local_size()), "ssp_fill");
+  check(ssp_fill(dev->ctx(), 0.0, v.data_wo(), v.local_size()), "ssp_fill");
   return v;
 }
 
+// write-only outputs (the problems' actions overwrite them in full)
 std::vector<double*> ptrs(const VecRef<Vec>& v) {
   std::vector<double*> p;
-  for (auto& x : v) p.push_back(x.get().data());
+  for (auto& x : v) p.push_back(x.get().data_wo());
   return p;
 }
 std::vector<const double*> cptrs(const CVecRef<Vec>& v) {
@@ -46,14 +47,14 @@ std::vector<const double*> cptrs(const CVecRef<Vec>& v) {
   return p;
 }
 
-// H = diag(1+g) + rho sum_l u_l u_l^T, applied on the device.
+// H = diag(d) + rho sum_l u_l u_l^T (itsolv_hbm/problems.h SyntheticSpec), applied on the device.
 class SyntheticProblem : public Problem<Vec, SparseP> {
  public:
-  SyntheticProblem(std::shared_ptr<Device> dev, const pr::SyntheticSpec& s) : m_dev(std::move(dev)), m_s(s) {}
+  SyntheticProblem(std::shared_ptr<Device> dev, const pr::SyntheticSpec& s)
+      : m_dev(std::move(dev)), m_s(s), m_c(s.c_spec()) {}
 
   bool diagonals(Vec& d) const override {
-    check(sspx_synthetic_diagonal(ctx(), d.data(), d.local_size(), d.offset(), m_s.rho, m_s.rank),
-          "sspx_synthetic_diagonal");
+    check(sspx_synth_diagonal(ctx(), &m_c, d.data_wo(), d.local_size(), d.offset()), "sspx_synth_diagonal");
     return true;
   }
   void action(const CVecRef<Vec>& params, const VecRef<Vec>& actions) const override {
@@ -61,20 +62,18 @@ class SyntheticProblem : public Problem<Vec, SparseP> {
     auto x = cptrs(params);
     auto y = ptrs(actions);
     const auto& v0 = params.front().get();
-    check(sspx_synthetic_action(ctx(), x.data(), y.data(), int(params.size()), v0.local_size(), v0.offset(), m_s.rho,
-                                m_s.rank, m_s.seed),
-          "sspx_synthetic_action");
+    check(sspx_synth_action(ctx(), &m_c, x.data(), y.data(), int(params.size()), v0.local_size(), v0.offset()),
+          "sspx_synth_action");
   }
   // r = H (x - 1); value = 0 (unused by DIIS)
   double residual(const Vec& x, Vec& r) const override {
     Vec t(x);
     Vec ones(m_dev, x.size());
-    check(ssp_fill(ctx(), 1.0, ones.data(), ones.local_size()), "ssp_fill");
-    check(ssp_axpy(ctx(), -1.0, ones.data(), t.data(), t.local_size()), "ssp_axpy");
+    check(ssp_fill(ctx(), 1.0, ones.data_wo(), ones.local_size()), "ssp_fill");
+    check(ssp_axpy(ctx(), -1.0, ones.data(), t.data_rw(), t.local_size()), "ssp_axpy");
     const double* xp[1] = {t.data()};
-    double* yp[1] = {r.data()};
-    check(sspx_synthetic_action(ctx(), xp, yp, 1, t.local_size(), t.offset(), m_s.rho, m_s.rank, m_s.seed),
-          "sspx_synthetic_action");
+    double* yp[1] = {r.data_wo()};
+    check(sspx_synth_action(ctx(), &m_c, xp, yp, 1, t.local_size(), t.offset()), "sspx_synth_action");
     return 0;
   }
   std::vector<double> pp_action_matrix(const std::vector<SparseP>& pp) const override {
@@ -96,15 +95,15 @@ class SyntheticProblem : public Problem<Vec, SparseP> {
       for (size_t p = 0; p < pp.size(); ++p) {
         for (auto& [i, coef] : pp[p].get()) {
           idx.push_back(i);
-          val.push_back((1.0 + double(i)) * coef * c[k][p]);
+          val.push_back(m_s.d(i) * coef * c[k][p]);
           for (int l = 0; l < m_s.rank; ++l) w[size_t(l)] += c[k][p] * coef * m_s.u(l, i);
         }
       }
-      check(ssp_sparse_axpy(ctx(), 1.0, idx.data(), val.data(), idx.size(), a.data(), a.local_size(), a.offset()),
+      check(ssp_sparse_axpy(ctx(), 1.0, idx.data(), val.data(), idx.size(), a.data_rw(), a.local_size(), a.offset()),
             "ssp_sparse_axpy");
-      double* yp[1] = {a.data()};
-      check(sspx_synthetic_add_lowrank(ctx(), yp, 1, a.local_size(), a.offset(), m_s.rho, m_s.rank, m_s.seed, w.data()),
-            "sspx_synthetic_add_lowrank");
+      double* yp[1] = {a.data_rw()};
+      check(sspx_synth_add_lowrank(ctx(), &m_c, yp, 1, a.local_size(), a.offset(), w.data()),
+            "sspx_synth_add_lowrank");
     }
   }
 
@@ -112,7 +111,13 @@ class SyntheticProblem : public Problem<Vec, SparseP> {
   ssp_ctx* ctx() const { return m_dev->ctx(); }
   std::shared_ptr<Device> m_dev;
   pr::SyntheticSpec m_s;
+  sspx_synth m_c;
 };
+
+pr::SyntheticSpec spec_of(size_t n, const sspx_synth* s) {
+  if (!s) throw std::invalid_argument("null sspx_synth");
+  return pr::SyntheticSpec(n, s->rho, s->rank, s->seed, s->diag_kind, s->alpha);
+}
 
 // Dense row-major H, single rank: H resident in HBM, action by a row-per-lane kernel.
 class DenseProblem : public Problem<Vec, SparseP> {
@@ -138,10 +143,10 @@ class DenseProblem : public Problem<Vec, SparseP> {
   double residual(const Vec& x, Vec& r) const override {
     Vec t(x);
     Vec ones(m_dev, x.size());
-    check(ssp_fill(ctx(), 1.0, ones.data(), m_n), "ssp_fill");
-    check(ssp_axpy(ctx(), -1.0, ones.data(), t.data(), m_n), "ssp_axpy");
+    check(ssp_fill(ctx(), 1.0, ones.data_wo(), m_n), "ssp_fill");
+    check(ssp_axpy(ctx(), -1.0, ones.data(), t.data_rw(), m_n), "ssp_axpy");
     const double* xp[1] = {t.data()};
-    double* yp[1] = {r.data()};
+    double* yp[1] = {r.data_wo()};
     check(sspx_dense_action(ctx(), m_dh, m_n, xp, yp, 1, m_n, 0), "sspx_dense_action");
     return 0;
   }
@@ -161,7 +166,7 @@ class DenseProblem : public Problem<Vec, SparseP> {
       Vec t(m_dev, m_n);
       t.set_local_values(add);
       auto& a = actions[k].get();
-      check(ssp_axpy(ctx(), 1.0, t.data(), a.data(), m_n), "ssp_axpy");
+      check(ssp_axpy(ctx(), 1.0, t.data(), a.data_rw(), m_n), "ssp_axpy");
     }
   }
 
@@ -184,8 +189,8 @@ class RayleighProblem : public DenseProblem {
     check(ssp_dot(x.ctx(), x.data(), x.data(), x.local_size(), &xx), "ssp_dot");
     check(ssp_dot(x.ctx(), x.data(), g.data(), x.local_size(), &xg), "ssp_dot");
     const double f = xg / xx;
-    check(ssp_axpy(x.ctx(), -f, x.data(), g.data(), g.local_size()), "ssp_axpy");
-    check(ssp_scal(x.ctx(), 2 / xx, g.data(), g.local_size()), "ssp_scal");
+    check(ssp_axpy(x.ctx(), -f, x.data(), g.data_rw(), g.local_size()), "ssp_axpy");
+    check(ssp_scal(x.ctx(), 2 / xx, g.data_rw(), g.local_size()), "ssp_scal");
     return f;
   }
 };
@@ -194,7 +199,7 @@ template <class P>
 double residual_norm(const P& problem, const std::shared_ptr<Device>& dev, const Vec& x, double e) {
   Vec ax(dev, x.size());
   problem.action(CVecRef<Vec>{std::cref(x)}, VecRef<Vec>{std::ref(ax)});
-  check(ssp_axpy(dev->ctx(), -e, x.data(), ax.data(), ax.local_size()), "ssp_axpy");
+  check(ssp_axpy(dev->ctx(), -e, x.data(), ax.data_rw(), ax.local_size()), "ssp_axpy");
   double rr = 0, xx = 0;
   check(ssp_dot(dev->ctx(), ax.data(), ax.data(), ax.local_size(), &rr), "ssp_dot");
   check(ssp_dot(dev->ctx(), x.data(), x.data(), x.local_size(), &xx), "ssp_dot");
@@ -228,10 +233,16 @@ void itsolv_default_options(itsolv_options* opt) { pr::default_options(opt); }
 
 int itsolv_davidson_synthetic(ssp_ctx* ctx, size_t n, double rho, int rank, unsigned long long seed,
                               const itsolv_options* opt, itsolv_result* out, double* solutions_out) {
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  return itsolv_davidson_synth(ctx, n, &s, opt, out, solutions_out);
+}
+
+int itsolv_davidson_synth(ssp_ctx* ctx, size_t n, const sspx_synth* spec, const itsolv_options* opt,
+                          itsolv_result* out, double* solutions_out) {
   return guarded([&] {
     auto dev = borrow(ctx);
     const auto o = opts_or_default(opt);
-    SyntheticProblem problem(dev, pr::SyntheticSpec(n, rho, rank, seed));
+    SyntheticProblem problem(dev, spec_of(n, spec));
     std::memset(out, 0, sizeof(*out));
     pr::run_davidson<Vec, Vec, SparseP>(
         molpro::linalg::hbm::make_handlers(), problem, [&] { return zero_vec(dev, n); },
@@ -264,17 +275,23 @@ int itsolv_davidson_dense(ssp_ctx* ctx, const double* h, size_t n, const itsolv_
 
 int itsolv_diis_synthetic(ssp_ctx* ctx, size_t n, double rho, int rank, unsigned long long seed,
                           const itsolv_options* opt, itsolv_result* out, double* x_out) {
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  return itsolv_diis_synth(ctx, n, &s, opt, out, x_out);
+}
+
+int itsolv_diis_synth(ssp_ctx* ctx, size_t n, const sspx_synth* spec, const itsolv_options* opt, itsolv_result* out,
+                      double* x_out) {
   return guarded([&] {
     auto dev = borrow(ctx);
     const auto o = opts_or_default(opt);
-    SyntheticProblem problem(dev, pr::SyntheticSpec(n, rho, rank, seed));
+    SyntheticProblem problem(dev, spec_of(n, spec));
     std::memset(out, 0, sizeof(*out));
     pr::run_diis<Vec, Vec, SparseP>(
         molpro::linalg::hbm::make_handlers(), problem, [&] { return zero_vec(dev, n); },
         [&](Vec& x) {
           const size_t i0 = 0;
           const double one = 1.0;
-          check(ssp_sparse_copy(x.ctx(), x.data(), x.local_size(), x.offset(), &i0, &one, 1), "ssp_sparse_copy");
+          check(ssp_sparse_copy(x.ctx(), x.data_wo(), x.local_size(), x.offset(), &i0, &one, 1), "ssp_sparse_copy");
         },
         o, *out,
         [&](const Vec& x) {
@@ -295,7 +312,7 @@ int itsolv_linear_equations_dense(ssp_ctx* ctx, const double* a, size_t n, const
     std::vector<Vec> b;
     for (int r = 0; r < nrhs; ++r) {
       b.emplace_back(dev, n);
-      check(ssp_upload(dev->ctx(), b.back().data(), rhs + size_t(r) * n + b.back().offset(), b.back().local_size()),
+      check(ssp_upload(dev->ctx(), b.back().data_wo(), rhs + size_t(r) * n + b.back().offset(), b.back().local_size()),
             "ssp_upload");
     }
     pr::run_linear_equations<Vec, Vec, SparseP>(
@@ -303,7 +320,7 @@ int itsolv_linear_equations_dense(ssp_ctx* ctx, const double* a, size_t n, const
         [&](const Vec& x, size_t r) {
           Vec ax(dev, x.size());
           problem.action(CVecRef<Vec>{std::cref(x)}, VecRef<Vec>{std::ref(ax)});
-          check(ssp_axpy(dev->ctx(), -1.0, b[r].data(), ax.data(), ax.local_size()), "ssp_axpy");
+          check(ssp_axpy(dev->ctx(), -1.0, b[r].data(), ax.data_rw(), ax.local_size()), "ssp_axpy");
           double rr = 0, bb = 0;
           check(ssp_dot(dev->ctx(), ax.data(), ax.data(), ax.local_size(), &rr), "ssp_dot");
           check(ssp_dot(dev->ctx(), b[r].data(), b[r].data(), b[r].local_size(), &bb), "ssp_dot");
@@ -330,7 +347,7 @@ int itsolv_optimize_dense(ssp_ctx* ctx, const double* h, size_t n, int algorithm
         [&](Vec& x) {
           const size_t i0 = 0;
           const double one = 1.0;
-          check(ssp_sparse_copy(x.ctx(), x.data(), x.local_size(), x.offset(), &i0, &one, 1), "ssp_sparse_copy");
+          check(ssp_sparse_copy(x.ctx(), x.data_wo(), x.local_size(), x.offset(), &i0, &one, 1), "ssp_sparse_copy");
         },
         algorithm, o, *out,
         [&](const Vec& x) {
@@ -353,7 +370,7 @@ int itsolv_diis_dense(ssp_ctx* ctx, const double* h, size_t n, const itsolv_opti
         [&](Vec& x) {
           const size_t i0 = 0;
           const double one = 1.0;
-          check(ssp_sparse_copy(x.ctx(), x.data(), x.local_size(), x.offset(), &i0, &one, 1), "ssp_sparse_copy");
+          check(ssp_sparse_copy(x.ctx(), x.data_wo(), x.local_size(), x.offset(), &i0, &one, 1), "ssp_sparse_copy");
         },
         o, *out,
         [&](const Vec& x) {

@@ -14,6 +14,7 @@
 #pragma once
 #include <cmath>
 #include <complex>
+#include <exception>
 #include <functional>
 #include <list>
 #include <map>
@@ -200,7 +201,16 @@ class ArrayHandler {
     using ref_wrap = std::reference_wrapper<T>;
 
     explicit LazyHandle(ArrayHandler<AL, AR>& handler) : m_handler{handler} {}
-    virtual ~LazyHandle() { LazyHandle::eval(); }
+    // As the reference, destruction evaluates what is still registered -- except while an exception
+    // unwinds the stack (a failed eval() or handler call in the caller's scope): then the register
+    // is dropped, so a recoverable device or size error reaches the caller (e.g. the C API's status
+    // codes) instead of std::terminate from a second throw in this destructor.
+    virtual ~LazyHandle() {
+      if (std::uncaught_exceptions() > 0)
+        clear();
+      else
+        LazyHandle::eval();
+    }
 
     virtual void axpy(value_type alpha, const AR& x, AL& y) {
       if (!register_op_type("axpy"))
@@ -212,20 +222,23 @@ class ArrayHandler {
         return error("Failed to register operation type dot with the current state of the LazyHandle");
       m_dot.push(std::cref(x), std::cref(y), std::ref(out));
     }
+    // The registers are taken and cleared before the handler runs them, so an operation that throws
+    // leaves nothing behind to be evaluated again.
     virtual void eval() {
       if (m_invalid) return;
-      if (!m_axpy.empty()) {
-        auto [reg, alphas, xx, yy] =
-            util::remove_duplicates(m_axpy.m_register, std::equal_to<value_type>{}, util::RefEqual<const AR>{},
-                                    util::RefEqual<AL>{});
+      auto axpys = std::move(m_axpy.m_register);
+      auto dots = std::move(m_dot.m_register);
+      clear();
+      if (!axpys.empty()) {
+        auto [reg, alphas, xx, yy] = util::remove_duplicates(axpys, std::equal_to<value_type>{},
+                                                             util::RefEqual<const AR>{}, util::RefEqual<AL>{});
         m_handler.fused_axpy(reg, alphas, xx, yy);
       }
-      if (!m_dot.empty()) {
-        auto [reg, xx, yy, out] = util::remove_duplicates(m_dot.m_register, util::RefEqual<const AL>{},
-                                                          util::RefEqual<const AR>{}, util::RefEqual<value_type>{});
+      if (!dots.empty()) {
+        auto [reg, xx, yy, out] = util::remove_duplicates(dots, util::RefEqual<const AL>{}, util::RefEqual<const AR>{},
+                                                          util::RefEqual<value_type>{});
         m_handler.fused_dot(reg, xx, yy, out);
       }
-      clear();
     }
     void invalidate() { m_invalid = true; }
     bool invalid() { return m_invalid; }

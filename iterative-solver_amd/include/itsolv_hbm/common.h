@@ -118,25 +118,24 @@ class StringFacet {
     s.erase(std::find_if(s.rbegin(), s.rend(), not_space).base(), s.end());
   }
   //! "k1=v1, k2 : v2; k3=" -> {k1: v1, k2: v2, k3: ""}: fields split at ',' or ';', key from value at
-  //! the first '=' or ':', both trimmed; a non-empty field without a separator throws.
+  //! the first '=' or ':', both trimmed; a non-empty field without a separator throws, and parsing
+  //! stops at the first empty field ("A=1,,B=2" -> {A: 1}), as reference itsolv/util.cpp:38-56 does.
   static std::map<std::string, std::string> parse_keyval_string(std::string s) {
     std::map<std::string, std::string> out;
     auto trimmed = [](std::string x) {
       crop_space(x);
       return x;
     };
-    size_t pos = 0;
-    while (pos <= s.size()) {
-      const size_t end = std::min(s.find_first_of(",;", pos), s.size());
-      const std::string field = trimmed(s.substr(pos, end - pos));
-      pos = end + 1;
-      if (field.empty()) {
-        if (end == s.size()) break;
-        continue;
-      }
+    s += ",;";
+    crop_space(s);
+    while (!s.empty()) {
+      const size_t end = s.find_first_of(",;");
+      const std::string field = trimmed(s.substr(0, end));
+      if (field.empty()) break;
       const size_t eq = field.find_first_of("=:");
       if (eq == std::string::npos) throw std::runtime_error("String " + field + " cannot be parsed as key,value");
       out[trimmed(field.substr(0, eq))] = trimmed(field.substr(eq + 1));
+      s = trimmed(s.substr(end + 1));
     }
     return out;
   }

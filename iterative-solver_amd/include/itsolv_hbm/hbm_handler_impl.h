@@ -51,11 +51,20 @@ std::vector<const double*> cptrs(const Refs& v) {
   for (auto& x : v) p.push_back(x.get().data());
   return p;
 }
+// Destinations: read-modify-write (a shared block is copied first) or write-only (a shared block is
+// replaced without a copy), hbm_vec.h.
 template <class Refs>
-std::vector<double*> mptrs(const Refs& v) {
+std::vector<double*> rw_ptrs(const Refs& v) {
   std::vector<double*> p;
   p.reserve(v.size());
-  for (auto& x : v) p.push_back(x.get().data());
+  for (auto& x : v) p.push_back(x.get().data_rw());
+  return p;
+}
+template <class Refs>
+std::vector<double*> wo_ptrs(const Refs& v) {
+  std::vector<double*> p;
+  p.reserve(v.size());
+  for (auto& x : v) p.push_back(x.get().data_wo());
   return p;
 }
 // (ptr, idx, val) CSR packing of sparse P vectors, indices ascending (std::map order).
@@ -91,6 +100,7 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
   using Base::lazy_handle;
   ProxyHandle lazy_handle() override { return this->lazy_handle(*this); }
 
+  // Copies share the source's HBM block until one side is written (hbm_vec.h): no bytes move here.
   Vec copy(const Vec& source) override {
     m_counter->copy++;
     return Vec(source);
@@ -98,18 +108,18 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
   void copy(Vec& x, const Vec& y) override {
     m_counter->copy++;
     same(x, y, "copy");
-    check(ssp_copy(x.ctx(), x.data(), y.data(), x.local_size()), "ssp_copy");
+    x.assign_shared(y);
   }
   void scal(double alpha, Vec& x) override {
     m_counter->scal++;
-    check(ssp_scal(x.ctx(), alpha, x.data(), x.local_size()), "ssp_scal");
+    check(ssp_scal(x.ctx(), alpha, x.data_rw(), x.local_size()), "ssp_scal");
   }
-  void fill(double alpha, Vec& x) override { check(ssp_fill(x.ctx(), alpha, x.data(), x.local_size()), "ssp_fill"); }
+  void fill(double alpha, Vec& x) override { check(ssp_fill(x.ctx(), alpha, x.data_wo(), x.local_size()), "ssp_fill"); }
   void axpy(double alpha, const Vec& x, Vec& y) override {
     m_counter->axpy++;
     if (x.size() < y.size()) error("ArrayHandlerHbm::axpy() incompatible x and y arrays, x.size() < y.size()");
     same(x, y, "axpy");
-    check(ssp_axpy(y.ctx(), alpha, x.data(), y.data(), y.local_size()), "ssp_axpy");
+    check(ssp_axpy(y.ctx(), alpha, x.data(), y.data_rw(), y.local_size()), "ssp_axpy");
   }
   double dot(const Vec& x, const Vec& y) override {
     m_counter->dot++;
@@ -133,7 +143,8 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
                               " " + std::to_string(yy.size()));
     for (auto& x : xx) same(x.get(), yy.front().get(), "gemm_outer");
     auto xp = detail::cptrs(xx);
-    auto yp = detail::mptrs(yy);
+    // only the alphas.cols() destinations the kernel updates
+    auto yp = detail::rw_ptrs(itsolv::VecRef<Vec>(yy.begin(), yy.begin() + long(alphas.cols())));
     const auto& y0 = yy.front().get();
     check(ssp_gemm_outer(y0.ctx(), alphas.data().data(), xp.data(), int(xx.size()), yp.data(), int(alphas.cols()),
                          y0.local_size()),
@@ -209,7 +220,7 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
     for (size_t x = 0; x < nx; ++x) same(xx[x].get(), yy[0].get(), "fused_axpy");
     m_counter->gemm_outer++;
     auto xp = detail::cptrs(xx);
-    auto yp = detail::mptrs(yy);
+    auto yp = detail::rw_ptrs(yy);
     const auto& y0 = yy.front().get();
     check(ssp_gemm_outer(y0.ctx(), coef.data(), xp.data(), int(nx), yp.data(), int(ny), y0.local_size()),
           "ssp_gemm_outer");
@@ -237,7 +248,7 @@ class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
       idx.push_back(i);
       val.push_back(v);
     }
-    check(ssp_sparse_copy(x.ctx(), x.data(), x.local_size(), x.offset(), idx.data(), val.data(), idx.size()),
+    check(ssp_sparse_copy(x.ctx(), x.data_wo(), x.local_size(), x.offset(), idx.data(), val.data(), idx.size()),
           "ssp_sparse_copy");
   }
   void scal(double, Vec&) override {}
@@ -251,7 +262,7 @@ class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
         idx.push_back(i);
         val.push_back(v);
       }
-    check(ssp_sparse_axpy(y.ctx(), alpha, idx.data(), val.data(), idx.size(), y.data(), y.local_size(), y.offset()),
+    check(ssp_sparse_axpy(y.ctx(), alpha, idx.data(), val.data(), idx.size(), y.data_rw(), y.local_size(), y.offset()),
           "ssp_sparse_axpy");
   }
   double dot(const Vec& x, const SparseP& y) override {
@@ -277,7 +288,7 @@ class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
     std::vector<size_t> ptr, idx;
     std::vector<double> val;
     detail::pack(xx, ptr, idx, val);
-    auto yp = detail::mptrs(yy);
+    auto yp = detail::rw_ptrs(itsolv::VecRef<Vec>(yy.begin(), yy.begin() + long(alphas.cols())));
     const auto& y0 = yy.front().get();
     check(ssp_gemm_outer_sparse(y0.ctx(), alphas.data().data(), ptr.data(), idx.data(), val.data(), int(xx.size()),
                                 yp.data(), int(alphas.cols()), y0.local_size(), y0.offset()),
@@ -299,9 +310,19 @@ class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
     }
     return itsolv::subspace::Matrix<double>(std::move(buf), {xx.size(), yy.size()});
   }
-  // |x_i v_i| over the entries of y, reduced over ranks, then the reference's top-n rule.
+  // |x_i v_i| over the entries of y, reduced over ranks, then the reference's top-n rule of
+  // select_max_dot_iter_sparse (util/select_max_dot.h:59-85): the first n entries of y are pushed
+  // onto its heap without pops, out-of-range ones skipped, and every later in-range entry is pushed
+  // and then the smallest popped -- so the result holds the largest n - k in-range products, k = the
+  // number of out-of-range indices among y's first n entries (ties: the larger index stays).
   std::map<size_t, double> select_max_dot(size_t n, const Vec& x, const SparseP& y) override {
     if (n > x.size() || n > y.size()) error("ArrayHandlerHbmSparse::select_max_dot() n is too large");
+    size_t keep = n;
+    {
+      auto it = y.begin();
+      for (size_t e = 0; e < n; ++e, ++it)
+        if (it->first >= x.size()) --keep;
+    }
     std::vector<SparseP> storage;
     for (auto& [i, v] : y)
       if (i < x.size()) storage.push_back(SparseP{{i, v}});
@@ -311,7 +332,7 @@ class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
     for (size_t e = 0; e < storage.size(); ++e) c.emplace_back(std::abs(prod(0, e)), storage[e].begin()->first);
     std::sort(c.begin(), c.end(), [](auto& a, auto& b) { return b < a; });
     std::map<size_t, double> out;
-    for (size_t k = 0; k < std::min(n, c.size()); ++k) out.emplace(c[k].second, c[k].first);
+    for (size_t k = 0; k < std::min(keep, c.size()); ++k) out.emplace(c[k].second, c[k].first);
     return out;
   }
   std::map<size_t, double> select(size_t n, const Vec& x, bool max = false, bool ignore_sign = false) override {

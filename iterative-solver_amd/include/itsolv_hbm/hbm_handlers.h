@@ -45,8 +45,7 @@ inline std::shared_ptr<itsolv::ArrayHandlers<Vec, Vec, SparseP>> make_handlers()
 // Fused MGS step on HBM vectors (array::fused_axpy_inner hook, found by argument-dependent lookup).
 inline bool fused_axpy_inner(array::ArrayHandler<Vec, Vec>&, const std::vector<double>& c, const Vec& x,
                              const itsolv::VecRef<Vec>& rr, const Vec& z, std::vector<double>& dots) {
-  std::vector<double*> y;
-  for (auto& r : rr) y.push_back(r.get().data());
+  auto y = detail::rw_ptrs(rr);
   check(ssp_axpy_inner(x.ctx(), c.data(), x.data(), y.data(), int(y.size()), z.data(), x.local_size(), dots.data()),
         "ssp_axpy_inner");
   return true;
@@ -64,7 +63,9 @@ inline bool fused_construct_solution(array::ArrayHandler<Vec, SparseP>&, const i
   std::vector<double> val;
   if (!pp.empty()) detail::pack(pp, ptr, idx, val);
   auto xp = detail::cptrs(qd);
-  auto yp = detail::mptrs(yy);
+  // write-only destinations: a solution vector still sharing storage with a Q copy is given a fresh
+  // block instead of being copied first
+  auto yp = detail::wo_ptrs(itsolv::VecRef<Vec>(yy.begin(), yy.begin() + long(cqd.cols())));
   const auto& y0 = yy.front().get();
   check(ssp_construct_solution(y0.ctx(), cp.data().data(), ptr.data(), idx.data(), val.data(), int(pp.size()),
                                cqd.data().data(), xp.data(), int(qd.size()), yp.data(), int(cqd.cols()),
@@ -89,7 +90,7 @@ inline bool fused_new_combinations(array::ArrayHandler<Vec, Vec>&, const itsolv:
   const size_t first = out.size();
   for (size_t j = 0; j < nout; ++j) out.push_back(src.front()->alloc_like());
   std::vector<double*> yp;
-  for (size_t j = first; j < out.size(); ++j) yp.push_back(out[j].data());
+  for (size_t j = first; j < out.size(); ++j) yp.push_back(out[j].data_wo());
   const Vec& v0 = *src.front();
   check(ssp_gemm_outer_set(v0.ctx(), alphas.data(), xp.data(), int(k), yp.data(), int(nout), v0.local_size()),
         "ssp_gemm_outer_set");
@@ -116,10 +117,10 @@ inline bool fused_orthonormalise(array::ArrayHandler<Vec, Vec>&, const itsolv::V
       std::vector<double*> y;
       for (size_t j = i + 1; j < nR; ++j) {
         yc.push_back(rr[j].get().data());
-        y.push_back(rr[j].get().data());
+        y.push_back(rr[j].get().data_rw());
       }
       std::vector<double> ov(std::max<size_t>(1, y.size()));
-      check(ssp_scal_inner(ctx, 1. / nrm, rr[i].get().data(), yc.data(), int(yc.size()), n, ov.data()),
+      check(ssp_scal_inner(ctx, 1. / nrm, rr[i].get().data_rw(), yc.data(), int(yc.size()), n, ov.data()),
             "ssp_scal_inner");
       if (y.empty()) break;
       for (auto& o : ov) o = -o;
@@ -138,8 +139,7 @@ inline bool fused_orthonormalise(array::ArrayHandler<Vec, Vec>&, const itsolv::V
 inline void precondition_default(const itsolv::VecRef<Vec>& action, const std::vector<double>& shift,
                                  const Vec& diagonals) {
   if (action.empty()) return;
-  std::vector<double*> a;
-  for (auto& v : action) a.push_back(v.get().data());
+  auto a = detail::rw_ptrs(action);
   check(ssp_precondition(diagonals.ctx(), a.data(), int(a.size()), diagonals.data(), shift.data(),
                          diagonals.local_size()),
         "ssp_precondition");

@@ -72,7 +72,31 @@ class Device {
   bool m_owned = true;
 };
 
+// Storage is shared copy-on-write.  The reference's solvers copy R vectors into new Q vectors
+// (QSpace.h:80-84), the preconditioner's diagonals into params[0] (IterativeSolverTemplate.h:391)
+// and the new working set into params (propose_rspace.h:617-619), and then overwrite the source or
+// the copy with a write-only kernel (construct_solution, the action) -- so a copy shares the
+// source's HBM block and costs no bytes.  Access is explicit about what a kernel does with the
+// storage:
+//   data()     const, for operands that are only read;
+//   data_rw()  for read-modify-write destinations: a block still shared is first copied (exactly
+//              the bytes the eager copy would have moved);
+//   data_wo()  for destinations a kernel writes in full without reading: a shared block is
+//              replaced by a fresh one, nothing is copied.
+// The shared block outlives every holder's kernels: blocks return to the context's arena, whose
+// reuse is ordered on the context's one stream.
 class Vec {
+  struct Block {
+    std::shared_ptr<Device> dev;
+    double* p = nullptr;
+    Block(std::shared_ptr<Device> d, size_t n) : dev(std::move(d)) { check_status(ssp_alloc(dev->ctx(), n, &p), "ssp_alloc"); }
+    Block(const Block&) = delete;
+    Block& operator=(const Block&) = delete;
+    ~Block() {
+      if (p) ssp_free(dev->ctx(), p);
+    }
+  };
+
  public:
   using value_type = double;
 
@@ -81,60 +105,71 @@ class Vec {
     auto [off, n] = m_dev->shard(n_global);
     m_offset = off;
     m_local = n;
-    check_status(ssp_alloc(m_dev->ctx(), m_local, &m_data), "ssp_alloc");
+    m_block = std::make_shared<Block>(m_dev, m_local);
   }
-  Vec(const Vec& o) : Vec(o.m_dev, o.m_size) {
-    check_status(ssp_copy(ctx(), m_data, o.m_data, m_local), "ssp_copy");
-  }
+  //! A copy: shares the storage until either side writes (see above).
+  Vec(const Vec& o) = default;
   Vec(Vec&& o) noexcept { swap(o); }
   // A vector of the same length and distribution whose contents are not initialised (for
   // destinations that a kernel writes without reading).
   Vec alloc_like() const { return Vec(m_dev, m_size); }
-  Vec& operator=(const Vec& o) {
-    if (this != &o) {
-      Vec t(o);
-      swap(t);
-    }
-    return *this;
-  }
+  Vec& operator=(const Vec& o) = default;
   Vec& operator=(Vec&& o) noexcept {
     Vec t(std::move(o));
     swap(t);
     return *this;
   }
-  ~Vec() {
-    if (m_data) ssp_free(ctx(), m_data);
-  }
+  ~Vec() = default;
   void swap(Vec& o) noexcept {
     std::swap(m_dev, o.m_dev);
-    std::swap(m_data, o.m_data);
+    std::swap(m_block, o.m_block);
     std::swap(m_size, o.m_size);
     std::swap(m_local, o.m_local);
     std::swap(m_offset, o.m_offset);
+  }
+  //! Becomes a copy of o (o's distribution): shares o's storage.
+  void assign_shared(const Vec& o) {
+    if (this != &o) *this = o;
   }
 
   size_t size() const { return m_size; }
   size_t local_size() const { return m_local; }
   size_t offset() const { return m_offset; }
-  double* data() { return m_data; }
-  const double* data() const { return m_data; }
+  const double* data() const { return m_block ? m_block->p : nullptr; }
+  double* data_rw() {
+    detach(true);
+    return m_block ? m_block->p : nullptr;
+  }
+  double* data_wo() {
+    detach(false);
+    return m_block ? m_block->p : nullptr;
+  }
+  //! Whether another Vec holds the same storage.
+  bool shares_storage() const { return m_block && m_block.use_count() > 1; }
   ssp_ctx* ctx() const { return m_dev->ctx(); }
   const std::shared_ptr<Device>& device() const { return m_dev; }
   bool compatible(const Vec& o) const { return m_size == o.m_size && m_offset == o.m_offset && m_local == o.m_local; }
 
   std::vector<double> local_values() const {
     std::vector<double> v(m_local);
-    check_status(ssp_download(ctx(), v.data(), m_data, m_local), "ssp_download");
+    check_status(ssp_download(ctx(), v.data(), data(), m_local), "ssp_download");
     return v;
   }
   void set_local_values(const std::vector<double>& v) {
     if (v.size() != m_local) throw std::invalid_argument("Vec::set_local_values: wrong length");
-    check_status(ssp_upload(ctx(), m_data, v.data(), m_local), "ssp_upload");
+    check_status(ssp_upload(ctx(), data_wo(), v.data(), m_local), "ssp_upload");
   }
 
  private:
+  void detach(bool keep_values) {
+    if (!m_block || m_block.use_count() <= 1) return;
+    auto fresh = std::make_shared<Block>(m_dev, m_local);
+    if (keep_values) check_status(ssp_copy(ctx(), fresh->p, m_block->p, m_local), "ssp_copy");
+    m_block = std::move(fresh);
+  }
+
   std::shared_ptr<Device> m_dev;
-  double* m_data = nullptr;
+  std::shared_ptr<Block> m_block;
   size_t m_size = 0, m_local = 0, m_offset = 0;
 };
 

@@ -24,23 +24,64 @@ inline uint64_t splitmix64(uint64_t z) {
 }
 inline uint64_t stream_key(uint64_t seed, uint64_t stream) { return splitmix64(seed ^ (stream * 0xD1B54A32D192ED03ull)); }
 
+// Equidistributed fractions frac(g * phi) for the bounded diagonal (exact in IEEE double on host and
+// device: one rounded product, an exact floor and an exact subtraction; csrc/synthetic.hip evaluates
+// the same expressions with contraction off).
+constexpr double kPhi1 = 0x1.3c6ef372fe950p-1;  // (sqrt(5) - 1) / 2
+constexpr double kPhi2 = 0x1.827f5352054c6p-1;  // 1 / plastic number
+inline double frac_phi(size_t g, double phi) {
+  const double f = double(g) * phi;
+  return f - std::floor(f);
+}
+
+// Diagonal families of the synthetic H (SSPX_DIAG_* in include/subspace_hip.h):
+//   SSPX_DIAG_LINEAR   d_g = 1 + g: the Davidson configurations C1-C4.
+//   SSPX_DIAG_BOUNDED  d_g = 1 + 2 frac(g phi1) in [1, 3): the C5 DIIS instance.  Its problem hands
+//                      the preconditioner an approximate diagonal p_g = d_g (1 + alpha (2 frac(g phi2)
+//                      - 1)) (an approximate Jacobian diagonal, as orbital-energy differences are for
+//                      the DIIS of SCF / coupled cluster), so the preconditioned operator has a
+//                      continuous spectrum and DIIS converges geometrically (~0.4 per iteration), and
+//                      the coupling rho is O(1/N), so |r_0| = |H (e_0 - 1)| ~ 3 sqrt(N): the
+//                      threshold 1e-8 sits four orders above the rounding floor eps |H| |x| ~ 1e-12.
 struct SyntheticSpec {
   size_t n;
   double rho;
   int rank;
   uint64_t seed;
+  int diag_kind = SSPX_DIAG_LINEAR;
+  double alpha = 0;
   std::vector<uint64_t> keys;  // per low-rank vector
-  SyntheticSpec(size_t n_, double rho_, int rank_, uint64_t seed_) : n(n_), rho(rho_), rank(rank_), seed(seed_) {
+  SyntheticSpec(size_t n_, double rho_, int rank_, uint64_t seed_, int diag_kind_ = SSPX_DIAG_LINEAR,
+                double alpha_ = 0)
+      : n(n_), rho(rho_), rank(rank_), seed(seed_), diag_kind(diag_kind_), alpha(alpha_) {
     for (int l = 0; l < rank; ++l) keys.push_back(stream_key(seed, 1000 + uint64_t(l)));
   }
   double u(int l, size_t g) const { return l == 0 ? 1.0 : ((splitmix64(keys[l] ^ uint64_t(g)) & 1ull) ? -1.0 : 1.0); }
+  //! The diagonal part d_g of H (without the low-rank term).
+  double d(size_t g) const { return diag_kind == SSPX_DIAG_BOUNDED ? 1.0 + 2.0 * frac_phi(g, kPhi1) : 1.0 + double(g); }
   double h(size_t i, size_t j) const {
     double s = 0;
     for (int l = 0; l < rank; ++l) s += u(l, i) * u(l, j);
-    return (i == j ? 1.0 + double(i) : 0.0) + rho * s;
+    return (i == j ? d(i) : 0.0) + rho * s;
   }
-  double diagonal(size_t g) const { return 1.0 + double(g) + rank * rho; }
+  //! What the problem's diagonals() reports (the preconditioner's diagonal).
+  double diagonal(size_t g) const {
+    if (diag_kind == SSPX_DIAG_BOUNDED) {
+      const double t = 2.0 * frac_phi(g, kPhi2) - 1.0;
+      const double s = alpha * t;
+      return d(g) * (1.0 + s);
+    }
+    return 1.0 + double(g) + rank * rho;
+  }
+  sspx_synth c_spec() const { return sspx_synth{rho, rank, seed, diag_kind, alpha}; }
 };
+
+//! BASELINE config C5 as a well-posed instance: r = H (x - 1), H = diag(1 + 2 frac(g phi1)) + (1/N) 1 1^T
+//! (the reference's DIIS test form 1 1^T + diag, test_NonLinearEquations.cpp:25-31, with the coupling
+//! scaled to the length and the diagonal bounded), preconditioner mismatch alpha = 0.5.
+inline SyntheticSpec c5_spec(size_t n, int rank = 1, uint64_t seed = 3, double alpha = 0.5) {
+  return SyntheticSpec(n, 1.0 / double(n), rank, seed, SSPX_DIAG_BOUNDED, alpha);
+}
 
 // One row of itsolv_result's per-iteration trace (called from solve()'s iteration_hook).
 template <class S>

@@ -18,7 +18,23 @@ TRACE_ITER, TRACE_ROOTS = 256, 8
 EXPORTS = [
     "itsolv_last_error", "itsolv_default_options", "itsolv_davidson_synthetic", "itsolv_davidson_dense",
     "itsolv_diis_synthetic", "itsolv_diis_dense", "itsolv_linear_equations_dense", "itsolv_optimize_dense",
+    "itsolv_davidson_synth", "itsolv_diis_synth",
 ]
+
+# Diagonal families of the synthetic H (include/subspace_hip.h sspx_synth, itsolv_hbm/problems.h).
+DIAG_LINEAR, DIAG_BOUNDED = 0, 1
+
+
+class Synth(C.Structure):
+    _fields_ = [("rho", C.c_double), ("rank", C.c_int), ("seed", C.c_ulonglong), ("diag_kind", C.c_int),
+                ("alpha", C.c_double)]
+
+
+def c5_spec(n: int, rank: int = 1, seed: int = 3, alpha: float = 0.5) -> dict:
+    """BASELINE config C5's well-posed DIIS instance (itsolv_hbm/problems.h c5_spec): r = H (x - 1),
+    H = diag(1 + 2 frac(g phi1)) + (1/n) sum_l u_l u_l^T, preconditioner diagonal mismatched by alpha.
+    Keyword arguments of diis_synthetic / oracle.diis_synthetic."""
+    return dict(rho=1.0 / n, rank=rank, seed=seed, diag_kind=DIAG_BOUNDED, alpha=alpha)
 
 
 class Options(C.Structure):
@@ -116,6 +132,8 @@ def load_library():
             "itsolv_diis_dense": (I, [P, PD, Z, PO, PR, PD]),
             "itsolv_linear_equations_dense": (I, [P, PD, Z, PD, I, PO, PR, PD]),
             "itsolv_optimize_dense": (I, [P, PD, Z, I, PO, PR, PD]),
+            "itsolv_davidson_synth": (I, [P, Z, C.POINTER(Synth), PO, PR, PD]),
+            "itsolv_diis_synth": (I, [P, Z, C.POINTER(Synth), PO, PR, PD]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -137,10 +155,11 @@ def _call(fn, args, nout):
 
 
 def davidson_synthetic(ctx: sh.Context, n: int, rho: float, rank: int, seed: int, n_local: int | None = None,
-                       solutions: bool = True, **opts):
+                       solutions: bool = True, *, diag_kind: int = DIAG_LINEAR, alpha: float = 0.0, **opts):
     o = make_options(**opts)
     nl = n if n_local is None else n_local
-    r, sol = _call(load_library().itsolv_davidson_synthetic, (ctx.handle, n, rho, rank, seed, C.byref(o)),
+    spec = Synth(rho, rank, seed, diag_kind, alpha)
+    r, sol = _call(load_library().itsolv_davidson_synth, (ctx.handle, n, C.byref(spec), C.byref(o)),
                    o.nroots * nl if solutions else 0)
     if solutions:
         r["solutions"] = sol[: o.nroots * nl].reshape(o.nroots, nl)
@@ -158,10 +177,11 @@ def davidson_dense(ctx: sh.Context, h: np.ndarray, **opts):
 
 
 def diis_synthetic(ctx: sh.Context, n: int, rho: float, rank: int, seed: int, n_local: int | None = None,
-                   solutions: bool = True, **opts):
+                   solutions: bool = True, *, diag_kind: int = DIAG_LINEAR, alpha: float = 0.0, **opts):
     o = make_options(**opts)
     nl = n if n_local is None else n_local
-    r, x = _call(load_library().itsolv_diis_synthetic, (ctx.handle, n, rho, rank, seed, C.byref(o)),
+    spec = Synth(rho, rank, seed, diag_kind, alpha)
+    r, x = _call(load_library().itsolv_diis_synth, (ctx.handle, n, C.byref(spec), C.byref(o)),
                  nl if solutions else 0)
     if solutions:
         r["x"] = x[:nl]

@@ -39,6 +39,7 @@ EXPORTS = [
     "ssp_sparse_copy", "ssp_sparse_axpy", "ssp_sparse_dot", "ssp_gemm_inner_sparse", "ssp_gemm_outer_sparse",
     "ssp_construct_solution",
     "sspx_synthetic_action", "sspx_synthetic_add_lowrank", "sspx_synthetic_diagonal", "sspx_fill_random", "sspx_dense_action",
+    "sspx_synth_action", "sspx_synth_add_lowrank", "sspx_synth_diagonal",
 ]
 
 
@@ -125,6 +126,9 @@ def _declare(lib):
         "sspx_synthetic_action": (I, [P, P, P, I, Z, Z, D, I, C.c_ulonglong]),
         "sspx_synthetic_add_lowrank": (I, [P, P, I, Z, Z, D, I, C.c_ulonglong, PD]),
         "sspx_synthetic_diagonal": (I, [P, P, Z, Z, D, I]),
+        "sspx_synth_action": (I, [P, P, P, P, I, Z, Z]),
+        "sspx_synth_add_lowrank": (I, [P, P, P, I, Z, Z, PD]),
+        "sspx_synth_diagonal": (I, [P, P, P, Z, Z]),
         "sspx_fill_random": (I, [P, P, Z, Z, C.c_ulonglong, C.c_ulonglong]),
         "sspx_dense_action": (I, [P, P, Z, P, P, I, Z, Z]),
     }
@@ -600,6 +604,14 @@ class Context:
 
     def synthetic_diagonal(self, d: DeviceVector, rho: float, rank: int, offset: int = 0):
         _check(self.lib.sspx_synthetic_diagonal(self.handle, d.ptr, d.n, offset, rho, rank))
+
+    def synth_action(self, xx, yy, spec, offset: int = 0):
+        """Any synthetic family; spec = itsolv_hbm.Synth."""
+        _check(self.lib.sspx_synth_action(self.handle, C.byref(spec), _ptrs(xx), _ptrs(yy), len(xx), xx[0].n,
+                                          offset))
+
+    def synth_diagonal(self, d: DeviceVector, spec, offset: int = 0):
+        _check(self.lib.sspx_synth_diagonal(self.handle, C.byref(spec), d.ptr, d.n, offset))
 
     def fill_random(self, x: DeviceVector, seed: int, vec: int, offset: int = 0):
         _check(self.lib.sspx_fill_random(self.handle, x.ptr, x.n, offset, seed, vec))

@@ -144,11 +144,15 @@ def splitmix64(z):
 
 
 class SyntheticProblem:
-    """H = diag(1 + g) + rho sum_l u_l u_l^T, u_0 = 1, u_l(g) = +-1 from splitmix64 (the
-    rank-one case is test_rayleigh_quotient.cpp:37-42)."""
+    """H = diag(d) + rho sum_l u_l u_l^T, u_0 = 1, u_l(g) = +-1 from splitmix64 (the
+    rank-one case is test_rayleigh_quotient.cpp:37-42).  d_g = 1 + g (diag_kind 0), or for C5's
+    well-posed DIIS instance (diag_kind 1) d_g = 1 + 2 frac(g phi1) with the preconditioner handed the
+    approximate diagonal d_g (1 + alpha (2 frac(g phi2) - 1))."""
 
-    def __init__(self, n, rho, rank, seed):
-        self.n, self.rho, self.rank = n, rho, rank
+    PHI1, PHI2 = float.fromhex("0x1.3c6ef372fe950p-1"), float.fromhex("0x1.827f5352054c6p-1")
+
+    def __init__(self, n, rho, rank, seed, diag_kind=0, alpha=0.0):
+        self.n, self.rho, self.rank, self.diag_kind = n, rho, rank, diag_kind
         g = np.arange(n, dtype=np.uint64)
         with np.errstate(over="ignore"):
             self.u = np.empty((rank, n))
@@ -159,13 +163,20 @@ class SyntheticProblem:
                 key = splitmix64(np.array([np.uint64(seed) ^ np.uint64((1000 + l) * 0xD1B54A32D192ED03 % 2**64)],
                                           dtype=np.uint64))[0]
                 self.u[l] = np.where(splitmix64(np.uint64(key) ^ g) & np.uint64(1), -1.0, 1.0)
-        self.d0 = 1.0 + np.arange(n, dtype=np.float64)
+        g = np.arange(n, dtype=np.float64)
+        if diag_kind == 1:
+            f1, f2 = g * self.PHI1, g * self.PHI2
+            self.d0 = 1.0 + 2.0 * (f1 - np.floor(f1))
+            self.pre = self.d0 * (1.0 + alpha * (2.0 * (f2 - np.floor(f2)) - 1.0))
+        else:
+            self.d0 = 1.0 + g
+            self.pre = self.d0 + self.rank * self.rho
 
     def action(self, x):
         return self.d0 * x + self.rho * (self.u.T @ (self.u @ x))
 
     def diagonals(self):
-        return self.d0 + self.rank * self.rho
+        return self.pre
 
     def pp_action_matrix(self, p):
         up = self.u[:, p]

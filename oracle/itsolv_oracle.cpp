@@ -57,7 +57,7 @@ class SyntheticCpu : public Problem<V, SP> {
     for (size_t g = 0; g < x.size(); ++g) {
       double s = 0;
       for (int l = 0; l < m_s.rank; ++l) s += m_u[l][g] * c[l];
-      y[g] = (1.0 + double(g)) * x[g] + m_s.rho * s;
+      y[g] = m_s.d(g) * x[g] + m_s.rho * s;
     }
   }
   void action(const CVecRef<V>& p, const VecRef<V>& a) const override {
@@ -81,7 +81,7 @@ class SyntheticCpu : public Problem<V, SP> {
       std::vector<double> w(size_t(m_s.rank), 0.0);
       for (size_t p = 0; p < pp.size(); ++p)
         for (auto& [i, coef] : pp[p].get()) {
-          y[i] += (1.0 + double(i)) * coef * c[k][p];
+          y[i] += m_s.d(i) * coef * c[k][p];
           for (int l = 0; l < m_s.rank; ++l) w[l] += c[k][p] * coef * m_s.u(l, i);
         }
       for (size_t g = 0; g < y.size(); ++g) {
@@ -504,6 +504,18 @@ int oracle_davidson_synthetic(size_t n, double rho, int rank, unsigned long long
                               itsolv_result* out, double* solutions_out) {
   SyntheticCpu p(pr::SyntheticSpec(n, rho, rank, seed));
   return davidson(p, n, opt, out, solutions_out);
+}
+
+// itsolv_davidson_synth / itsolv_diis_synth's twins (any synthetic family, include/subspace_hip.h sspx_synth)
+int oracle_davidson_synth(size_t n, const sspx_synth* s, const itsolv_options* opt, itsolv_result* out,
+                          double* solutions_out) {
+  SyntheticCpu p(pr::SyntheticSpec(n, s->rho, s->rank, s->seed, s->diag_kind, s->alpha));
+  return davidson(p, n, opt, out, solutions_out);
+}
+
+int oracle_diis_synth(size_t n, const sspx_synth* s, const itsolv_options* opt, itsolv_result* out, double* x_out) {
+  SyntheticCpu p(pr::SyntheticSpec(n, s->rho, s->rank, s->seed, s->diag_kind, s->alpha));
+  return diis(p, n, opt, out, x_out);
 }
 
 int oracle_davidson_dense(const double* h, size_t n, const itsolv_options* opt, itsolv_result* out,

@@ -197,7 +197,7 @@ def itsolv_lib():
     if _itsolv is None:
         if not os.path.exists(ITSOLV_PATH):
             build()
-        from itsolv_hbm import Options, Result  # struct layouts shared with the device library
+        from itsolv_hbm import Options, Result, Synth  # struct layouts shared with the device library
 
         L = C.CDLL(ITSOLV_PATH)
         Z, D, I, U = C.c_size_t, C.c_double, C.c_int, C.c_ulonglong
@@ -209,6 +209,8 @@ def itsolv_lib():
             "oracle_diis_dense": [PDd, Z, PO, PR, PDd],
             "oracle_linear_equations_dense": [PDd, Z, PDd, I, PO, PR, PDd],
             "oracle_optimize_dense": [PDd, Z, I, PO, PR, PDd],
+            "oracle_davidson_synth": [Z, C.POINTER(Synth), PO, PR, PDd],
+            "oracle_diis_synth": [Z, C.POINTER(Synth), PO, PR, PDd],
         }.items():
             f = getattr(L, name)
             f.restype = I
@@ -378,11 +380,12 @@ def _solve(fn, args, nout):
     return res.as_dict(), out
 
 
-def davidson_synthetic(n, rho, rank, seed, solutions=True, **opts):
-    from itsolv_hbm import make_options
+def davidson_synthetic(n, rho, rank, seed, solutions=True, *, diag_kind=0, alpha=0.0, **opts):
+    from itsolv_hbm import Synth, make_options
 
     o = make_options(**opts)
-    r, sol = _solve(itsolv_lib().oracle_davidson_synthetic, (n, rho, rank, seed, C.byref(o)),
+    spec = Synth(rho, rank, seed, diag_kind, alpha)
+    r, sol = _solve(itsolv_lib().oracle_davidson_synth, (n, C.byref(spec), C.byref(o)),
                     o.nroots * n if solutions else 0)
     if solutions:
         r["solutions"] = sol[: o.nroots * n].reshape(o.nroots, n)
@@ -400,11 +403,13 @@ def davidson_dense(h, **opts):
     return r
 
 
-def diis_synthetic(n, rho, rank, seed, solutions=True, **opts):
-    from itsolv_hbm import make_options
+def diis_synthetic(n, rho, rank, seed, solutions=True, *, diag_kind=0, alpha=0.0, **opts):
+    """diag_kind / alpha: the synthetic family (itsolv_hbm.DIAG_*, itsolv_hbm.c5_spec)."""
+    from itsolv_hbm import Synth, make_options
 
     o = make_options(**opts)
-    r, x = _solve(itsolv_lib().oracle_diis_synthetic, (n, rho, rank, seed, C.byref(o)), n if solutions else 0)
+    spec = Synth(rho, rank, seed, diag_kind, alpha)
+    r, x = _solve(itsolv_lib().oracle_diis_synth, (n, C.byref(spec), C.byref(o)), n if solutions else 0)
     if solutions:
         r["x"] = x[:n]
     return r

@@ -121,17 +121,23 @@ class IterableSparseHandler : public ArrayHandler<V, SP> {
       for (size_t j = 0; j < m.cols(); ++j) m(i, j) = dot(xx.at(i).get(), yy.at(j).get());
     return m;
   }
+  // reference select_max_dot_iter_sparse (util/select_max_dot.h:59-85): a min-heap that receives the
+  // in-range entries among y's first n without pops, then push + pop for every later in-range entry
   std::map<size_t, double> select_max_dot(size_t n, const V& x, const SP& y) override {
+    if (n > x.size() || n > y.size()) error("ArrayHandlerIterableSparse::select_max_dot() n is too large");
     std::vector<double> prod;
     std::vector<size_t> keys;
-    for (auto& [i, v] : y)
+    size_t keep = 0, e = 0;
+    for (auto& [i, v] : y) {
       if (i < x.size()) {
         keys.push_back(i);
         prod.push_back(std::abs(x[i] * v));
+        if (e < n) ++keep;
       }
-    auto sel = IterableHandler::to_map(std::min(n, prod.size()), [&](size_t* i, double* v, size_t* c) {
-      return or_select_max_dot(prod.data(), std::vector<double>(prod.size(), 1.0).data(), prod.size(),
-                               std::min(n, prod.size()), i, v, c);
+      ++e;
+    }
+    auto sel = IterableHandler::to_map(keep, [&](size_t* i, double* v, size_t* c) {
+      return or_select_max_dot(prod.data(), std::vector<double>(prod.size(), 1.0).data(), prod.size(), keep, i, v, c);
     });
     std::map<size_t, double> out;
     for (auto& [k, v] : sel) out.emplace(keys[k], v);

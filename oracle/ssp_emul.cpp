@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -119,11 +120,26 @@ extern "C" {
 
 const char* ssp_last_error(void) { return g_err.c_str(); }
 const char* ssp_version(void) { return "ssp-emul (host emulation, test infrastructure)"; }
-int ssp_device_count(void) { return 0; }
-int ssp_ctx_create(int, ssp_ctx** out) {
+// The emulation's devices: SSP_EMUL_DEVICES of them (default 1), narrowed as the HIP runtime narrows
+// them by HIP_VISIBLE_DEVICES (a comma-separated list), so the C API's device choice can be tested.
+int ssp_device_count(void) {
+  const char* e = std::getenv("SSP_EMUL_DEVICES");
+  int n = (e && *e) ? std::atoi(e) : 1;
+  if (const char* v = std::getenv("HIP_VISIBLE_DEVICES")) {
+    int k = *v ? 1 : 0;
+    for (const char* c = v; *c; ++c) k += *c == ',';
+    n = std::min(n, k);
+  }
+  return n;
+}
+static int g_last_device = -1;
+int ssp_ctx_create(int device, ssp_ctx** out) {
+  g_last_device = device;
   *out = new ssp_ctx();
   return SSP_OK;
 }
+// test hook: the device of the last ssp_ctx_create
+int ssp_emul_last_device(void) { return g_last_device; }
 int ssp_ctx_destroy(ssp_ctx* c) {
   delete c;
   return SSP_OK;
@@ -414,11 +430,21 @@ int ssp_gemm_outer_sparse(ssp_ctx*, const double* al, const size_t* ptr, const s
   return SSP_OK;
 }
 
-int sspx_synthetic_action(ssp_ctx* c, const double* const* xx, double* const* yy, int nvec, size_t n, size_t off,
-                          double rho, int rank, unsigned long long seed) {
+// The diagonal families of itsolv_hbm/problems.h SyntheticSpec (same IEEE operations).
+static double emul_frac_phi(size_t g, double phi) {
+  const double f = double(g) * phi;
+  return f - std::floor(f);
+}
+static double emul_d(const sspx_synth* s, size_t g) {
+  return s->diag_kind == SSPX_DIAG_BOUNDED ? 1.0 + 2.0 * emul_frac_phi(g, 0x1.3c6ef372fe950p-1) : 1.0 + double(g);
+}
+
+int sspx_synth_action(ssp_ctx* c, const sspx_synth* sp, const double* const* xx, double* const* yy, int nvec,
+                      size_t n, size_t off) {
+  const int rank = sp->rank;
   std::vector<double> coef(size_t(nvec) * rank, 0.0);
   std::vector<uint64_t> key(rank);
-  for (int l = 0; l < rank; ++l) key[l] = stream_key(seed, 1000 + l);
+  for (int l = 0; l < rank; ++l) key[l] = stream_key(sp->seed, 1000 + l);
   for (int v = 0; v < nvec; ++v)
     for (int l = 0; l < rank; ++l) {
       double s = 0;
@@ -430,24 +456,46 @@ int sspx_synthetic_action(ssp_ctx* c, const double* const* xx, double* const* yy
     for (size_t i = 0; i < n; ++i) {
       double t = 0;
       for (int l = 0; l < rank; ++l) t += (l == 0 ? 1.0 : sign_of(key[l], off + i)) * coef[size_t(v) * rank + l];
-      yy[v][i] = (1.0 + double(off + i)) * xx[v][i] + rho * t;
+      yy[v][i] = emul_d(sp, off + i) * xx[v][i] + sp->rho * t;
     }
   return SSP_OK;
 }
-int sspx_synthetic_add_lowrank(ssp_ctx*, double* const* yy, int nvec, size_t n, size_t off, double rho, int rank,
-                               unsigned long long seed, const double* w) {
+int sspx_synth_add_lowrank(ssp_ctx*, const sspx_synth* sp, double* const* yy, int nvec, size_t n, size_t off,
+                           const double* w) {
   for (int v = 0; v < nvec; ++v)
     for (size_t i = 0; i < n; ++i) {
       double t = 0;
-      for (int l = 0; l < rank; ++l)
-        t += (l == 0 ? 1.0 : sign_of(stream_key(seed, 1000 + l), off + i)) * w[size_t(v) * rank + l];
-      yy[v][i] += rho * t;
+      for (int l = 0; l < sp->rank; ++l)
+        t += (l == 0 ? 1.0 : sign_of(stream_key(sp->seed, 1000 + l), off + i)) * w[size_t(v) * sp->rank + l];
+      yy[v][i] += sp->rho * t;
     }
   return SSP_OK;
 }
-int sspx_synthetic_diagonal(ssp_ctx*, double* d, size_t n, size_t off, double rho, int rank) {
-  for (size_t i = 0; i < n; ++i) d[i] = 1.0 + double(off + i) + rank * rho;
+int sspx_synth_diagonal(ssp_ctx*, const sspx_synth* sp, double* d, size_t n, size_t off) {
+  for (size_t i = 0; i < n; ++i) {
+    if (sp->diag_kind == SSPX_DIAG_BOUNDED) {
+      const double t = 2.0 * emul_frac_phi(off + i, 0x1.827f5352054c6p-1) - 1.0;
+      const double s = sp->alpha * t;
+      d[i] = emul_d(sp, off + i) * (1.0 + s);
+    } else {
+      d[i] = 1.0 + double(off + i) + sp->rank * sp->rho;
+    }
+  }
   return SSP_OK;
+}
+int sspx_synthetic_action(ssp_ctx* c, const double* const* xx, double* const* yy, int nvec, size_t n, size_t off,
+                          double rho, int rank, unsigned long long seed) {
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  return sspx_synth_action(c, &s, xx, yy, nvec, n, off);
+}
+int sspx_synthetic_add_lowrank(ssp_ctx* c, double* const* yy, int nvec, size_t n, size_t off, double rho, int rank,
+                               unsigned long long seed, const double* w) {
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  return sspx_synth_add_lowrank(c, &s, yy, nvec, n, off, w);
+}
+int sspx_synthetic_diagonal(ssp_ctx* c, double* d, size_t n, size_t off, double rho, int rank) {
+  const sspx_synth s{rho, rank, 0, SSPX_DIAG_LINEAR, 0.0};
+  return sspx_synth_diagonal(c, &s, d, n, off);
 }
 int sspx_fill_random(ssp_ctx*, double* x, size_t n, size_t off, unsigned long long seed, unsigned long long vec) {
   const uint64_t key = stream_key(seed, vec);

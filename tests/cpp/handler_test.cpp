@@ -25,6 +25,7 @@
 #include <memory>
 #include <numeric>
 #include <random>
+#include <stdexcept>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -367,6 +368,42 @@ void op_cases() {
            "gemm_outer alphas rows");
     expect(throws<array::util::ArrayHandlerError>([&] { hb.select(4, x); }), "select n too large");
   });
+#ifndef WITH_REFERENCE_BASE
+  // A lazy register whose evaluation fails (here a distribution mismatch inside the batched
+  // gemm_inner) reports the error to the caller of eval(), and the handle's destruction during the
+  // unwinding neither re-evaluates nor terminates; a handle destroyed normally still evaluates.
+  // (The restated base only: the reference's LazyHandle destructor re-evaluates unconditionally.)
+  run("lazy_error_reaches_caller", [] {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    auto x = make({1, 2, 3});
+    auto y = make({1, 2, 3, 4});
+    double out = -1;
+    bool caught = false;
+    try {
+      auto lazy = hb.lazy_handle();
+      lazy.dot(x, y, out);
+      lazy.eval();
+    } catch (const array::util::ArrayHandlerError&) {
+      caught = true;
+    }
+    expect(caught && out == -1, "eval() error reaches the caller");
+    caught = false;
+    try {
+      auto lazy = hb.lazy_handle();
+      lazy.dot(x, y, out);
+      throw std::runtime_error("caller error while the register is pending");
+    } catch (const std::runtime_error&) {
+      caught = true;
+    }
+    expect(caught && out == -1, "pending register dropped during unwinding");
+    {
+      auto lazy = hb.lazy_handle();
+      lazy.dot(x, x, out);
+    }
+    expect(out == 14, "destruction evaluates");
+  });
+#endif
   run("sparse_handler", [] {
     ArrayHandlerHbmSparse handler;
     array::ArrayHandler<Vec, SparseP>& hb = handler;
@@ -385,6 +422,16 @@ void op_cases() {
     // testArrayHandlerIterableSparse.cpp:22-29 analogue: largest |x_i p_i|
     auto sel = hb.select_max_dot(2, x, p);
     expect(sel == std::map<size_t, double>({{1, 4.0}, {4, 3.0}}), "sparse select_max_dot");
+    // select_max_dot_iter_sparse (util/select_max_dot.h:59-85) with out-of-range entries among y's
+    // first n: each shrinks the heap by one and is never pushed, so n = 4 and n = 5 both return the
+    // three in-range products (fewer than n), and n = 2 the two largest of them
+    SparseP r{{1, 2.0}, {4, -1.0}, {6, 0.5}, {100, 7.0}, {200, 1.0}};
+    const std::map<size_t, double> three{{1, 4.0}, {4, 3.0}, {6, 2.0}};
+    expect(hb.select_max_dot(4, x, r) == three, "sparse select_max_dot, 1 of the first 4 out of range");
+    expect(hb.select_max_dot(5, x, r) == three, "sparse select_max_dot, 2 of the first 5 out of range");
+    expect(hb.select_max_dot(2, x, r) == std::map<size_t, double>({{1, 4.0}, {4, 3.0}}),
+           "sparse select_max_dot, none of the first 2 out of range");
+    expect(throws<array::util::ArrayHandlerError>([&] { hb.select_max_dot(6, x, r); }), "sparse select_max_dot n > y");
   });
 }
 

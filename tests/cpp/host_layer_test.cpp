@@ -245,6 +245,15 @@ void itsolv_util_cases() {
     expect(throws<std::runtime_error>([] { StringFacet::parse_keyval_string("keywithoutvalue"); }), "bad");
     auto m2 = StringFacet::parse_keyval_string("a:1; b = 2;");
     expect(m2.size() == 2 && m2["a"] == "1" && m2["b"] == "2", "':' and ';' separators");
+    // reference util.cpp:47-48: parsing stops at the first empty field
+    auto m3 = StringFacet::parse_keyval_string("A=1,,B=2");
+    expect(m3.size() == 1 && m3["A"] == "1", "consecutive separators end the list");
+    auto m4 = StringFacet::parse_keyval_string("A=1; ;B=2");
+    expect(m4.size() == 1, "a blank field ends the list");
+    expect(StringFacet::parse_keyval_string("").empty() && StringFacet::parse_keyval_string(" , A=1").empty(),
+           "leading empty field");
+    auto m5 = StringFacet::parse_keyval_string("k=a=b");
+    expect(m5["k"] == "a=b", "value keeps later separators");
   });
 }
 

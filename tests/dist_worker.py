@@ -10,7 +10,7 @@ Cases:
   reductions  (CPU) oracle shard pieces + the product's host exchange + ssp_select_merge
   gpu_ops     (GPU) every reducing op of libsubspace_hip.so on shards, host communicator attached
   gpu_solver  (GPU) Davidson / DIIS on sharded HBM vectors vs the single-rank CPU reference path
-  gpu_traces  (GPU) the committed BASELINE-size traces (C4 shape, C2, C5 descent) on shards
+  gpu_traces  (GPU) the committed BASELINE-size traces (C4 shape, C2, C5) on shards
 
 Exit status 0 = every assertion held on this rank.
 """
@@ -157,58 +157,41 @@ def case_gpu_solver(comm):
     ctx.close()
 
 
+# SSP_TRACES_FULL selects the full-size traces: BASELINE C4 (N = 1e8, 8 roots + P 16) or C5 (DIIS, N = 1e8)
+FULL_TRACES = {"C4": ("C3_n1e8_rank1",), "C5": ("C5_n1e8",)}
+
+
 def case_gpu_traces(comm):
-    """North-star traces on shards: the C4 shape (8 roots + P 16, rank-8 H, N = 1e7), C2 and C5's
-    fixed-length DIIS descent, sharded over this world on HBM, against the committed per-iteration
-    traces of the single-rank reference CPU path (tests/golden/traces.json) under the same bar as the
-    single-GPU runs (trace_check.assert_trace)."""
+    """North-star traces on shards: the C4 shape (8 roots + P 16, rank-8 H, N = 1e7), C2 and C5 (the
+    well-posed DIIS instance, and the chaotic round-1 instance's fixed-length descent), sharded over
+    this world on HBM, against the committed per-iteration traces of the single-rank reference CPU
+    path (tests/golden/traces.json) under the same bar as the single-GPU runs
+    (trace_check.assert_trace)."""
     import numpy as np
 
     import itsolv_hbm as ih
     import subspace_hip as sh
-    from trace_check import EIG_REL, T, assert_trace
+    from trace_check import EIG_REL, T, assert_trace, run_case
 
     rank, world = comm.rank, comm.nranks
     ctx = sh.Context(0)
     ctx.attach_host_comm(comm)
-    names = ("C3_n1e7_rank8", "C2_rank8", "C5_n1e7_traj12")
-    if os.environ.get("SSP_TRACES_FULL"):  # BASELINE C4 itself: N = 1e8, 8 roots + P 16
-        names = ("C3_n1e8_rank1",)
+    names = ("C3_n1e7_rank8", "C2_rank8", "C5_n1e7", "C5x_n1e7_traj12")
+    if os.environ.get("SSP_TRACES_FULL"):
+        names = FULL_TRACES[os.environ["SSP_TRACES_FULL"]]
     for name in names:
         ref = T[name]
         c = ref["case"]
         nl = sh.shard_range(c["n"], world, rank)[1]
-        run = ih.diis_synthetic if c["kind"] == "diis" else ih.davidson_synthetic
-        g = run(ctx, c["n"], c["rho"], c["rank"], c["seed"], n_local=nl, solutions=False, **ref["options"])
+        g = run_case(ih, ctx, ref, n_local=nl, solutions=c["kind"] == "diis")
         assert_trace(g, ref, f"{name} on {world} shards")
+        if c["kind"] == "diis" and ref["converged"]:  # x = 1 on every shard
+            assert np.max(np.abs(g["x"] - 1.0)) <= ref["options"]["convergence_threshold"], name
         if rank == 0:
             print(f"{name} on {world} shards: {g['iterations']} iterations (CPU path {ref['iterations']}), "
                   f"{g['seconds']:.3f} s", flush=True)
         if c["kind"] == "davidson":
             np.testing.assert_allclose(g["eigenvalues"], ref["eigenvalues"], rtol=EIG_REL, atol=0)
-    ctx.close()
-
-
-def case_gpu_c5_full(comm):
-    """BASELINE C5 at full size (NonLinearEquationsDIIS, N = 1e8) sharded over this world: converges
-    to x = 1 at the threshold on every shard (past the 1e-6 plateau the reference algorithm itself
-    is rounding-chaotic, so the iteration count is reported, not compared; test_traces_gpu.py)."""
-    import numpy as np
-
-    import itsolv_hbm as ih
-    import subspace_hip as sh
-
-    rank, world = comm.rank, comm.nranks
-    ctx = sh.Context(0)
-    ctx.attach_host_comm(comm)
-    n = 100_000_000
-    nl = sh.shard_range(n, world, rank)[1]
-    r = ih.diis_synthetic(ctx, n, 0.01, 3, 3, n_local=nl, convergence_threshold=1e-8, max_size_qspace=6)
-    assert r["converged"], r["iterations"]
-    assert r["errors"][0] < 1e-8 and r["residual_norms"][0] < 1e-8
-    assert np.max(np.abs(r["x"] - 1.0)) <= 1e-8  # |x - 1| <= |H (x - 1)| / lambda_min(H), lambda_min >= 1
-    if rank == 0:
-        print(f"C5 N=1e8 on {world} shards: {r['iterations']} iterations, {r['seconds']:.3f} s", flush=True)
     ctx.close()
 
 
@@ -226,12 +209,12 @@ def case_gpu_distr(comm):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--comm", choices=["gloo", "hub"], required=True)
-    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver", "gpu_distr", "gpu_traces", "gpu_c5_full"],
+    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver", "gpu_distr", "gpu_traces"],
                     required=True)
     a = ap.parse_args()
     comm = make_comm(a.comm)
     {"reductions": case_reductions, "gpu_ops": case_gpu_ops, "gpu_solver": case_gpu_solver,
-     "gpu_distr": case_gpu_distr, "gpu_traces": case_gpu_traces, "gpu_c5_full": case_gpu_c5_full}[a.case](comm)
+     "gpu_distr": case_gpu_distr, "gpu_traces": case_gpu_traces}[a.case](comm)
     if a.comm == "gloo":
         import torch.distributed as dist
 

@@ -193,6 +193,17 @@ def case_c4(gloo=False):
     assert np.allclose(e, ei, rtol=1e-4, atol=0), (e, ei)
 
 
+def case_devsel():
+    """The reference C API's instances take the device of the node-local rank the launcher exported
+    (iterative_solver_c.cpp default_device) modulo the visible device count; argv[2] = expected."""
+    import ctypes
+
+    s = iterative_solver.LinearEigensystem(8, 1)
+    got = ctypes.CDLL(sh.LIB_PATH).ssp_emul_last_device()
+    s.finalize()
+    assert got == int(sys.argv[2]), (got, sys.argv[2])
+
+
 def case_distr():
     """The reference's distributed-array known answers (tests/distr_cases.py) at this world size."""
     import distr_cases
@@ -207,5 +218,6 @@ def case_distr():
 
 
 if __name__ == "__main__":
-    {"api": case_api, "spmd": case_spmd, "spmd-gloo": lambda: case_spmd(gloo=True), "c4": case_c4, "distr": case_distr}[sys.argv[1]]()
+    {"api": case_api, "spmd": case_spmd, "spmd-gloo": lambda: case_spmd(gloo=True), "c4": case_c4, "distr": case_distr,
+     "devsel": case_devsel}[sys.argv[1]]()
     print(f"{sys.argv[1]} OK", flush=True)

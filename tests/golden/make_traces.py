@@ -22,9 +22,17 @@ reference's test_rayleigh_quotient.cpp:37-42 matrix at large n), options of §8d
   C3  Davidson  8 roots + P 16      N = 1e7   (C3's shape at a tenth of its length: the CPU path
                                                at N = 1e8 needs > 64 GB with 112 vectors)
   C3  Davidson  8 roots + P 16      N = 1e8   rank 1 (Q stays small: fits this container)
-  C5  DIIS      max_size_qspace 6   N = 1e7   fixed 12-iteration trajectory (the descent to
-                                              the 1e-6 plateau) (threshold 1e-14) and the
-                                              converged run (threshold 1e-8)
+  C5  DIIS      max_size_qspace 6   N = 1e7 and N = 1e8: the well-posed instance
+                                              (itsolv_hbm/problems.h c5_spec: the reference test's
+                                              1 1^T + diag form with the coupling scaled by 1/N, a
+                                              bounded diagonal and an approximate preconditioner
+                                              diagonal; |r_0| ~ 3 sqrt(N), geometric convergence to
+                                              the 1e-8 threshold four orders above the rounding floor)
+  C5x DIIS      max_size_qspace 6   N = 1e7   the round-1 instance (diag(1+g), rank 3, rho 0.01):
+                                              |r_0| = 1.9e10, so the threshold lies below its rounding
+                                              floor and the count past the 1e-6 plateau is decided by
+                                              rounding (kept as the documented chaotic case: the
+                                              12-iteration descent, threshold 1e-14, and the run)
 
 Run (about 5 minutes on 8 cores, < 48 GB):  python tests/golden/make_traces.py [--only NAME ...]
 """
@@ -49,11 +57,21 @@ CASES = {
     "C3_n1e7_rank1": dict(kind="davidson", n=10_000_000, rho=RHO, rank=1, seed=SEED, nroots=8, max_p=16),
     "C3_n1e7_rank8": dict(kind="davidson", n=10_000_000, rho=RHO, rank=8, seed=SEED, nroots=8, max_p=16),
     "C3_n1e8_rank1": dict(kind="davidson", n=100_000_000, rho=RHO, rank=1, seed=SEED, nroots=8, max_p=16),
-    # C5: the DIIS problem of profiles/r1/solver_ledger_v10.json (rho 0.01, rank 3, seed 3)
-    "C5_n1e7_traj12": dict(kind="diis", n=10_000_000, rho=0.01, rank=3, seed=3, max_iter=12,
-                           convergence_threshold=1e-14),
-    "C5_n1e7": dict(kind="diis", n=10_000_000, rho=0.01, rank=3, seed=3, convergence_threshold=1e-8),
+    # C5: the well-posed DIIS instance (itsolv_hbm.c5_spec)
+    "C5_n1e7": dict(kind="diis", n=10_000_000, rho=1.0 / 10_000_000, rank=1, seed=3, diag_kind=1, alpha=0.5,
+                    convergence_threshold=1e-8),
+    "C5_n1e8": dict(kind="diis", n=100_000_000, rho=1.0 / 100_000_000, rank=1, seed=3, diag_kind=1, alpha=0.5,
+                    convergence_threshold=1e-8),
+    # C5x: the round-1 DIIS problem (profiles/r1/solver_ledger_v10.json: rho 0.01, rank 3, seed 3), chaotic
+    "C5x_n1e7_traj12": dict(kind="diis", n=10_000_000, rho=0.01, rank=3, seed=3, max_iter=12,
+                            convergence_threshold=1e-14),
+    "C5x_n1e7": dict(kind="diis", n=10_000_000, rho=0.01, rank=3, seed=3, convergence_threshold=1e-8),
 }
+
+
+def problem_kw(c):
+    """The synthetic family of a case (diag_kind / alpha; absent = the Davidson family d_g = 1 + g)."""
+    return {k: c[k] for k in ("diag_kind", "alpha") if k in c}
 
 
 def options(c):
@@ -76,9 +94,9 @@ def run(name):
     # the same CPU path with its dots summed in another valid order (8 interleaved partial sums):
     # how far the REFERENCE algorithm itself moves under a change of rounding
     oracle.set_sum_order(1)
-    v = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **options(c))
+    v = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **problem_kw(c), **options(c))
     oracle.set_sum_order(0)
-    r = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **options(c))
+    r = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **problem_kw(c), **options(c))
     tr, tv = r["trace"], v["trace"]
     k = min(len(tr["nq"]), len(tv["nq"]))
     reordered = {

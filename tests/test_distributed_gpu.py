@@ -31,8 +31,9 @@ def test_world2_reference_distributed_array_known_answers():
 
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_sharded_traces_match_reference_path(world):
-    # C4's shape (8 roots + P 16, rank-8 H) at N = 1e7, C2 and C5's DIIS descent, sharded over 2, 3 (ragged), 4 and 8
-    # ranks on HBM: step for step with the single-rank reference CPU path's committed traces
+    # C4's shape (8 roots + P 16, rank-8 H) at N = 1e7, C2 and C5 (the well-posed DIIS instance, and the
+    # chaotic instance's descent), sharded over 2, 3 (ragged), 4 and 8 ranks on HBM: step for step with
+    # the single-rank reference CPU path's committed traces
     print(run_hub("gpu_traces", world=world, timeout=600)[0])
 
 
@@ -41,11 +42,13 @@ def test_c4_full_size_on_8_shards(monkeypatch):
     # 100 MB per vector per rank, 90 GB in all) -- here 8 processes on one MI355X with the host
     # communicator in place of RCCL -- against the committed single-rank CPU-path trace (traces.json
     # C3_n1e8_rank1) under the same bar as the one-GPU run.
-    monkeypatch.setenv("SSP_TRACES_FULL", "1")
+    monkeypatch.setenv("SSP_TRACES_FULL", "C4")
     print(run_hub("gpu_traces", world=8, timeout=600)[0])
 
 
-def test_c5_full_size_on_8_shards():
+def test_c5_full_size_on_8_shards(monkeypatch):
     # BASELINE config C5 at full size (DIIS, N = 1e8) over 8 ranks (8 processes on one MI355X, host
-    # communicator): converges to x = 1 on every shard
-    print(run_hub("gpu_c5_full", world=8, timeout=600)[0])
+    # communicator): the committed CPU-path trace (traces.json C5_n1e8) step for step -- iterations,
+    # R/Q creations, Q-space and working-set sizes -- and x = 1 on every shard
+    monkeypatch.setenv("SSP_TRACES_FULL", "C5")
+    print(run_hub("gpu_traces", world=8, timeout=600)[0])

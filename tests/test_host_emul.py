@@ -72,3 +72,23 @@ def test_reference_distributed_array_known_answers(world):
     outs = [p.communicate(timeout=300)[0] for p in procs]
     for p, out in zip(procs, outs):
         assert p.returncode == 0 and "distr OK" in out, out[-3000:]
+
+
+LAUNCHER_VARS = ("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "SLURM_LOCALID", "HIP_VISIBLE_DEVICES",
+                 "SSP_EMUL_DEVICES")
+
+
+@pytest.mark.parametrize("env,want", [
+    ({"SSP_EMUL_DEVICES": "8"}, 0),                                          # no launcher: device 0
+    ({"SSP_EMUL_DEVICES": "4", "LOCAL_RANK": "5"}, 1),                       # torchrun, 5 mod 4
+    ({"SSP_EMUL_DEVICES": "8", "OMPI_COMM_WORLD_LOCAL_RANK": "3"}, 3),       # Open MPI
+    ({"SSP_EMUL_DEVICES": "8", "MPI_LOCALRANKID": "6"}, 6),                  # MPICH
+    ({"SSP_EMUL_DEVICES": "8", "SLURM_LOCALID": "7"}, 7),                    # Slurm
+    ({"SSP_EMUL_DEVICES": "8", "LOCAL_RANK": "5", "HIP_VISIBLE_DEVICES": "5"}, 0),  # one visible device
+    ({"SSP_EMUL_DEVICES": "8", "LOCAL_RANK": "3", "SLURM_LOCALID": "1"}, 3),  # LOCAL_RANK first
+])
+def test_c_api_default_device_follows_node_local_rank(env, want):
+    base = {k: v for k, v in os.environ.items() if k not in LAUNCHER_VARS}
+    r = subprocess.run([sys.executable, WORKER, "devsel", str(want)], env=dict(base, **env), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "devsel OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

@@ -37,8 +37,26 @@ def test_rank_one_traces_end_on_exact_eigenvalues(name):
 
 
 def test_traces_cover_the_baseline_configs():
-    # C1, C2, C3 (shape at 1e7 and the real size at 1e8, rank 1), C5 (trajectory + converged run)
-    for k in ("C1_rank1", "C2_rank1", "C2_rank8", "C3_n1e7_rank8", "C3_n1e8_rank1", "C5_n1e7_traj12", "C5_n1e7"):
+    # C1, C2, C3 (shape at 1e7 and the real size at 1e8), C5 (the well-posed instance at 1e7 and 1e8;
+    # the round-1 chaotic instance C5x as its 12-iteration descent + converged run)
+    for k in ("C1_rank1", "C2_rank1", "C2_rank8", "C3_n1e7_rank8", "C3_n1e8_rank1", "C5_n1e7", "C5_n1e8",
+              "C5x_n1e7_traj12", "C5x_n1e7"):
         assert k in T
     assert T["C3_n1e8_rank1"]["case"]["n"] == 100_000_000 and T["C3_n1e8_rank1"]["options"]["max_p"] == 16
     assert T["C2_rank8"]["options"]["nroots"] == 4 and T["C2_rank8"]["case"]["n"] == 10_000_000
+
+
+@pytest.mark.parametrize("name", ["C5_n1e7", "C5_n1e8"])
+def test_c5_traces_are_well_posed(name):
+    # C5's parity observables are not decided by rounding: the CPU path takes the same steps when only
+    # its summation order changes (make_traces.py "reordered"), it converges, and every error it
+    # decides on lies at least 20 % away from the threshold (no knife edge), while the rounding floor
+    # eps |r_0| sits four orders below it.
+    ref = T[name]
+    assert ref["converged"] and ref["reordered"]["same_steps"] and ref["reordered"]["converged"]
+    assert ref["iterations"] >= 20 and ref["r_creations"] == ref["iterations"] + 1
+    e = np.array(ref["trace"]["errors"])[:, 0]
+    thr = ref["options"]["convergence_threshold"]
+    assert np.all(np.abs(e / thr - 1.0) > 0.2)
+    assert 2.2e-16 * e[0] < 1e-3 * thr
+    assert e[-1] < thr and np.all(e[:-1] > thr)

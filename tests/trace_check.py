@@ -8,6 +8,19 @@ import os
 import numpy as np
 
 T = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "traces.json")))
+C5 = sorted(k for k, v in T.items() if not k.startswith("_") and k.startswith("C5_"))
+
+
+def problem_kw(c):
+    """The synthetic family of a trace case (diag_kind / alpha; absent = d_g = 1 + g), make_traces.py."""
+    return {k: c[k] for k in ("diag_kind", "alpha") if k in c}
+
+
+def run_case(ih, ctx, ref, **kw):
+    """The product solver (itsolv_hbm) on a trace case's problem and options."""
+    c = ref["case"]
+    run = ih.diis_synthetic if c["kind"] == "diis" else ih.davidson_synthetic
+    return run(ctx, c["n"], c["rho"], c["rank"], c["seed"], **problem_kw(c), **kw, **ref["options"])
 DAVIDSON = sorted(k for k, v in T.items() if not k.startswith("_") and v["case"]["kind"] == "davidson")
 EIG_REL, ERR_REL, ERR_ABS, DEV_FACTOR = 1e-10, 1e-6, 1e-13, 10.0
 
