@@ -33,6 +33,12 @@ using oracle::cpu_handlers;
 using oracle::IterableHandler;
 using oracle::ok;
 
+#ifdef OR_OMP  // liboracle_itsolv_omp.so: independent elements on several threads, bit-identical
+#define OR_PAR_FOR _Pragma("omp parallel for schedule(static)")
+#else
+#define OR_PAR_FOR
+#endif
+
 namespace {
 
 thread_local std::string g_error;
@@ -44,16 +50,21 @@ class SyntheticCpu : public Problem<V, SP> {
     m_u.resize(size_t(s.rank));
     for (int l = 0; l < s.rank; ++l) {
       m_u[l].resize(s.n);
-      for (size_t g = 0; g < s.n; ++g) m_u[l][g] = s.u(l, g);
+      auto& u = m_u[l];
+      OR_PAR_FOR
+      for (size_t g = 0; g < s.n; ++g) u[g] = s.u(l, g);
     }
   }
   bool diagonals(V& d) const override {
+    OR_PAR_FOR
     for (size_t g = 0; g < d.size(); ++g) d[g] = m_s.diagonal(g);
     return true;
   }
   void apply(const V& x, V& y) const {
     std::vector<double> c(size_t(m_s.rank));
+    OR_PAR_FOR
     for (int l = 0; l < m_s.rank; ++l) or_dot(m_u[l].data(), x.size(), x.data(), x.size(), &c[l]);
+    OR_PAR_FOR
     for (size_t g = 0; g < x.size(); ++g) {
       double s = 0;
       for (int l = 0; l < m_s.rank; ++l) s += m_u[l][g] * c[l];
@@ -84,6 +95,7 @@ class SyntheticCpu : public Problem<V, SP> {
           y[i] += m_s.d(i) * coef * c[k][p];
           for (int l = 0; l < m_s.rank; ++l) w[l] += c[k][p] * coef * m_s.u(l, i);
         }
+      OR_PAR_FOR
       for (size_t g = 0; g < y.size(); ++g) {
         double s = 0;
         for (int l = 0; l < m_s.rank; ++l) s += m_u[l][g] * w[l];

@@ -187,7 +187,10 @@ def max_(n):
     return n if n > 0 else 1
 
 
-ITSOLV_PATH = os.path.join(_HERE, "build", "liboracle_itsolv.so")
+# ORACLE_OMP=1: the bit-identical OpenMP build (elementwise loops and whole pairwise dots on several
+# threads; make_traces.py --omp for the N = 1e8 traces)
+ITSOLV_PATH = os.path.join(_HERE, "build", "liboracle_itsolv_omp.so" if os.environ.get("ORACLE_OMP") == "1"
+                           else "liboracle_itsolv.so")
 _itsolv = None
 
 
@@ -361,7 +364,8 @@ class RcSolver:
 def set_sum_order(order):
     """Summation order of the CPU path's dot / gemm_inner (oracle_ops.c or_set_sum_order): 0 = the
     reference's sequential loop (default), 1 = 8 interleaved partial sums (a vectorised build of the
-    same loop).  Used only to measure the reference algorithm's own rounding sensitivity."""
+    same loop), 2 = sequential sums over 1024-element blocks folded pairwise (a blocked / threaded
+    reduction).  Used only to measure the reference algorithm's own rounding sensitivity."""
     L = itsolv_lib()
     L.or_set_sum_order.argtypes = [C.c_int]
     L.or_set_sum_order.restype = C.c_int

@@ -58,8 +58,25 @@ class IterableHandler : public ArrayHandler<V, V> {
   Matrix<double> gemm_inner(const CVecRef<V>& xx, const CVecRef<V>& yy) override {
     Matrix<double> m({xx.size(), yy.size()});
     if (xx.empty() || yy.empty()) return m;
+#ifdef OR_OMP
+    // the pairwise dots are independent: whole (sequential) dots spread over threads, bit-identical
+    const long np = long(m.rows() * m.cols()), nc = long(m.cols());
+    std::vector<int> st(size_t(np), 0);
+    std::vector<double> out(size_t(np), 0.0);
+#pragma omp parallel for schedule(dynamic) if (np > 1 && xx.at(0).get().size() > 65536)
+    for (long ij = 0; ij < np; ++ij) {
+      const V& x = xx.at(size_t(ij / nc)).get();
+      const V& y = yy.at(size_t(ij % nc)).get();
+      st[size_t(ij)] = or_dot(x.data(), x.size(), y.data(), y.size(), &out[size_t(ij)]);
+    }
+    for (long ij = 0; ij < np; ++ij) {
+      ok(st[size_t(ij)], "dot");
+      m(size_t(ij / nc), size_t(ij % nc)) = out[size_t(ij)];
+    }
+#else
     for (size_t i = 0; i < m.rows(); ++i)
       for (size_t j = 0; j < m.cols(); ++j) m(i, j) = dot(xx.at(i).get(), yy.at(j).get());
+#endif
     return m;
   }
   std::map<size_t, double> select_max_dot(size_t n, const V& x, const V& y) override {

@@ -6,24 +6,38 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* OR_OMP (liboracle_itsolv_omp.so, tests/golden/make_traces.py --omp only): the loops whose elements are
+ * independent run on several threads.  Every element sees the same operations in the same order as
+ * the sequential build, so results are bit-identical; the sequential sums of dot stay sequential. */
+#ifdef OR_OMP
+#define OR_PRAGMA(x) _Pragma(#x)
+#define OR_PAR_FOR(len) OR_PRAGMA(omp parallel for schedule(static) if ((len) > 65536))
+#else
+#define OR_PAR_FOR(len)
+#endif
+
 int or_fill(double alpha, double* x, size_t n) {
+  OR_PAR_FOR(n)
   for (size_t i = 0; i < n; ++i) x[i] = alpha;
   return 0;
 }
 
 int or_scal(double alpha, double* x, size_t n) {
+  OR_PAR_FOR(n)
   for (size_t i = 0; i < n; ++i) x[i] *= alpha;
   return 0;
 }
 
 int or_copy(double* x, size_t nx, const double* y, size_t ny) {
   if (ny > nx) return 1; /* std::copy(begin(y), end(y), begin(x)) would overrun x */
+  OR_PAR_FOR(ny)
   for (size_t i = 0; i < ny; ++i) x[i] = y[i];
   return 0;
 }
 
 int or_axpy(double alpha, const double* x, size_t nx, double* y, size_t ny) {
   if (nx < ny) return 1;
+  OR_PAR_FOR(ny)
   for (size_t i = 0; i < ny; ++i) y[i] = y[i] + alpha * x[i];
   return 0;
 }
@@ -33,17 +47,45 @@ int or_axpy(double alpha, const double* x, size_t nx, double* y, size_t ny) {
  * parity fixtures are generated with; 1 = 8 interleaved partial sums folded pairwise, the order a
  * vectorising build of the same loop (-ffast-math / AVX-512) produces.  Order 1 exists to measure
  * how sensitive the REFERENCE algorithm itself is to a valid change of summation order
- * (tests/golden/make_traces.py: the "reordered" runs). */
+ * (tests/golden/make_traces.py: the "reordered" runs).  2 = sequential partial sums over consecutive
+ * 1024-element blocks, the block sums folded pairwise: the shape of a blocked / threaded reduction
+ * (an OpenMP-parallel build of the loop, numpy's pairwise sum) and of the GPU's ("reordered_blocked"). */
 static int g_sum_order = 0;
 
 int or_set_sum_order(int order) {
-  if (order < 0 || order > 1) return 1;
+  if (order < 0 || order > 2) return 1;
   g_sum_order = order;
   return 0;
 }
 
 int or_dot(const double* x, size_t nx, const double* y, size_t ny, double* out) {
   if (nx > ny) return 1;
+  if (g_sum_order == 2) {
+    const size_t B = 1024;
+    size_t nb = (nx + B - 1) / B;
+    if (nb == 0) {
+      *out = 0;
+      return 0;
+    }
+    double* p = (double*)malloc(nb * sizeof(double));
+    if (!p) return 3;
+    OR_PAR_FOR(nx)
+    for (size_t b = 0; b < nb; ++b) {
+      double s = 0;
+      size_t e = (b + 1) * B < nx ? (b + 1) * B : nx;
+      for (size_t i = b * B; i < e; ++i) s = s + x[i] * y[i];
+      p[b] = s;
+    }
+    while (nb > 1) {
+      size_t h = nb / 2;
+      for (size_t j = 0; j < h; ++j) p[j] = p[2 * j] + p[2 * j + 1];
+      if (nb & 1) p[h] = p[nb - 1];
+      nb = h + (nb & 1);
+    }
+    *out = p[0];
+    free(p);
+    return 0;
+  }
   if (g_sum_order == 1) {
     double p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     size_t i = 0;
@@ -60,12 +102,19 @@ int or_dot(const double* x, size_t nx, const double* y, size_t ny, double* out) 
 }
 
 int or_gemm_inner(const double* const* xx, int m, const double* const* yy, int k, size_t n, double* out) {
-  for (int i = 0; i < m; ++i)
-    for (int j = 0; j < k; ++j) {
-      int s = or_dot(xx[i], n, yy[j], n, &out[(size_t)i * k + j]);
-      if (s) return s;
+  int status = 0;
+  /* the m*k dots are independent: OR_OMP spreads whole (sequential) dots over threads */
+  OR_PAR_FOR((size_t)m * k * n)
+  for (int ij = 0; ij < m * k; ++ij) {
+    int s = or_dot(xx[ij / k], n, yy[ij % k], n, &out[ij]);
+    if (s) {
+#ifdef OR_OMP
+#pragma omp critical
+#endif
+      if (!status) status = s;
     }
-  return 0;
+  }
+  return status;
 }
 
 int or_gemm_outer(const double* alphas, const double* const* xx, int k, double* const* yy, int m, size_t n) {
@@ -155,6 +204,7 @@ int or_select(const double* x, size_t n, size_t nsel, int max, int ignore_sign, 
   if (nsel > n) return 1; /* "ArrayHandlerIterable::select() n is too large" */
   double* v = (double*)malloc((n ? n : 1) * sizeof(double));
   if (!v) return 3;
+  OR_PAR_FOR(n)
   for (size_t i = 0; i < n; ++i)
     v[i] = max ? (ignore_sign ? fabs(x[i]) : x[i]) : (ignore_sign ? -fabs(x[i]) : -x[i]);
   int s = select_pairs(v, n, nsel, !max, idx_out, val_out, nout);
@@ -167,6 +217,7 @@ int or_select_max_dot(const double* x, const double* y, size_t n, size_t nsel, s
   if (nsel > n) return 1;
   double* v = (double*)malloc((n ? n : 1) * sizeof(double));
   if (!v) return 3;
+  OR_PAR_FOR(n)
   for (size_t i = 0; i < n; ++i) v[i] = fabs(x[i] * y[i]);
   int s = select_pairs(v, n, nsel, 0, idx_out, val_out, nout);
   free(v);
@@ -197,8 +248,10 @@ int or_sparse_dot(const double* x, size_t n, const size_t* idx, const double* va
 }
 
 int or_precondition(double* const* a, int nvec, const double* d, const double* shift, size_t n) {
-  for (int k = 0; k < nvec; ++k)
+  for (int k = 0; k < nvec; ++k) {
+    OR_PAR_FOR(n)
     for (size_t i = 0; i < n; ++i) a[k][i] = a[k][i] / (d[i] - shift[k] + 1e-15);
+  }
   return 0;
 }
 

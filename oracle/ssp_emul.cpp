@@ -14,7 +14,9 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+#include <initializer_list>
 #include <map>
 #include <string>
 #include <vector>
@@ -77,6 +79,32 @@ int reduce(ssp_ctx* c, double* v, size_t n) {
   if (c->nranks <= 1 || n == 0) return SSP_OK;
   if (!c->allreduce || c->allreduce(v, n, c->user) != 0) return fail(SSP_ERR_COMM, "emul: allreduce failed");
   return SSP_OK;
+}
+
+// SSP_EMUL_TRACE=1: every device call on stderr as "op reads -> writes" with vector ids (allocation
+// order), to see which vectors a solver's call sequence reads after which writes (a checker aid).
+static bool trace_on() {
+  static const bool on = std::getenv("SSP_EMUL_TRACE") != nullptr;
+  return on;
+}
+static std::map<const void*, int>& trace_ids() {
+  static std::map<const void*, int> ids;
+  return ids;
+}
+static void trace(const char* op, std::initializer_list<const double*> rd, std::initializer_list<const double*> wr,
+                  const double* const* rl = nullptr, int nr = 0, const double* const* wl = nullptr, int nw = 0) {
+  if (!trace_on()) return;
+  auto id = [](const double* p) {
+    auto it = trace_ids().find(p);
+    return it == trace_ids().end() ? -1 : it->second;
+  };
+  std::string line = op;
+  for (auto p : rd) line += " " + std::to_string(id(p));
+  for (int i = 0; i < nr; ++i) line += " " + std::to_string(id(rl[i]));
+  line += " ->";
+  for (auto p : wr) line += " " + std::to_string(id(p));
+  for (int i = 0; i < nw; ++i) line += " " + std::to_string(id(wl[i]));
+  std::fprintf(stderr, "%s\n", line.c_str());
 }
 
 struct Led {
@@ -147,6 +175,12 @@ int ssp_ctx_destroy(ssp_ctx* c) {
 void* ssp_ctx_stream(ssp_ctx*) { return nullptr; }
 int ssp_synchronize(ssp_ctx*) { return SSP_OK; }
 int ssp_alloc(ssp_ctx*, size_t n, double** out) {
+  struct Reg {
+    double** o;
+    ~Reg() {
+      if (trace_on() && *o) trace_ids()[*o] = int(trace_ids().size());
+    }
+  } reg{out};
   *out = static_cast<double*>(std::calloc(std::max<size_t>(n, 1), sizeof(double)));
   return *out ? SSP_OK : fail(SSP_ERR_NOMEM, "emul: calloc");
 }
@@ -222,16 +256,19 @@ int ssp_ledger_entry(ssp_ctx* c, int i, const char** name, long long* calls, dou
 
 int ssp_fill(ssp_ctx* c, double a, double* x, size_t n) {
   Led l(c, "fill", 8.0 * n);
+  trace("fill", {}, {x});
   for (size_t i = 0; i < n; ++i) x[i] = a;
   return SSP_OK;
 }
 int ssp_scal(ssp_ctx* c, double a, double* x, size_t n) {
   Led l(c, "scal", 16.0 * n);
+  trace("scal", {x}, {x});
   for (size_t i = 0; i < n; ++i) x[i] *= a;
   return SSP_OK;
 }
 int ssp_copy(ssp_ctx* c, double* x, const double* y, size_t n) {
   Led l(c, "copy", 16.0 * n);
+  trace("copy", {y}, {x});
   if (n && x != y) std::memmove(x, y, n * sizeof(double));
   return SSP_OK;
 }
@@ -243,11 +280,13 @@ int ssp_emul_set_arith(int sum_order, int fma) {
 }
 int ssp_axpy(ssp_ctx* c, double a, const double* x, double* y, size_t n) {
   Led l(c, "axpy", 24.0 * n);
+  trace("axpy", {x, y}, {y});
   for (size_t i = 0; i < n; ++i) y[i] = madd(a, x[i], y[i]);
   return SSP_OK;
 }
 int ssp_dot(ssp_ctx* c, const double* x, const double* y, size_t n, double* out) {
   Led l(c, "dot", (x == y ? 8.0 : 16.0) * n);
+  trace("dot", {x, y}, {});
   *out = dot_n(x, y, n);
   return reduce(c, out, 1);
 }
@@ -256,6 +295,8 @@ int ssp_gemm_inner(ssp_ctx* c, const double* const* xx, int m, const double* con
   distinct.insert(distinct.end(), yy, yy + k);
   std::sort(distinct.begin(), distinct.end());
   Led l(c, "gemm_inner", 8.0 * n * double(std::unique(distinct.begin(), distinct.end()) - distinct.begin()));
+  trace("gemm_inner", {}, {}, xx, m);
+  trace("  with", {}, {}, yy, k);
   for (int i = 0; i < m; ++i)
     for (int j = 0; j < k; ++j) out[size_t(i) * k + j] = dot_n(xx[i], yy[j], n);
   return reduce(c, out, size_t(m) * k);
@@ -265,6 +306,7 @@ int ssp_gemm_outer_sparse(ssp_ctx*, const double* alphas, const size_t* ptr, con
 int ssp_construct_solution(ssp_ctx* c, const double* palphas, const size_t* ptr, const size_t* idx,
                            const double* val, int kp, const double* alphas, const double* const* xx, int k,
                            double* const* yy, int m, size_t n, size_t offset) {
+  trace("construct_solution", {}, {}, xx, k, yy, m);
   for (int j = 0; j < m; ++j)
     for (size_t e = 0; e < n; ++e) yy[j][e] = 0;
   if (kp > 0) ssp_gemm_outer_sparse(c, palphas, ptr, idx, val, kp, yy, m, n, offset);
@@ -281,16 +323,19 @@ static int gemm_outer_body(const double* al, const double* const* xx, int k, dou
 int ssp_gemm_outer_set(ssp_ctx* c, const double* al, const double* const* xx, int k, double* const* yy, int m,
                        size_t n) {
   Led l(c, "gemm_outer_set", 8.0 * n * (k + 1.0 * m));
+  trace("gemm_outer_set", {}, {}, xx, k, yy, m);
   for (int j = 0; j < m; ++j)
     for (size_t e = 0; e < n; ++e) yy[j][e] = 0;
   return gemm_outer_body(al, xx, k, yy, m, n);
 }
 int ssp_gemm_outer(ssp_ctx* c, const double* al, const double* const* xx, int k, double* const* yy, int m, size_t n) {
   Led l(c, "gemm_outer", 8.0 * n * (k + 2.0 * m));
+  trace("gemm_outer", {}, {}, xx, k, yy, m);
   return gemm_outer_body(al, xx, k, yy, m, n);
 }
 int ssp_axpy_inner(ssp_ctx* c, const double* cc, const double* x, double* const* yy, int m, const double* z, size_t n,
                    double* out) {
+  trace("axpy_inner", {x, z}, {}, nullptr, 0, yy, m);
   for (int j = 0; j < m; ++j) {
     for (size_t e = 0; e < n; ++e) yy[j][e] = madd(cc[j], x[e], yy[j][e]);
     out[j] = dot_n(yy[j], z, n);
@@ -298,17 +343,20 @@ int ssp_axpy_inner(ssp_ctx* c, const double* cc, const double* x, double* const*
   return reduce(c, out, size_t(m));
 }
 int ssp_scal_inner(ssp_ctx* c, double alpha, double* x, const double* const* yy, int m, size_t n, double* out) {
+  trace("scal_inner", {x}, {x}, yy, m);
   for (size_t e = 0; e < n; ++e) x[e] *= alpha;
   for (int j = 0; j < m; ++j) out[j] = dot_n(x, yy[j], n);
   return reduce(c, out, size_t(m));
 }
 int ssp_axpy_norm(ssp_ctx* c, const double* cc, const double* x, double* const* yy, int m, size_t n, double* out) {
+  trace("axpy_norm", {x}, {}, nullptr, 0, yy, m);
   for (int j = 0; j < m; ++j)
     for (size_t e = 0; e < n; ++e) yy[j][e] = madd(cc[j], x[e], yy[j][e]);
   *out = dot_n(yy[0], yy[0], n);
   return reduce(c, out, 1);
 }
 int ssp_precondition(ssp_ctx*, double* const* a, int nvec, const double* d, const double* shift, size_t n) {
+  trace("precondition", {d}, {}, nullptr, 0, a, nvec);
   for (int v = 0; v < nvec; ++v)
     for (size_t i = 0; i < n; ++i) a[v][i] = a[v][i] / ((d[i] - shift[v]) + 1e-15);
   return SSP_OK;
@@ -441,6 +489,7 @@ static double emul_d(const sspx_synth* s, size_t g) {
 
 int sspx_synth_action(ssp_ctx* c, const sspx_synth* sp, const double* const* xx, double* const* yy, int nvec,
                       size_t n, size_t off) {
+  trace("synth_action", {}, {}, xx, nvec, yy, nvec);
   const int rank = sp->rank;
   std::vector<double> coef(size_t(nvec) * rank, 0.0);
   std::vector<uint64_t> key(rank);
@@ -462,6 +511,7 @@ int sspx_synth_action(ssp_ctx* c, const sspx_synth* sp, const double* const* xx,
 }
 int sspx_synth_add_lowrank(ssp_ctx*, const sspx_synth* sp, double* const* yy, int nvec, size_t n, size_t off,
                            const double* w) {
+  trace("synth_add_lowrank", {}, {}, yy, nvec, yy, nvec);
   for (int v = 0; v < nvec; ++v)
     for (size_t i = 0; i < n; ++i) {
       double t = 0;

@@ -7,11 +7,12 @@ oracle/oracle_ops.c, built with -ffp-contract=off), i.e. the reference's CPU alg
 records what the reference's driver exposes as parity observables (IterativeSolverTemplate.h:322-408,
 LinearEigensystemDavidson.h:79): the iteration count, R/Q creations, convergence, and after every
 iteration the eigenvalues and errors of every root, the Q-space size and the working-set size.
-Each case is also run with the CPU path's dots summed in another valid order ("reordered": 8
-interleaved partial sums, what a vectorising build of the same loops does): that measures the
+Each case is also run with the CPU path's dots summed in other valid orders ("reordered": 8
+interleaved partial sums, what a vectorising build of the same loops does; "reordered_blocked":
+1024-element blocks folded pairwise, what a blocked or threaded build does): that measures the
 reference algorithm's own sensitivity to rounding, which is what a GPU (whose reductions also sum in
-another order) can be held to -- same steps where the reordered CPU path takes the same steps, and
-per-iteration errors within a few times the reordered CPU path's own deviation.
+another order) can be held to -- same steps where every reordered CPU path takes the same steps, and
+per-iteration errors within a few times the reordered CPU paths' own deviation.
 
 Problem: H = diag(1 + i) + rho * sum_{l<rank} u_l u_l^T (rank 1 with u = 1 is the
 reference's test_rayleigh_quotient.cpp:37-42 matrix at large n), options of §8d
@@ -21,7 +22,9 @@ reference's test_rayleigh_quotient.cpp:37-42 matrix at large n), options of §8d
   C2  Davidson  4 roots             N = 1e7   (rank 1 and the rank-8 perf problem)
   C3  Davidson  8 roots + P 16      N = 1e7   (C3's shape at a tenth of its length: the CPU path
                                                at N = 1e8 needs > 64 GB with 112 vectors)
-  C3  Davidson  8 roots + P 16      N = 1e8   rank 1 (Q stays small: fits this container)
+  C3  Davidson  8 roots + P 16      N = 1e8   rank 1 (Q stays small: fits this container) and rank 8 (the
+                                               bench's solve and C4's problem; Q grows to 48: ~100 GB,
+                                               generated with --omp on a host with the memory)
   C5  DIIS      max_size_qspace 6   N = 1e7 and N = 1e8: the well-posed instance
                                               (itsolv_hbm/problems.h c5_spec: the reference test's
                                               1 1^T + diag form with the coupling scaled by 1/N, a
@@ -34,7 +37,8 @@ reference's test_rayleigh_quotient.cpp:37-42 matrix at large n), options of §8d
                                               rounding (kept as the documented chaotic case: the
                                               12-iteration descent, threshold 1e-14, and the run)
 
-Run (about 5 minutes on 8 cores, < 48 GB):  python tests/golden/make_traces.py [--only NAME ...]
+Run (about 10 minutes on 8 cores, < 48 GB):  python tests/golden/make_traces.py [--only NAME ...]
+C3_n1e8_rank8 (~100 GB):  ORACLE threads via OMP_NUM_THREADS; python tests/golden/make_traces.py --omp --only C3_n1e8_rank8
 """
 import argparse
 import json
@@ -57,6 +61,9 @@ CASES = {
     "C3_n1e7_rank1": dict(kind="davidson", n=10_000_000, rho=RHO, rank=1, seed=SEED, nroots=8, max_p=16),
     "C3_n1e7_rank8": dict(kind="davidson", n=10_000_000, rho=RHO, rank=8, seed=SEED, nroots=8, max_p=16),
     "C3_n1e8_rank1": dict(kind="davidson", n=100_000_000, rho=RHO, rank=1, seed=SEED, nroots=8, max_p=16),
+    # the bench's own solve (bench.py in_solver) and C4's problem at full size: ~100 GB, run on a host
+    # with the memory (--omp, the bit-identical OpenMP build of the CPU path)
+    "C3_n1e8_rank8": dict(kind="davidson", n=100_000_000, rho=RHO, rank=8, seed=SEED, nroots=8, max_p=16),
     # C5: the well-posed DIIS instance (itsolv_hbm.c5_spec)
     "C5_n1e7": dict(kind="diis", n=10_000_000, rho=1.0 / 10_000_000, rank=1, seed=3, diag_kind=1, alpha=0.5,
                     convergence_threshold=1e-8),
@@ -84,35 +91,53 @@ def options(c):
     return o
 
 
-def run(name):
-    import numpy as np
-    import oracle
+# The CPU path re-run with its dots summed in other valid orders (oracle_ops.c or_set_sum_order):
+# how far the REFERENCE algorithm itself moves under a change of rounding.
+VARIANTS = {"reordered": 1,          # 8 interleaved partial sums (a vectorising build)
+            "reordered_blocked": 2}  # 1024-element blocks folded pairwise (a blocked / threaded build)
 
-    c = CASES[name]
-    t0 = time.time()
-    fn = oracle.davidson_synthetic if c["kind"] == "davidson" else oracle.diis_synthetic
-    # the same CPU path with its dots summed in another valid order (8 interleaved partial sums):
-    # how far the REFERENCE algorithm itself moves under a change of rounding
-    oracle.set_sum_order(1)
-    v = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **problem_kw(c), **options(c))
-    oracle.set_sum_order(0)
-    r = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **problem_kw(c), **options(c))
+
+def variant_record(c, r, v):
+    """Deviation of variant run v from the reference run r (dict of trace arrays)."""
+    import numpy as np
+
     tr, tv = r["trace"], v["trace"]
     k = min(len(tr["nq"]), len(tv["nq"]))
-    reordered = {
+    return {
         "iterations": v["iterations"],
         "r_creations": v["r_creations"],
         "q_creations": v["q_creations"],
         "converged": v["converged"],
         "same_steps": bool(v["iterations"] == r["iterations"] and v["r_creations"] == r["r_creations"]
-                           and tv["nq"].tolist() == tr["nq"].tolist()
-                           and tv["nwork"].tolist() == tr["nwork"].tolist()),
-        # per iteration (over the common prefix): max |error_reordered - error_reference| over roots
-        "error_abs_dev": np.max(np.abs(tv["errors"][:k] - tr["errors"][:k]), axis=1).tolist(),
-        "eigenvalue_rel_dev": (np.max(np.abs(tv["eigenvalues"][:k] - tr["eigenvalues"][:k])
-                                      / np.maximum(np.abs(tr["eigenvalues"][:k]), 1.0), axis=1).tolist()
+                           and list(tv["nq"]) == list(tr["nq"]) and list(tv["nwork"]) == list(tr["nwork"])),
+        # per iteration (over the common prefix): max |error_variant - error_reference| over roots
+        "error_abs_dev": np.max(np.abs(np.asarray(tv["errors"])[:k] - np.asarray(tr["errors"])[:k]),
+                                axis=1).tolist(),
+        "eigenvalue_rel_dev": (np.max(np.abs(np.asarray(tv["eigenvalues"])[:k] - np.asarray(tr["eigenvalues"])[:k])
+                                      / np.maximum(np.abs(np.asarray(tr["eigenvalues"])[:k]), 1.0), axis=1).tolist()
                                if c["kind"] == "davidson" else []),
     }
+
+
+def run(name, variants=tuple(VARIANTS), base=None):
+    """The reference run of case `name` (or `base`, its committed record) and the given variants."""
+    import oracle
+
+    c = CASES[name]
+    t0 = time.time()
+    fn = oracle.davidson_synthetic if c["kind"] == "davidson" else oracle.diis_synthetic
+    runs = {}
+    for key in variants:
+        oracle.set_sum_order(VARIANTS[key])
+        runs[key] = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **problem_kw(c), **options(c))
+    oracle.set_sum_order(0)
+    if base is not None:
+        out = dict(base)
+        for key in variants:
+            out[key] = variant_record(c, base, runs[key])
+        return name, out
+    r = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **problem_kw(c), **options(c))
+    tr = r["trace"]
     out = {
         "case": c,
         "options": options(c),
@@ -128,10 +153,55 @@ def run(name):
             "nq": tr["nq"].tolist(),
             "nwork": tr["nwork"].tolist(),
         },
-        "reordered": reordered,
         "cpu_seconds": round(time.time() - t0, 1),
     }
+    for key in variants:
+        out[key] = variant_record(c, r, runs[key])
     return name, out
+
+
+def _run_args(args):
+    return run(*args)
+
+
+PARTS = ("base",) + tuple(VARIANTS)
+
+
+def run_part(name, part):
+    """One run of case `name` in one process: the reference order ("base") or one variant; the raw
+    trace (for hosts where the runs of a case do not fit in memory together: --part / --merge)."""
+    import oracle
+
+    c = CASES[name]
+    t0 = time.time()
+    fn = oracle.davidson_synthetic if c["kind"] == "davidson" else oracle.diis_synthetic
+    oracle.set_sum_order(0 if part == "base" else VARIANTS[part])
+    r = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **problem_kw(c), **options(c))
+    oracle.set_sum_order(0)
+    tr = r["trace"]
+    return {
+        "case": name, "part": part, "converged": r["converged"], "iterations": r["iterations"],
+        "r_creations": r["r_creations"], "q_creations": r["q_creations"],
+        "eigenvalues": [float(x) for x in r["eigenvalues"]] if c["kind"] == "davidson" else [],
+        "errors": [float(x) for x in r["errors"]],
+        "trace": {"eigenvalues": tr["eigenvalues"].tolist() if c["kind"] == "davidson" else [],
+                  "errors": tr["errors"].tolist(), "nq": tr["nq"].tolist(), "nwork": tr["nwork"].tolist()},
+        "cpu_seconds": round(time.time() - t0, 1),
+    }
+
+
+def merge_parts(parts):
+    """The traces.json record of a case from its --part runs (one base, the variants)."""
+    base = next(p for p in parts if p["part"] == "base")
+    c = CASES[base["case"]]
+    out = {"case": c, "options": options(c)}
+    out.update({k: base[k] for k in ("converged", "iterations", "r_creations", "q_creations", "eigenvalues", "errors",
+                                     "trace")})
+    out["cpu_seconds"] = max(p["cpu_seconds"] for p in parts)
+    for p in parts:
+        if p["part"] != "base":
+            out[p["part"]] = variant_record(c, base, p)
+    return base["case"], out
 
 
 def main():
@@ -139,21 +209,47 @@ def main():
     ap.add_argument("--only", nargs="*")
     ap.add_argument("--jobs", type=int, default=3)
     ap.add_argument("--out", default=os.path.join(HERE, "traces.json"))
+    ap.add_argument("--omp", action="store_true",
+                    help="the bit-identical OpenMP build of the CPU path (oracle/build/liboracle_itsolv_omp.so)")
+    ap.add_argument("--add-variants", nargs="*", choices=list(VARIANTS),
+                    help="only run these sum-order variants against the committed reference runs")
+    ap.add_argument("--part", choices=PARTS, help="one run of the single --only case, written to --out as is")
+    ap.add_argument("--merge", nargs="*", help="--part outputs of one case to merge into --out")
     a = ap.parse_args()
-    names = a.only or list(CASES)
+    if a.omp:
+        os.environ["ORACLE_OMP"] = "1"
+    if a.part:
+        (name,) = a.only
+        r = run_part(name, a.part)
+        json.dump(r, open(a.out, "w"))
+        print(name, a.part, r["iterations"], r["r_creations"], r["cpu_seconds"], "s", flush=True)
+        return
+    if a.merge:
+        name, rec = merge_parts([json.load(open(f)) for f in a.merge])
+        old = json.load(open(a.out))
+        old[name] = rec
+        json.dump(dict(sorted(old.items())), open(a.out, "w"), indent=1)
+        print(name, rec["iterations"], {k: rec[k]["same_steps"] for k in VARIANTS if k in rec}, flush=True)
+        return
+    names = a.only or [n for n in CASES if n != "C3_n1e8_rank8"]
     old = json.load(open(a.out)) if os.path.exists(a.out) else {}
-    old = {k: v for k, v in old.items() if k in CASES}
-    # the N = 1e8 case alone holds ~40 GB: run it by itself
+    old = {k: v for k, v in old.items() if k in CASES or k.startswith("_")}
+    variants = tuple(a.add_variants) if a.add_variants else tuple(VARIANTS)
+
+    def job(n):
+        return (n, variants, old[n]) if a.add_variants else (n, variants)
+
+    # the N = 1e8 cases hold up to ~40 GB each: run them one at a time
     big = [n for n in names if CASES[n]["n"] >= 100_000_000]
     small = [n for n in names if n not in big]
     with ProcessPoolExecutor(a.jobs) as ex:
-        for name, out in ex.map(run, small):
+        for name, out in ex.map(_run_args, [job(n) for n in small]):
             old[name] = out
-            print(name, out["iterations"], out["converged"], out["cpu_seconds"], "s", flush=True)
+            print(name, out["iterations"], {k: out[k]["same_steps"] for k in VARIANTS if k in out}, flush=True)
     for n in big:
-        name, out = run(n)
+        name, out = run(*job(n))
         old[name] = out
-        print(name, out["iterations"], out["converged"], out["cpu_seconds"], "s", flush=True)
+        print(name, out["iterations"], {k: out[k]["same_steps"] for k in VARIANTS if k in out}, flush=True)
     old["_generator"] = ("tests/golden/make_traces.py: oracle (reference CPU path restated over "
                          "ArrayHandlerIterable loops, -ffp-contract=off)")
     json.dump(dict(sorted(old.items())), open(a.out, "w"), indent=1)

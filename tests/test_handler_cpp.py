@@ -19,6 +19,7 @@ import tempfile
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+SAN = os.environ.get("ITSOLV_SAN_FLAGS", "").split()  # tools/asan_cpu.sh: the sanitizer build
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "cpp", "handler_test.cpp")
 REF_SRC = "/root/reference/src"
@@ -28,7 +29,7 @@ INC = ["-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "iterativ
 def build_and_run(libdir, lib, extra=()):
     with tempfile.TemporaryDirectory() as d:
         exe = os.path.join(d, "handler_test")
-        cmd = ["g++", "-std=c++17", "-O1", "-Wall", *extra, *INC, SRC, "-o", exe, "-L" + libdir, "-l" + lib,
+        cmd = ["g++", "-std=c++17", "-O1", "-Wall", *extra, *SAN, *INC, SRC, "-o", exe, "-L" + libdir, "-l" + lib,
                "-Wl,-rpath," + libdir]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-4000:]

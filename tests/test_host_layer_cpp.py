@@ -21,6 +21,7 @@ import numpy as np
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+SAN = os.environ.get("ITSOLV_SAN_FLAGS", "").split()  # tools/asan_cpu.sh: the sanitizer build
 ROOT = os.path.dirname(HERE)
 REF_SRC = "/root/reference/src"
 INC = ["-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "iterative-solver_amd", "include"),
@@ -31,7 +32,7 @@ ORACLE_BUILD = os.path.join(ROOT, "oracle", "build")
 def build(src, extra=(), libs=()):
     d = tempfile.mkdtemp()
     exe = os.path.join(d, "t")
-    r = subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", *extra, *INC, os.path.join(HERE, "cpp", src), "-o", exe,
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", *extra, *SAN, *INC, os.path.join(HERE, "cpp", src), "-o", exe,
                         *libs], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
     return exe

@@ -49,14 +49,54 @@ def test_traces_cover_the_baseline_configs():
 @pytest.mark.parametrize("name", ["C5_n1e7", "C5_n1e8"])
 def test_c5_traces_are_well_posed(name):
     # C5's parity observables are not decided by rounding: the CPU path takes the same steps when only
-    # its summation order changes (make_traces.py "reordered"), it converges, and every error it
+    # its summation order changes (make_traces.py "reordered" and "reordered_blocked"), it converges,
+    # and every error it
     # decides on lies at least 20 % away from the threshold (no knife edge), while the rounding floor
     # eps |r_0| sits four orders below it.
     ref = T[name]
-    assert ref["converged"] and ref["reordered"]["same_steps"] and ref["reordered"]["converged"]
+    assert ref["converged"]
+    for v in ("reordered", "reordered_blocked"):
+        assert ref[v]["same_steps"] and ref[v]["converged"], v
     assert ref["iterations"] >= 20 and ref["r_creations"] == ref["iterations"] + 1
     e = np.array(ref["trace"]["errors"])[:, 0]
     thr = ref["options"]["convergence_threshold"]
     assert np.all(np.abs(e / thr - 1.0) > 0.2)
     assert 2.2e-16 * e[0] < 1e-3 * thr
     assert e[-1] < thr and np.all(e[:-1] > thr)
+
+
+_OMP_CASE = r"""
+import json, sys
+sys.path[:0] = sys.argv[1:3]
+import oracle
+out = {}
+for order in (0, 2):
+    oracle.set_sum_order(order)
+    r = oracle.davidson_synthetic(300_000, 0.1, 8, 1, solutions=False, nroots=4, max_p=4, convergence_threshold=1e-8,
+                                  max_size_qspace=24, reset_D=8)
+    out[order] = [r["iterations"], r["r_creations"], r["trace"]["eigenvalues"].tolist(), r["trace"]["errors"].tolist(),
+                  r["trace"]["nq"].tolist()]
+print(json.dumps(out))
+"""
+
+
+def test_openmp_oracle_is_bit_identical_to_the_sequential_cpu_path():
+    # make_traces.py --omp (the C3_n1e8_rank8 trace, ~100 GB) runs the CPU path with its independent
+    # elements on several threads (oracle/build/liboracle_itsolv_omp.so): every number must equal the
+    # sequential build's, in the reference order and in the blocked reordering
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    paths = [os.path.join(root, "iterative-solver_amd"), os.path.join(root, "oracle")]
+    if not os.path.exists(os.path.join(root, "oracle", "build", "liboracle_itsolv_omp.so")):
+        subprocess.run(["make", "-C", os.path.join(root, "oracle")], check=True, capture_output=True)
+    runs = []
+    for omp in ("0", "1"):
+        env = dict(os.environ, ORACLE_OMP=omp, OMP_NUM_THREADS="4")
+        r = subprocess.run([sys.executable, "-c", _OMP_CASE, *paths], env=env, capture_output=True, text=True,
+                           timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        runs.append(r.stdout)
+    assert runs[0] == runs[1]

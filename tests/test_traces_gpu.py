@@ -5,15 +5,15 @@ every vector in HBM) against committed per-iteration traces of the reference CPU
 Bar (BASELINE.json north_star; IterativeSolverTemplate.h:322-408, LinearEigensystemDavidson.h:79):
   * identical iteration count and convergence flag;
   * identical R and Q creations and, after EVERY iteration, identical Q-space and working-set
-    sizes -- wherever the reference CPU path itself keeps them under a valid reordering of its sums
-    (the fixture's "reordered" run, make_traces.py).  Where it does not (C3 rank 1: the redundancy
+    sizes -- wherever the reference CPU path itself keeps them under valid reorderings of its sums
+    (the fixture's "reordered" and "reordered_blocked" runs, make_traces.py).  Where it does not (C3 rank 1: the redundancy
     screen of propose_rspace.h:481-512 meets near-dependent residuals of a rank-one problem, and the
     CPU path's own R-creation count moves 11 -> 10 at N = 1e7 and 8 -> 11 at N = 1e8 when only its
     summation order changes), the creation counts are not a parity observable and are not compared;
   * after every iteration, eigenvalues of every root within 1e-10 relative;
   * after every iteration, errors within 1e-6 relative plus 10x the reference CPU path's own
-    deviation under reordering at that point of the trajectory (max over the iteration and its
-    neighbours): a residual norm is a difference of O(|H x|) quantities, so its rounding floor
+    deviation under reordering at that point of the trajectory (max over the two reordered runs, the
+    iteration and its neighbours): a residual norm is a difference of O(|H x|) quantities, so its rounding floor
     (~1e-10 at N = 1e7) is a property of the problem, measured, not assumed;
   * final eigenvalues within 1e-10 relative; for rank 1 also the exact eigenvalues of
     diag(1 + i) + rho 11^T (secular equation, oracle.rank_one_eigenvalues).
