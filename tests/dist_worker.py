@@ -158,7 +158,7 @@ def case_gpu_solver(comm):
 
 
 # SSP_TRACES_FULL selects the full-size traces: BASELINE C4 (N = 1e8, 8 roots + P 16) or C5 (DIIS, N = 1e8)
-FULL_TRACES = {"C4": ("C3_n1e8_rank1",), "C5": ("C5_n1e8",)}
+FULL_TRACES = {"C4": ("C3_n1e8_rank8",), "C5": ("C5_n1e8",)}
 
 
 def case_gpu_traces(comm):

@@ -38,10 +38,12 @@ def test_sharded_traces_match_reference_path(world):
 
 
 def test_c4_full_size_on_8_shards(monkeypatch):
-    # BASELINE config C4 at full size: N = 1e8, 8 roots + P 16, sharded over 8 ranks (12.5e6 elements,
-    # 100 MB per vector per rank, 90 GB in all) -- here 8 processes on one MI355X with the host
-    # communicator in place of RCCL -- against the committed single-rank CPU-path trace (traces.json
-    # C3_n1e8_rank1) under the same bar as the one-GPU run.
+    # BASELINE config C4 at full size: N = 1e8, 8 roots + P 16, rank-8 H, sharded over 8 ranks (12.5e6
+    # elements, 100 MB per vector per rank, 90 GB in all) -- here 8 processes on one MI355X with the
+    # host communicator in place of RCCL -- against the committed single-rank CPU-path trace of the same
+    # problem at full size (traces.json C3_n1e8_rank8: 7 iterations, 48 R creations, the same steps
+    # under both reordered sums) with the full bar: iterations, R/Q creations, Q-space and working-set
+    # sizes after every iteration, eigenvalues within 1e-10, errors within the tolerance.
     monkeypatch.setenv("SSP_TRACES_FULL", "C4")
     print(run_hub("gpu_traces", world=8, timeout=600)[0])
 

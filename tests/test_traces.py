@@ -39,9 +39,15 @@ def test_rank_one_traces_end_on_exact_eigenvalues(name):
 def test_traces_cover_the_baseline_configs():
     # C1, C2, C3 (shape at 1e7 and the real size at 1e8), C5 (the well-posed instance at 1e7 and 1e8;
     # the round-1 chaotic instance C5x as its 12-iteration descent + converged run)
-    for k in ("C1_rank1", "C2_rank1", "C2_rank8", "C3_n1e7_rank8", "C3_n1e8_rank1", "C5_n1e7", "C5_n1e8",
-              "C5x_n1e7_traj12", "C5x_n1e7"):
+    for k in ("C1_rank1", "C2_rank1", "C2_rank8", "C3_n1e7_rank8", "C3_n1e8_rank1", "C3_n1e8_rank8", "C5_n1e7",
+              "C5_n1e8", "C5x_n1e7_traj12", "C5x_n1e7"):
         assert k in T
+    # the bench's own solve at full size (bench.py in_solver, C4's problem): the full trace bar applies
+    # (the CPU path takes the same steps under both reordered sums)
+    c3 = T["C3_n1e8_rank8"]
+    assert c3["case"]["n"] == 100_000_000 and c3["case"]["rank"] == 8 and c3["options"]["max_p"] == 16
+    assert c3["options"]["max_size_qspace"] == 48 and c3["converged"]
+    assert c3["reordered"]["same_steps"] and c3["reordered_blocked"]["same_steps"]
     assert T["C3_n1e8_rank1"]["case"]["n"] == 100_000_000 and T["C3_n1e8_rank1"]["options"]["max_p"] == 16
     assert T["C2_rank8"]["options"]["nroots"] == 4 and T["C2_rank8"]["case"]["n"] == 10_000_000
 
