@@ -129,10 +129,13 @@ class Workload:
 
 def op_kernels(op, m):
     """rocprofv3 kernel-name prefixes of `op`'s main kernel for m destinations / rows (the template
-    instance the launcher picks; older summaries predate the SET parameter)."""
+    instance the launcher picks, unscaled operands; older summaries predate the SET and SC parameters)."""
     mt = next(v for v in (1, 2, 4, 8, 16) if m <= v or v == 16)
-    return {"gemm_inner": ("k_gemm_inner<",), "gemm_outer": (f"k_gemm_outer<{mt}, false, false>", f"k_gemm_outer<{mt}, false>"),
-            "gemm_outer_set": (f"k_gemm_outer<{mt}, false, true>",), "axpy": ("k_axpy",), "fill": ("k_fill(",),
+    return {"gemm_inner": ("k_gemm_inner<",),
+            "gemm_outer": (f"k_gemm_outer<{mt}, false, false, false>", f"k_gemm_outer<{mt}, false, false>",
+                           f"k_gemm_outer<{mt}, false>"),
+            "gemm_outer_set": (f"k_gemm_outer<{mt}, false, true, false>", f"k_gemm_outer<{mt}, false, true>"),
+            "axpy": ("k_axpy",), "fill": ("k_fill(",),
             "dot": ("k_dot_partial",)}.get(op, ())
 
 

@@ -135,6 +135,38 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
 /* a[v][i] /= (d[i] - shift[v] + 1e-15) for v in [0,nvec)   reference itsolv/IterativeSolver.h:34-55 */
 int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n);
 
+/* ---- deferred scal (itsolv_hbm/hbm_vec.h, Vec::scale_by): an operand's value is s * (its stored
+ *      contents); the kernel multiplies each element by s as it loads it -- the one rounding the
+ *      reference's scal loop stores -- so every *_scaled call is bit-identical to ssp_scal(s, v) on
+ *      each operand v with s != 1 followed by the unscaled call, without that pass over v (16 bytes
+ *      per element).  Scale arrays may be null (all 1).  A read-modify-write destination's scale
+ *      (ys) applies to the values read; what is stored is the plain result.  Replaces the separate
+ *      scal pass of reference ArrayHandlerIterable.h:54-57 at the call sites of propose_rspace.h:17-28
+ *      and :450-465 (normalisation of the new R vectors). ------------------------------------------ */
+/* x[:] = alpha * y[:]  (the stored form of a scaled vector whose block is shared) */
+int ssp_scal_copy(ssp_ctx* ctx, double alpha, double* x, const double* y, size_t n);
+int ssp_axpy_scaled(ssp_ctx* ctx, double alpha, const double* x, double xs, double* y, double ys, size_t n);
+int ssp_dot_scaled(ssp_ctx* ctx, const double* x, double xs, const double* y, double ys, size_t n, double* out);
+int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, const double* const* yy,
+                          const double* ys, int k, size_t n, double* out);
+int ssp_gemm_outer_scaled(ssp_ctx* ctx, const double* alphas, const double* const* xx, const double* xs, int k,
+                          double* const* yy, const double* ys, int m, size_t n);
+int ssp_gemm_outer_set_scaled(ssp_ctx* ctx, const double* alphas, const double* const* xx, const double* xs, int k,
+                              double* const* yy, int m, size_t n);
+int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, size_t n,
+                                 size_t offset, const size_t* ptr, const size_t* idx, const double* val, int k,
+                                 double* out);
+int ssp_construct_solution_scaled(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const size_t* idx,
+                                  const double* val, int kp, const double* alphas, const double* const* xx,
+                                  const double* xs, int k, double* const* yy, int m, size_t n, size_t offset);
+/* Block update of the block Gram-Schmidt step (itsolv_hbm/rspace.h block_gram_schmidt):
+ *   yy[j] = ys[j] yy[j] + sum_i palphas[i*m + j] p_i + sum_s alphas[s*m + j] xs[s] xx[s]
+ * bit-identical to ssp_scal(ys) + ssp_gemm_outer_sparse (P) + ssp_gemm_outer (dense sources), in one
+ * pass over the destinations (the indices the P vectors touch are recomputed in that order). */
+int ssp_block_update(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const size_t* idx, const double* val,
+                     int kp, const double* alphas, const double* const* xx, const double* xs, int k, double* const* yy,
+                     const double* ys, int m, size_t n, size_t offset);
+
 /* ---- selection: reference util/select.h:28-55, util/select_max_dot.h:166-190,
  *      DistrArray.cpp:170-276.  Local shard [offset, offset+n) of a global array.  Returns up
  *      to nsel (global index, value) pairs in ASCENDING INDEX order (std::map order), chosen
@@ -198,6 +230,9 @@ typedef struct {
 } sspx_synth;
 int sspx_synth_action(ssp_ctx* ctx, const sspx_synth* spec, const double* const* xx, double* const* yy, int nvec,
                       size_t n, size_t offset);
+/* yy[v] = H (xs[v] xx[v]): the action on deferred-scaled parameters (xs may be null) */
+int sspx_synth_action_scaled(ssp_ctx* ctx, const sspx_synth* spec, const double* const* xx, const double* xs,
+                             double* const* yy, int nvec, size_t n, size_t offset);
 /* yy[v] += rho * sum_l w[v*rank + l] u_l */
 int sspx_synth_add_lowrank(ssp_ctx* ctx, const sspx_synth* spec, double* const* yy, int nvec, size_t n,
                            size_t offset, const double* w);

@@ -26,10 +26,21 @@ namespace {
 using ssp::kBlock;
 
 __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+// Deferred scal (include/subspace_hip.h *_scaled): v * s is the one rounding an eager scal stores.
+template <bool SC>
+__device__ __forceinline__ double2 sc2(double2 v, double s) {
+  return SC ? make_double2(v.x * s, v.y * s) : v;
+}
+template <bool SC>
+__device__ __forceinline__ double sc1(double v, double s) {
+  return SC ? v * s : v;
+}
 
 struct InnerArgs {
   const double* x[ssp::kInnerRows];  // rows: MG groups of 4
   const double* y[ssp::kInnerCols];  // columns: NG groups of 4
+  double xs[ssp::kInnerRows];        // SC: deferred scales of the rows / columns
+  double ys[ssp::kInnerCols];
   int m;
   int k;
   size_t n;
@@ -38,18 +49,26 @@ struct InnerArgs {
 };
 
 // SYM: xx == yy (a symmetric overlap, MG == NG): each vector is loaded once and used as both
-// operands of the MFMA.
-template <int MG, int NG, bool SYM = false>
+// operands of the MFMA.  SC: operands with deferred scales (each loaded element times its vector's
+// scale before the MFMA).
+template <int MG, int NG, bool SYM = false, bool SC = false>
 __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
   static_assert(!SYM || MG == NG, "symmetric panel needs square groups");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 3, p = lane >> 2;
   const double* xp[MG];
   const double* yp[NG];
+  double xsc[MG], ysc[NG];
 #pragma unroll
-  for (int g = 0; g < MG; ++g) xp[g] = (4 * g + r < a.m) ? a.x[4 * g + r] : nullptr;
+  for (int g = 0; g < MG; ++g) {
+    xp[g] = (4 * g + r < a.m) ? a.x[4 * g + r] : nullptr;
+    xsc[g] = (SC && 4 * g + r < a.m) ? a.xs[4 * g + r] : 1.0;
+  }
 #pragma unroll
-  for (int h = 0; h < NG; ++h) yp[h] = (4 * h + r < a.k) ? a.y[4 * h + r] : nullptr;
+  for (int h = 0; h < NG; ++h) {
+    yp[h] = (4 * h + r < a.k) ? a.y[4 * h + r] : nullptr;
+    ysc[h] = (SC && 4 * h + r < a.k) ? a.ys[4 * h + r] : 1.0;
+  }
   double acc[MG][NG];
 #pragma unroll
   for (int g = 0; g < MG; ++g)
@@ -64,9 +83,9 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
     const size_t e = ch * 32 + 2 * p;
     double2 xv[MG], yv[NG];
 #pragma unroll
-    for (int g = 0; g < MG; ++g) xv[g] = xp[g] ? ssp::ld2nt(xp[g] + e) : z2;
+    for (int g = 0; g < MG; ++g) xv[g] = xp[g] ? sc2<SC>(ssp::ld2nt(xp[g] + e), xsc[g]) : z2;
 #pragma unroll
-    for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : (yp[h] ? ssp::ld2nt(yp[h] + e) : z2);
+    for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : (yp[h] ? sc2<SC>(ssp::ld2nt(yp[h] + e), ysc[h]) : z2);
 #pragma unroll
     for (int g = 0; g < MG; ++g)
 #pragma unroll
@@ -81,13 +100,13 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
     double x0[MG], x1[MG];
 #pragma unroll
     for (int g = 0; g < MG; ++g) {
-      x0[g] = (xp[g] && i0 < a.n) ? xp[g][i0] : 0.0;
-      x1[g] = (xp[g] && i1 < a.n) ? xp[g][i1] : 0.0;
+      x0[g] = (xp[g] && i0 < a.n) ? sc1<SC>(xp[g][i0], xsc[g]) : 0.0;
+      x1[g] = (xp[g] && i1 < a.n) ? sc1<SC>(xp[g][i1], xsc[g]) : 0.0;
     }
 #pragma unroll
     for (int h = 0; h < NG; ++h) {
-      const double y0 = SYM ? x0[h] : ((yp[h] && i0 < a.n) ? yp[h][i0] : 0.0);
-      const double y1 = SYM ? x1[h] : ((yp[h] && i1 < a.n) ? yp[h][i1] : 0.0);
+      const double y0 = SYM ? x0[h] : ((yp[h] && i0 < a.n) ? sc1<SC>(yp[h][i0], ysc[h]) : 0.0);
+      const double y1 = SYM ? x1[h] : ((yp[h] && i1 < a.n) ? sc1<SC>(yp[h][i1], ysc[h]) : 0.0);
 #pragma unroll
       for (int g = 0; g < MG; ++g) {
         acc[g][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(x0[g], y0, acc[g][h], 0, 0, 0);
@@ -131,21 +150,25 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
 // rounding, and an independent restatement with LAPACK subspace solves takes 14
 // (tests/test_davidson_independent.py) -- the stride shape is kept because it converges there in the
 // reference's count, not because any summation order is exact.
-template <int K>
+template <int K, bool SC = false>
 __global__ __launch_bounds__(kBlock) void k_gemm_inner_row(const InnerArgs a) {
   using ssp::ld2nt;
   const size_t n2 = a.n >> 1, stride = size_t(gridDim.x) * kBlock;
   double acc[K][2] = {};
-  const bool same = K == 1 && a.y[0] == a.x[0];  // a norm: one load stream
+  const bool same = K == 1 && a.y[0] == a.x[0] && (!SC || a.ys[0] == a.xs[0]);  // a norm: one load stream
+  const double xs = SC ? a.xs[0] : 1.0;
+  double ys[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) ys[j] = SC ? a.ys[j] : 1.0;
   size_t p = size_t(blockIdx.x) * kBlock + threadIdx.x;
   for (; p + 3 * stride < n2; p += 4 * stride) {
     double2 xv[4], yv[K][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) xv[u] = ld2nt(a.x[0] + 2 * (p + u * stride));
+    for (int u = 0; u < 4; ++u) xv[u] = sc2<SC>(ld2nt(a.x[0] + 2 * (p + u * stride)), xs);
 #pragma unroll
     for (int j = 0; j < K; ++j)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) yv[j][u] = same ? xv[u] : ld2nt(a.y[j] + 2 * (p + u * stride));
+      for (int u = 0; u < 4; ++u) yv[j][u] = same ? xv[u] : sc2<SC>(ld2nt(a.y[j] + 2 * (p + u * stride)), ys[j]);
 #pragma unroll
     for (int j = 0; j < K; ++j)
 #pragma unroll
@@ -155,17 +178,18 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner_row(const InnerArgs a) {
       }
   }
   for (; p < n2; p += stride) {
-    const double2 xv = ld2(a.x[0] + 2 * p);
+    const double2 xv = sc2<SC>(ld2(a.x[0] + 2 * p), xs);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const double2 yv = ld2(a.y[j] + 2 * p);
+      const double2 yv = sc2<SC>(ld2(a.y[j] + 2 * p), ys[j]);
       acc[j][0] = fma(xv.x, yv.x, acc[j][0]);
       acc[j][0] = fma(xv.y, yv.y, acc[j][0]);
     }
   }
   if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0)
 #pragma unroll
-    for (int j = 0; j < K; ++j) acc[j][0] = fma(a.x[0][a.n - 1], a.y[j][a.n - 1], acc[j][0]);
+    for (int j = 0; j < K; ++j)
+      acc[j][0] = fma(sc1<SC>(a.x[0][a.n - 1], xs), sc1<SC>(a.y[j][a.n - 1], ys[j]), acc[j][0]);
   __shared__ double red[kBlock / 64][K];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -193,6 +217,7 @@ struct OuterArgs {
   int set;  // 1: yy[j] = sum (destinations not read: fill(0) + gemm_outer in one pass)
   size_t n;
   const double* alpha_dev;         // k*m > kOuterAlpha: alpha[i*m + j] in device memory
+  const double* scale_dev;         // SC: deferred scales, sources [0, k) then destinations [k, k + m)
   double alpha[ssp::kOuterAlpha];  // alpha[i*m + j] in the argument block
 };
 static_assert(sizeof(OuterArgs) <= 4000, "kernel argument block too large");
@@ -207,7 +232,9 @@ constexpr int kOuterWin = 4;
 
 // SET (a.set = 1) is a separate instantiation: the write-only construct_solution form shows under its
 // own name in rocprofv3 statistics, so its launches are not averaged with the read-modify-write ones.
-template <int M, bool DEV, bool SET>
+// SC: sources and (read-modify-write) destinations with deferred scales, applied as each element is
+// loaded (include/subspace_hip.h ssp_gemm_outer_scaled).
+template <int M, bool DEV, bool SET, bool SC = false>
 __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
   using ssp::ld2nt;
   using ssp::st2nt;
@@ -215,6 +242,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
   // argument block's are): they are uniform across the wave and read-only in the kernel.
   using cdouble = const __attribute__((address_space(4))) double;
   const auto alpha = [&](int idx) { return DEV ? ((cdouble*)a.alpha_dev)[idx] : a.alpha[idx]; };
+  const auto scale = [&](int idx) { return SC ? ((cdouble*)a.scale_dev)[idx] : 1.0; };
   constexpr int U = M > 8 ? 2 : kOuterWin;  // 16 destinations: 2 windows keep 2 waves per SIMD
   const int lane = threadIdx.x & 63;
   const size_t gw = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
@@ -230,14 +258,15 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int j = 0; j < M; ++j) acc[u][j] = (j < a.m && ok[u] && !SET) ? ld2nt(a.y[j] + 2 * (p0 + 64 * u)) : z2;
+      for (int j = 0; j < M; ++j)
+        acc[u][j] = (j < a.m && ok[u] && !SET) ? sc2<SC>(ld2nt(a.y[j] + 2 * (p0 + 64 * u)), scale(a.k + j)) : z2;
     int i = 0;
     for (; i + 4 <= a.k; i += 4) {
       double2 xv[4][U];
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int u = 0; u < U; ++u) xv[b][u] = ok[u] ? ld2nt(a.x[i + b] + 2 * (p0 + 64 * u)) : z2;
+        for (int u = 0; u < U; ++u) xv[b][u] = ok[u] ? sc2<SC>(ld2nt(a.x[i + b] + 2 * (p0 + 64 * u)), scale(i + b)) : z2;
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -255,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
     for (; i < a.k; ++i) {
       double2 xv[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) xv[u] = ok[u] ? ld2nt(a.x[i] + 2 * (p0 + 64 * u)) : z2;
+      for (int u = 0; u < U; ++u) xv[u] = ok[u] ? sc2<SC>(ld2nt(a.x[i] + 2 * (p0 + 64 * u)), scale(i)) : z2;
 #pragma unroll
       for (int j = 0; j < M; ++j) {
         if (j < a.m) {
@@ -278,8 +307,8 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
   if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x < a.m) {
     const size_t e = a.n - 1;
     const int j = threadIdx.x;
-    double v = SET ? 0.0 : a.y[j][e];
-    for (int i = 0; i < a.k; ++i) v = fma(alpha(i * a.m + j), a.x[i][e], v);
+    double v = SET ? 0.0 : sc1<SC>(a.y[j][e], scale(a.k + j));
+    for (int i = 0; i < a.k; ++i) v = fma(alpha(i * a.m + j), sc1<SC>(a.x[i][e], scale(i)), v);
     a.y[j][e] = v;
   }
 }
@@ -545,73 +574,94 @@ unsigned inner_grid(const ssp_ctx* ctx, size_t n) {
   return unsigned(std::max<size_t>(1, std::min(blocks, cap)));
 }
 
-template <int MG, int NG>
+template <int MG, int NG, bool SC>
 void launch_inner_t(ssp_ctx* ctx, unsigned grid, const InnerArgs& a) {
-  hipLaunchKernelGGL((k_gemm_inner<MG, NG>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  hipLaunchKernelGGL((k_gemm_inner<MG, NG, false, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
 }
 
 // Smallest instantiated NG >= need (need <= ng_max(MG)).
-template <int MG>
+template <int MG, bool SC>
 int launch_inner_mg(ssp_ctx* ctx, unsigned grid, const InnerArgs& a, int need) {
-  if (need <= 1) launch_inner_t<MG, 1>(ctx, grid, a);
-  else if (need <= 2) launch_inner_t<MG, 2>(ctx, grid, a);
-  else if (need <= 3) launch_inner_t<MG, 3>(ctx, grid, a);
-  else if (need <= 4) launch_inner_t<MG, 4>(ctx, grid, a);
-  else if (need <= 6) launch_inner_t<MG, 6>(ctx, grid, a);
+  if (need <= 1) launch_inner_t<MG, 1, SC>(ctx, grid, a);
+  else if (need <= 2) launch_inner_t<MG, 2, SC>(ctx, grid, a);
+  else if (need <= 3) launch_inner_t<MG, 3, SC>(ctx, grid, a);
+  else if (need <= 4) launch_inner_t<MG, 4, SC>(ctx, grid, a);
+  else if (need <= 6) launch_inner_t<MG, 6, SC>(ctx, grid, a);
   else if constexpr (ng_max(MG) >= 8) {
-    if (need <= 8) launch_inner_t<MG, 8>(ctx, grid, a);
+    if (need <= 8) launch_inner_t<MG, 8, SC>(ctx, grid, a);
     else if constexpr (ng_max(MG) >= 12) {
-      if (need <= 12) launch_inner_t<MG, 12>(ctx, grid, a);
-      else if constexpr (ng_max(MG) >= 16) launch_inner_t<MG, 16>(ctx, grid, a);
+      if (need <= 12) launch_inner_t<MG, 12, SC>(ctx, grid, a);
+      else if constexpr (ng_max(MG) >= 16) launch_inner_t<MG, 16, SC>(ctx, grid, a);
     }
   }
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
 
-int launch_inner_sym(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
+template <bool SC>
+int launch_inner_sym_t(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
   switch ((a.m + 3) / 4) {
-    case 1: hipLaunchKernelGGL((k_gemm_inner<1, 1, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
-    case 2: hipLaunchKernelGGL((k_gemm_inner<2, 2, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
-    case 3: hipLaunchKernelGGL((k_gemm_inner<3, 3, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
-    default: hipLaunchKernelGGL((k_gemm_inner<4, 4, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    case 1: hipLaunchKernelGGL((k_gemm_inner<1, 1, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    case 2: hipLaunchKernelGGL((k_gemm_inner<2, 2, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    case 3: hipLaunchKernelGGL((k_gemm_inner<3, 3, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    default: hipLaunchKernelGGL((k_gemm_inner<4, 4, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
   }
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
 
-int launch_inner(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
+int launch_inner_sym(ssp_ctx* ctx, const InnerArgs& a, unsigned grid, bool sc) {
+  return sc ? launch_inner_sym_t<true>(ctx, a, grid) : launch_inner_sym_t<false>(ctx, a, grid);
+}
+
+template <bool SC>
+int launch_inner_sc(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
   const int mg = (a.m + 3) / 4, need = (a.k + 3) / 4;
   switch (mg) {
-    case 1: return launch_inner_mg<1>(ctx, grid, a, need);
-    case 2: return launch_inner_mg<2>(ctx, grid, a, need);
-    case 3: return launch_inner_mg<3>(ctx, grid, a, need);
-    default: return launch_inner_mg<4>(ctx, grid, a, need);
+    case 1: return launch_inner_mg<1, SC>(ctx, grid, a, need);
+    case 2: return launch_inner_mg<2, SC>(ctx, grid, a, need);
+    case 3: return launch_inner_mg<3, SC>(ctx, grid, a, need);
+    default: return launch_inner_mg<4, SC>(ctx, grid, a, need);
   }
 }
 
-template <bool DEV, bool SET>
+int launch_inner(ssp_ctx* ctx, const InnerArgs& a, unsigned grid, bool sc) {
+  return sc ? launch_inner_sc<true>(ctx, a, grid) : launch_inner_sc<false>(ctx, a, grid);
+}
+
+template <bool DEV, bool SET, bool SC>
 void launch_outer_t(ssp_ctx* ctx, unsigned grid, const OuterArgs& a) {
   if (a.m <= 1)
-    hipLaunchKernelGGL((k_gemm_outer<1, DEV, SET>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    hipLaunchKernelGGL((k_gemm_outer<1, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
   else if (a.m <= 2)
-    hipLaunchKernelGGL((k_gemm_outer<2, DEV, SET>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    hipLaunchKernelGGL((k_gemm_outer<2, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
   else if (a.m <= 4)
-    hipLaunchKernelGGL((k_gemm_outer<4, DEV, SET>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    hipLaunchKernelGGL((k_gemm_outer<4, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
   else if (a.m <= 8)
-    hipLaunchKernelGGL((k_gemm_outer<8, DEV, SET>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    hipLaunchKernelGGL((k_gemm_outer<8, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
   else
-    hipLaunchKernelGGL((k_gemm_outer<16, DEV, SET>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    hipLaunchKernelGGL((k_gemm_outer<16, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+}
+
+template <bool SC>
+void launch_outer_sc(ssp_ctx* ctx, unsigned grid, const OuterArgs& a) {
+  if (a.alpha_dev)
+    a.set ? launch_outer_t<true, true, SC>(ctx, grid, a) : launch_outer_t<true, false, SC>(ctx, grid, a);
+  else
+    a.set ? launch_outer_t<false, true, SC>(ctx, grid, a) : launch_outer_t<false, false, SC>(ctx, grid, a);
 }
 
 int launch_outer(ssp_ctx* ctx, const OuterArgs& a) {
   const unsigned grid = ssp::stream_grid(ctx, a.n / 2 + 1, kOuterWin);
-  if (a.alpha_dev)
-    a.set ? launch_outer_t<true, true>(ctx, grid, a) : launch_outer_t<true, false>(ctx, grid, a);
-  else
-    a.set ? launch_outer_t<false, true>(ctx, grid, a) : launch_outer_t<false, false>(ctx, grid, a);
+  a.scale_dev ? launch_outer_sc<true>(ctx, grid, a) : launch_outer_sc<false>(ctx, grid, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
+}
+
+bool any_scaled(const double* s, int n) {
+  for (int i = 0; s && i < n; ++i)
+    if (s[i] != 1.0) return true;
+  return false;
 }
 
 }  // namespace
@@ -620,6 +670,11 @@ extern "C" {
 
 int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* const* yy, int k, size_t n,
                    double* out) {
+  return ssp_gemm_inner_scaled(ctx, xx, nullptr, m, yy, nullptr, k, n, out);
+}
+
+int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, const double* const* yy,
+                          const double* ys, int k, size_t n, double* out) {
   SSP_CHECK_CTX(ctx);
   if (m < 0 || k < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner: negative dimension");
   if (m * k > 0 && !out) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner: null out");
@@ -631,6 +686,11 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
   const double* const* rows = swap ? yy : xx;
   const double* const* cols = swap ? xx : yy;
   const int R = swap ? k : m, C = swap ? m : k;
+  // deferred scales (null: all 1), following the swap
+  std::vector<double> rs(size_t(R), 1.0), cs(size_t(C), 1.0);
+  for (int i = 0; i < m; ++i) (swap ? cs : rs)[size_t(i)] = xs ? xs[i] : 1.0;
+  for (int j = 0; j < k; ++j) (swap ? rs : cs)[size_t(j)] = ys ? ys[j] : 1.0;
+  const bool sc = any_scaled(rs.data(), R) || any_scaled(cs.data(), C);
   const size_t total = size_t(R) * C;
   SSP_TRY(ssp::ensure_result(ctx, total));
   ssp::FoldTail tail{};
@@ -650,30 +710,41 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
       a.k = C;
       a.n = n;
       a.x[0] = rows[0];
-      for (int j = 0; j < C; ++j) a.y[j] = cols[j];
+      a.xs[0] = rs[0];
+      for (int j = 0; j < C; ++j) {
+        a.y[j] = cols[j];
+        a.ys[j] = cs[size_t(j)];
+      }
       const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 4);
       SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * C));
       a.partial = ctx->partial;
       SSP_TRY(ssp::fold_begin(ctx, C, &tail));
       a.tail = tail;
-      if (C == 1)
+      if (C == 1 && sc)
+        hipLaunchKernelGGL((k_gemm_inner_row<1, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      else if (C == 1)
         hipLaunchKernelGGL((k_gemm_inner_row<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      else if (sc)
+        hipLaunchKernelGGL((k_gemm_inner_row<2, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       else
         hipLaunchKernelGGL((k_gemm_inner_row<2>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
     }
     // A symmetric overlap <xx_i, xx_j> of up to 16 vectors: one panel that loads each vector once.
     bool sym = m == k && m <= ssp::kInnerRows && !(R == 1 && C <= 2);
-    for (int i = 0; sym && i < m; ++i) sym = xx[i] == yy[i];
+    for (int i = 0; sym && i < m; ++i) sym = xx[i] == yy[i] && rs[size_t(i)] == cs[size_t(i)];
     if (sym) {
       InnerArgs a{};
       a.m = a.k = m;
       a.n = n;
-      for (int i = 0; i < m; ++i) a.x[i] = a.y[i] = xx[i];
+      for (int i = 0; i < m; ++i) {
+        a.x[i] = a.y[i] = xx[i];
+        a.xs[i] = a.ys[i] = rs[size_t(i)];
+      }
       const unsigned grid = inner_grid(ctx, n);
       SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * m * m));
       a.partial = ctx->partial;
-      SSP_TRY(launch_inner_sym(ctx, a, grid));
+      SSP_TRY(launch_inner_sym(ctx, a, grid, sc));
       SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), m, m, ctx->result_dev, m, 0, 0));
     }
     for (int r0 = 0; !sym && !(R == 1 && C <= 2) && r0 < R; r0 += ssp::kInnerRows) {
@@ -684,12 +755,19 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
         a.m = mr;
         a.k = std::min(cols_per_launch, C - c0);
         a.n = n;
-        for (int i = 0; i < a.m; ++i) a.x[i] = rows[r0 + i];
-        for (int j = 0; j < a.k; ++j) a.y[j] = cols[c0 + j];
+        for (int i = 0; i < a.m; ++i) {
+          a.x[i] = rows[r0 + i];
+          a.xs[i] = rs[size_t(r0 + i)];
+        }
+        for (int j = 0; j < a.k; ++j) {
+          a.y[j] = cols[c0 + j];
+          a.ys[j] = cs[size_t(c0 + j)];
+        }
+        const bool sc_launch = any_scaled(a.xs, a.m) || any_scaled(a.ys, a.k);
         const unsigned grid = inner_grid(ctx, n);
         SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * a.m * a.k));
         a.partial = ctx->partial;
-        SSP_TRY(launch_inner(ctx, a, grid));
+        SSP_TRY(launch_inner(ctx, a, grid, sc_launch));
         SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), a.m, a.k, ctx->result_dev, C, r0, c0));
       }
     }
@@ -711,15 +789,20 @@ int ssp_gemm_inner(ssp_ctx* ctx, const double* const* xx, int m, const double* c
 }  // extern "C"
 
 namespace {
-int gemm_outer_impl(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
-                    size_t n, bool set) {
+int gemm_outer_impl(ssp_ctx* ctx, const double* alphas, const double* const* xx, const double* xs, int k,
+                    double* const* yy, const double* ys, int m, size_t n, bool set) {
   SSP_CHECK_CTX(ctx);
   if (m < 0 || k < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_outer: negative dimension");
   if (set && k == 0) {
     for (int j = 0; j < m; ++j) SSP_TRY(ssp_fill(ctx, 0.0, yy[j], n));
     return SSP_OK;
   }
-  if (m == 0 || k == 0 || n == 0) return SSP_OK;
+  if (m == 0 || n == 0) return SSP_OK;
+  if (k == 0) {  // no sources: the destinations' deferred scales still have to be stored
+    for (int j = 0; j < m; ++j)
+      if (!set && ys && ys[j] != 1.0) SSP_TRY(ssp_scal(ctx, ys[j], yy[j], n));
+    return SSP_OK;
+  }
   if (!alphas) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_outer: null alphas");
   SSP_TRY(check_ptrs(xx, k, n, "ssp_gemm_outer"));
   SSP_TRY(check_ptrs(const_cast<const double* const*>(yy), m, n, "ssp_gemm_outer"));
@@ -742,6 +825,15 @@ int gemm_outer_impl(ssp_ctx* ctx, const double* alphas, const double* const* xx,
       a.n = n;
       for (int i = 0; i < a.k; ++i) a.x[i] = xx[i0 + i];
       for (int j = 0; j < mm; ++j) a.y[j] = yy[j0 + j];
+      // deferred scales: every source's; the destinations' on their first read only (i0 == 0)
+      std::vector<double> scl(size_t(a.k + mm), 1.0);
+      for (int i = 0; i < a.k; ++i) scl[size_t(i)] = xs ? xs[i0 + i] : 1.0;
+      for (int j = 0; j < mm; ++j) scl[size_t(a.k + j)] = (ys && i0 == 0 && !set) ? ys[j0 + j] : 1.0;
+      if (any_scaled(scl.data(), int(scl.size()))) {
+        void* ps;
+        SSP_TRY(ssp::upload_small(ctx, scl.data(), scl.size() * sizeof(double), &ps));
+        a.scale_dev = static_cast<const double*>(ps);
+      }
       const bool dev = a.k * mm > ssp::kOuterAlpha;
       std::vector<double> block(dev ? size_t(a.k) * mm : 0);
       double* dst = dev ? block.data() : a.alpha;
@@ -763,12 +855,22 @@ extern "C" {
 
 int ssp_gemm_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
                    size_t n) {
-  return gemm_outer_impl(ctx, alphas, xx, k, yy, m, n, false);
+  return gemm_outer_impl(ctx, alphas, xx, nullptr, k, yy, nullptr, m, n, false);
 }
 
 int ssp_gemm_outer_set(ssp_ctx* ctx, const double* alphas, const double* const* xx, int k, double* const* yy, int m,
                        size_t n) {
-  return gemm_outer_impl(ctx, alphas, xx, k, yy, m, n, true);
+  return gemm_outer_impl(ctx, alphas, xx, nullptr, k, yy, nullptr, m, n, true);
+}
+
+int ssp_gemm_outer_scaled(ssp_ctx* ctx, const double* alphas, const double* const* xx, const double* xs, int k,
+                          double* const* yy, const double* ys, int m, size_t n) {
+  return gemm_outer_impl(ctx, alphas, xx, xs, k, yy, ys, m, n, false);
+}
+
+int ssp_gemm_outer_set_scaled(ssp_ctx* ctx, const double* alphas, const double* const* xx, const double* xs, int k,
+                              double* const* yy, int m, size_t n) {
+  return gemm_outer_impl(ctx, alphas, xx, xs, k, yy, nullptr, m, n, true);
 }
 
 int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* yy, int m, size_t n, double* out) {

@@ -32,6 +32,8 @@ __global__ void k_scatter(double* __restrict__ x, const unsigned long long* __re
 // out[i*k + j] = sum over entries e of p_j (in order) of x_i[li_e] * v_e.
 struct SparseInnerArgs {
   const double* x[64];
+  double xs[64];  // deferred scales (sc = 1)
+  int sc;
   int m;
   int k;
   const unsigned long long* ptr;  // k+1 offsets into li/v (local entries only)
@@ -45,7 +47,11 @@ __global__ void k_sparse_inner(const SparseInnerArgs a) {
   if (o >= a.m * a.k) return;
   const int i = o / a.k, j = o % a.k;
   double s = 0;
-  for (unsigned long long e = a.ptr[j]; e < a.ptr[j + 1]; ++e) s += a.x[i][a.li[e]] * a.v[e];
+  const double xs = a.xs[i];
+  for (unsigned long long e = a.ptr[j]; e < a.ptr[j + 1]; ++e) {
+    const double xv = a.sc ? a.x[i][a.li[e]] * xs : a.x[i][a.li[e]];
+    s += xv * a.v[e];
+  }
   a.out[o] = s;
 }
 
@@ -75,7 +81,14 @@ __global__ void k_sparse_outer(const SparseOuterArgs a) {
 // recomputes the reference's sequence: v = 0; v += alpha(i,j) * p_i[idx] for P vectors i and their
 // entries in order (no contraction); then v = fma(beta(s,j), x_s[idx], v) for the dense sources s in
 // order, the arithmetic of k_gemm_outer.
+// rmw (ssp_block_update): the destinations are read -- v starts from the value saved before the
+// dense pass times the destination's deferred scale instead of 0.  xs: the dense sources' deferred
+// scales (null: 1).
 struct ConstructFixArgs {
+  const double* saved;             // rmw: [u * m + j] = yy[j][uidx[u]] before the dense pass
+  const double* ys;                // rmw: m destination scales
+  const double* xs;                // k source scales or null
+  int rmw;
   const unsigned long long* uidx;  // distinct local indices touched by P
   size_t nu;
   int m;
@@ -97,13 +110,24 @@ __global__ void k_construct_fixup(const ConstructFixArgs a) {
   const int j = int(t % a.m);
   const unsigned long long g = a.uidx[u];
   double v = 0;
+  if (a.rmw) v = a.saved[t] * a.ys[j];  // t = u * m + j
   for (int i = 0; i < a.kp; ++i) {
     const double al = a.palpha[size_t(i) * a.m + j];
     for (unsigned long long e = a.ptr[i]; e < a.ptr[i + 1]; ++e)
       if (a.li[e] == g) v += al * a.v[e];
   }
-  for (int s = 0; s < a.k; ++s) v = fma(a.alpha[size_t(s) * a.m + j], a.x[s][g], v);
+  for (int s = 0; s < a.k; ++s) {
+    const double xv = a.xs ? a.x[s][g] * a.xs[s] : a.x[s][g];
+    v = fma(a.alpha[size_t(s) * a.m + j], xv, v);
+  }
   a.y[j][g] = v;
+}
+
+// saved[u * m + j] = yy[j][uidx[u]] (ssp_block_update: the P-touched values before the dense pass)
+__global__ void k_gather_touched(const unsigned long long* uidx, size_t nu, int m, double* const* y, double* saved) {
+  const size_t t = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= nu * size_t(m)) return;
+  saved[t] = y[t % m][uidx[t / m]];
 }
 
 // Local entries of one sparse vector: indices in [offset, offset+n), converted to local indices.
@@ -181,6 +205,12 @@ int ssp_sparse_axpy(ssp_ctx* ctx, double alpha, const size_t* idx, const double*
 
 int ssp_gemm_inner_sparse(ssp_ctx* ctx, const double* const* xx, int m, size_t n, size_t offset, const size_t* ptr,
                           const size_t* idx, const double* val, int k, double* out) {
+  return ssp_gemm_inner_sparse_scaled(ctx, xx, nullptr, m, n, offset, ptr, idx, val, k, out);
+}
+
+int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, size_t n,
+                                 size_t offset, const size_t* ptr, const size_t* idx, const double* val, int k,
+                                 double* out) {
   SSP_CHECK_CTX(ctx);
   if (m < 0 || k < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner_sparse: negative dimension");
   if (m == 0 || k == 0) return SSP_OK;
@@ -202,7 +232,11 @@ int ssp_gemm_inner_sparse(ssp_ctx* ctx, const double* const* xx, int m, size_t n
     SparseInnerArgs a{};
     a.m = std::min(64, m - i0);
     a.k = k;
-    for (int i = 0; i < a.m; ++i) a.x[i] = xx[i0 + i];
+    for (int i = 0; i < a.m; ++i) {
+      a.x[i] = xx[i0 + i];
+      a.xs[i] = xs ? xs[i0 + i] : 1.0;
+      if (a.xs[i] != 1.0) a.sc = 1;
+    }
     a.ptr = dptr;
     a.li = dli;
     a.v = dv;
@@ -260,26 +294,48 @@ int ssp_gemm_outer_sparse(ssp_ctx* ctx, const double* alphas, const size_t* ptr,
   return SSP_OK;
 }
 
-int ssp_construct_solution(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const size_t* idx,
-                           const double* val, int kp, const double* alphas, const double* const* xx, int k,
-                           double* const* yy, int m, size_t n, size_t offset) {
+}  // extern "C"
+
+namespace {
+// construct_solution (rmw = false: destinations written without being read) and the block update
+// (rmw = true: yy[j] = ys[j] yy[j] + P + dense): the dense pass over every element, then the fix-up
+// that recomputes the indices the P vectors touch in the reference's order (P first).
+int solution_impl(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const size_t* idx, const double* val,
+                  int kp, const double* alphas, const double* const* xx, const double* xs, int k, double* const* yy,
+                  const double* ys, int m, size_t n, size_t offset, bool rmw, const char* what) {
   SSP_CHECK_CTX(ctx);
-  if (m < 0 || k < 0 || kp < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_construct_solution: negative dimension");
+  if (m < 0 || k < 0 || kp < 0) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": negative dimension");
   if (m == 0) return SSP_OK;
-  if (kp > 0 && (!palphas || !ptr)) return ssp::set_error(SSP_ERR_ARG, "ssp_construct_solution: null P argument");
-  SSP_TRY(ssp_gemm_outer_set(ctx, alphas, xx, k, yy, m, n));
-  if (kp == 0 || n == 0) return SSP_OK;
+  if (kp > 0 && (!palphas || !ptr)) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null P argument");
   std::vector<unsigned long long> lptr{0}, li;
   std::vector<double> lv;
-  for (int i = 0; i < kp; ++i) {
-    SSP_TRY(check_entries(idx + ptr[i], val + ptr[i], ptr[i + 1] - ptr[i], "ssp_construct_solution"));
+  for (int i = 0; i < kp && n > 0; ++i) {
+    SSP_TRY(check_entries(idx + ptr[i], val + ptr[i], ptr[i + 1] - ptr[i], what));
     filter_local(idx + ptr[i], val + ptr[i], ptr[i + 1] - ptr[i], n, offset, li, lv);
     lptr.push_back(li.size());
   }
-  if (li.empty()) return SSP_OK;
   std::vector<unsigned long long> uidx(li);
   std::sort(uidx.begin(), uidx.end());
   uidx.erase(std::unique(uidx.begin(), uidx.end()), uidx.end());
+  void* p;
+  double* const* ydev = nullptr;
+  const double* saved = nullptr;
+  if (rmw && !uidx.empty()) {  // the values the dense pass is about to overwrite at the P indices
+    SSP_TRY(ssp::upload_small(ctx, yy, size_t(m) * sizeof(double*), &p));
+    ydev = static_cast<double* const*>(p);
+    SSP_TRY(ssp::upload_small(ctx, uidx.data(), uidx.size() * sizeof(unsigned long long), &p));
+    const size_t cnt = uidx.size() * size_t(m);
+    SSP_TRY(ssp::ensure_partial(ctx, cnt));
+    hipLaunchKernelGGL(k_gather_touched, dim3(unsigned((cnt + 255) / 256)), dim3(256), 0, ctx->stream,
+                       static_cast<const unsigned long long*>(p), uidx.size(), m, ydev, ctx->partial);
+    SSP_TRY_HIP(hipGetLastError());
+    saved = ctx->partial;
+  }
+  if (rmw)
+    SSP_TRY(ssp_gemm_outer_scaled(ctx, alphas, xx, xs, k, yy, ys, m, n));
+  else
+    SSP_TRY(ssp_gemm_outer_set_scaled(ctx, alphas, xx, xs, k, yy, m, n));
+  if (uidx.empty()) return SSP_OK;
   ConstructFixArgs a{};
   unsigned long long *dptr, *dli;
   double* dv;
@@ -287,7 +343,6 @@ int ssp_construct_solution(ssp_ctx* ctx, const double* palphas, const size_t* pt
   a.ptr = dptr;
   a.li = dli;
   a.v = dv;
-  void* p;
   SSP_TRY(ssp::upload_small(ctx, uidx.data(), uidx.size() * sizeof(unsigned long long), &p));
   a.uidx = static_cast<const unsigned long long*>(p);
   SSP_TRY(ssp::upload_small(ctx, palphas, size_t(kp) * m * sizeof(double), &p));
@@ -297,18 +352,57 @@ int ssp_construct_solution(ssp_ctx* ctx, const double* palphas, const size_t* pt
     a.alpha = static_cast<const double*>(p);
     SSP_TRY(ssp::upload_small(ctx, xx, size_t(k) * sizeof(double*), &p));
     a.x = static_cast<const double* const*>(p);
+    if (xs) {
+      SSP_TRY(ssp::upload_small(ctx, xs, size_t(k) * sizeof(double), &p));
+      a.xs = static_cast<const double*>(p);
+    }
   }
-  SSP_TRY(ssp::upload_small(ctx, yy, size_t(m) * sizeof(double*), &p));
-  a.y = static_cast<double* const*>(p);
+  if (!ydev) {
+    SSP_TRY(ssp::upload_small(ctx, yy, size_t(m) * sizeof(double*), &p));
+    ydev = static_cast<double* const*>(p);
+  }
+  a.y = ydev;
+  if (rmw) {
+    std::vector<double> one(size_t(m), 1.0);
+    SSP_TRY(ssp::upload_small(ctx, ys ? ys : one.data(), size_t(m) * sizeof(double), &p));
+    a.ys = static_cast<const double*>(p);
+    a.saved = saved;
+    a.rmw = 1;
+  }
   a.nu = uidx.size();
   a.m = m;
   a.kp = kp;
   a.k = k;
-  ssp::LedgerScope ls(ctx, "construct_solution_sparse", 8.0 * a.nu * m * (2.0 + k));
+  ssp::LedgerScope ls(ctx, rmw ? "block_update_sparse" : "construct_solution_sparse",
+                      8.0 * a.nu * m * (2.0 + k + (rmw ? 1.0 : 0.0)));
   const size_t threads = a.nu * size_t(m);
   hipLaunchKernelGGL(k_construct_fixup, dim3(unsigned((threads + 255) / 256)), dim3(256), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ssp_construct_solution(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const size_t* idx,
+                           const double* val, int kp, const double* alphas, const double* const* xx, int k,
+                           double* const* yy, int m, size_t n, size_t offset) {
+  return solution_impl(ctx, palphas, ptr, idx, val, kp, alphas, xx, nullptr, k, yy, nullptr, m, n, offset, false,
+                       "ssp_construct_solution");
+}
+
+int ssp_construct_solution_scaled(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const size_t* idx,
+                                  const double* val, int kp, const double* alphas, const double* const* xx,
+                                  const double* xs, int k, double* const* yy, int m, size_t n, size_t offset) {
+  return solution_impl(ctx, palphas, ptr, idx, val, kp, alphas, xx, xs, k, yy, nullptr, m, n, offset, false,
+                       "ssp_construct_solution_scaled");
+}
+
+int ssp_block_update(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const size_t* idx, const double* val,
+                     int kp, const double* alphas, const double* const* xx, const double* xs, int k, double* const* yy,
+                     const double* ys, int m, size_t n, size_t offset) {
+  return solution_impl(ctx, palphas, ptr, idx, val, kp, alphas, xx, xs, k, yy, ys, m, n, offset, true,
+                       "ssp_block_update");
 }
 
 }  // extern "C"

@@ -22,6 +22,15 @@ using ssp::kBlock;
 
 __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
 __device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
+// Deferred scal (include/subspace_hip.h): v * s is the one rounding an eager scal would have stored.
+template <bool SC>
+__device__ __forceinline__ double2 sc2(double2 v, double s) {
+  return SC ? make_double2(v.x * s, v.y * s) : v;
+}
+template <bool SC>
+__device__ __forceinline__ double sc1(double v, double s) {
+  return SC ? v * s : v;
+}
 
 // Window shape: a wave covers kWinU x 64 consecutive double2 (kWinU KiB) of each vector per visit.
 constexpr int kWinU = 8;
@@ -74,7 +83,10 @@ __global__ __launch_bounds__(kBlock) void k_scal(double* __restrict__ x, size_t 
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) x[n - 1] *= alpha;
 }
 
-__global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ x, const double* __restrict__ y, size_t n) {
+// x = y (SC: x = alpha * y, the stored form of a scaled vector, ssp_scal_copy).
+template <bool SC>
+__global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ x, const double* __restrict__ y, size_t n,
+                                                 double alpha) {
   using ssp::ld2nt;
   using ssp::st2nt;
   const size_t n2 = n >> 1;
@@ -83,38 +95,41 @@ __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ x, const d
   for (; i + 3 * stride < n2; i += 4 * stride) {
     double2 a0 = ld2nt(y + 2 * i), a1 = ld2nt(y + 2 * (i + stride)), a2 = ld2nt(y + 2 * (i + 2 * stride)),
             a3 = ld2nt(y + 2 * (i + 3 * stride));
-    st2nt(x + 2 * i, a0);
-    st2nt(x + 2 * (i + stride), a1);
-    st2nt(x + 2 * (i + 2 * stride), a2);
-    st2nt(x + 2 * (i + 3 * stride), a3);
+    st2nt(x + 2 * i, sc2<SC>(a0, alpha));
+    st2nt(x + 2 * (i + stride), sc2<SC>(a1, alpha));
+    st2nt(x + 2 * (i + 2 * stride), sc2<SC>(a2, alpha));
+    st2nt(x + 2 * (i + 3 * stride), sc2<SC>(a3, alpha));
   }
-  for (; i < n2; i += stride) st2(x + 2 * i, ld2(y + 2 * i));
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) x[n - 1] = y[n - 1];
+  for (; i < n2; i += stride) st2(x + 2 * i, sc2<SC>(ld2(y + 2 * i), alpha));
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) x[n - 1] = sc1<SC>(y[n - 1], alpha);
 }
 
 // y += alpha * x, element order as std::transform(y, x): y + alpha*x (one fma rounding).
+// SC: operands with deferred scales, y = (y*ys) + alpha*(x*xs) with the same single fma.
+template <bool SC>
 __global__ __launch_bounds__(kBlock) void k_axpy(const double* __restrict__ x, double* __restrict__ y, size_t n,
-                                                 double alpha) {
+                                                 double alpha, double xs, double ys) {
   const size_t n2 = n >> 1;
   const size_t stride = size_t(gridDim.x) * kBlock;
   size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
   for (; i + 3 * stride < n2; i += 4 * stride) {
     using ssp::ld2nt;
     using ssp::st2nt;
-    double2 x0 = ld2nt(x + 2 * i), x1 = ld2nt(x + 2 * (i + stride)), x2 = ld2nt(x + 2 * (i + 2 * stride)),
-            x3 = ld2nt(x + 2 * (i + 3 * stride));
-    double2 y0 = ld2nt(y + 2 * i), y1 = ld2nt(y + 2 * (i + stride)), y2 = ld2nt(y + 2 * (i + 2 * stride)),
-            y3 = ld2nt(y + 2 * (i + 3 * stride));
-    st2nt(y + 2 * i, make_double2(fma(alpha, x0.x, y0.x), fma(alpha, x0.y, y0.y)));
-    st2nt(y + 2 * (i + stride), make_double2(fma(alpha, x1.x, y1.x), fma(alpha, x1.y, y1.y)));
-    st2nt(y + 2 * (i + 2 * stride), make_double2(fma(alpha, x2.x, y2.x), fma(alpha, x2.y, y2.y)));
-    st2nt(y + 2 * (i + 3 * stride), make_double2(fma(alpha, x3.x, y3.x), fma(alpha, x3.y, y3.y)));
+    double2 xv[4], yv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xv[u] = sc2<SC>(ld2nt(x + 2 * (i + u * stride)), xs);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) yv[u] = sc2<SC>(ld2nt(y + 2 * (i + u * stride)), ys);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      st2nt(y + 2 * (i + u * stride), make_double2(fma(alpha, xv[u].x, yv[u].x), fma(alpha, xv[u].y, yv[u].y)));
   }
   for (; i < n2; i += stride) {
-    double2 a = ld2(x + 2 * i), b = ld2(y + 2 * i);
+    double2 a = sc2<SC>(ld2(x + 2 * i), xs), b = sc2<SC>(ld2(y + 2 * i), ys);
     st2(y + 2 * i, make_double2(fma(alpha, a.x, b.x), fma(alpha, a.y, b.y)));
   }
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) y[n - 1] = fma(alpha, x[n - 1], y[n - 1]);
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0)
+    y[n - 1] = fma(alpha, sc1<SC>(x[n - 1], xs), sc1<SC>(y[n - 1], ys));
 }
 
 __global__ __launch_bounds__(kBlock) void k_scal_win(double* __restrict__ x, size_t n, double alpha) {
@@ -136,7 +151,9 @@ __global__ __launch_bounds__(kBlock) void k_scal_win(double* __restrict__ x, siz
       [&](size_t e) { x[e] *= alpha; });
 }
 
-__global__ __launch_bounds__(kBlock) void k_copy_win(double* __restrict__ x, const double* __restrict__ y, size_t n) {
+template <bool SC>
+__global__ __launch_bounds__(kBlock) void k_copy_win(double* __restrict__ x, const double* __restrict__ y, size_t n,
+                                                     double alpha) {
   using ssp::ld2nt;
   using ssp::st2nt;
   ssp::for_windows<kWinU>(
@@ -146,14 +163,16 @@ __global__ __launch_bounds__(kBlock) void k_copy_win(double* __restrict__ x, con
 #pragma unroll
         for (int u = 0; u < kWinU; ++u) v[u] = ld2nt(y + 2 * (p0 + 64 * u));
 #pragma unroll
-        for (int u = 0; u < kWinU; ++u) st2nt(x + 2 * (p0 + 64 * u), v[u]);
+        for (int u = 0; u < kWinU; ++u) st2nt(x + 2 * (p0 + 64 * u), sc2<SC>(v[u], alpha));
       },
-      [&](size_t i) { st2(x + 2 * i, ld2(y + 2 * i)); }, [&](size_t e) { x[e] = y[e]; });
+      [&](size_t i) { st2(x + 2 * i, sc2<SC>(ld2(y + 2 * i), alpha)); },
+      [&](size_t e) { x[e] = sc1<SC>(y[e], alpha); });
 }
 
 // y += alpha * x in the window shape; the same single fma per element as k_axpy.
+template <bool SC>
 __global__ __launch_bounds__(kBlock) void k_axpy_win(const double* __restrict__ x, double* __restrict__ y, size_t n,
-                                                     double alpha) {
+                                                     double alpha, double xs, double ys) {
   using ssp::ld2nt;
   using ssp::st2nt;
   ssp::for_windows<kWinU>(
@@ -161,27 +180,27 @@ __global__ __launch_bounds__(kBlock) void k_axpy_win(const double* __restrict__ 
       [&](size_t p0) {
         double2 xv[kWinU], yv[kWinU];
 #pragma unroll
-        for (int u = 0; u < kWinU; ++u) xv[u] = ld2nt(x + 2 * (p0 + 64 * u));
+        for (int u = 0; u < kWinU; ++u) xv[u] = sc2<SC>(ld2nt(x + 2 * (p0 + 64 * u)), xs);
 #pragma unroll
-        for (int u = 0; u < kWinU; ++u) yv[u] = ld2nt(y + 2 * (p0 + 64 * u));
+        for (int u = 0; u < kWinU; ++u) yv[u] = sc2<SC>(ld2nt(y + 2 * (p0 + 64 * u)), ys);
 #pragma unroll
         for (int u = 0; u < kWinU; ++u)
           st2nt(y + 2 * (p0 + 64 * u), make_double2(fma(alpha, xv[u].x, yv[u].x), fma(alpha, xv[u].y, yv[u].y)));
       },
       [&](size_t i) {
-        const double2 a = ld2(x + 2 * i), b = ld2(y + 2 * i);
+        const double2 a = sc2<SC>(ld2(x + 2 * i), xs), b = sc2<SC>(ld2(y + 2 * i), ys);
         st2(y + 2 * i, make_double2(fma(alpha, a.x, b.x), fma(alpha, a.y, b.y)));
       },
-      [&](size_t e) { y[e] = fma(alpha, x[e], y[e]); });
+      [&](size_t e) { y[e] = fma(alpha, sc1<SC>(x[e], xs), sc1<SC>(y[e], ys)); });
 }
 
 // SAME: x == y (norms), one load stream.  Window shape (kDotU KiB per vector per wave visit),
 // 4 accumulators per lane (window position u into accumulator u % 4), then the positions past the
 // last whole window and the odd element into accumulator 0.
-template <bool SAME>
+template <bool SAME, bool SC>
 __global__ __launch_bounds__(kBlock) void k_dot_partial(const double* __restrict__ x, const double* __restrict__ y,
                                                         size_t n, double* __restrict__ partial,
-                                                        const ssp::FoldTail tail) {
+                                                        const ssp::FoldTail tail, double xs, double ys) {
   using ssp::ld2nt;
   double acc[4] = {0, 0, 0, 0};
   ssp::for_windows<kDotU>(
@@ -189,9 +208,9 @@ __global__ __launch_bounds__(kBlock) void k_dot_partial(const double* __restrict
       [&](size_t p0) {
         double2 xv[kDotU], yv[kDotU];
 #pragma unroll
-        for (int u = 0; u < kDotU; ++u) xv[u] = ld2nt(x + 2 * (p0 + 64 * u));
+        for (int u = 0; u < kDotU; ++u) xv[u] = sc2<SC>(ld2nt(x + 2 * (p0 + 64 * u)), xs);
 #pragma unroll
-        for (int u = 0; u < kDotU; ++u) yv[u] = SAME ? xv[u] : ld2nt(y + 2 * (p0 + 64 * u));
+        for (int u = 0; u < kDotU; ++u) yv[u] = SAME ? xv[u] : sc2<SC>(ld2nt(y + 2 * (p0 + 64 * u)), ys);
 #pragma unroll
         for (int u = 0; u < kDotU; ++u) {
           acc[u & 3] = fma(xv[u].x, yv[u].x, acc[u & 3]);
@@ -199,11 +218,15 @@ __global__ __launch_bounds__(kBlock) void k_dot_partial(const double* __restrict
         }
       },
       [&](size_t i) {
-        const double2 a = ld2(x + 2 * i), b = ld2(y + 2 * i);
+        const double2 a = sc2<SC>(ld2(x + 2 * i), xs);
+        const double2 b = SAME ? a : sc2<SC>(ld2(y + 2 * i), ys);
         acc[0] = fma(a.x, b.x, acc[0]);
         acc[0] = fma(a.y, b.y, acc[0]);
       },
-      [&](size_t e) { acc[0] = fma(x[e], y[e], acc[0]); });
+      [&](size_t e) {
+        const double a = sc1<SC>(x[e], xs);
+        acc[0] = fma(a, SAME ? a : sc1<SC>(y[e], ys), acc[0]);
+      });
   const double s0 = acc[0], s1 = acc[1], s2 = acc[2], s3 = acc[3];
   double s = block_sum((s0 + s1) + (s2 + s3));
   if (threadIdx.x == 0) ssp::store_partial(partial + blockIdx.x, s);
@@ -313,40 +336,56 @@ int ssp_scal(ssp_ctx* ctx, double alpha, double* x, size_t n) {
   return SSP_OK;
 }
 
-int ssp_copy(ssp_ctx* ctx, double* x, const double* y, size_t n) {
+}  // extern "C"
+
+namespace {
+int copy_impl(ssp_ctx* ctx, double alpha, double* x, const double* y, size_t n, bool scaled, const char* what) {
   SSP_CHECK_CTX(ctx);
-  SSP_TRY(check_vec(x, n, "ssp_copy"));
-  SSP_TRY(check_vec(y, n, "ssp_copy"));
-  if (n == 0 || x == y) return SSP_OK;
-  ssp::LedgerScope ls(ctx, "copy", 16.0 * n);
-  if (n >= kWinMin)
-    hipLaunchKernelGGL(k_copy_win, dim3(ssp::win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, y, n);
-  else
-    hipLaunchKernelGGL(k_copy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, y, n);
+  SSP_TRY(check_vec(x, n, what));
+  SSP_TRY(check_vec(y, n, what));
+  if (n == 0 || (x == y && !scaled)) return SSP_OK;
+  if (x == y) return ssp_scal(ctx, alpha, x, n);
+  ssp::LedgerScope ls(ctx, scaled ? "scal_copy" : "copy", 16.0 * n);
+  if (n >= kWinMin) {
+    const dim3 g(ssp::win_grid(ctx, n, kWinU, 16));
+    if (scaled) hipLaunchKernelGGL(k_copy_win<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+    else hipLaunchKernelGGL(k_copy_win<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+  } else {
+    const dim3 g(ssp::stream_grid(ctx, n / 2 + 1, 4, 64));
+    if (scaled) hipLaunchKernelGGL(k_copy<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+    else hipLaunchKernelGGL(k_copy<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+  }
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
 
-int ssp_axpy(ssp_ctx* ctx, double alpha, const double* x, double* y, size_t n) {
+int axpy_impl(ssp_ctx* ctx, double alpha, const double* x, double xs, double* y, double ys, size_t n,
+              const char* what) {
   SSP_CHECK_CTX(ctx);
-  SSP_TRY(check_vec(x, n, "ssp_axpy"));
-  SSP_TRY(check_vec(y, n, "ssp_axpy"));
+  SSP_TRY(check_vec(x, n, what));
+  SSP_TRY(check_vec(y, n, what));
   if (n == 0) return SSP_OK;
+  const bool sc = xs != 1.0 || ys != 1.0;
   ssp::LedgerScope ls(ctx, "axpy", 24.0 * n);
-  if (n >= kWinMin)
-    hipLaunchKernelGGL(k_axpy_win, dim3(ssp::win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
-  else
-    hipLaunchKernelGGL(k_axpy, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, y, n,
-                       alpha);
+  if (n >= kWinMin) {
+    const dim3 g(ssp::win_grid(ctx, n, kWinU, 16));
+    if (sc) hipLaunchKernelGGL(k_axpy_win<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
+    else hipLaunchKernelGGL(k_axpy_win<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
+  } else {
+    const dim3 g(ssp::stream_grid(ctx, n / 2 + 1, 4, 64));
+    if (sc) hipLaunchKernelGGL(k_axpy<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
+    else hipLaunchKernelGGL(k_axpy<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
+  }
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
 
-int ssp_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, double* out) {
+int dot_impl(ssp_ctx* ctx, const double* x, double xs, const double* y, double ys, size_t n, double* out,
+             const char* what) {
   SSP_CHECK_CTX(ctx);
-  if (!out) return ssp::set_error(SSP_ERR_ARG, "ssp_dot: null out");
-  SSP_TRY(check_vec(x, n, "ssp_dot"));
-  SSP_TRY(check_vec(y, n, "ssp_dot"));
+  if (!out) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null out");
+  SSP_TRY(check_vec(x, n, what));
+  SSP_TRY(check_vec(y, n, what));
   if (n == 0) {
     SSP_TRY(ssp::ensure_result(ctx, 1));
     SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, sizeof(double), ctx->stream));
@@ -358,14 +397,42 @@ int ssp_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, double* ou
   ssp::FoldTail tail{};
   SSP_TRY(ssp::fold_begin(ctx, 1, &tail));
   {
-    ssp::LedgerScope ls(ctx, "dot", (x == y ? 8.0 : 16.0) * n);
-    if (x == y)
-      hipLaunchKernelGGL(k_dot_partial<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, x, y, n, ctx->partial, tail);
-    else
-      hipLaunchKernelGGL(k_dot_partial<false>, dim3(grid), dim3(kBlock), 0, ctx->stream, x, y, n, ctx->partial, tail);
+    const bool same = x == y && xs == ys, sc = xs != 1.0 || ys != 1.0;
+    ssp::LedgerScope ls(ctx, "dot", (same ? 8.0 : 16.0) * n);
+    const dim3 g(grid);
+    double* part = ctx->partial;
+    if (same && sc) hipLaunchKernelGGL((k_dot_partial<true, true>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
+    else if (same) hipLaunchKernelGGL((k_dot_partial<true, false>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
+    else if (sc) hipLaunchKernelGGL((k_dot_partial<false, true>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
+    else hipLaunchKernelGGL((k_dot_partial<false, false>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
     SSP_TRY_HIP(hipGetLastError());
   }
   return ssp::fold_finish(ctx, tail, out);
+}
+}  // namespace
+
+extern "C" {
+
+int ssp_copy(ssp_ctx* ctx, double* x, const double* y, size_t n) { return copy_impl(ctx, 1.0, x, y, n, false, "ssp_copy"); }
+
+int ssp_scal_copy(ssp_ctx* ctx, double alpha, double* x, const double* y, size_t n) {
+  return copy_impl(ctx, alpha, x, y, n, true, "ssp_scal_copy");
+}
+
+int ssp_axpy(ssp_ctx* ctx, double alpha, const double* x, double* y, size_t n) {
+  return axpy_impl(ctx, alpha, x, 1.0, y, 1.0, n, "ssp_axpy");
+}
+
+int ssp_axpy_scaled(ssp_ctx* ctx, double alpha, const double* x, double xs, double* y, double ys, size_t n) {
+  return axpy_impl(ctx, alpha, x, xs, y, ys, n, "ssp_axpy_scaled");
+}
+
+int ssp_dot(ssp_ctx* ctx, const double* x, const double* y, size_t n, double* out) {
+  return dot_impl(ctx, x, 1.0, y, 1.0, n, out, "ssp_dot");
+}
+
+int ssp_dot_scaled(ssp_ctx* ctx, const double* x, double xs, const double* y, double ys, size_t n, double* out) {
+  return dot_impl(ctx, x, xs, y, ys, n, out, "ssp_dot_scaled");
 }
 
 int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n) {

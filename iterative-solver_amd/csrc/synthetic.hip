@@ -61,6 +61,7 @@ __device__ __forceinline__ double synth_d(int kind, unsigned long long g) {
 
 struct SynthArgs {
   const double* x[kMaxVec];
+  double xs[kMaxVec];  // deferred scales of the parameters (1: none); x * xs is the eager scal's value
   double* y[kMaxVec];
   unsigned long long key[kMaxRank];
   const unsigned short* mask;  // [n] sign masks of this shard
@@ -115,7 +116,9 @@ __global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a) {
 #pragma unroll
       for (int v = 0; v < G; ++v) {
         if (v0 + v < a.nvec) {
-          const double2 xv = ld2nt(a.x[v0 + v] + 2 * i);
+          double2 xv = ld2nt(a.x[v0 + v] + 2 * i);
+          xv.x *= a.xs[v0 + v];
+          xv.y *= a.xs[v0 + v];
 #pragma unroll
           for (int l = 0; l < R; ++l) s[v][l] += flip(mm, l, xv.x) + flip(mm >> 16, l, xv.y);
         }
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a) {
       for (int v = 0; v < G; ++v)
         if (v0 + v < a.nvec)
 #pragma unroll
-          for (int l = 0; l < R; ++l) s[v][l] += flip(mm, l, a.x[v0 + v][a.n - 1]);
+          for (int l = 0; l < R; ++l) s[v][l] += flip(mm, l, a.x[v0 + v][a.n - 1] * a.xs[v0 + v]);
     }
 #pragma unroll
     for (int v = 0; v < G; ++v) {
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
         out = make_double2(fma(a.rho, s0, y.x), fma(a.rho, s1, y.y));
       } else {
         const double2 x = ld2nt(a.x[v] + 2 * i);
-        out = make_double2(fma(d0, x.x, a.rho * s0), fma(d1, x.y, a.rho * s1));
+        out = make_double2(fma(d0, x.x * a.xs[v], a.rho * s0), fma(d1, x.y * a.xs[v], a.rho * s1));
       }
       ssp::st2nt(a.y[v] + 2 * i, out);
     }
@@ -179,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
     const double d = synth_d(a.diag_kind, a.offset + e);
     for (int v = 0; v < a.nvec; ++v) {
       const double s = lowrank<R>(mm, a.coeff + v * R);
-      a.y[v][e] = ADD ? fma(a.rho, s, a.y[v][e]) : fma(d, a.x[v][e], a.rho * s);
+      a.y[v][e] = ADD ? fma(a.rho, s, a.y[v][e]) : fma(d, a.x[v][e] * a.xs[v], a.rho * s);
     }
   }
 }
@@ -308,6 +311,11 @@ extern "C" {
 
 int sspx_synth_action(ssp_ctx* ctx, const sspx_synth* spec, const double* const* xx, double* const* yy, int nvec,
                       size_t n, size_t offset) {
+  return sspx_synth_action_scaled(ctx, spec, xx, nullptr, yy, nvec, n, offset);
+}
+
+int sspx_synth_action_scaled(ssp_ctx* ctx, const sspx_synth* spec, const double* const* xx, const double* xs,
+                             double* const* yy, int nvec, size_t n, size_t offset) {
   SSP_CHECK_CTX(ctx);
   if (!spec) return ssp::set_error(SSP_ERR_ARG, "sspx_synth_action: null spec");
   const int rank = spec->rank;
@@ -332,6 +340,7 @@ int sspx_synth_action(ssp_ctx* ctx, const sspx_synth* spec, const double* const*
     a.rho = spec->rho;
     for (int v = 0; v < a.nvec; ++v) {
       a.x[v] = xx[v0 + v];
+      a.xs[v] = xs ? xs[v0 + v] : 1.0;
       a.y[v] = yy[v0 + v];
     }
     for (int l = 0; l < rank; ++l) a.key[l] = stream_key(seed, 1000 + l);

@@ -59,11 +59,18 @@ class SyntheticProblem : public Problem<Vec, SparseP> {
   }
   void action(const CVecRef<Vec>& params, const VecRef<Vec>& actions) const override {
     if (params.empty()) return;
-    auto x = cptrs(params);
+    // the parameters' deferred normalisation scal (hbm_vec.h) is applied as they are read
+    std::vector<const double*> x;
+    std::vector<double> xs;
+    for (auto& p : params) {
+      x.push_back(p.get().data_deferred());
+      xs.push_back(p.get().scale());
+    }
     auto y = ptrs(actions);
     const auto& v0 = params.front().get();
-    check(sspx_synth_action(ctx(), &m_c, x.data(), y.data(), int(params.size()), v0.local_size(), v0.offset()),
-          "sspx_synth_action");
+    check(sspx_synth_action_scaled(ctx(), &m_c, x.data(), xs.data(), y.data(), int(params.size()), v0.local_size(),
+                                   v0.offset()),
+          "sspx_synth_action_scaled");
   }
   // r = H (x - 1); value = 0 (unused by DIIS)
   double residual(const Vec& x, Vec& r) const override {

@@ -342,6 +342,15 @@ bool fused_construct_solution(HP&, const Matrix<double>&, const RefP&, const Mat
   return false;
 }
 
+// Hook for the block Gram-Schmidt update (rspace.h block_gram_schmidt): yy[j] += P and Q/D
+// combinations in that order, as one pass over the destinations; returns false when the handler has
+// no such form (the caller then issues the two gemm_outer).  `hp` is the R x P handler.  Found by
+// argument-dependent lookup.
+template <class HP, class RefP, class RefQ, class RefR>
+bool fused_block_update(HP&, const Matrix<double>&, const RefP&, const Matrix<double>&, const RefQ&, const RefR&) {
+  return false;
+}
+
 // Hook for new Q vectors that are linear combinations of existing ones (construct_dspace,
 // reference propose_rspace.h:380-394: a copy of a prototype, fill(0), then the axpy loops):
 // out[i] = sum_j coeff(i, j) src[j], sources applied in order j = 0..; returns false when the

@@ -60,6 +60,26 @@ std::vector<double*> rw_ptrs(const Refs& v) {
   for (auto& x : v) p.push_back(x.get().data_rw());
   return p;
 }
+// Operands of the *_scaled entry points (deferred scal, hbm_vec.h): the stored blocks and their
+// pending scales; read-modify-write destinations hand their scale to the kernel.
+template <class Refs>
+std::vector<const double*> deferred_ptrs(const Refs& v, std::vector<double>& scales) {
+  std::vector<const double*> p;
+  p.reserve(v.size());
+  scales.clear();
+  for (auto& x : v) {
+    p.push_back(x.get().data_deferred());
+    scales.push_back(x.get().scale());
+  }
+  return p;
+}
+template <class Refs>
+std::vector<double*> rw_deferred_ptrs(const Refs& v, std::vector<double>& scales) {
+  std::vector<double*> p(v.size());
+  scales.assign(v.size(), 1.0);
+  for (size_t i = 0; i < v.size(); ++i) p[i] = v[i].get().data_rw_deferred(&scales[i]);
+  return p;
+}
 template <class Refs>
 std::vector<double*> wo_ptrs(const Refs& v) {
   std::vector<double*> p;
@@ -110,23 +130,29 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
     same(x, y, "copy");
     x.assign_shared(y);
   }
+  // Deferred (hbm_vec.h): applied by the next kernel that reads x.
   void scal(double alpha, Vec& x) override {
     m_counter->scal++;
-    check(ssp_scal(x.ctx(), alpha, x.data_rw(), x.local_size()), "ssp_scal");
+    x.scale_by(alpha);
   }
   void fill(double alpha, Vec& x) override { check(ssp_fill(x.ctx(), alpha, x.data_wo(), x.local_size()), "ssp_fill"); }
   void axpy(double alpha, const Vec& x, Vec& y) override {
     m_counter->axpy++;
     if (x.size() < y.size()) error("ArrayHandlerHbm::axpy() incompatible x and y arrays, x.size() < y.size()");
     same(x, y, "axpy");
-    check(ssp_axpy(y.ctx(), alpha, x.data(), y.data_rw(), y.local_size()), "ssp_axpy");
+    const double* xp = x.data_deferred();
+    const double xs = x.scale();
+    double ys = 1.0;
+    double* yp = y.data_rw_deferred(&ys);
+    check(ssp_axpy_scaled(y.ctx(), alpha, xp, xs, yp, ys, y.local_size()), "ssp_axpy_scaled");
   }
   double dot(const Vec& x, const Vec& y) override {
     m_counter->dot++;
     if (x.size() > y.size()) error("ArrayHandlerHbm::dot() incompatible x and y arrays, x.size() > y.size()");
     same(x, y, "dot");
     double out = 0;
-    check(ssp_dot(x.ctx(), x.data(), y.data(), x.local_size(), &out), "ssp_dot");
+    check(ssp_dot_scaled(x.ctx(), x.data_deferred(), x.scale(), y.data_deferred(), y.scale(), x.local_size(), &out),
+          "ssp_dot_scaled");
     return out;
   }
   void gemm_outer(const itsolv::subspace::Matrix<double> alphas, const itsolv::CVecRef<Vec>& xx,
@@ -142,25 +168,27 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
       throw std::out_of_range("gemm_outer: dimensions of yy and alphas are different: " + std::to_string(alphas.cols()) +
                               " " + std::to_string(yy.size()));
     for (auto& x : xx) same(x.get(), yy.front().get(), "gemm_outer");
-    auto xp = detail::cptrs(xx);
+    std::vector<double> xs, ys;
+    auto xp = detail::deferred_ptrs(xx, xs);
     // only the alphas.cols() destinations the kernel updates
-    auto yp = detail::rw_ptrs(itsolv::VecRef<Vec>(yy.begin(), yy.begin() + long(alphas.cols())));
+    auto yp = detail::rw_deferred_ptrs(itsolv::VecRef<Vec>(yy.begin(), yy.begin() + long(alphas.cols())), ys);
     const auto& y0 = yy.front().get();
-    check(ssp_gemm_outer(y0.ctx(), alphas.data().data(), xp.data(), int(xx.size()), yp.data(), int(alphas.cols()),
-                         y0.local_size()),
-          "ssp_gemm_outer");
+    check(ssp_gemm_outer_scaled(y0.ctx(), alphas.data().data(), xp.data(), xs.data(), int(xx.size()), yp.data(),
+                                ys.data(), int(alphas.cols()), y0.local_size()),
+          "ssp_gemm_outer_scaled");
   }
   itsolv::subspace::Matrix<double> gemm_inner(const itsolv::CVecRef<Vec>& xx, const itsolv::CVecRef<Vec>& yy) override {
     m_counter->gemm_inner++;
     std::vector<double> buf(xx.size() * yy.size(), 0.0);
     if (!xx.empty() && !yy.empty()) {
       for (auto& y : yy) same(xx.front().get(), y.get(), "gemm_inner");
-      auto xp = detail::cptrs(xx);
-      auto yp = detail::cptrs(yy);
+      std::vector<double> xs, ys;
+      auto xp = detail::deferred_ptrs(xx, xs);
+      auto yp = detail::deferred_ptrs(yy, ys);
       const auto& x0 = xx.front().get();
-      check(ssp_gemm_inner(x0.ctx(), xp.data(), int(xx.size()), yp.data(), int(yy.size()), x0.local_size(),
-                           buf.data()),
-            "ssp_gemm_inner");
+      check(ssp_gemm_inner_scaled(x0.ctx(), xp.data(), xs.data(), int(xx.size()), yp.data(), ys.data(), int(yy.size()),
+                                  x0.local_size(), buf.data()),
+            "ssp_gemm_inner_scaled");
     }
     return itsolv::subspace::Matrix<double>(std::move(buf), {xx.size(), yy.size()});
   }
@@ -219,11 +247,13 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
     for (size_t y = 1; y < ny; ++y) same(yy[y].get(), yy[0].get(), "fused_axpy");
     for (size_t x = 0; x < nx; ++x) same(xx[x].get(), yy[0].get(), "fused_axpy");
     m_counter->gemm_outer++;
-    auto xp = detail::cptrs(xx);
-    auto yp = detail::rw_ptrs(yy);
+    std::vector<double> xs, ys;
+    auto xp = detail::deferred_ptrs(xx, xs);
+    auto yp = detail::rw_deferred_ptrs(yy, ys);
     const auto& y0 = yy.front().get();
-    check(ssp_gemm_outer(y0.ctx(), coef.data(), xp.data(), int(nx), yp.data(), int(ny), y0.local_size()),
-          "ssp_gemm_outer");
+    check(ssp_gemm_outer_scaled(y0.ctx(), coef.data(), xp.data(), xs.data(), int(nx), yp.data(), ys.data(), int(ny),
+                                y0.local_size()),
+          "ssp_gemm_outer_scaled");
   }
 };
 
@@ -275,7 +305,11 @@ class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
         val.push_back(v);
       }
     double out = 0;
-    check(ssp_sparse_dot(x.ctx(), x.data(), x.local_size(), x.offset(), idx.data(), val.data(), idx.size(), &out),
+    const size_t ptr[2] = {0, idx.size()};
+    const double* xp = x.data_deferred();
+    const double xs = x.scale();
+    check(ssp_gemm_inner_sparse_scaled(x.ctx(), &xp, &xs, 1, x.local_size(), x.offset(), ptr, idx.data(), val.data(),
+                                       1, &out),
           "ssp_sparse_dot");
     return out;
   }
@@ -302,11 +336,12 @@ class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
       std::vector<size_t> ptr, idx;
       std::vector<double> val;
       detail::pack(yy, ptr, idx, val);
-      auto xp = detail::cptrs(xx);
+      std::vector<double> xs;
+      auto xp = detail::deferred_ptrs(xx, xs);
       const auto& x0 = xx.front().get();
-      check(ssp_gemm_inner_sparse(x0.ctx(), xp.data(), int(xx.size()), x0.local_size(), x0.offset(), ptr.data(),
-                                  idx.data(), val.data(), int(yy.size()), buf.data()),
-            "ssp_gemm_inner_sparse");
+      check(ssp_gemm_inner_sparse_scaled(x0.ctx(), xp.data(), xs.data(), int(xx.size()), x0.local_size(), x0.offset(),
+                                         ptr.data(), idx.data(), val.data(), int(yy.size()), buf.data()),
+            "ssp_gemm_inner_sparse_scaled");
     }
     return itsolv::subspace::Matrix<double>(std::move(buf), {xx.size(), yy.size()});
   }

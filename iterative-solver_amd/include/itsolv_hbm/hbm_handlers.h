@@ -62,15 +62,41 @@ inline bool fused_construct_solution(array::ArrayHandler<Vec, SparseP>&, const i
   std::vector<size_t> ptr{0}, idx;
   std::vector<double> val;
   if (!pp.empty()) detail::pack(pp, ptr, idx, val);
-  auto xp = detail::cptrs(qd);
+  std::vector<double> xs;
+  auto xp = detail::deferred_ptrs(qd, xs);
   // write-only destinations: a solution vector still sharing storage with a Q copy is given a fresh
   // block instead of being copied first
   auto yp = detail::wo_ptrs(itsolv::VecRef<Vec>(yy.begin(), yy.begin() + long(cqd.cols())));
   const auto& y0 = yy.front().get();
-  check(ssp_construct_solution(y0.ctx(), cp.data().data(), ptr.data(), idx.data(), val.data(), int(pp.size()),
-                               cqd.data().data(), xp.data(), int(qd.size()), yp.data(), int(cqd.cols()),
-                               y0.local_size(), y0.offset()),
-        "ssp_construct_solution");
+  check(ssp_construct_solution_scaled(y0.ctx(), cp.data().data(), ptr.data(), idx.data(), val.data(), int(pp.size()),
+                                      cqd.data().data(), xp.data(), xs.data(), int(qd.size()), yp.data(),
+                                      int(cqd.cols()), y0.local_size(), y0.offset()),
+        "ssp_construct_solution_scaled");
+  return true;
+}
+
+// The block Gram-Schmidt update (array::fused_block_update hook, rspace.h block_gram_schmidt):
+// yy[j] += sum_i cp(i, j) p_i + sum_s cqd(s, j) qd_s as one ssp_block_update -- bit-identical to
+// gemm_outer(P) then gemm_outer(Q, D), and the destinations' deferred normalisation scal
+// (rspace.h normalise) is applied as they are read.
+inline bool fused_block_update(array::ArrayHandler<Vec, SparseP>&, const itsolv::subspace::Matrix<double>& cp,
+                               const itsolv::CVecRef<SparseP>& pp, const itsolv::subspace::Matrix<double>& cqd,
+                               const itsolv::CVecRef<Vec>& qd, const itsolv::VecRef<Vec>& yy) {
+  const size_t m = yy.size();
+  if (m == 0 || cqd.rows() != qd.size() || cp.rows() != pp.size() || (!qd.empty() && cqd.cols() != m) ||
+      (!pp.empty() && cp.cols() != m))
+    return false;
+  std::vector<size_t> ptr{0}, idx;
+  std::vector<double> val;
+  if (!pp.empty()) detail::pack(pp, ptr, idx, val);
+  std::vector<double> xs, ys;
+  auto xp = detail::deferred_ptrs(qd, xs);
+  auto yp = detail::rw_deferred_ptrs(yy, ys);
+  const auto& y0 = yy.front().get();
+  check(ssp_block_update(y0.ctx(), cp.data().data(), ptr.data(), idx.data(), val.data(), int(pp.size()),
+                         cqd.data().data(), xp.data(), xs.data(), int(qd.size()), yp.data(), ys.data(), int(m),
+                         y0.local_size(), y0.offset()),
+        "ssp_block_update");
   return true;
 }
 
@@ -83,7 +109,11 @@ inline bool fused_new_combinations(array::ArrayHandler<Vec, Vec>&, const itsolv:
   const size_t nout = coeff.rows(), k = src.size();
   if (k == 0 || coeff.cols() != k) return false;
   std::vector<const double*> xp;
-  for (auto* v : src) xp.push_back(v->data());
+  std::vector<double> xs;
+  for (auto* v : src) {
+    xp.push_back(v->data_deferred());
+    xs.push_back(v->scale());
+  }
   std::vector<double> alphas(k * nout);  // alphas[i * m + j]: source i, destination j
   for (size_t j = 0; j < nout; ++j)
     for (size_t i = 0; i < k; ++i) alphas[i * nout + j] = coeff(j, i);
@@ -92,8 +122,9 @@ inline bool fused_new_combinations(array::ArrayHandler<Vec, Vec>&, const itsolv:
   std::vector<double*> yp;
   for (size_t j = first; j < out.size(); ++j) yp.push_back(out[j].data_wo());
   const Vec& v0 = *src.front();
-  check(ssp_gemm_outer_set(v0.ctx(), alphas.data(), xp.data(), int(k), yp.data(), int(nout), v0.local_size()),
-        "ssp_gemm_outer_set");
+  check(ssp_gemm_outer_set_scaled(v0.ctx(), alphas.data(), xp.data(), xs.data(), int(k), yp.data(), int(nout),
+                                  v0.local_size()),
+        "ssp_gemm_outer_set_scaled");
   return true;
 }
 

@@ -85,6 +85,15 @@ class Device {
 //              replaced by a fresh one, nothing is copied.
 // The shared block outlives every holder's kernels: blocks return to the context's arena, whose
 // reuse is ordered on the context's one stream.
+//
+// A scal is deferred: the vector's value is its block times a pending scale s (scale_by, the
+// handlers' scal), which the next kernel that reads the vector applies as it loads each element --
+// x_i * s is the one rounding the reference's scal loop stores (ArrayHandlerIterable.h:46-50), so the
+// kernel sees bit for bit the values an eager scal would have left -- instead of a separate pass
+// that reads and writes the vector (16 bytes per element).  Kernels that take scales read through
+// data_deferred() / data_rw_deferred() (the *_scaled entry points of include/subspace_hip.h); every
+// other access (data(), data_rw()) first stores the scaled values (materialize()), so a caller that
+// knows nothing of the scale sees the eager result.  data_wo() drops the scale with the contents.
 class Vec {
   struct Block {
     std::shared_ptr<Device> dev;
@@ -123,6 +132,7 @@ class Vec {
   void swap(Vec& o) noexcept {
     std::swap(m_dev, o.m_dev);
     std::swap(m_block, o.m_block);
+    std::swap(m_scale, o.m_scale);
     std::swap(m_size, o.m_size);
     std::swap(m_local, o.m_local);
     std::swap(m_offset, o.m_offset);
@@ -135,14 +145,53 @@ class Vec {
   size_t size() const { return m_size; }
   size_t local_size() const { return m_local; }
   size_t offset() const { return m_offset; }
-  const double* data() const { return m_block ? m_block->p : nullptr; }
+  //! Read-only operand, scale applied (stored) first.
+  const double* data() const {
+    materialize();
+    return m_block ? m_block->p : nullptr;
+  }
+  //! Read-modify-write destination, scale applied first; the block is this vector's alone.
   double* data_rw() {
+    materialize();
     detach(true);
     return m_block ? m_block->p : nullptr;
   }
+  //! Destination written in full without being read: contents and scale are dropped.
   double* data_wo() {
+    m_scale = 1.0;
     detach(false);
     return m_block ? m_block->p : nullptr;
+  }
+  //! The pending scale: the vector's value is scale() * (the block's contents).
+  double scale() const { return m_scale; }
+  //! Read-only operand of a kernel that multiplies each element by scale() as it loads it.
+  const double* data_deferred() const { return m_block ? m_block->p : nullptr; }
+  //! Read-modify-write destination of a kernel that multiplies each element it reads by *s (set to
+  //! the pending scale here) and stores the result in full: the vector's scale becomes 1.
+  double* data_rw_deferred(double* s) {
+    detach(true);
+    *s = m_scale;
+    m_scale = 1.0;
+    return m_block ? m_block->p : nullptr;
+  }
+  //! The handlers' scal: x *= a, deferred to the next kernel that reads x (see above).  A second
+  //! scal before any kernel has applied the first stores the first (two roundings, as the reference).
+  void scale_by(double a) {
+    materialize();
+    m_scale = a;
+  }
+  //! Stores the pending scale into the block (one scal pass, or a scaled copy into a fresh block
+  //! when the block is shared); a no-op when the scale is 1.
+  void materialize() const {
+    if (m_scale == 1.0 || !m_block) return;
+    if (m_block.use_count() > 1) {
+      auto fresh = std::make_shared<Block>(m_dev, m_local);
+      check_status(ssp_scal_copy(ctx(), m_scale, fresh->p, m_block->p, m_local), "ssp_scal_copy");
+      m_block = std::move(fresh);
+    } else {
+      check_status(ssp_scal(ctx(), m_scale, m_block->p, m_local), "ssp_scal");
+    }
+    m_scale = 1.0;
   }
   //! Whether another Vec holds the same storage.
   bool shares_storage() const { return m_block && m_block.use_count() > 1; }
@@ -169,8 +218,9 @@ class Vec {
   }
 
   std::shared_ptr<Device> m_dev;
-  std::shared_ptr<Block> m_block;
+  mutable std::shared_ptr<Block> m_block;  // mutable: materialize() on a const operand
   size_t m_size = 0, m_local = 0, m_offset = 0;
+  mutable double m_scale = 1.0;
 };
 
 }  // namespace molpro::linalg::hbm

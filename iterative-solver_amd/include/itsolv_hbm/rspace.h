@@ -399,11 +399,12 @@ std::vector<int> block_gram_schmidt(const VecRef<R>& rparams, const Matrix<doubl
         for (size_t j = 0; j < nR; ++j) a(i, j) = c(o + i, j);
       return a;
     };
-    if (d.nP) h.rp().gemm_outer(block(d.oP, d.nP), pp, rparams);
-    if (d.nQ + d.nD) {
-      CVecRef<Q> qd(qp.begin(), qp.end());
-      qd.insert(qd.end(), dp.begin(), dp.end());
-      h.rq().gemm_outer(block(d.oQ, d.nQ + d.nD), qd, rparams);
+    CVecRef<Q> qd(qp.begin(), qp.end());
+    qd.insert(qd.end(), dp.begin(), dp.end());
+    using array::fused_block_update;
+    if (!fused_block_update(h.rp(), block(d.oP, d.nP), pp, block(d.oQ, d.nQ + d.nD), qd, rparams)) {
+      if (d.nP) h.rp().gemm_outer(block(d.oP, d.nP), pp, rparams);
+      if (d.nQ + d.nD) h.rq().gemm_outer(block(d.oQ, d.nQ + d.nD), qd, rparams);
     }
   }
   return orthonormalise_among(rparams, norm_thresh, h.rr());

@@ -40,6 +40,10 @@ EXPORTS = [
     "ssp_construct_solution",
     "sspx_synthetic_action", "sspx_synthetic_add_lowrank", "sspx_synthetic_diagonal", "sspx_fill_random", "sspx_dense_action",
     "sspx_synth_action", "sspx_synth_add_lowrank", "sspx_synth_diagonal",
+    # deferred scal (hbm_vec.h): operands with pending scales
+    "ssp_scal_copy", "ssp_axpy_scaled", "ssp_dot_scaled", "ssp_gemm_inner_scaled", "ssp_gemm_outer_scaled",
+    "ssp_gemm_outer_set_scaled", "ssp_gemm_inner_sparse_scaled", "ssp_construct_solution_scaled", "ssp_block_update",
+    "sspx_synth_action_scaled",
 ]
 
 
@@ -131,6 +135,16 @@ def _declare(lib):
         "sspx_synth_diagonal": (I, [P, P, P, Z, Z]),
         "sspx_fill_random": (I, [P, P, Z, Z, C.c_ulonglong, C.c_ulonglong]),
         "sspx_dense_action": (I, [P, P, Z, P, P, I, Z, Z]),
+        "ssp_scal_copy": (I, [P, D, P, P, Z]),
+        "ssp_axpy_scaled": (I, [P, D, P, D, P, D, Z]),
+        "ssp_dot_scaled": (I, [P, P, D, P, D, Z, PD]),
+        "ssp_gemm_inner_scaled": (I, [P, P, PD, I, P, PD, I, Z, PD]),
+        "ssp_gemm_outer_scaled": (I, [P, PD, P, PD, I, P, PD, I, Z]),
+        "ssp_gemm_outer_set_scaled": (I, [P, PD, P, PD, I, P, I, Z]),
+        "ssp_gemm_inner_sparse_scaled": (I, [P, P, PD, I, Z, Z, PZ, PZ, PD, I, PD]),
+        "ssp_construct_solution_scaled": (I, [P, PD, PZ, PZ, PD, I, PD, P, PD, I, P, I, Z, Z]),
+        "ssp_block_update": (I, [P, PD, PZ, PZ, PD, I, PD, P, PD, I, P, PD, I, Z, Z]),
+        "sspx_synth_action_scaled": (I, [P, P, P, PD, P, I, Z, Z]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -596,6 +610,82 @@ class Context:
         n = yy[0].n if m else 0
         _check(self.lib.ssp_gemm_outer_sparse(self.handle, _dptr(alphas), _zptr(ptr), _zptr(idx), _dptr(val), k,
                                               _ptrs(yy), m, n, offset))
+
+    # -- deferred scal (include/subspace_hip.h *_scaled): each operand with a pending scale ---------
+    @staticmethod
+    def _scales(s, cnt):
+        return np.ascontiguousarray(np.ones(cnt) if s is None else s, dtype=np.float64).reshape(cnt)
+
+    def scal_copy(self, alpha: float, x: DeviceVector, y: DeviceVector):
+        _check(self.lib.ssp_scal_copy(self.handle, float(alpha), x.ptr, y.ptr, x.n))
+
+    def axpy_scaled(self, alpha: float, x: DeviceVector, xs: float, y: DeviceVector, ys: float):
+        _check(self.lib.ssp_axpy_scaled(self.handle, float(alpha), x.ptr, float(xs), y.ptr, float(ys), y.n))
+
+    def dot_scaled(self, x: DeviceVector, xs: float, y: DeviceVector, ys: float) -> float:
+        out = np.zeros(1)
+        _check(self.lib.ssp_dot_scaled(self.handle, x.ptr, float(xs), y.ptr, float(ys), x.n, _dptr(out)))
+        return float(out[0])
+
+    def gemm_inner_scaled(self, xx, xs, yy, ys) -> np.ndarray:
+        m, k = len(xx), len(yy)
+        out = np.zeros((m, k))
+        a, b = self._scales(xs, m), self._scales(ys, k)
+        n = xx[0].n if m else 0
+        _check(self.lib.ssp_gemm_inner_scaled(self.handle, _ptrs(xx), _dptr(a), m, _ptrs(yy), _dptr(b), k, n,
+                                              _dptr(out)))
+        return out
+
+    def gemm_outer_scaled(self, alphas, xx, xs, yy, ys):
+        alphas = np.ascontiguousarray(alphas, dtype=np.float64).reshape(len(xx), len(yy))
+        a, b = self._scales(xs, len(xx)), self._scales(ys, len(yy))
+        n = yy[0].n if yy else 0
+        _check(self.lib.ssp_gemm_outer_scaled(self.handle, _dptr(alphas), _ptrs(xx), _dptr(a), len(xx), _ptrs(yy),
+                                              _dptr(b), len(yy), n))
+
+    def gemm_outer_set_scaled(self, alphas, xx, xs, yy):
+        alphas = np.ascontiguousarray(alphas, dtype=np.float64).reshape(len(xx), len(yy))
+        a = self._scales(xs, len(xx))
+        n = yy[0].n if yy else 0
+        _check(self.lib.ssp_gemm_outer_set_scaled(self.handle, _dptr(alphas), _ptrs(xx), _dptr(a), len(xx),
+                                                  _ptrs(yy), len(yy), n))
+
+    def gemm_inner_sparse_scaled(self, xx, xs, ps, offset: int = 0) -> np.ndarray:
+        ptr, idx, val = self._pack_sparse(ps)
+        m, k = len(xx), len(ps)
+        out = np.zeros((m, k))
+        a = self._scales(xs, m)
+        n = xx[0].n if m else 0
+        _check(self.lib.ssp_gemm_inner_sparse_scaled(self.handle, _ptrs(xx), _dptr(a), m, n, offset, _zptr(ptr),
+                                                     _zptr(idx), _dptr(val), k, _dptr(out)))
+        return out
+
+    def construct_solution_scaled(self, palphas, ps, alphas, xx, xs, yy, offset: int = 0):
+        m = len(yy)
+        pa = np.ascontiguousarray(palphas, dtype=np.float64).reshape(len(ps), m)
+        al = np.ascontiguousarray(alphas, dtype=np.float64).reshape(len(xx), m)
+        a = self._scales(xs, len(xx))
+        ptr, idx, val = self._pack_sparse(ps)
+        n = yy[0].n if m else 0
+        _check(self.lib.ssp_construct_solution_scaled(self.handle, _dptr(pa), _zptr(ptr), _zptr(idx), _dptr(val),
+                                                      len(ps), _dptr(al), _ptrs(xx), _dptr(a), len(xx), _ptrs(yy), m,
+                                                      n, offset))
+
+    def block_update(self, palphas, ps, alphas, xx, xs, yy, ys, offset: int = 0):
+        """yy[j] = ys[j] yy[j] + sum_i palphas[i, j] p_i + sum_s alphas[s, j] xs[s] xx[s]."""
+        m = len(yy)
+        pa = np.ascontiguousarray(palphas, dtype=np.float64).reshape(len(ps), m)
+        al = np.ascontiguousarray(alphas, dtype=np.float64).reshape(len(xx), m)
+        a, b = self._scales(xs, len(xx)), self._scales(ys, m)
+        ptr, idx, val = self._pack_sparse(ps)
+        n = yy[0].n if m else 0
+        _check(self.lib.ssp_block_update(self.handle, _dptr(pa), _zptr(ptr), _zptr(idx), _dptr(val), len(ps),
+                                         _dptr(al), _ptrs(xx), _dptr(a), len(xx), _ptrs(yy), _dptr(b), m, n, offset))
+
+    def synth_action_scaled(self, xx, xs, yy, spec, offset: int = 0):
+        a = self._scales(xs, len(xx))
+        _check(self.lib.sspx_synth_action_scaled(self.handle, C.byref(spec), _ptrs(xx), _dptr(a), _ptrs(yy), len(xx),
+                                                 xx[0].n, offset))
 
     # -- synthetic problem (harness) ------------------------------------------------------------
     def synthetic_action(self, xx, yy, rho: float, rank: int, seed: int, offset: int = 0):

@@ -432,6 +432,7 @@ int ssp_select_max_dot(ssp_ctx* c, const double* x, const double* y, size_t n, s
 }
 
 int ssp_sparse_copy(ssp_ctx*, double* x, size_t n, size_t off, const size_t* idx, const double* val, size_t nnz) {
+  trace("sparse_copy", {}, {x});
   std::vector<size_t> li;
   std::vector<double> lv;
   filter(idx, val, nnz, n, off, li, lv);
@@ -441,6 +442,7 @@ int ssp_sparse_copy(ssp_ctx*, double* x, size_t n, size_t off, const size_t* idx
 }
 int ssp_sparse_axpy(ssp_ctx*, double a, const size_t* idx, const double* val, size_t nnz, double* x, size_t n,
                     size_t off) {
+  trace("sparse_axpy", {x}, {x});
   std::vector<size_t> li;
   std::vector<double> lv;
   filter(idx, val, nnz, n, off, li, lv);
@@ -449,6 +451,7 @@ int ssp_sparse_axpy(ssp_ctx*, double a, const size_t* idx, const double* val, si
 }
 int ssp_gemm_inner_sparse(ssp_ctx* c, const double* const* xx, int m, size_t n, size_t off, const size_t* ptr,
                           const size_t* idx, const double* val, int k, double* out) {
+  trace("gemm_inner_sparse", {}, {}, xx, m);
   for (int i = 0; i < m; ++i)
     for (int j = 0; j < k; ++j) {
       std::vector<size_t> li;
@@ -468,6 +471,7 @@ int ssp_sparse_dot(ssp_ctx* c, const double* x, size_t n, size_t off, const size
 }
 int ssp_gemm_outer_sparse(ssp_ctx*, const double* al, const size_t* ptr, const size_t* idx, const double* val, int k,
                           double* const* yy, int m, size_t n, size_t off) {
+  trace("gemm_outer_sparse", {}, {}, nullptr, 0, yy, m);
   for (int j = 0; j < m; ++j)
     for (int i = 0; i < k; ++i) {
       std::vector<size_t> li;
@@ -561,6 +565,112 @@ int sspx_dense_action(ssp_ctx*, const double* a, size_t ng, const double* const*
       yy[v][r] = s;
     }
   return SSP_OK;
+}
+
+// ---- deferred scal (include/subspace_hip.h): restated by definition -- each operand with a scale
+// s != 1 is first stored scaled (the eager ssp_scal), then the unscaled call runs.
+namespace {
+struct Scaled {  // read operands: scaled temporaries where s != 1
+  std::vector<std::vector<double>> tmp;
+  std::vector<const double*> p;
+  Scaled(const double* const* v, const double* s, int cnt, size_t n) {
+    tmp.reserve(size_t(cnt));
+    for (int i = 0; i < cnt; ++i) {
+      if (s && s[i] != 1.0) {
+        tmp.emplace_back(v[i], v[i] + n);
+        for (auto& e : tmp.back()) e *= s[i];
+        p.push_back(tmp.back().data());
+      } else {
+        p.push_back(v[i]);
+      }
+    }
+  }
+};
+void scale_dest(double* const* y, const double* s, int cnt, size_t n) {
+  for (int j = 0; s && j < cnt; ++j)
+    if (s[j] != 1.0)
+      for (size_t e = 0; e < n; ++e) y[j][e] *= s[j];
+}
+}  // namespace
+
+int ssp_scal_copy(ssp_ctx* c, double a, double* x, const double* y, size_t n) {
+  Led l(c, "scal_copy", 16.0 * n);
+  trace("scal_copy", {y}, {x});
+  for (size_t i = 0; i < n; ++i) x[i] = y[i] * a;
+  return SSP_OK;
+}
+int ssp_axpy_scaled(ssp_ctx* c, double a, const double* x, double xs, double* y, double ys, size_t n) {
+  Scaled sx(&x, &xs, 1, n);
+  scale_dest(&y, &ys, 1, n);
+  return ssp_axpy(c, a, sx.p[0], y, n);
+}
+int ssp_dot_scaled(ssp_ctx* c, const double* x, double xs, const double* y, double ys, size_t n, double* out) {
+  if (x == y && xs == ys) {
+    Scaled sx(&x, &xs, 1, n);
+    return ssp_dot(c, sx.p[0], sx.p[0], n, out);
+  }
+  Scaled sx(&x, &xs, 1, n), sy(&y, &ys, 1, n);
+  return ssp_dot(c, sx.p[0], sy.p[0], n, out);
+}
+int ssp_gemm_inner_scaled(ssp_ctx* c, const double* const* xx, const double* xs, int m, const double* const* yy,
+                          const double* ys, int k, size_t n, double* out) {
+  // the same vector on both sides stays one operand (the symmetric panel)
+  std::map<std::pair<const double*, double>, std::vector<double>> cache;
+  auto sc = [&](const double* const* v, const double* s, int cnt) {
+    std::vector<const double*> p;
+    for (int i = 0; i < cnt; ++i) {
+      if (!s || s[i] == 1.0) {
+        p.push_back(v[i]);
+        continue;
+      }
+      auto& t = cache[{v[i], s[i]}];
+      if (t.empty()) {
+        t.assign(v[i], v[i] + n);
+        for (auto& e : t) e *= s[i];
+      }
+      p.push_back(t.data());
+    }
+    return p;
+  };
+  auto px = sc(xx, xs, m), py = sc(yy, ys, k);
+  return ssp_gemm_inner(c, px.data(), m, py.data(), k, n, out);
+}
+int ssp_gemm_outer_scaled(ssp_ctx* c, const double* al, const double* const* xx, const double* xs, int k,
+                          double* const* yy, const double* ys, int m, size_t n) {
+  Scaled sx(xx, xs, k, n);
+  scale_dest(yy, ys, m, n);
+  return ssp_gemm_outer(c, al, sx.p.data(), k, yy, m, n);
+}
+int ssp_gemm_outer_set_scaled(ssp_ctx* c, const double* al, const double* const* xx, const double* xs, int k,
+                              double* const* yy, int m, size_t n) {
+  Scaled sx(xx, xs, k, n);
+  return ssp_gemm_outer_set(c, al, sx.p.data(), k, yy, m, n);
+}
+int ssp_gemm_inner_sparse_scaled(ssp_ctx* c, const double* const* xx, const double* xs, int m, size_t n, size_t off,
+                                 const size_t* ptr, const size_t* idx, const double* val, int k, double* out) {
+  Scaled sx(xx, xs, m, n);
+  return ssp_gemm_inner_sparse(c, sx.p.data(), m, n, off, ptr, idx, val, k, out);
+}
+int ssp_construct_solution_scaled(ssp_ctx* c, const double* palphas, const size_t* ptr, const size_t* idx,
+                                  const double* val, int kp, const double* alphas, const double* const* xx,
+                                  const double* xs, int k, double* const* yy, int m, size_t n, size_t offset) {
+  Scaled sx(xx, xs, k, n);
+  return ssp_construct_solution(c, palphas, ptr, idx, val, kp, alphas, sx.p.data(), k, yy, m, n, offset);
+}
+int ssp_block_update(ssp_ctx* c, const double* palphas, const size_t* ptr, const size_t* idx, const double* val,
+                     int kp, const double* alphas, const double* const* xx, const double* xs, int k, double* const* yy,
+                     const double* ys, int m, size_t n, size_t offset) {
+  trace("block_update", {}, {}, xx, k, yy, m);
+  Scaled sx(xx, xs, k, n);
+  scale_dest(yy, ys, m, n);
+  if (kp > 0)
+    if (int st = ssp_gemm_outer_sparse(c, palphas, ptr, idx, val, kp, yy, m, n, offset)) return st;
+  return k > 0 ? ssp_gemm_outer(c, alphas, sx.p.data(), k, yy, m, n) : SSP_OK;
+}
+int sspx_synth_action_scaled(ssp_ctx* c, const sspx_synth* sp, const double* const* xx, const double* xs,
+                             double* const* yy, int nvec, size_t n, size_t off) {
+  Scaled sx(xx, xs, nvec, n);
+  return sspx_synth_action(c, sp, sx.p.data(), yy, nvec, n, off);
 }
 
 }  // extern "C"

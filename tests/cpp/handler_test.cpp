@@ -356,6 +356,75 @@ void op_cases() {
     auto sel = hb.select(2, x, true);
     expect(sel == std::map<size_t, double>({{2, 3}, {3, 4}}), "select max");
   });
+  // Deferred scal (hbm_vec.h): a scal is applied by the next kernel that reads the vector; every
+  // result equals the eager sequence (ssp_scal on the stored values, then the op) bit for bit.
+  run("deferred_scal_matches_eager", [] {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    const size_t n = 1001;
+    auto v = random_values(n, 11), w = random_values(n, 12);
+    v[5] = 0.0;  // 0 * negative scale = -0
+    const double s = -0.3711, t = 1.7;
+    auto eager = [&](const std::vector<double>& vals, double a) {
+      auto e = make(vals);
+      molpro::linalg::hbm::check_status(ssp_scal(e.ctx(), a, e.data_rw(), n), "ssp_scal");
+      return e;
+    };
+    auto bits_equal = [](const std::vector<double>& a, const std::vector<double>& b) {
+      if (a.size() != b.size()) return false;
+      for (size_t i = 0; i < a.size(); ++i)
+        if (std::signbit(a[i]) != std::signbit(b[i]) || !(a[i] == b[i] || (std::isnan(a[i]) && std::isnan(b[i]))))
+          return false;
+      return true;
+    };
+    // scal is deferred, then stored on the first plain read
+    auto x = make(v);
+    hb.scal(s, x);
+    expect(x.scale() == s, "scal pending");
+    std::vector<double> vs(v);
+    for (auto& e : vs) e *= s;
+    expect(bits_equal(x.local_values(), vs), "materialised = the eager scal (incl. -0)");
+    expect(x.scale() == 1.0, "materialised scale");
+    // a copy shares storage and scale; scaling the copy leaves the source alone (two roundings)
+    auto x2 = make(v);
+    hb.scal(s, x2);
+    auto y = hb.copy(x2);
+    hb.scal(t, y);
+    std::vector<double> vst(vs);
+    for (auto& e : vst) e *= t;
+    expect(bits_equal(y.local_values(), vst), "scal of a scaled copy");
+    expect(bits_equal(x2.local_values(), vs), "source unchanged");
+    // dot, axpy, gemm_inner, gemm_outer with pending scales on sources and destinations
+    auto xa = make(v), za = make(w);
+    hb.scal(s, xa);
+    hb.scal(t, za);
+    auto xe = eager(v, s), ze = eager(w, t);
+    expect(hb.dot(xa, za) == hb.dot(xe, ze), "dot");
+    expect(hb.dot(xa, xa) == hb.dot(xe, xe), "norm");
+    const Mat ga = hb.gemm_inner(CVecRef<Vec>{std::cref(xa), std::cref(za)}, CVecRef<Vec>{std::cref(xa), std::cref(za)});
+    const Mat ge = hb.gemm_inner(CVecRef<Vec>{std::cref(xe), std::cref(ze)}, CVecRef<Vec>{std::cref(xe), std::cref(ze)});
+    expect(ga.data() == ge.data(), "gemm_inner");
+    hb.axpy(0.25, xa, za);
+    hb.axpy(0.25, xe, ze);
+    expect(bits_equal(za.local_values(), ze.local_values()), "axpy");
+    auto ya = make(w), ye = eager(w, s);
+    auto xb = make(v), xbe = eager(v, t);
+    hb.scal(s, ya);
+    hb.scal(t, xb);
+    Mat a(std::vector<double>{0.5, -2.0}, {2, 1});
+    hb.gemm_outer(a, CVecRef<Vec>{std::cref(xb), std::cref(xa)}, VecRef<Vec>{std::ref(ya)});
+    hb.gemm_outer(a, CVecRef<Vec>{std::cref(xbe), std::cref(xe)}, VecRef<Vec>{std::ref(ye)});
+    expect(bits_equal(ya.local_values(), ye.local_values()), "gemm_outer");
+    // a second scal stores the first (two roundings); a fill drops the pending scale
+    auto xc = make(v);
+    hb.scal(s, xc);
+    hb.scal(t, xc);
+    expect(bits_equal(xc.local_values(), vst), "scal twice");
+    hb.scal(3.0, xc);
+    hb.fill(0.5, xc);
+    expect(xc.local_values() == std::vector<double>(n, 0.5) && xc.scale() == 1.0, "fill drops the scale");
+    expect(hb.counter().scal == 10, "scal counted");
+  });
   run("error_types", [] {
     ArrayHandlerHbm handler;
     array::ArrayHandler<Vec, Vec>& hb = handler;
