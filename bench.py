@@ -378,9 +378,9 @@ def main():
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
                     help="rank transport at N > 1: RCCL (the product path) or the host socket hub, which "
                          "lets tests run several ranks on ONE device (RCCL refuses duplicate GPUs)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r2", "pmc_traffic_n1e8.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r3", "pmc_traffic_n1e8.json"),
                     help="rocprofv3 --pmc summary of this workload (roofline.traffic)")
-    ap.add_argument("--mfma-json", default=os.path.join(ROOT, "profiles", "r2", "mfma_util_n1e8.json"),
+    ap.add_argument("--mfma-json", default=os.path.join(ROOT, "profiles", "r3", "mfma_util_n1e8.json"),
                     help="rocprofv3 --pmc MfmaUtil summary of this workload (mfma.mfma_util_pct)")
     args = ap.parse_args()
 

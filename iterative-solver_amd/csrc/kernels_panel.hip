@@ -83,9 +83,17 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
     const size_t e = ch * 32 + 2 * p;
     double2 xv[MG], yv[NG];
 #pragma unroll
-    for (int g = 0; g < MG; ++g) xv[g] = xp[g] ? sc2<SC>(ssp::ld2nt(xp[g] + e), xsc[g]) : z2;
+    for (int g = 0; g < MG; ++g) xv[g] = xp[g] ? ssp::ld2nt(xp[g] + e) : z2;
 #pragma unroll
-    for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : (yp[h] ? sc2<SC>(ssp::ld2nt(yp[h] + e), ysc[h]) : z2);
+    for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : (yp[h] ? ssp::ld2nt(yp[h] + e) : z2);
+    // scales after every load of the chunk is in flight (a multiply inside the guarded load would
+    // make each load wait for the previous one)
+    if constexpr (SC) {
+#pragma unroll
+      for (int g = 0; g < MG; ++g) xv[g] = sc2<SC>(xv[g], xsc[g]);
+#pragma unroll
+      for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : sc2<SC>(yv[h], ysc[h]);
+    }
 #pragma unroll
     for (int g = 0; g < MG; ++g)
 #pragma unroll
@@ -258,15 +266,26 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int j = 0; j < M; ++j)
-        acc[u][j] = (j < a.m && ok[u] && !SET) ? sc2<SC>(ld2nt(a.y[j] + 2 * (p0 + 64 * u)), scale(a.k + j)) : z2;
+      for (int j = 0; j < M; ++j) acc[u][j] = (j < a.m && ok[u] && !SET) ? ld2nt(a.y[j] + 2 * (p0 + 64 * u)) : z2;
+    if constexpr (SC && !SET) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < M; ++j) acc[u][j] = sc2<SC>(acc[u][j], scale(a.k + j));
+    }
     int i = 0;
     for (; i + 4 <= a.k; i += 4) {
       double2 xv[4][U];
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int u = 0; u < U; ++u) xv[b][u] = ok[u] ? sc2<SC>(ld2nt(a.x[i + b] + 2 * (p0 + 64 * u)), scale(i + b)) : z2;
+        for (int u = 0; u < U; ++u) xv[b][u] = ok[u] ? ld2nt(a.x[i + b] + 2 * (p0 + 64 * u)) : z2;
+      if constexpr (SC) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int u = 0; u < U; ++u) xv[b][u] = sc2<SC>(xv[b][u], scale(i + b));
+      }
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -284,7 +303,11 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
     for (; i < a.k; ++i) {
       double2 xv[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) xv[u] = ok[u] ? sc2<SC>(ld2nt(a.x[i] + 2 * (p0 + 64 * u)), scale(i)) : z2;
+      for (int u = 0; u < U; ++u) xv[u] = ok[u] ? ld2nt(a.x[i] + 2 * (p0 + 64 * u)) : z2;
+      if constexpr (SC) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u] = sc2<SC>(xv[u], scale(i));
+      }
 #pragma unroll
       for (int j = 0; j < M; ++j) {
         if (j < a.m) {
