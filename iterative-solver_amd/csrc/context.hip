@@ -7,6 +7,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -336,6 +337,7 @@ int ssp_ctx_create(int device, ssp_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->num_cus = prop.multiProcessorCount;
+  if (const char* rs = std::getenv("SSP_ROW_SHAPE")) ctx->row_stride = std::string(rs) == "stride";
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return ssp::set_error(SSP_ERR_HIP, "hipStreamCreate failed");

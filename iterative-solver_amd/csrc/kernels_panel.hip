@@ -151,13 +151,15 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
 
 // Panels of 1 x 1 and 1 x 2 (or 2 x 1) vectors: with only one or two MFMA operand rows live, the
 // 4x4x4 layout leaves 3/4 of the lanes idle on loads (tools/shapes_bench.py: 1 x 1 at 3.4 TB/s),
-// so these run on the VALU with every lane streaming 16 B per vector, 4 positions in flight.  This
-// kernel keeps the grid-stride shape (the other streaming kernels moved to windows): with the window
-// order DIIS on (n = 1e5, rank 2, rho = 0.01) took 30 iterations instead of 15.  That case is not a
-// parity guarantee either way -- from its sixth step DIIS's residual-overlap matrix is singular to
-// rounding, and an independent restatement with LAPACK subspace solves takes 14
-// (tests/test_davidson_independent.py) -- the stride shape is kept because it converges there in the
-// reference's count, not because any summation order is exact.
+// so these run on the VALU with every lane streaming 16 B per vector.  Two shapes:
+//   k_gemm_inner_row_win  (default) each wave owns 4 consecutive KiB of every vector per visit, the
+//                         shape of k_dot_partial;
+//   k_gemm_inner_row      4 grid-strided positions in flight (round 2's shape, kept for the A/B:
+//                         SSP_ROW_SHAPE=stride, tools/row_shape_ab.py).
+// Round 2 kept the stride shape because the window order moved an ill-conditioned DIIS case (n = 1e5,
+// rank 2, rho = 0.01, singular to rounding from its sixth step) from 15 to 30 iterations; with C5's
+// well-posed instance (tests/golden/traces.json C5_*) the shape is decided by bandwidth
+// (DESIGN.md section 4), and that case is held to its converged solution only.
 template <int K, bool SC = false>
 __global__ __launch_bounds__(kBlock) void k_gemm_inner_row(const InnerArgs a) {
   using ssp::ld2nt;
@@ -198,6 +200,74 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner_row(const InnerArgs a) {
 #pragma unroll
     for (int j = 0; j < K; ++j)
       acc[j][0] = fma(sc1<SC>(a.x[0][a.n - 1], xs), sc1<SC>(a.y[j][a.n - 1], ys[j]), acc[j][0]);
+  __shared__ double red[kBlock / 64][K];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    double v = acc[j][0] + acc[j][1];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) red[wave][j] = v;
+  }
+  __syncthreads();
+  if (int(threadIdx.x) < K) {
+    double v = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) v += red[w][threadIdx.x];
+    ssp::store_partial(a.partial + size_t(blockIdx.x) * K + threadIdx.x, v);
+  }
+  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+}
+
+template <int K, bool SC = false>
+__global__ __launch_bounds__(kBlock) void k_gemm_inner_row_win(const InnerArgs a) {
+  using ssp::ld2nt;
+  constexpr int U = 4;  // 4 KiB of each vector per wave visit
+  double acc[K][2] = {};
+  const bool same = K == 1 && a.y[0] == a.x[0] && (!SC || a.ys[0] == a.xs[0]);  // a norm: one load stream
+  const double xs = SC ? a.xs[0] : 1.0;
+  double ys[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) ys[j] = SC ? a.ys[j] : 1.0;
+  ssp::for_windows<U>(
+      a.n,
+      [&](size_t p0) {
+        double2 xv[U], yv[K][U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u] = ld2nt(a.x[0] + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+#pragma unroll
+          for (int u = 0; u < U; ++u) yv[j][u] = same ? xv[u] : ld2nt(a.y[j] + 2 * (p0 + 64 * u));
+        if constexpr (SC) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) xv[u] = sc2<SC>(xv[u], xs);
+#pragma unroll
+          for (int j = 0; j < K; ++j)
+#pragma unroll
+            for (int u = 0; u < U; ++u) yv[j][u] = same ? xv[u] : sc2<SC>(yv[j][u], ys[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            acc[j][u & 1] = fma(xv[u].x, yv[j][u].x, acc[j][u & 1]);
+            acc[j][u & 1] = fma(xv[u].y, yv[j][u].y, acc[j][u & 1]);
+          }
+      },
+      [&](size_t p) {
+        const double2 xv = sc2<SC>(ld2(a.x[0] + 2 * p), xs);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const double2 yv = sc2<SC>(ld2(a.y[j] + 2 * p), ys[j]);
+          acc[j][0] = fma(xv.x, yv.x, acc[j][0]);
+          acc[j][0] = fma(xv.y, yv.y, acc[j][0]);
+        }
+      },
+      [&](size_t e) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) acc[j][0] = fma(sc1<SC>(a.x[0][e], xs), sc1<SC>(a.y[j][e], ys[j]), acc[j][0]);
+      });
   __shared__ double red[kBlock / 64][K];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -738,19 +808,24 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
         a.y[j] = cols[j];
         a.ys[j] = cs[size_t(j)];
       }
-      const unsigned grid = ssp::stream_grid(ctx, n / 2 + 1, 4);
+      const bool stride = ctx->row_stride;
+      const unsigned grid = stride ? ssp::stream_grid(ctx, n / 2 + 1, 4) : ssp::win_grid(ctx, n, 4, 8);
       SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * C));
       a.partial = ctx->partial;
       SSP_TRY(ssp::fold_begin(ctx, C, &tail));
       a.tail = tail;
-      if (C == 1 && sc)
-        hipLaunchKernelGGL((k_gemm_inner_row<1, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
-      else if (C == 1)
-        hipLaunchKernelGGL((k_gemm_inner_row<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
-      else if (sc)
-        hipLaunchKernelGGL((k_gemm_inner_row<2, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
-      else
-        hipLaunchKernelGGL((k_gemm_inner_row<2>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      const dim3 g(grid), b(kBlock);
+      if (stride) {
+        if (C == 1 && sc) hipLaunchKernelGGL((k_gemm_inner_row<1, true>), g, b, 0, ctx->stream, a);
+        else if (C == 1) hipLaunchKernelGGL((k_gemm_inner_row<1>), g, b, 0, ctx->stream, a);
+        else if (sc) hipLaunchKernelGGL((k_gemm_inner_row<2, true>), g, b, 0, ctx->stream, a);
+        else hipLaunchKernelGGL((k_gemm_inner_row<2>), g, b, 0, ctx->stream, a);
+      } else {
+        if (C == 1 && sc) hipLaunchKernelGGL((k_gemm_inner_row_win<1, true>), g, b, 0, ctx->stream, a);
+        else if (C == 1) hipLaunchKernelGGL((k_gemm_inner_row_win<1>), g, b, 0, ctx->stream, a);
+        else if (sc) hipLaunchKernelGGL((k_gemm_inner_row_win<2, true>), g, b, 0, ctx->stream, a);
+        else hipLaunchKernelGGL((k_gemm_inner_row_win<2>), g, b, 0, ctx->stream, a);
+      }
       SSP_TRY_HIP(hipGetLastError());
     }
     // A symmetric overlap <xx_i, xx_j> of up to 16 vectors: one panel that loads each vector once.

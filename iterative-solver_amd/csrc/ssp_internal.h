@@ -29,6 +29,9 @@ struct ssp_ctx {
   std::vector<ssp_ledger_entry_t> ledger;
   std::vector<hipEvent_t> event_pool;
   int num_cus = 256;
+  // Shape of the 1 x 1 / 1 x 2 gemm_inner row kernel: window (default) or, with SSP_ROW_SHAPE=stride
+  // in the environment at context creation, the round-2 grid-stride shape (A/B: tools/row_shape_ab.py).
+  bool row_stride = false;
   hipStream_t stream = nullptr;
 
   // HBM arena: freed blocks are kept by rounded size and recycled (Q vectors are created and
