@@ -269,8 +269,9 @@ def host_parallel(m, k, seconds):
 
 C3 = dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48, reset_D=8, convergence_threshold=1e-8)
 # BASELINE config C5 (NonLinearEquationsDIIS, N = 1e8): the well-posed instance of tests/golden/traces.json
-# C5_n1e7 / C5_n1e8 (itsolv_hbm.c5_spec: r = H (x - 1), x from e_0, the reference test's 1 1^T + diag
-# form of test_NonLinearEquations.cpp:25-49 with the coupling scaled by 1/N and a bounded diagonal)
+# C5_n1e7 / C5_n1e8 (itsolv_hbm.c5_spec: r = H (x - t 1), t = 1/sqrt(N), x from e_0, the reference test's
+# 1 1^T + diag form of test_NonLinearEquations.cpp:25-49 with the coupling scaled by 1/N and a bounded
+# diagonal)
 C5_OPTIONS = dict(max_size_qspace=6, convergence_threshold=1e-8)
 TRACES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "traces.json")
 
@@ -329,8 +330,10 @@ def in_solver(ctx, n_global, world, barrier, repeat=2, kind="davidson"):
         parity = {"cpu_path_trace": f"tests/golden/traces.json:{tname}", "cpu_path_iterations": ref["iterations"],
                   "same_steps_as_cpu_path": bool(same)}
     if kind == "diis":
-        config = ("NonLinearEquationsDIIS C5: r = H (x - 1), H = diag(1 + 2 frac(i phi)) + (1/N) 1 1^T, x from e_0, "
-                  "approximate preconditioner diagonal (alpha 0.5), max_size_qspace 6, threshold 1e-8"
+        c5 = ih.c5_spec(n_global)
+        config = ("NonLinearEquationsDIIS C5: r = H (x - t 1), t = 1/sqrt(N), H = diag(1 + 2 frac(i phi)) + (1/N) 1 1^T, "
+                  f"x from e_0, approximate preconditioner diagonal (alpha {c5['alpha']}), max_size_qspace 6, "
+                  "threshold 1e-8"
                   + (f", sharded over {world} ranks" if world > 1 else ""))
     else:
         config = ("LinearEigensystemDavidson " + ("C3" if world == 1 else "C4") + ": 8 roots + P 16, rank-8 "

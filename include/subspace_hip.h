@@ -227,6 +227,8 @@ typedef struct {
   unsigned long long seed;
   int diag_kind;           /* SSPX_DIAG_* */
   double alpha;            /* SSPX_DIAG_BOUNDED: preconditioner mismatch */
+  double target;           /* NonLinearEquations residual r = H (x - target 1); 0 is read as 1 (the
+                              reference test's x = 1) */
 } sspx_synth;
 int sspx_synth_action(ssp_ctx* ctx, const sspx_synth* spec, const double* const* xx, double* const* yy, int nvec,
                       size_t n, size_t offset);

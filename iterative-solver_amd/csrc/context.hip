@@ -174,9 +174,15 @@ int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen) {
 int fetch_result(ssp_ctx* ctx, double* out, size_t n) {
   if (n > ctx->result_cap) return set_error(SSP_ERR_ARG, "fetch_result: result larger than the staging buffer");
   const unsigned long long seq = ++ctx->pub_seq;
-  hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, ctx->stream, ctx->result_dev, n, ctx->result_host,
-                     ctx->pub_flag, seq);
-  SSP_TRY_HIP(hipGetLastError());
+  if (ctx->publish_copy) {
+    SSP_TRY_HIP(hipMemcpyAsync(ctx->result_host, ctx->result_dev, n * sizeof(double), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    SSP_TRY_HIP(hipStreamWriteValue64(ctx->stream, ctx->pub_flag, seq, 0));
+  } else {
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, ctx->stream, ctx->result_dev, n, ctx->result_host,
+                       ctx->pub_flag, seq);
+    SSP_TRY_HIP(hipGetLastError());
+  }
   bool seen = true;
   SSP_TRY(wait_flag(ctx, seq, &seen));
   if (!seen)
@@ -338,6 +344,7 @@ int ssp_ctx_create(int device, ssp_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->num_cus = prop.multiProcessorCount;
   if (const char* rs = std::getenv("SSP_ROW_SHAPE")) ctx->row_stride = std::string(rs) == "stride";
+  if (const char* pc = std::getenv("SSP_PUBLISH")) ctx->publish_copy = std::string(pc) == "copy";
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return ssp::set_error(SSP_ERR_HIP, "hipStreamCreate failed");

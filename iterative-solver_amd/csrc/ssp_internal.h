@@ -32,6 +32,10 @@ struct ssp_ctx {
   // Shape of the 1 x 1 / 1 x 2 gemm_inner row kernel: window (default) or, with SSP_ROW_SHAPE=stride
   // in the environment at context creation, the round-2 grid-stride shape (A/B: tools/row_shape_ab.py).
   bool row_stride = false;
+  // Hand-off of a device-resident reduction result (after k_reduce_partials / an allreduce) to the
+  // host: the one-workgroup k_publish kernel (default), or with SSP_PUBLISH=copy a D2H copy of the
+  // result followed by a stream write of the sequence flag (A/B: tools/latency_probe.py).
+  bool publish_copy = false;
   hipStream_t stream = nullptr;
 
   // HBM arena: freed blocks are kept by rounded size and recycled (Q vectors are created and

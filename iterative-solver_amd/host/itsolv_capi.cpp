@@ -72,11 +72,11 @@ class SyntheticProblem : public Problem<Vec, SparseP> {
                                    v0.offset()),
           "sspx_synth_action_scaled");
   }
-  // r = H (x - 1); value = 0 (unused by DIIS)
+  // r = H (x - target 1); value = 0 (unused by DIIS)
   double residual(const Vec& x, Vec& r) const override {
     Vec t(x);
     Vec ones(m_dev, x.size());
-    check(ssp_fill(ctx(), 1.0, ones.data_wo(), ones.local_size()), "ssp_fill");
+    check(ssp_fill(ctx(), m_s.target, ones.data_wo(), ones.local_size()), "ssp_fill");
     check(ssp_axpy(ctx(), -1.0, ones.data(), t.data_rw(), t.local_size()), "ssp_axpy");
     const double* xp[1] = {t.data()};
     double* yp[1] = {r.data_wo()};
@@ -123,7 +123,7 @@ class SyntheticProblem : public Problem<Vec, SparseP> {
 
 pr::SyntheticSpec spec_of(size_t n, const sspx_synth* s) {
   if (!s) throw std::invalid_argument("null sspx_synth");
-  return pr::SyntheticSpec(n, s->rho, s->rank, s->seed, s->diag_kind, s->alpha);
+  return pr::SyntheticSpec(n, s->rho, s->rank, s->seed, s->diag_kind, s->alpha, s->target);
 }
 
 // Dense row-major H, single rank: H resident in HBM, action by a row-per-lane kernel.

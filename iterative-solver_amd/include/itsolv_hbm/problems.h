@@ -50,10 +50,14 @@ struct SyntheticSpec {
   uint64_t seed;
   int diag_kind = SSPX_DIAG_LINEAR;
   double alpha = 0;
+  //! The nonlinear-equations solution's components: r = H (x - target 1) (the reference test's x = 1,
+  //! test_NonLinearEquations.cpp:25-49, is target 1; C5 uses 1 / sqrt(n), a unit-norm solution).
+  double target = 1.0;
   std::vector<uint64_t> keys;  // per low-rank vector
   SyntheticSpec(size_t n_, double rho_, int rank_, uint64_t seed_, int diag_kind_ = SSPX_DIAG_LINEAR,
-                double alpha_ = 0)
-      : n(n_), rho(rho_), rank(rank_), seed(seed_), diag_kind(diag_kind_), alpha(alpha_) {
+                double alpha_ = 0, double target_ = 1.0)
+      : n(n_), rho(rho_), rank(rank_), seed(seed_), diag_kind(diag_kind_), alpha(alpha_),
+        target(target_ == 0.0 ? 1.0 : target_) {
     for (int l = 0; l < rank; ++l) keys.push_back(stream_key(seed, 1000 + uint64_t(l)));
   }
   double u(int l, size_t g) const { return l == 0 ? 1.0 : ((splitmix64(keys[l] ^ uint64_t(g)) & 1ull) ? -1.0 : 1.0); }
@@ -73,14 +77,18 @@ struct SyntheticSpec {
     }
     return 1.0 + double(g) + rank * rho;
   }
-  sspx_synth c_spec() const { return sspx_synth{rho, rank, seed, diag_kind, alpha}; }
+  sspx_synth c_spec() const { return sspx_synth{rho, rank, seed, diag_kind, alpha, target}; }
 };
 
-//! BASELINE config C5 as a well-posed instance: r = H (x - 1), H = diag(1 + 2 frac(g phi1)) + (1/N) 1 1^T
+//! BASELINE config C5 as a well-posed instance: r = H (x - t 1), H = diag(1 + 2 frac(g phi1)) + (1/N) 1 1^T
 //! (the reference's DIIS test form 1 1^T + diag, test_NonLinearEquations.cpp:25-31, with the coupling
-//! scaled to the length and the diagonal bounded), preconditioner mismatch alpha = 0.5.
-inline SyntheticSpec c5_spec(size_t n, int rank = 1, uint64_t seed = 3, double alpha = 0.5) {
-  return SyntheticSpec(n, 1.0 / double(n), rank, seed, SSPX_DIAG_BOUNDED, alpha);
+//! scaled to the length and the diagonal bounded), preconditioner mismatch alpha = 0.2 and the solution
+//! t 1 of unit norm (t = 1/sqrt(N)).  10 steps at every N from |r_0| = 3.2 to the 1e-8 threshold, the
+//! last two errors 2.8x above and 1.5x below it, while valid reorderings of the CPU path's sums move
+//! them by at most 3 %.  Round 2's alpha = 0.5 with x = 1 stagnated at ~1.4e-8
+//! for its last steps, where reorderings moved the errors by up to 43 % and the count followed.
+inline SyntheticSpec c5_spec(size_t n, int rank = 1, uint64_t seed = 3, double alpha = 0.2) {
+  return SyntheticSpec(n, 1.0 / double(n), rank, seed, SSPX_DIAG_BOUNDED, alpha, 1.0 / std::sqrt(double(n)));
 }
 
 // One row of itsolv_result's per-iteration trace (called from solve()'s iteration_hook).

@@ -4,6 +4,7 @@ oracle's CPU twin (oracle/itsolv_oracle.cpp)."""
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 
 import numpy as np
@@ -27,14 +28,14 @@ DIAG_LINEAR, DIAG_BOUNDED = 0, 1
 
 class Synth(C.Structure):
     _fields_ = [("rho", C.c_double), ("rank", C.c_int), ("seed", C.c_ulonglong), ("diag_kind", C.c_int),
-                ("alpha", C.c_double)]
+                ("alpha", C.c_double), ("target", C.c_double)]
 
 
-def c5_spec(n: int, rank: int = 1, seed: int = 3, alpha: float = 0.5) -> dict:
-    """BASELINE config C5's well-posed DIIS instance (itsolv_hbm/problems.h c5_spec): r = H (x - 1),
-    H = diag(1 + 2 frac(g phi1)) + (1/n) sum_l u_l u_l^T, preconditioner diagonal mismatched by alpha.
-    Keyword arguments of diis_synthetic / oracle.diis_synthetic."""
-    return dict(rho=1.0 / n, rank=rank, seed=seed, diag_kind=DIAG_BOUNDED, alpha=alpha)
+def c5_spec(n: int, rank: int = 1, seed: int = 3, alpha: float = 0.2) -> dict:
+    """BASELINE config C5's well-posed DIIS instance (itsolv_hbm/problems.h c5_spec): r = H (x - t 1),
+    H = diag(1 + 2 frac(g phi1)) + (1/n) sum_l u_l u_l^T, preconditioner diagonal mismatched by alpha,
+    t = 1/sqrt(n) (a unit-norm solution).  Keyword arguments of diis_synthetic / oracle.diis_synthetic."""
+    return dict(rho=1.0 / n, rank=rank, seed=seed, diag_kind=DIAG_BOUNDED, alpha=alpha, target=1.0 / math.sqrt(n))
 
 
 class Options(C.Structure):
@@ -155,10 +156,11 @@ def _call(fn, args, nout):
 
 
 def davidson_synthetic(ctx: sh.Context, n: int, rho: float, rank: int, seed: int, n_local: int | None = None,
-                       solutions: bool = True, *, diag_kind: int = DIAG_LINEAR, alpha: float = 0.0, **opts):
+                       solutions: bool = True, *, diag_kind: int = DIAG_LINEAR, alpha: float = 0.0,
+                       target: float = 1.0, **opts):
     o = make_options(**opts)
     nl = n if n_local is None else n_local
-    spec = Synth(rho, rank, seed, diag_kind, alpha)
+    spec = Synth(rho, rank, seed, diag_kind, alpha, target)
     r, sol = _call(load_library().itsolv_davidson_synth, (ctx.handle, n, C.byref(spec), C.byref(o)),
                    o.nroots * nl if solutions else 0)
     if solutions:
@@ -177,10 +179,11 @@ def davidson_dense(ctx: sh.Context, h: np.ndarray, **opts):
 
 
 def diis_synthetic(ctx: sh.Context, n: int, rho: float, rank: int, seed: int, n_local: int | None = None,
-                   solutions: bool = True, *, diag_kind: int = DIAG_LINEAR, alpha: float = 0.0, **opts):
+                   solutions: bool = True, *, diag_kind: int = DIAG_LINEAR, alpha: float = 0.0,
+                       target: float = 1.0, **opts):
     o = make_options(**opts)
     nl = n if n_local is None else n_local
-    spec = Synth(rho, rank, seed, diag_kind, alpha)
+    spec = Synth(rho, rank, seed, diag_kind, alpha, target)
     r, x = _call(load_library().itsolv_diis_synth, (ctx.handle, n, C.byref(spec), C.byref(o)),
                  nl if solutions else 0)
     if solutions:

@@ -151,8 +151,9 @@ class SyntheticProblem:
 
     PHI1, PHI2 = float.fromhex("0x1.3c6ef372fe950p-1"), float.fromhex("0x1.827f5352054c6p-1")
 
-    def __init__(self, n, rho, rank, seed, diag_kind=0, alpha=0.0):
+    def __init__(self, n, rho, rank, seed, diag_kind=0, alpha=0.0, target=1.0):
         self.n, self.rho, self.rank, self.diag_kind = n, rho, rank, diag_kind
+        self.target = target  # r = H (x - target 1)
         g = np.arange(n, dtype=np.uint64)
         with np.errstate(over="ignore"):
             self.u = np.empty((rank, n))
@@ -188,7 +189,7 @@ class SyntheticProblem:
         return c
 
     def residual(self, x):
-        return self.action(x - 1.0)
+        return self.action(x - self.target)
 
 
 # ---- the solver ----------------------------------------------------------------------------------

@@ -76,7 +76,7 @@ class SyntheticCpu : public Problem<V, SP> {
   }
   double residual(const V& x, V& r) const override {
     V t(x);
-    for (auto& v : t) v -= 1.0;
+    for (auto& v : t) v -= m_s.target;
     apply(t, r);
     return 0;
   }
@@ -521,12 +521,12 @@ int oracle_davidson_synthetic(size_t n, double rho, int rank, unsigned long long
 // itsolv_davidson_synth / itsolv_diis_synth's twins (any synthetic family, include/subspace_hip.h sspx_synth)
 int oracle_davidson_synth(size_t n, const sspx_synth* s, const itsolv_options* opt, itsolv_result* out,
                           double* solutions_out) {
-  SyntheticCpu p(pr::SyntheticSpec(n, s->rho, s->rank, s->seed, s->diag_kind, s->alpha));
+  SyntheticCpu p(pr::SyntheticSpec(n, s->rho, s->rank, s->seed, s->diag_kind, s->alpha, s->target));
   return davidson(p, n, opt, out, solutions_out);
 }
 
 int oracle_diis_synth(size_t n, const sspx_synth* s, const itsolv_options* opt, itsolv_result* out, double* x_out) {
-  SyntheticCpu p(pr::SyntheticSpec(n, s->rho, s->rank, s->seed, s->diag_kind, s->alpha));
+  SyntheticCpu p(pr::SyntheticSpec(n, s->rho, s->rank, s->seed, s->diag_kind, s->alpha, s->target));
   return diis(p, n, opt, out, x_out);
 }
 

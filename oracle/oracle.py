@@ -384,11 +384,11 @@ def _solve(fn, args, nout):
     return res.as_dict(), out
 
 
-def davidson_synthetic(n, rho, rank, seed, solutions=True, *, diag_kind=0, alpha=0.0, **opts):
+def davidson_synthetic(n, rho, rank, seed, solutions=True, *, diag_kind=0, alpha=0.0, target=1.0, **opts):
     from itsolv_hbm import Synth, make_options
 
     o = make_options(**opts)
-    spec = Synth(rho, rank, seed, diag_kind, alpha)
+    spec = Synth(rho, rank, seed, diag_kind, alpha, target)
     r, sol = _solve(itsolv_lib().oracle_davidson_synth, (n, C.byref(spec), C.byref(o)),
                     o.nroots * n if solutions else 0)
     if solutions:
@@ -407,12 +407,12 @@ def davidson_dense(h, **opts):
     return r
 
 
-def diis_synthetic(n, rho, rank, seed, solutions=True, *, diag_kind=0, alpha=0.0, **opts):
+def diis_synthetic(n, rho, rank, seed, solutions=True, *, diag_kind=0, alpha=0.0, target=1.0, **opts):
     """diag_kind / alpha: the synthetic family (itsolv_hbm.DIAG_*, itsolv_hbm.c5_spec)."""
     from itsolv_hbm import Synth, make_options
 
     o = make_options(**opts)
-    spec = Synth(rho, rank, seed, diag_kind, alpha)
+    spec = Synth(rho, rank, seed, diag_kind, alpha, target)
     r, x = _solve(itsolv_lib().oracle_diis_synth, (n, C.byref(spec), C.byref(o)), n if solutions else 0)
     if solutions:
         r["x"] = x[:n]

@@ -171,7 +171,7 @@ def case_gpu_traces(comm):
 
     import itsolv_hbm as ih
     import subspace_hip as sh
-    from trace_check import EIG_REL, T, assert_trace, run_case
+    from trace_check import EIG_REL, T, assert_trace, run_case, solution_target
 
     rank, world = comm.rank, comm.nranks
     ctx = sh.Context(0)
@@ -186,7 +186,7 @@ def case_gpu_traces(comm):
         g = run_case(ih, ctx, ref, n_local=nl, solutions=c["kind"] == "diis")
         assert_trace(g, ref, f"{name} on {world} shards")
         if c["kind"] == "diis" and ref["converged"]:  # x = 1 on every shard
-            assert np.max(np.abs(g["x"] - 1.0)) <= ref["options"]["convergence_threshold"], name
+            assert np.max(np.abs(g["x"] - solution_target(ref))) <= ref["options"]["convergence_threshold"], name
         if rank == 0:
             print(f"{name} on {world} shards: {g['iterations']} iterations (CPU path {ref['iterations']}), "
                   f"{g['seconds']:.3f} s", flush=True)

@@ -28,9 +28,10 @@ reference's test_rayleigh_quotient.cpp:37-42 matrix at large n), options of §8d
   C5  DIIS      max_size_qspace 6   N = 1e7 and N = 1e8: the well-posed instance
                                               (itsolv_hbm/problems.h c5_spec: the reference test's
                                               1 1^T + diag form with the coupling scaled by 1/N, a
-                                              bounded diagonal and an approximate preconditioner
-                                              diagonal; |r_0| ~ 3 sqrt(N), geometric convergence to
-                                              the 1e-8 threshold four orders above the rounding floor)
+                                              bounded diagonal, a preconditioner diagonal mismatched
+                                              by up to 20 % and the unit-norm solution 1/sqrt(N);
+                                              |r_0| = 3.2, 10 steps to the 1e-8 threshold, the last
+                                              two errors 2.8x above / 1.5x below it)
   C5x DIIS      max_size_qspace 6   N = 1e7   the round-1 instance (diag(1+g), rank 3, rho 0.01):
                                               |r_0| = 1.9e10, so the threshold lies below its rounding
                                               floor and the count past the 1e-6 plateau is decided by
@@ -65,10 +66,10 @@ CASES = {
     # with the memory (--omp, the bit-identical OpenMP build of the CPU path)
     "C3_n1e8_rank8": dict(kind="davidson", n=100_000_000, rho=RHO, rank=8, seed=SEED, nroots=8, max_p=16),
     # C5: the well-posed DIIS instance (itsolv_hbm.c5_spec)
-    "C5_n1e7": dict(kind="diis", n=10_000_000, rho=1.0 / 10_000_000, rank=1, seed=3, diag_kind=1, alpha=0.5,
-                    convergence_threshold=1e-8),
-    "C5_n1e8": dict(kind="diis", n=100_000_000, rho=1.0 / 100_000_000, rank=1, seed=3, diag_kind=1, alpha=0.5,
-                    convergence_threshold=1e-8),
+    "C5_n1e7": dict(kind="diis", n=10_000_000, rho=1.0 / 10_000_000, rank=1, seed=3, diag_kind=1, alpha=0.2,
+                    target=10_000_000 ** -0.5, convergence_threshold=1e-8),
+    "C5_n1e8": dict(kind="diis", n=100_000_000, rho=1.0 / 100_000_000, rank=1, seed=3, diag_kind=1, alpha=0.2,
+                    target=100_000_000 ** -0.5, convergence_threshold=1e-8),
     # C5x: the round-1 DIIS problem (profiles/r1/solver_ledger_v10.json: rho 0.01, rank 3, seed 3), chaotic
     "C5x_n1e7_traj12": dict(kind="diis", n=10_000_000, rho=0.01, rank=3, seed=3, max_iter=12,
                             convergence_threshold=1e-14),
@@ -78,7 +79,7 @@ CASES = {
 
 def problem_kw(c):
     """The synthetic family of a case (diag_kind / alpha; absent = the Davidson family d_g = 1 + g)."""
-    return {k: c[k] for k in ("diag_kind", "alpha") if k in c}
+    return {k: c[k] for k in ("diag_kind", "alpha", "target") if k in c}
 
 
 def options(c):

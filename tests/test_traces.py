@@ -56,14 +56,14 @@ def test_traces_cover_the_baseline_configs():
 def test_c5_traces_are_well_posed(name):
     # C5's parity observables are not decided by rounding: the CPU path takes the same steps when only
     # its summation order changes (make_traces.py "reordered" and "reordered_blocked"), it converges,
-    # and every error it
+    # every error it
     # decides on lies at least 20 % away from the threshold (no knife edge), while the rounding floor
     # eps |r_0| sits four orders below it.
     ref = T[name]
     assert ref["converged"]
     for v in ("reordered", "reordered_blocked"):
         assert ref[v]["same_steps"] and ref[v]["converged"], v
-    assert ref["iterations"] >= 20 and ref["r_creations"] == ref["iterations"] + 1
+    assert ref["iterations"] >= 8 and ref["r_creations"] == ref["iterations"] + 1
     e = np.array(ref["trace"]["errors"])[:, 0]
     thr = ref["options"]["convergence_threshold"]
     assert np.all(np.abs(e / thr - 1.0) > 0.2)

@@ -25,7 +25,7 @@ import pytest
 
 import itsolv_hbm as ih
 import oracle
-from trace_check import C5, DAVIDSON, EIG_REL, T, assert_trace, run_case
+from trace_check import C5, DAVIDSON, EIG_REL, T, assert_trace, run_case, solution_target
 
 pytestmark = pytest.mark.gpu
 
@@ -65,8 +65,8 @@ def test_c5_trace_matches_reference_path(ctx, name):
     gpu = run_case(ih, ctx, ref, solutions=True)
     assert_trace(gpu, ref, name)
     assert gpu["residual_norms"][0] < ref["options"]["convergence_threshold"]
-    # |x - 1| <= |H (x - 1)| / lambda_min(H), lambda_min(H) >= 1
-    assert np.max(np.abs(gpu["x"] - 1.0)) <= ref["options"]["convergence_threshold"]
+    # |x - t 1| <= |H (x - t 1)| / lambda_min(H), lambda_min(H) >= 1
+    assert np.max(np.abs(gpu["x"] - solution_target(ref))) <= ref["options"]["convergence_threshold"]
     print(f"{name}: GPU {gpu['iterations']} iterations = CPU path {ref['iterations']}, {gpu['seconds']:.3f} s")
 
 

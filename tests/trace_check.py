@@ -12,8 +12,9 @@ C5 = sorted(k for k, v in T.items() if not k.startswith("_") and k.startswith("C
 
 
 def problem_kw(c):
-    """The synthetic family of a trace case (diag_kind / alpha; absent = d_g = 1 + g), make_traces.py."""
-    return {k: c[k] for k in ("diag_kind", "alpha") if k in c}
+    """The synthetic family of a trace case (diag_kind / alpha / target; absent = d_g = 1 + g and the
+    solution x = 1), make_traces.py."""
+    return {k: c[k] for k in ("diag_kind", "alpha", "target") if k in c}
 
 
 def run_case(ih, ctx, ref, **kw):
@@ -73,3 +74,8 @@ def assert_trace(gpu, ref, name):
     # the reported run ends where the reference's does: converged errors below the threshold
     if ref["converged"]:
         assert np.max(g["errors"][-1]) <= ref["options"]["convergence_threshold"], name
+
+
+def solution_target(ref):
+    """The component value of a nonlinear-equations trace case's solution (r = H (x - target 1))."""
+    return ref["case"].get("target", 1.0)

@@ -31,8 +31,7 @@ CONFIGS = {
     "C2-mgs": ("davidson", 10_000_000, dict(rho=0.1, rank=8, seed=1, nroots=4, max_size_qspace=24, reset_D=8,
                                              convergence_threshold=1e-8, block_gram_schmidt=0)),
     # C5's well-posed DIIS instance (itsolv_hbm.c5_spec; tests/golden/traces.json C5_n1e8)
-    "C5": ("diis", 100_000_000, dict(rho=1.0 / 100_000_000, rank=1, seed=3, diag_kind=1, alpha=0.5, max_size_qspace=6,
-                                     convergence_threshold=1e-8)),
+    "C5": ("diis", 100_000_000, dict(**ih.c5_spec(100_000_000), max_size_qspace=6, convergence_threshold=1e-8)),
     # the round-1 instance (chaotic past its 1e-6 plateau)
     "C5x": ("diis", 100_000_000, dict(rho=0.01, rank=3, seed=3, max_size_qspace=6, convergence_threshold=1e-8)),
     # one rank's shard of C4 (N = 1e8 over 8 GPUs): the C3 problem at N = 1.25e7 (run with --rccl for
