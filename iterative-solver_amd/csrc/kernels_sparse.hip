@@ -329,7 +329,7 @@ int solution_impl(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const 
     hipLaunchKernelGGL(k_gather_touched, dim3(unsigned((cnt + 255) / 256)), dim3(256), 0, ctx->stream,
                        static_cast<const unsigned long long*>(p), uidx.size(), m, ydev, ctx->partial);
     SSP_TRY_HIP(hipGetLastError());
-    saved = ctx->partial;
+    saved = ctx->partial;  // nothing below resizes the partials workspace before the fix-up reads it
   }
   if (rmw)
     SSP_TRY(ssp_gemm_outer_scaled(ctx, alphas, xx, xs, k, yy, ys, m, n));

@@ -80,6 +80,11 @@ std::vector<double*> rw_deferred_ptrs(const Refs& v, std::vector<double>& scales
   for (size_t i = 0; i < v.size(); ++i) p[i] = v[i].get().data_rw_deferred(&scales[i]);
   return p;
 }
+// After a successful *_scaled call: the destinations' pending scales are in their blocks now.
+template <class Refs>
+void scales_applied(const Refs& v) {
+  for (auto& x : v) x.get().scale_applied();
+}
 template <class Refs>
 std::vector<double*> wo_ptrs(const Refs& v) {
   std::vector<double*> p;
@@ -145,6 +150,7 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
     double ys = 1.0;
     double* yp = y.data_rw_deferred(&ys);
     check(ssp_axpy_scaled(y.ctx(), alpha, xp, xs, yp, ys, y.local_size()), "ssp_axpy_scaled");
+    y.scale_applied();
   }
   double dot(const Vec& x, const Vec& y) override {
     m_counter->dot++;
@@ -171,11 +177,13 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
     std::vector<double> xs, ys;
     auto xp = detail::deferred_ptrs(xx, xs);
     // only the alphas.cols() destinations the kernel updates
-    auto yp = detail::rw_deferred_ptrs(itsolv::VecRef<Vec>(yy.begin(), yy.begin() + long(alphas.cols())), ys);
+    const itsolv::VecRef<Vec> dest(yy.begin(), yy.begin() + long(alphas.cols()));
+    auto yp = detail::rw_deferred_ptrs(dest, ys);
     const auto& y0 = yy.front().get();
     check(ssp_gemm_outer_scaled(y0.ctx(), alphas.data().data(), xp.data(), xs.data(), int(xx.size()), yp.data(),
                                 ys.data(), int(alphas.cols()), y0.local_size()),
           "ssp_gemm_outer_scaled");
+    detail::scales_applied(dest);
   }
   itsolv::subspace::Matrix<double> gemm_inner(const itsolv::CVecRef<Vec>& xx, const itsolv::CVecRef<Vec>& yy) override {
     m_counter->gemm_inner++;
@@ -254,6 +262,7 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
     check(ssp_gemm_outer_scaled(y0.ctx(), coef.data(), xp.data(), xs.data(), int(nx), yp.data(), ys.data(), int(ny),
                                 y0.local_size()),
           "ssp_gemm_outer_scaled");
+    detail::scales_applied(yy);
   }
 };
 

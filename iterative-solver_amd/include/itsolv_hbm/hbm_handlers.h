@@ -97,6 +97,7 @@ inline bool fused_block_update(array::ArrayHandler<Vec, SparseP>&, const itsolv:
                          cqd.data().data(), xp.data(), xs.data(), int(qd.size()), yp.data(), ys.data(), int(m),
                          y0.local_size(), y0.offset()),
         "ssp_block_update");
+  detail::scales_applied(yy);
   return true;
 }
 

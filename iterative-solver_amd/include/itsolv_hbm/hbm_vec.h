@@ -167,13 +167,15 @@ class Vec {
   //! Read-only operand of a kernel that multiplies each element by scale() as it loads it.
   const double* data_deferred() const { return m_block ? m_block->p : nullptr; }
   //! Read-modify-write destination of a kernel that multiplies each element it reads by *s (set to
-  //! the pending scale here) and stores the result in full: the vector's scale becomes 1.
+  //! the pending scale here) and stores the result in full; call scale_applied() once that kernel
+  //! has been issued successfully (on an error the vector keeps its value: block and scale).
   double* data_rw_deferred(double* s) {
     detach(true);
     *s = m_scale;
-    m_scale = 1.0;
     return m_block ? m_block->p : nullptr;
   }
+  //! The pending scale has been written into the block by a *_scaled kernel (data_rw_deferred).
+  void scale_applied() { m_scale = 1.0; }
   //! The handlers' scal: x *= a, deferred to the next kernel that reads x (see above).  A second
   //! scal before any kernel has applied the first stores the first (two roundings, as the reference).
   void scale_by(double a) {
