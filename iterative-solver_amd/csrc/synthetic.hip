@@ -416,18 +416,18 @@ int sspx_synth_diagonal(ssp_ctx* ctx, const sspx_synth* spec, double* d, size_t 
 // The SSPX_DIAG_LINEAR entry points of round 1 (d_g = 1 + g).
 int sspx_synthetic_action(ssp_ctx* ctx, const double* const* xx, double* const* yy, int nvec, size_t n, size_t offset,
                           double rho, int rank, unsigned long long seed) {
-  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0, 1.0};
   return sspx_synth_action(ctx, &s, xx, yy, nvec, n, offset);
 }
 
 int sspx_synthetic_add_lowrank(ssp_ctx* ctx, double* const* yy, int nvec, size_t n, size_t offset, double rho,
                                int rank, unsigned long long seed, const double* w) {
-  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0, 1.0};
   return sspx_synth_add_lowrank(ctx, &s, yy, nvec, n, offset, w);
 }
 
 int sspx_synthetic_diagonal(ssp_ctx* ctx, double* d, size_t n, size_t offset, double rho, int rank) {
-  const sspx_synth s{rho, rank, 0, SSPX_DIAG_LINEAR, 0.0};
+  const sspx_synth s{rho, rank, 0, SSPX_DIAG_LINEAR, 0.0, 1.0};
   return sspx_synth_diagonal(ctx, &s, d, n, offset);
 }
 

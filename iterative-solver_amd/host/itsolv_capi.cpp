@@ -240,7 +240,7 @@ void itsolv_default_options(itsolv_options* opt) { pr::default_options(opt); }
 
 int itsolv_davidson_synthetic(ssp_ctx* ctx, size_t n, double rho, int rank, unsigned long long seed,
                               const itsolv_options* opt, itsolv_result* out, double* solutions_out) {
-  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0, 1.0};
   return itsolv_davidson_synth(ctx, n, &s, opt, out, solutions_out);
 }
 
@@ -282,7 +282,7 @@ int itsolv_davidson_dense(ssp_ctx* ctx, const double* h, size_t n, const itsolv_
 
 int itsolv_diis_synthetic(ssp_ctx* ctx, size_t n, double rho, int rank, unsigned long long seed,
                           const itsolv_options* opt, itsolv_result* out, double* x_out) {
-  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0, 1.0};
   return itsolv_diis_synth(ctx, n, &s, opt, out, x_out);
 }
 

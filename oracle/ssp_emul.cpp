@@ -539,16 +539,16 @@ int sspx_synth_diagonal(ssp_ctx*, const sspx_synth* sp, double* d, size_t n, siz
 }
 int sspx_synthetic_action(ssp_ctx* c, const double* const* xx, double* const* yy, int nvec, size_t n, size_t off,
                           double rho, int rank, unsigned long long seed) {
-  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0, 1.0};
   return sspx_synth_action(c, &s, xx, yy, nvec, n, off);
 }
 int sspx_synthetic_add_lowrank(ssp_ctx* c, double* const* yy, int nvec, size_t n, size_t off, double rho, int rank,
                                unsigned long long seed, const double* w) {
-  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0};
+  const sspx_synth s{rho, rank, seed, SSPX_DIAG_LINEAR, 0.0, 1.0};
   return sspx_synth_add_lowrank(c, &s, yy, nvec, n, off, w);
 }
 int sspx_synthetic_diagonal(ssp_ctx* c, double* d, size_t n, size_t off, double rho, int rank) {
-  const sspx_synth s{rho, rank, 0, SSPX_DIAG_LINEAR, 0.0};
+  const sspx_synth s{rho, rank, 0, SSPX_DIAG_LINEAR, 0.0, 1.0};
   return sspx_synth_diagonal(c, &s, d, n, off);
 }
 int sspx_fill_random(ssp_ctx*, double* x, size_t n, size_t off, unsigned long long seed, unsigned long long vec) {

@@ -152,3 +152,27 @@ def test_synth_action_scaled(ctx, rank):
     ctx.synth_action(ex, yb, spec)
     for a, b in zip(ya, yb):
         assert np.array_equal(bits(a.numpy()), bits(b.numpy()))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 1023])
+def test_scaled_tails(ctx, n):
+    # the element-wise tail paths (odd elements, partial windows, fewer elements than lanes)
+    rng = np.random.default_rng(n)
+    xv = [rand(rng, n, zeros=False) for _ in range(5)]
+    yv = [rand(rng, n, zeros=False) for _ in range(3)]
+    xs = np.array([-0.5, 1.0, 3.25, 0.1, -2.0])
+    ys = np.array([2.5, -0.75, 1.0])
+    rx, ex = scaled_copies(ctx, xv, xs)
+    ry, ey = scaled_copies(ctx, yv, ys)
+    assert ctx.dot_scaled(rx[0], xs[0], ry[0], ys[0]) == ctx.dot(ex[0], ey[0])
+    assert np.array_equal(bits(ctx.gemm_inner_scaled(rx, xs, ry, ys)), bits(ctx.gemm_inner(ex, ey)))
+    assert np.array_equal(bits(ctx.gemm_inner_scaled(rx[:1], xs[:1], ry[:2], ys[:2])),
+                          bits(ctx.gemm_inner(ex[:1], ey[:2])))
+    al = rng.uniform(-1, 1, (5, 3))
+    ctx.gemm_outer_scaled(al, rx, xs, ry, ys)
+    ctx.gemm_outer(al, ex, ey)
+    for a, b in zip(ry, ey):
+        assert np.array_equal(bits(a.numpy()), bits(b.numpy()))
+    ctx.axpy_scaled(0.3, rx[1], xs[1], rx[2], xs[2])
+    ctx.axpy(0.3, ex[1], ex[2])
+    assert np.array_equal(bits(rx[2].numpy()), bits(ex[2].numpy()))
