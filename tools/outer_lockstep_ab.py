@@ -5,6 +5,9 @@ the read-modify-write 48 -> 8 (the bench's dominant kernel), the write-only 48 -
 64 -> 16 and 1 -> 8 at N = 1e8, library HIP-event ledger, median of 7.
 
 usage: python tools/outer_lockstep_ab.py [--rounds 3] [--out gpurun_out/outer_lockstep_ab.json]
+
+Result (profiles/r3/outer_lockstep_ab.json): no gain, so the lockstep form and its SSP_OUTER_LOCKSTEP
+knob were removed from the library again; rerunning this tool needs that change re-applied.
 """
 import argparse
 import json
