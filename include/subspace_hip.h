@@ -132,6 +132,15 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
  *                    then ssp_dot(yy[0], yy[0]), yy bit-identical)             bytes 8N(1 + 2m) */
 int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* yy, int m, size_t n, double* out);
 int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const* yy, int m, size_t n, double* out);
+/* One pass per step of that loop (the HBM handlers' default since round 3):
+ *   ssp_axpy_gram:   x_s = x * xs (stored into x when store_x and xs != 1: the scal's one rounding),
+ *                    yy[j] += c[j] * x_s, then out[j] = <yy[0], yy[j]> for j < m summed over ranks --
+ *                    the Gram row of the next vector to normalise, from which the caller takes its
+ *                    norm (out[0]) and the next overlaps <r_{i+1}, r_j> = out[j - i - 1] / |r_{i+1}|
+ *                    (= ssp_gemm_outer_scaled({x} -> yy) then ssp_gemm_inner({yy[0]}, yy), yy and x
+ *                    bit-identical)                                           bytes 8N(1 + store + 2m) */
+int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store_x, double* const* yy, int m,
+                  size_t n, double* out);
 /* a[v][i] /= (d[i] - shift[v] + 1e-15) for v in [0,nvec)   reference itsolv/IterativeSolver.h:34-55 */
 int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n);
 

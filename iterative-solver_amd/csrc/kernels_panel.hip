@@ -642,6 +642,97 @@ __global__ __launch_bounds__(kBlock) void k_axpy_norm(const AxpyInnerArgs a) {
   if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
 }
 
+// One pass per step of the self-orthonormalisation: x_s = x * xs (the scal's one rounding, stored
+// when store_x), y_j += c_j x_s, then the Gram row of the next vector, acc_j += y_0_new * y_j_new.
+struct AxpyGramArgs {
+  double* x;
+  double* y[ssp::kOuterDst];
+  double c[ssp::kOuterDst];
+  double xs;
+  int store_x;
+  int m;
+  size_t n;
+  double* partial;     // [gridDim.x][m]
+  ssp::FoldTail tail;  // fused fold when tail.counter is set
+};
+
+template <int M>
+__global__ __launch_bounds__(kBlock) void k_axpy_gram(const AxpyGramArgs a) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  double acc[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) acc[j] = 0;
+  ssp::for_windows<kFusedU>(
+      a.n,
+      [&](size_t p0) {
+        double2 xv[kFusedU], y0[kFusedU];
+#pragma unroll
+        for (int u = 0; u < kFusedU; ++u) xv[u] = ld2nt(a.x + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int u = 0; u < kFusedU; ++u) {
+          xv[u].x *= a.xs;
+          xv[u].y *= a.xs;
+        }
+        if (a.store_x) {
+#pragma unroll
+          for (int u = 0; u < kFusedU; ++u) st2nt(a.x + 2 * (p0 + 64 * u), xv[u]);
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            double2 y[kFusedU];
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) y[u] = ld2nt(a.y[j] + 2 * (p0 + 64 * u));
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) {
+              y[u].x = fma(a.c[j], xv[u].x, y[u].x);
+              y[u].y = fma(a.c[j], xv[u].y, y[u].y);
+              st2nt(a.y[j] + 2 * (p0 + 64 * u), y[u]);
+              if (j == 0) y0[u] = y[u];
+              acc[j] = fma(y0[u].x, y[u].x, acc[j]);
+              acc[j] = fma(y0[u].y, y[u].y, acc[j]);
+            }
+          }
+        }
+      },
+      [&](size_t p) {
+        double2 xv = ld2(a.x + 2 * p);
+        xv.x *= a.xs;
+        xv.y *= a.xs;
+        if (a.store_x) *reinterpret_cast<double2*>(a.x + 2 * p) = xv;
+        double2 y0 = make_double2(0, 0);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            double2 y = ld2(a.y[j] + 2 * p);
+            y.x = fma(a.c[j], xv.x, y.x);
+            y.y = fma(a.c[j], xv.y, y.y);
+            *reinterpret_cast<double2*>(a.y[j] + 2 * p) = y;
+            if (j == 0) y0 = y;
+            acc[j] = fma(y0.x, y.x, acc[j]);
+            acc[j] = fma(y0.y, y.y, acc[j]);
+          }
+        }
+      },
+      [&](size_t e) {
+        const double xe = a.x[e] * a.xs;
+        if (a.store_x) a.x[e] = xe;
+        double y0 = 0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            const double y = fma(a.c[j], xe, a.y[j][e]);
+            a.y[j][e] = y;
+            if (j == 0) y0 = y;
+            acc[j] = fma(y0, y, acc[j]);
+          }
+        }
+      });
+  block_partials<M>(acc, a.m, a.partial);
+  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+}
+
 int check_ptrs(const double* const* v, int count, size_t n, const char* what) {
   if (count > 0 && !v) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null vector list");
   if (n == 0) return SSP_OK;
@@ -1060,6 +1151,62 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
   SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, 1));
   return ssp::fetch_result(ctx, out, 1);
+}
+
+int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store_x, double* const* yy, int m,
+                  size_t n, double* out) {
+  SSP_CHECK_CTX(ctx);
+  if (m < 1) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_gram: needs at least one destination");
+  if (!c || !out) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_gram: null coefficients or out");
+  SSP_TRY(check_ptrs(const_cast<const double* const*>(&x), 1, n, "ssp_axpy_gram"));
+  SSP_TRY(check_ptrs(const_cast<const double* const*>(yy), m, n, "ssp_axpy_gram"));
+  for (int j = 0; j < m; ++j) {
+    if (yy[j] == x) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_gram: a destination aliases x");
+    for (int i = 0; i < j; ++i)
+      if (yy[i] == yy[j]) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_gram: repeated destination");
+  }
+  if (m > ssp::kOuterDst) {  // more than one launch: the unfused sequence, same values
+    const double* xp = x;
+    SSP_TRY(ssp_gemm_outer_scaled(ctx, c, &xp, &xs, 1, yy, nullptr, m, n));
+    if (store_x && xs != 1.0) SSP_TRY(ssp_scal(ctx, xs, x, n));
+    const double* y0 = yy[0];
+    return ssp_gemm_inner(ctx, &y0, 1, const_cast<const double* const*>(yy), m, n, out);
+  }
+  SSP_TRY(ssp::ensure_result(ctx, size_t(m)));
+  ssp::FoldTail tail{};
+  if (n == 0) {
+    SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, size_t(m) * sizeof(double), ctx->stream));
+  } else {
+    SSP_TRY(ssp::fold_begin(ctx, m, &tail));
+    const bool st = store_x && xs != 1.0;
+    ssp::LedgerScope ls(ctx, "axpy_gram", 8.0 * n * ((st ? 2.0 : 1.0) + 2.0 * m));
+    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, 8);
+    AxpyGramArgs a{};
+    a.x = x;
+    a.xs = xs;
+    a.store_x = st ? 1 : 0;
+    a.m = m;
+    a.n = n;
+    for (int j = 0; j < m; ++j) {
+      a.y[j] = yy[j];
+      a.c[j] = c[j];
+    }
+    SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * m));
+    a.partial = ctx->partial;
+    a.tail = tail;
+    if (m <= 1)
+      hipLaunchKernelGGL((k_axpy_gram<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else if (m <= 4)
+      hipLaunchKernelGGL((k_axpy_gram<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else if (m <= 8)
+      hipLaunchKernelGGL((k_axpy_gram<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else
+      hipLaunchKernelGGL((k_axpy_gram<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_TRY_HIP(hipGetLastError());
+  }
+  if (tail.counter) return ssp::fold_finish(ctx, tail, out);
+  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, size_t(m)));
+  return ssp::fetch_result(ctx, out, size_t(m));
 }
 
 int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const* yy, int m, const double* z, size_t n,

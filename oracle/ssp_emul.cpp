@@ -355,6 +355,22 @@ int ssp_axpy_norm(ssp_ctx* c, const double* cc, const double* x, double* const* 
   *out = dot_n(yy[0], yy[0], n);
   return reduce(c, out, 1);
 }
+int ssp_axpy_gram(ssp_ctx* c, const double* cc, double* x, double xs, int store_x, double* const* yy, int m, size_t n,
+                  double* out) {
+  if (m < 1 || !cc || !out) return fail(SSP_ERR_ARG, "ssp_axpy_gram: bad arguments");
+  const bool st = store_x && xs != 1.0;
+  if (st)
+    trace("axpy_gram", {x}, {x}, nullptr, 0, yy, m);
+  else
+    trace("axpy_gram", {x}, {}, nullptr, 0, yy, m);
+  std::vector<double> xv(n);
+  for (size_t e = 0; e < n; ++e) xv[e] = x[e] * xs;
+  if (st) std::copy(xv.begin(), xv.end(), x);
+  for (int j = 0; j < m; ++j)
+    for (size_t e = 0; e < n; ++e) yy[j][e] = madd(cc[j], xv[e], yy[j][e]);
+  for (int j = 0; j < m; ++j) out[j] = dot_n(yy[0], yy[j], n);
+  return reduce(c, out, size_t(m));
+}
 int ssp_precondition(ssp_ctx*, double* const* a, int nvec, const double* d, const double* shift, size_t n) {
   trace("precondition", {d}, {}, nullptr, 0, a, nvec);
   for (int v = 0; v < nvec; ++v)

@@ -24,8 +24,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "emul_worker.py")
 
 
-def test_single_rank_api_and_loop_parity():
-    r = subprocess.run([sys.executable, WORKER, "api"], capture_output=True, text=True, timeout=600)
+# SSP_ORTHO=one_pass: the one-pass self-orthonormalisation (ssp_axpy_gram), which the product selects
+# from 2^20 elements, forced on at these sizes (hbm_handlers.h fused_orthonormalise)
+ORTHO = [{}, {"SSP_ORTHO": "one_pass"}]
+
+
+@pytest.mark.parametrize("ortho", ORTHO, ids=["auto", "one_pass"])
+def test_single_rank_api_and_loop_parity(ortho):
+    r = subprocess.run([sys.executable, WORKER, "api"], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, **ortho))
     assert r.returncode == 0 and "api OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
 
 
@@ -46,14 +53,15 @@ def test_world2_sharded_solvers_gloo():
     assert r.returncode == 0 and r.stdout.count("OK") == 2, r.stdout[-3000:] + r.stderr[-3000:]
 
 
-def test_world8_c4_c5_sharded_against_independent_restatement():
+@pytest.mark.parametrize("ortho", ORTHO, ids=["auto", "one_pass"])
+def test_world8_c4_c5_sharded_against_independent_restatement(ortho):
     # the driver's 8-GPU configuration (C4: 8 roots + P 16 sharded over 8 ranks; C5: DIIS sharded) on
     # the host emulation, each rank holding its index range: the same steps as the independent
     # numpy restatement and the unsharded CPU path
     port = free_port()
     procs = [subprocess.Popen([sys.executable, WORKER, "c4"],
                               env=dict(os.environ, RANK=str(r), WORLD_SIZE="8", SSP_HUB_PORT=str(port),
-                                       OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1"),
+                                       OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", **ortho),
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(8)]
     outs = [p.communicate(timeout=900)[0] for p in procs]
     for p, out in zip(procs, outs):

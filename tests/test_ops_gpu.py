@@ -197,6 +197,33 @@ def test_scal_inner_and_axpy_norm_fused_orthonormalisation(ctx, m, n):
     assert abs(nrm2 - math.fsum(y0 * y0)) <= red_tol(y0 * y0)
 
 
+@pytest.mark.parametrize("store", [True, False])
+@pytest.mark.parametrize("m", [1, 3, 7, 16, 17])
+@pytest.mark.parametrize("n", [0, 1, 7, 1003, 100_003])
+def test_axpy_gram_one_pass_orthonormalisation_step(ctx, m, n, store):
+    # ssp_axpy_gram == scal(xs, x) (stored when store), gemm_outer({x_s} -> yy), gemm_inner({yy[0]}, yy):
+    # x and yy bit-identical to the unfused calls, the Gram row to reduction rounding.
+    r = rng(m * 13 + n + store)
+    x = r.uniform(-1, 1, n)
+    ys = [r.uniform(-1, 1, n) for _ in range(m)]
+    c = r.uniform(-1, 1, m)
+    xs = 0.37
+    dx, dy = ctx.upload(x), [ctx.upload(v) for v in ys]
+    got = ctx.axpy_gram(c, dx, xs, dy, store_x=store)
+    x_s = oracle.scal(xs, x)
+    assert np.array_equal(dx.numpy(), x_s if store else x)
+    ex, ey = ctx.upload(x_s), [ctx.upload(v) for v in ys]
+    if n:
+        ctx.gemm_outer(c.reshape(1, m), [ex], ey)
+    for v, w in zip(dy, ey):
+        assert np.array_equal(v.numpy(), w.numpy())  # bit-identical to scal + gemm_outer
+    ynew = [v.numpy() for v in dy]
+    for j in range(m):
+        assert abs(got[j] - math.fsum(ynew[0] * ynew[j])) <= red_tol(ynew[0] * ynew[j])
+    for v in [dx, ex] + dy + ey:
+        v.free()
+
+
 @pytest.mark.parametrize("k,m", [(0, 3), (1, 1), (48, 8), (60, 8), (5, 16), (65, 17)])
 @pytest.mark.parametrize("n", [1, 1003, 100_003])
 def test_gemm_outer_set_equals_fill_then_gemm_outer(ctx, k, m, n):
