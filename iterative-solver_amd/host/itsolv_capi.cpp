@@ -91,27 +91,33 @@ class SyntheticProblem : public Problem<Vec, SparseP> {
       for (size_t j : idx) m.push_back(m_s.h(i, j));
     return m;
   }
-  // actions[k] += sum_p c[k][p] H e_{i_p}: diagonal part as a sparse axpy, low-rank part on the device.
+  // actions[k] += sum_p c[k][p] H e_{i_p}: diagonal part as a sparse axpy per action, then the
+  // low-rank part of every action in one device pass (the sign table read once for all of them;
+  // per element the same two updates in the same order as action by action).
   void p_action(const std::vector<std::vector<double>>& c, const CVecRef<SparseP>& pp,
                 const VecRef<Vec>& actions) const override {
+    if (c.empty()) return;
+    const size_t rank = size_t(m_s.rank);
+    std::vector<double> w(c.size() * rank, 0.0);
+    std::vector<double*> yp;
     for (size_t k = 0; k < c.size(); ++k) {
       auto& a = actions[k].get();
       std::vector<size_t> idx;
       std::vector<double> val;
-      std::vector<double> w(size_t(m_s.rank), 0.0);
       for (size_t p = 0; p < pp.size(); ++p) {
         for (auto& [i, coef] : pp[p].get()) {
           idx.push_back(i);
           val.push_back(m_s.d(i) * coef * c[k][p]);
-          for (int l = 0; l < m_s.rank; ++l) w[size_t(l)] += c[k][p] * coef * m_s.u(l, i);
+          for (size_t l = 0; l < rank; ++l) w[k * rank + l] += c[k][p] * coef * m_s.u(int(l), i);
         }
       }
       check(ssp_sparse_axpy(ctx(), 1.0, idx.data(), val.data(), idx.size(), a.data_rw(), a.local_size(), a.offset()),
             "ssp_sparse_axpy");
-      double* yp[1] = {a.data_rw()};
-      check(sspx_synth_add_lowrank(ctx(), &m_c, yp, 1, a.local_size(), a.offset(), w.data()),
-            "sspx_synth_add_lowrank");
+      yp.push_back(a.data_rw());
     }
+    const auto& a0 = actions.front().get();
+    check(sspx_synth_add_lowrank(ctx(), &m_c, yp.data(), int(yp.size()), a0.local_size(), a0.offset(), w.data()),
+          "sspx_synth_add_lowrank");
   }
 
  private:

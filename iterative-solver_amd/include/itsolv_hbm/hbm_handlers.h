@@ -142,7 +142,7 @@ inline bool fused_new_combinations(array::ArrayHandler<Vec, Vec>&, const itsolv:
 // scale (a relative 1e-16), the decisions (norm > norm_thresh) come from the same norms.  Bytes for
 // nR = 8 vectors: 8N(8 + 7 (1 + 1) + 2 * 28) = 624N (+ the last vector's deferred scal), against 864N
 // in two passes per vector (ssp_scal_inner + ssp_axpy_norm, round 2), and 8 reductions instead of 15
-// (C3 at N = 1e8: solve 0.509 -> 0.479 s, 25.4 -> 13.4 reductions per iteration).
+// (C3 at N = 1e8: solve 0.509 -> 0.479 s, 25.4 -> 19.4 reductions per iteration).
 //
 // Vectors shorter than kOnePassMinSize (global length) keep the two-pass form, whose coefficients
 // are the reference's own dots of the scaled vector: there the passes are launch-bound, so one pass
