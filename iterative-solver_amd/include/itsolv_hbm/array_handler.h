@@ -361,6 +361,16 @@ bool fused_new_combinations(H&, const Matrix<double>&, const std::vector<const Q
   return false;
 }
 
+// Hook for the new rows of the subspace matrices (xspace::update_qspace_data, reference
+// XSpace.h:30-83, which issues one overlap per block): out = the overlaps of `rows` with the column
+// sets `cols` concatenated, in one batched gemm_inner that reads the rows once per launch instead of
+// once per block; returns false when the handler has no such form.  Found by argument-dependent
+// lookup.
+template <class H, class RefL, class RefC, class M>
+bool fused_overlap_rows(H&, const RefL&, const std::vector<RefC>&, M&) {
+  return false;
+}
+
 // Hook for a fused sequential self-orthonormalisation of R (reference propose_rspace.h:450-465):
 // returns false when the handler has no fused form (the caller then runs the reference loop of
 // dot / scal / dot / axpy calls).  Found by argument-dependent lookup.

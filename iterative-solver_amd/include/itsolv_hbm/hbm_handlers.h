@@ -131,6 +131,33 @@ inline bool fused_new_combinations(array::ArrayHandler<Vec, Vec>&, const itsolv:
   return true;
 }
 
+// Global vector length from which the solver's multi-block passes are fused (the one-pass
+// self-orthonormalisation, the batched overlap rows): below it the passes are launch-bound, fusing
+// saves nothing measurable, and the reference's small test problems keep the call-by-call sequence
+// whose rounding their knife-edge cases were signed off on.
+// SSP_FUSED_MIN_SIZE overrides it (tests run the fused forms at small sizes with 0).
+inline size_t fused_min_size() {
+  static const size_t v = [] {
+    const char* e = std::getenv("SSP_FUSED_MIN_SIZE");
+    return e ? size_t(std::strtoull(e, nullptr, 10)) : size_t(1) << 20;
+  }();
+  return v;
+}
+
+// The new rows of the subspace matrices as one batched gemm_inner (array::fused_overlap_rows hook,
+// xspace::update_qspace_data, append_overlap_with_r): the C ABI splits the columns over launches of
+// <= 64, each reading the rows once (kernels_panel.hip), where the block-by-block overlaps read them
+// once per block.  Each entry is the same dot either way, up to the kernel instance's summation order.
+inline bool fused_overlap_rows(array::ArrayHandler<Vec, Vec>& h, const itsolv::CVecRef<Vec>& rows,
+                               const std::vector<itsolv::CVecRef<Vec>>& cols, itsolv::subspace::Matrix<double>& out) {
+  if (rows.empty() || rows.front().get().size() < fused_min_size()) return false;
+  itsolv::CVecRef<Vec> all;
+  for (const auto& c : cols) all.insert(all.end(), c.begin(), c.end());
+  if (all.empty()) return false;
+  out = h.gemm_inner(rows, all);
+  return true;
+}
+
 // Sequential self-orthonormalisation of R (reference propose_rspace.h:450-465: for each i,
 // |r_i| = sqrt(<r_i, r_i>); r_i *= 1/|r_i|; for j > i: r_j -= <r_i, r_j> r_i), one pass per vector
 // (array::fused_orthonormalise hook, found by argument-dependent lookup).  The Gram row of r_0 is one
@@ -144,14 +171,13 @@ inline bool fused_new_combinations(array::ArrayHandler<Vec, Vec>&, const itsolv:
 // in two passes per vector (ssp_scal_inner + ssp_axpy_norm, round 2), and 8 reductions instead of 15
 // (C3 at N = 1e8: solve 0.509 -> 0.479 s, 25.4 -> 19.4 reductions per iteration).
 //
-// Vectors shorter than kOnePassMinSize (global length) keep the two-pass form, whose coefficients
+// Vectors shorter than fused_min_size() (global length) keep the two-pass form, whose coefficients
 // are the reference's own dots of the scaled vector: there the passes are launch-bound, so one pass
 // saves nothing measurable, and the reference's small test problems include near-singular linear
 // equations (test_LinearEquations.cpp symmetric_system, n <= 33, up to 13 roots) whose final
 // residual is decided by last-bit rounding -- the CPU path itself misses the reference test's 1e-4
 // residual criterion on a few of its last-bit-perturbed inputs -- and on them the one-pass rounding
 // drew an unlucky case where the two-pass one did not.
-constexpr size_t kOnePassMinSize = size_t(1) << 20;
 inline bool orthonormalise_two_pass(const itsolv::VecRef<Vec>& rr, double norm_thresh, std::vector<int>& null_params);
 
 inline bool fused_orthonormalise(array::ArrayHandler<Vec, Vec>&, const itsolv::VecRef<Vec>& rr, double norm_thresh,
@@ -165,7 +191,7 @@ inline bool fused_orthonormalise(array::ArrayHandler<Vec, Vec>&, const itsolv::V
     if (!e) return 0;
     return std::string(e) == "one_pass" ? 1 : std::string(e) == "two_pass" ? 2 : 0;
   }();
-  if (forced == 2 || (forced == 0 && rr[0].get().size() < kOnePassMinSize))
+  if (forced == 2 || (forced == 0 && rr[0].get().size() < fused_min_size()))
     return orthonormalise_two_pass(rr, norm_thresh, null_params);
   ssp_ctx* ctx = rr[0].get().ctx();
   const size_t n = rr[0].get().local_size();

@@ -18,6 +18,7 @@
 #include <set>
 #include <sstream>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "dense.h"
@@ -141,10 +142,27 @@ Matrix<double> append_overlap_with_r(const Matrix<double>& overlap, const CVecRe
   const size_t oQ = nP, oD = oQ + nQ, oN = oD + nD, nX = oN + nN;
   auto ov = overlap;
   ov.resize({nX, nX});
-  ov.slice({oN, oN}, {nX, nX}) = subspace::util::overlap(params, h.rr());
+  bool fused = false;
+  if constexpr (std::is_same_v<R, Q>) {
+    // the blocks whose rows are the new parameters as one batched overlap where the handler has it
+    // (array::fused_overlap_rows): columns [params, Q params, D params]
+    Matrix<double> g;
+    using array::fused_overlap_rows;
+    if (nN > 0 && fused_overlap_rows(h.rr(), params, std::vector<CVecRef<R>>{params, qp, dp}, g)) {
+      fused = true;
+      for (size_t i = 0; i < nN; ++i) {
+        for (size_t j = 0; j <= i; ++j) ov(oN + i, oN + j) = ov(oN + j, oN + i) = g(i, j);
+        for (size_t j = 0; j < nQ; ++j) ov(oN + i, oQ + j) = g(i, nN + j);
+        for (size_t j = 0; j < nD; ++j) ov(oN + i, oD + j) = g(i, nN + nQ + j);
+      }
+    }
+  }
+  if (!fused) {
+    ov.slice({oN, oN}, {nX, nX}) = subspace::util::overlap(params, h.rr());
+    ov.slice({oN, oQ}, {nX, oQ + nQ}) = subspace::util::overlap(params, qp, h.rq());
+    ov.slice({oN, oD}, {nX, oD + nD}) = subspace::util::overlap(params, dp, h.rq());
+  }
   ov.slice({oN, 0}, {nX, nP}) = subspace::util::overlap(params, pp, h.rp());
-  ov.slice({oN, oQ}, {nX, oQ + nQ}) = subspace::util::overlap(params, qp, h.rq());
-  ov.slice({oN, oD}, {nX, oD + nD}) = subspace::util::overlap(params, dp, h.rq());
   for (size_t i = 0; i < oN; ++i)
     for (size_t j = 0; j < nN; ++j) ov(i, oN + j) = ov(oN + j, i);
   return ov;

@@ -16,6 +16,7 @@
 #include <map>
 #include <memory>
 #include <stdexcept>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -348,13 +349,41 @@ class XSpace {
     const auto pp = cparamsp();
     const auto qp = cparamsq(), qa = cactionsq(), dp = cparamsd(), da = cactionsd();
     const auto& lhs_h = m_action_dot_action ? actions : params;
-    qq[EqnData::S] = util::overlap(params, h.rr());
+    bool fused = false;
+    if constexpr (std::is_same_v<R, Q>) {
+      // every block whose rows are the new parameters, as one batched overlap where the handler has
+      // it: columns [params, actions, Q params, Q actions, D params, D actions, rhs]
+      Matrix<double> g;
+      using array::fused_overlap_rows;
+      if (!m_action_dot_action && nn > 0 &&
+          fused_overlap_rows(h.rr(), params, std::vector<CVecRef<R>>{params, actions, qp, qa, dp, da, rhs()}, g)) {
+        fused = true;
+        const size_t cA = nn, cQ = 2 * nn, cQA = cQ + d.nQ, cD = cQA + d.nQ, cDA = cD + d.nD, cR = cDA + d.nD;
+        for (size_t i = 0; i < nn; ++i) {
+          for (size_t j = 0; j <= i; ++j) qq[EqnData::S](i, j) = qq[EqnData::S](j, i) = g(i, j);
+          for (size_t j = 0; j < nn; ++j) qq[EqnData::H](i, j) = g(i, cA + j);
+          for (size_t j = 0; j < d.nQ; ++j) {
+            qx[EqnData::S](i, d.oQ + j) = g(i, cQ + j);
+            qx[EqnData::H](i, d.oQ + j) = g(i, cQA + j);
+          }
+          for (size_t j = 0; j < d.nD; ++j) {
+            qx[EqnData::S](i, d.oD + j) = g(i, cD + j);
+            qx[EqnData::H](i, d.oD + j) = g(i, cDA + j);
+          }
+          for (size_t j = 0; j < m_rhs.size(); ++j) qq[EqnData::rhs](i, j) = g(i, cR + j);
+        }
+      }
+    }
+    if (!fused) {
+      qq[EqnData::S] = util::overlap(params, h.rr());
+      qx[EqnData::S].slice({0, d.oQ}, {nn, d.oQ + d.nQ}) = util::overlap(params, qp, h.rq());
+      qx[EqnData::S].slice({0, d.oD}, {nn, d.oD + d.nD}) = util::overlap(params, dp, h.rq());
+      qq[EqnData::H] = m_action_dot_action ? util::overlap(actions, h.rr()) : util::overlap(params, actions, h.rr());
+      qx[EqnData::H].slice({0, d.oQ}, {nn, d.oQ + d.nQ}) = util::overlap(lhs_h, qa, h.rq());
+      qx[EqnData::H].slice({0, d.oD}, {nn, d.oD + d.nD}) = util::overlap(lhs_h, da, h.rq());
+      qq[EqnData::rhs] = util::overlap(params, rhs(), h.rq());
+    }
     qx[EqnData::S].slice({0, d.oP}, {nn, d.oP + d.nP}) = util::overlap(params, pp, h.rp());
-    qx[EqnData::S].slice({0, d.oQ}, {nn, d.oQ + d.nQ}) = util::overlap(params, qp, h.rq());
-    qx[EqnData::S].slice({0, d.oD}, {nn, d.oD + d.nD}) = util::overlap(params, dp, h.rq());
-    qq[EqnData::H] = m_action_dot_action ? util::overlap(actions, h.rr()) : util::overlap(params, actions, h.rr());
-    qx[EqnData::H].slice({0, d.oQ}, {nn, d.oQ + d.nQ}) = util::overlap(lhs_h, qa, h.rq());
-    qx[EqnData::H].slice({0, d.oD}, {nn, d.oD + d.nD}) = util::overlap(lhs_h, da, h.rq());
     if (m_hermitian) {
       xq[EqnData::H].slice({d.oP, 0}, {d.oP + d.nP, nn}) = util::overlap(pp, actions, h.rp());
       transpose_copy(xq[EqnData::H].slice({d.oQ, 0}, {d.oQ + d.nQ, nn}), qx[EqnData::H].slice({0, d.oQ}, {nn, d.oQ + d.nQ}));
@@ -364,7 +393,6 @@ class XSpace {
       xq[EqnData::H].slice({d.oQ, 0}, {d.oQ + d.nQ, nn}) = util::overlap(qp, actions, h.rq());
       xq[EqnData::H].slice({d.oD, 0}, {d.oD + d.nD, nn}) = util::overlap(dp, actions, h.rq());
     }
-    qq[EqnData::rhs] = util::overlap(params, rhs(), h.rq());
     transpose_copy(xq[EqnData::S].slice({d.oP, 0}, {d.oP + d.nP, nn}), qx[EqnData::S].slice({0, d.oP}, {nn, d.oP + d.nP}));
     transpose_copy(xq[EqnData::S].slice({d.oQ, 0}, {d.oQ + d.nQ, nn}), qx[EqnData::S].slice({0, d.oQ}, {nn, d.oQ + d.nQ}));
     transpose_copy(xq[EqnData::S].slice({d.oD, 0}, {d.oD + d.nD, nn}), qx[EqnData::S].slice({0, d.oD}, {nn, d.oD + d.nD}));

@@ -24,12 +24,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "emul_worker.py")
 
 
-# SSP_ORTHO=one_pass: the one-pass self-orthonormalisation (ssp_axpy_gram), which the product selects
-# from 2^20 elements, forced on at these sizes (hbm_handlers.h fused_orthonormalise)
-ORTHO = [{}, {"SSP_ORTHO": "one_pass"}]
+# SSP_FUSED_MIN_SIZE=0: the fused solver passes the product selects from 2^20 elements -- the one-pass
+# self-orthonormalisation (ssp_axpy_gram) and the batched overlap rows (hbm_handlers.h) -- forced on
+# at these sizes
+ORTHO = [{}, {"SSP_FUSED_MIN_SIZE": "0"}]
 
 
-@pytest.mark.parametrize("ortho", ORTHO, ids=["auto", "one_pass"])
+@pytest.mark.parametrize("ortho", ORTHO, ids=["auto", "fused"])
 def test_single_rank_api_and_loop_parity(ortho):
     r = subprocess.run([sys.executable, WORKER, "api"], capture_output=True, text=True, timeout=600,
                        env=dict(os.environ, **ortho))
@@ -53,7 +54,7 @@ def test_world2_sharded_solvers_gloo():
     assert r.returncode == 0 and r.stdout.count("OK") == 2, r.stdout[-3000:] + r.stderr[-3000:]
 
 
-@pytest.mark.parametrize("ortho", ORTHO, ids=["auto", "one_pass"])
+@pytest.mark.parametrize("ortho", ORTHO, ids=["auto", "fused"])
 def test_world8_c4_c5_sharded_against_independent_restatement(ortho):
     # the driver's 8-GPU configuration (C4: 8 roots + P 16 sharded over 8 ranks; C5: DIIS sharded) on
     # the host emulation, each rank holding its index range: the same steps as the independent
