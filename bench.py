@@ -289,7 +289,7 @@ def cpu_trace(kind, n_global):
     if ref and kind == "davidson" and ref["options"].get("max_size_qspace") != C3["max_size_qspace"]:
         return None, None
     return name, ref
-REDUCING_OPS = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "axpy_gram", "select", "gemm_inner_sparse")
+REDUCING_OPS = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "axpy_gram", "axpy_pairs_norm", "select", "gemm_inner_sparse")
 
 
 def in_solver(ctx, n_global, world, barrier, repeat=2, kind="davidson"):

@@ -141,6 +141,12 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
  *                    bit-identical)                                           bytes 8N(1 + store + 2m) */
 int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store_x, double* const* yy, int m,
                   size_t n, double* out);
+/* Residuals and their norms (construct_residual + update_errors, reference
+ * LinearEigensystemDavidson.h:186-192, IterativeSolverTemplate.h:95-102) in one pass:
+ *   yy[j] = ys[j] yy[j] + c[j] (xs[j] xx[j])  (= ssp_axpy_scaled per pair, yy bit-identical),
+ *   out[j] = <yy[j], yy[j]> summed over ranks.  xs / ys may be null (all 1).   bytes 24N m */
+int ssp_axpy_pairs_norm(ssp_ctx* ctx, const double* c, const double* const* xx, const double* xs, double* const* yy,
+                        const double* ys, int m, size_t n, double* out);
 /* a[v][i] /= (d[i] - shift[v] + 1e-15) for v in [0,nvec)   reference itsolv/IterativeSolver.h:34-55 */
 int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n);
 

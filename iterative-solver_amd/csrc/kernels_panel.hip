@@ -734,6 +734,75 @@ __global__ __launch_bounds__(kBlock) void k_axpy_gram(const AxpyGramArgs a) {
   if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
 }
 
+// Residuals and their norms in one pass (construct_residual + update_errors, reference
+// LinearEigensystemDavidson.h:186-192 and IterativeSolverTemplate.h:95-102): y_j = y_j s^y_j +
+// c_j (x_j s^x_j) -- ssp_axpy_scaled's fma, element for element -- then acc_j += y_j^2.
+struct AxpyPairsArgs {
+  const double* x[ssp::kOuterDst];
+  double* y[ssp::kOuterDst];
+  double c[ssp::kOuterDst];
+  double xs[ssp::kOuterDst];
+  double ys[ssp::kOuterDst];
+  int m;
+  size_t n;
+  double* partial;     // [gridDim.x][m]
+  ssp::FoldTail tail;  // fused fold when tail.counter is set
+};
+
+template <int M>
+__global__ __launch_bounds__(kBlock) void k_axpy_pairs_norm(const AxpyPairsArgs a) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  double acc[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) acc[j] = 0;
+  ssp::for_windows<kFusedU>(
+      a.n,
+      [&](size_t p0) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            double2 xv[kFusedU], yv[kFusedU];
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) xv[u] = sc2<true>(ld2nt(a.x[j] + 2 * (p0 + 64 * u)), a.xs[j]);
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) yv[u] = sc2<true>(ld2nt(a.y[j] + 2 * (p0 + 64 * u)), a.ys[j]);
+#pragma unroll
+            for (int u = 0; u < kFusedU; ++u) {
+              const double2 r = make_double2(fma(a.c[j], xv[u].x, yv[u].x), fma(a.c[j], xv[u].y, yv[u].y));
+              st2nt(a.y[j] + 2 * (p0 + 64 * u), r);
+              acc[j] = fma(r.x, r.x, acc[j]);
+              acc[j] = fma(r.y, r.y, acc[j]);
+            }
+          }
+        }
+      },
+      [&](size_t p) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            const double2 xv = sc2<true>(ld2(a.x[j] + 2 * p), a.xs[j]), yv = sc2<true>(ld2(a.y[j] + 2 * p), a.ys[j]);
+            const double2 r = make_double2(fma(a.c[j], xv.x, yv.x), fma(a.c[j], xv.y, yv.y));
+            *reinterpret_cast<double2*>(a.y[j] + 2 * p) = r;
+            acc[j] = fma(r.x, r.x, acc[j]);
+            acc[j] = fma(r.y, r.y, acc[j]);
+          }
+        }
+      },
+      [&](size_t e) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          if (j < a.m) {
+            const double r = fma(a.c[j], sc1<true>(a.x[j][e], a.xs[j]), sc1<true>(a.y[j][e], a.ys[j]));
+            a.y[j][e] = r;
+            acc[j] = fma(r, r, acc[j]);
+          }
+        }
+      });
+  block_partials<M>(acc, a.m, a.partial);
+  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+}
+
 int check_ptrs(const double* const* v, int count, size_t n, const char* what) {
   if (count > 0 && !v) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null vector list");
   if (n == 0) return SSP_OK;
@@ -1209,6 +1278,60 @@ int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store
       hipLaunchKernelGGL((k_axpy_gram<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else
       hipLaunchKernelGGL((k_axpy_gram<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_TRY_HIP(hipGetLastError());
+  }
+  if (tail.counter) return ssp::fold_finish(ctx, tail, out);
+  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, size_t(m)));
+  return ssp::fetch_result(ctx, out, size_t(m));
+}
+
+int ssp_axpy_pairs_norm(ssp_ctx* ctx, const double* c, const double* const* xx, const double* xs, double* const* yy,
+                        const double* ys, int m, size_t n, double* out) {
+  SSP_CHECK_CTX(ctx);
+  if (m < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_pairs_norm: negative dimension");
+  if (m == 0) return SSP_OK;
+  if (!c || !out) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_pairs_norm: null coefficients or out");
+  SSP_TRY(check_ptrs(xx, m, n, "ssp_axpy_pairs_norm"));
+  SSP_TRY(check_ptrs(const_cast<const double* const*>(yy), m, n, "ssp_axpy_pairs_norm"));
+  for (int j = 0; j < m; ++j)
+    for (int i = 0; i < m; ++i)
+      if (yy[j] == xx[i] || (i < j && yy[i] == yy[j]))
+        return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_pairs_norm: a destination aliases another operand");
+  if (m > ssp::kOuterDst) {  // more than one launch: the unfused sequence, same values
+    for (int j = 0; j < m; ++j)
+      SSP_TRY(ssp_axpy_scaled(ctx, c[j], xx[j], xs ? xs[j] : 1.0, yy[j], ys ? ys[j] : 1.0, n));
+    for (int j = 0; j < m; ++j) SSP_TRY(ssp_dot(ctx, yy[j], yy[j], n, out + j));
+    return SSP_OK;
+  }
+  SSP_TRY(ssp::ensure_result(ctx, size_t(m)));
+  ssp::FoldTail tail{};
+  if (n == 0) {
+    SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, size_t(m) * sizeof(double), ctx->stream));
+  } else {
+    SSP_TRY(ssp::fold_begin(ctx, m, &tail));
+    ssp::LedgerScope ls(ctx, "axpy_pairs_norm", 24.0 * n * m);
+    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, 8);
+    AxpyPairsArgs a{};
+    a.m = m;
+    a.n = n;
+    for (int j = 0; j < m; ++j) {
+      a.x[j] = xx[j];
+      a.y[j] = yy[j];
+      a.c[j] = c[j];
+      a.xs[j] = xs ? xs[j] : 1.0;
+      a.ys[j] = ys ? ys[j] : 1.0;
+    }
+    SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * m));
+    a.partial = ctx->partial;
+    a.tail = tail;
+    if (m <= 1)
+      hipLaunchKernelGGL((k_axpy_pairs_norm<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else if (m <= 4)
+      hipLaunchKernelGGL((k_axpy_pairs_norm<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else if (m <= 8)
+      hipLaunchKernelGGL((k_axpy_pairs_norm<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    else
+      hipLaunchKernelGGL((k_axpy_pairs_norm<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);

@@ -371,6 +371,15 @@ bool fused_overlap_rows(H&, const RefL&, const std::vector<RefC>&, M&) {
   return false;
 }
 
+// Hook for the residuals and their norms in one pass (construct_residual, reference
+// LinearEigensystemDavidson.h:186-192: r_i += c_i x_i, then update_errors' self-dots,
+// IterativeSolverTemplate.h:95-102): norms2[i] = <r_i, r_i> of the updated residuals; returns false
+// when the handler has no such form.  Found by argument-dependent lookup.
+template <class H, class RefX, class RefR>
+bool fused_residual_norms(H&, const std::vector<double>&, const RefX&, const RefR&, std::vector<double>&) {
+  return false;
+}
+
 // Hook for a fused sequential self-orthonormalisation of R (reference propose_rspace.h:450-465):
 // returns false when the handler has no fused form (the caller then runs the reference loop of
 // dot / scal / dot / axpy calls).  Found by argument-dependent lookup.

@@ -158,6 +158,26 @@ inline bool fused_overlap_rows(array::ArrayHandler<Vec, Vec>& h, const itsolv::C
   return true;
 }
 
+// construct_residual's axpys and update_errors' self-dots as one pass (array::fused_residual_norms
+// hook, ssp_axpy_pairs_norm): the residuals element for element the handler's axpy, the norms the
+// same dots up to summation order; from fused_min_size() (as the other fused solver passes).
+inline bool fused_residual_norms(array::ArrayHandler<Vec, Vec>&, const std::vector<double>& c,
+                                 const itsolv::CVecRef<Vec>& xx, const itsolv::VecRef<Vec>& yy,
+                                 std::vector<double>& norms2) {
+  const size_t m = yy.size();
+  if (m == 0 || xx.size() < m || c.size() < m || yy.front().get().size() < fused_min_size()) return false;
+  std::vector<double> xs, ys;
+  auto xp = detail::deferred_ptrs(itsolv::CVecRef<Vec>(xx.begin(), xx.begin() + long(m)), xs);
+  auto yp = detail::rw_deferred_ptrs(yy, ys);
+  norms2.assign(m, 0.0);
+  const auto& y0 = yy.front().get();
+  check(ssp_axpy_pairs_norm(y0.ctx(), c.data(), xp.data(), xs.data(), yp.data(), ys.data(), int(m), y0.local_size(),
+                            norms2.data()),
+        "ssp_axpy_pairs_norm");
+  detail::scales_applied(yy);
+  return true;
+}
+
 // Sequential self-orthonormalisation of R (reference propose_rspace.h:450-465: for each i,
 // |r_i| = sqrt(<r_i, r_i>); r_i *= 1/|r_i|; for j > i: r_j -= <r_i, r_j> r_i), one pass per vector
 // (array::fused_orthonormalise hook, found by argument-dependent lookup).  The Gram row of r_0 is one

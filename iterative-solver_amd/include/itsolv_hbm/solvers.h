@@ -547,9 +547,15 @@ class IterativeSolverTemplate {
     for (const auto& [s0, s1] : batches) {
       std::vector<int> roots(s1 - s0);
       std::iota(roots.begin(), roots.end(), int(s0));
+      m_residual_norms2.clear();
       solution(roots, parameters, action);
       std::vector<double> errors(roots.size(), 0);
-      detail::update_errors(errors, cwrap(action), m_handlers->rr());
+      if (m_residual_norms2.size() == roots.size()) {  // from a fused construct_residual
+        for (size_t i = 0; i < errors.size(); ++i) errors[i] = std::sqrt(std::abs(m_residual_norms2[i]));
+      } else {
+        detail::update_errors(errors, cwrap(action), m_handlers->rr());
+      }
+      m_residual_norms2.clear();
       if (batches.size() > 1) {
         for (size_t i = 0; i < roots.size(); ++i)
           temp.emplace_back(m_handlers->qr().copy(parameters[i]), m_handlers->qr().copy(action[i]));
@@ -589,6 +595,7 @@ class IterativeSolverTemplate {
   std::shared_ptr<Statistics> m_stats;
   std::shared_ptr<Logger> m_logger;
   std::vector<double> m_errors, m_value_errors;
+  std::vector<double> m_residual_norms2;  // <r_i, r_i> left by a fused construct_residual (solution())
   std::vector<int> m_working_set;
   size_t m_nroots = 0;
   double m_convergence_threshold = 1.0e-8;
@@ -768,10 +775,18 @@ class LinearEigensystemDavidson : public DavidsonSolver<R, Q, P> {
     if (!this->m_resetting) m_last_values = cur;
   }
 
-  // r_i -= lambda_i x_i (reference LinearEigensystemDavidson.h:186-192)
+  // r_i -= lambda_i x_i (reference LinearEigensystemDavidson.h:186-192); where the handler fuses the
+  // axpys with the residual norms (array::fused_residual_norms), the norms are kept for
+  // solve_and_generate_working_set's update_errors instead of being read back in a second pass.
   void construct_residual(const std::vector<int>& roots, const CVecRef<R>& params, const VecRef<R>& actions) override {
     const auto& ev = eigenvalues();
-    for (size_t i = 0; i < roots.size(); ++i) this->m_handlers->rr().axpy(-ev.at(roots[i]), params.at(i), actions.at(i));
+    std::vector<double> c(roots.size());
+    for (size_t i = 0; i < roots.size(); ++i) c[i] = -ev.at(roots[i]);
+    using array::fused_residual_norms;
+    if (fused_residual_norms(this->m_handlers->rr(), c, params, VecRef<R>(actions.begin(), actions.begin() + long(roots.size())),
+                             this->m_residual_norms2))
+      return;
+    for (size_t i = 0; i < roots.size(); ++i) this->m_handlers->rr().axpy(c[i], params.at(i), actions.at(i));
   }
 
   std::vector<double> m_last_values;

@@ -35,7 +35,7 @@ EXPORTS = [
     "ssp_allreduce_sum", "ssp_allgather_host", "ssp_ctx_attach_host_comm", "ssp_shard_range", "ssp_select_merge",
     "ssp_ledger_enable", "ssp_ledger_reset", "ssp_ledger_count", "ssp_ledger_reserve",
     "ssp_ledger_entry", "ssp_fill", "ssp_scal", "ssp_copy", "ssp_axpy", "ssp_dot",
-    "ssp_gemm_inner", "ssp_gemm_outer", "ssp_gemm_outer_set", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_axpy_gram", "ssp_precondition", "ssp_select", "ssp_select_max_dot",
+    "ssp_gemm_inner", "ssp_gemm_outer", "ssp_gemm_outer_set", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_axpy_gram", "ssp_axpy_pairs_norm", "ssp_precondition", "ssp_select", "ssp_select_max_dot",
     "ssp_sparse_copy", "ssp_sparse_axpy", "ssp_sparse_dot", "ssp_gemm_inner_sparse", "ssp_gemm_outer_sparse",
     "ssp_construct_solution",
     "sspx_synthetic_action", "sspx_synthetic_add_lowrank", "sspx_synthetic_diagonal", "sspx_fill_random", "sspx_dense_action",
@@ -119,6 +119,7 @@ def _declare(lib):
         "ssp_scal_inner": (I, [P, C.c_double, P, P, I, Z, PD]),
         "ssp_axpy_norm": (I, [P, PD, P, P, I, Z, PD]),
         "ssp_axpy_gram": (I, [P, PD, P, D, I, P, I, Z, PD]),
+        "ssp_axpy_pairs_norm": (I, [P, PD, P, PD, P, PD, I, Z, PD]),
         "ssp_precondition": (I, [P, P, I, P, PD, Z]),
         "ssp_select": (I, [P, P, Z, Z, Z, I, I, PZ, PD, PZ]),
         "ssp_select_max_dot": (I, [P, P, P, Z, Z, Z, PZ, PD, PZ]),
@@ -541,6 +542,18 @@ class Context:
         out = np.zeros(max_(len(yy)))
         _check(self.lib.ssp_axpy_gram(self.handle, _dptr(cc), x.ptr, float(xs), int(store_x), _ptrs(yy), len(yy),
                                       x.n, _dptr(out)))
+        return out[:len(yy)]
+
+    def axpy_pairs_norm(self, c: Sequence[float], xx: Sequence[DeviceVector], yy: Sequence[DeviceVector],
+                        xs: Sequence[float] = None, ys: Sequence[float] = None) -> np.ndarray:
+        """yy[j] = ys[j] yy[j] + c[j] xs[j] xx[j], then returns <yy[j], yy[j]> (residuals and their norms)."""
+        cc = np.ascontiguousarray(c, dtype=np.float64)
+        sx = None if xs is None else np.ascontiguousarray(xs, dtype=np.float64)
+        sy = None if ys is None else np.ascontiguousarray(ys, dtype=np.float64)
+        out = np.zeros(max_(len(yy)))
+        _check(self.lib.ssp_axpy_pairs_norm(self.handle, _dptr(cc), _ptrs(xx), None if sx is None else _dptr(sx),
+                                            _ptrs(yy), None if sy is None else _dptr(sy), len(yy),
+                                            yy[0].n if yy else 0, _dptr(out)))
         return out[:len(yy)]
 
     def precondition(self, aa: Sequence[DeviceVector], d: DeviceVector, shift: Sequence[float]):

@@ -371,6 +371,17 @@ int ssp_axpy_gram(ssp_ctx* c, const double* cc, double* x, double xs, int store_
   for (int j = 0; j < m; ++j) out[j] = dot_n(yy[0], yy[j], n);
   return reduce(c, out, size_t(m));
 }
+int ssp_axpy_pairs_norm(ssp_ctx* c, const double* cc, const double* const* xx, const double* xs, double* const* yy,
+                        const double* ys, int m, size_t n, double* out) {
+  if (m < 0 || (m > 0 && (!cc || !out))) return fail(SSP_ERR_ARG, "ssp_axpy_pairs_norm: bad arguments");
+  trace("axpy_pairs_norm", {}, {}, xx, m, yy, m);
+  for (int j = 0; j < m; ++j) {
+    const double sx = xs ? xs[j] : 1.0, sy = ys ? ys[j] : 1.0;
+    for (size_t e = 0; e < n; ++e) yy[j][e] = madd(cc[j], xx[j][e] * sx, yy[j][e] * sy);
+    out[j] = dot_n(yy[j], yy[j], n);
+  }
+  return m ? reduce(c, out, size_t(m)) : SSP_OK;
+}
 int ssp_precondition(ssp_ctx*, double* const* a, int nvec, const double* d, const double* shift, size_t n) {
   trace("precondition", {d}, {}, nullptr, 0, a, nvec);
   for (int v = 0; v < nvec; ++v)

@@ -224,6 +224,31 @@ def test_axpy_gram_one_pass_orthonormalisation_step(ctx, m, n, store):
         v.free()
 
 
+@pytest.mark.parametrize("scaled", [False, True])
+@pytest.mark.parametrize("m", [1, 3, 8, 16, 17])
+@pytest.mark.parametrize("n", [0, 1, 7, 1003, 100_003])
+def test_axpy_pairs_norm_residuals_and_norms(ctx, m, n, scaled):
+    # ssp_axpy_pairs_norm == ssp_axpy_scaled per pair, then ssp_dot(yy[j], yy[j]): yy bit-identical,
+    # the norms to reduction rounding.
+    r = rng(m * 17 + n + scaled)
+    xs_ = [r.uniform(-1, 1, n) for _ in range(m)]
+    ys_ = [r.uniform(-1, 1, n) for _ in range(m)]
+    c = r.uniform(-2, 2, m)
+    sx = r.uniform(0.5, 2, m) if scaled else None
+    sy = r.uniform(0.5, 2, m) if scaled else None
+    dx, dy = [ctx.upload(v) for v in xs_], [ctx.upload(v) for v in ys_]
+    got = ctx.axpy_pairs_norm(c, dx, dy, sx, sy)
+    ey = [ctx.upload(v) for v in ys_]
+    for j in range(m):
+        ctx.axpy_scaled(c[j], dx[j], 1.0 if sx is None else sx[j], ey[j], 1.0 if sy is None else sy[j])
+    for j in range(m):
+        a, b = dy[j].numpy(), ey[j].numpy()
+        assert np.array_equal(a, b), j  # bit-identical to the per-pair axpy
+        assert abs(got[j] - math.fsum(a * a)) <= red_tol(a * a)
+    for v in dx + dy + ey:
+        v.free()
+
+
 @pytest.mark.parametrize("k,m", [(0, 3), (1, 1), (48, 8), (60, 8), (5, 16), (65, 17)])
 @pytest.mark.parametrize("n", [1, 1003, 100_003])
 def test_gemm_outer_set_equals_fill_then_gemm_outer(ctx, k, m, n):

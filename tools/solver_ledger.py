@@ -39,7 +39,7 @@ CONFIGS = {
     "C4-shard": ("davidson", 12_500_000, dict(rho=0.1, rank=8, seed=1, nroots=8, max_p=16, max_size_qspace=48,
                                               reset_D=8, convergence_threshold=1e-8)),
 }
-REDUCING = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "axpy_gram", "select", "gemm_inner_sparse")
+REDUCING = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "axpy_gram", "axpy_pairs_norm", "select", "gemm_inner_sparse")
 
 
 def run(ctx, name, repeat=2):
