@@ -373,6 +373,30 @@ class XSpace {
           for (size_t j = 0; j < m_rhs.size(); ++j) qq[EqnData::rhs](i, j) = g(i, cR + j);
         }
       }
+      // action . action (DIIS): the S rows from the parameters, the H rows from the actions -- two
+      // batched overlaps: [params, Q params, D params, rhs] and [actions, Q actions, D actions]
+      Matrix<double> ga;
+      if (m_action_dot_action && nn > 0 &&
+          fused_overlap_rows(h.rr(), params, std::vector<CVecRef<R>>{params, qp, dp, rhs()}, g) &&
+          fused_overlap_rows(h.rr(), actions, std::vector<CVecRef<R>>{actions, qa, da}, ga)) {
+        fused = true;
+        const size_t cQ = nn, cD = cQ + d.nQ, cR = cD + d.nD;
+        for (size_t i = 0; i < nn; ++i) {
+          for (size_t j = 0; j <= i; ++j) {
+            qq[EqnData::S](i, j) = qq[EqnData::S](j, i) = g(i, j);
+            qq[EqnData::H](i, j) = qq[EqnData::H](j, i) = ga(i, j);
+          }
+          for (size_t j = 0; j < d.nQ; ++j) {
+            qx[EqnData::S](i, d.oQ + j) = g(i, cQ + j);
+            qx[EqnData::H](i, d.oQ + j) = ga(i, nn + j);
+          }
+          for (size_t j = 0; j < d.nD; ++j) {
+            qx[EqnData::S](i, d.oD + j) = g(i, cD + j);
+            qx[EqnData::H](i, d.oD + j) = ga(i, nn + d.nQ + j);
+          }
+          for (size_t j = 0; j < m_rhs.size(); ++j) qq[EqnData::rhs](i, j) = g(i, cR + j);
+        }
+      }
     }
     if (!fused) {
       qq[EqnData::S] = util::overlap(params, h.rr());
