@@ -293,8 +293,10 @@ void run_diis(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R,
   out.nroots = 1;
   out.errors[0] = solver.errors().empty() ? 0.0 : solver.errors().front();
   out.eigenvalues[0] = 0;
+  // the solution's parameters only: its residual is recomputed from the problem right after (the
+  // solver's residual combination would be overwritten unread)
   R xs = make_vec(), gs = make_vec();
-  solver.solution(xs, gs);
+  solver.solution_params(std::vector<int>{0}, VecRef<R>{std::ref(xs)});
   problem.residual(xs, gs);
   out.residual_norms[0] = std::sqrt(std::abs(handlers->rr().dot(gs, gs)));
   if (emit) emit(xs);
