@@ -18,8 +18,8 @@ value = algorithmic bytes of all ranks per step x steps / (max over ranks of the
 Beside the headline the JSON line carries (none of them inside the timed region):
   product_step  the same update as the product's solver runs it: construct_solution as ONE
                 write-only pass per space (ssp_gemm_outer_set, IterativeSolverTemplate.h:33-65 fused,
-                8N(k + m) B) and the 8 root norms as one lazy-handle batch (ArrayHandler.h:298-437:
-                one gemm_inner launch, one reduction);
+                8N(k + m) B) and the residuals with their norms as one pass (construct_residual +
+                update_errors, ssp_axpy_pairs_norm: 24N B per root, one reduction);
   in_solver     whole LinearEigensystemDavidson solves (C3 at N = 1: 8 roots + P 16, rank-8 problem,
                 N = 1e8; at N > 1 the same solve sharded, BASELINE config C4): iterations, wall time,
                 kernel time and algorithmic bytes from the HIP-event ledger, reductions per iteration;
@@ -74,8 +74,7 @@ def step_bytes(n, m, k):
 def product_step_bytes(n, m, k):
     return (2 * 8 * n * (m + k)      # two gemm_inner
             + 2 * 8 * n * (k + m)    # two write-only construct_solution passes (gemm_outer_set)
-            + m * 24 * n             # residual axpy
-            + m * 8 * n)             # norms: one batched gemm_inner over the m residuals (x == y)
+            + m * 24 * n)            # residuals and their norms in one pass (ssp_axpy_pairs_norm)
 
 
 class Workload:
@@ -121,10 +120,8 @@ class Workload:
         c.gemm_inner(self.rp, self.qa)
         c.gemm_outer_set(self.coef, self.qp, self.rp)
         c.gemm_outer_set(self.coef, self.qa, self.ra)
-        for i in range(self.m):
-            c.axpy(-self.lam[i], self.rp[i], self.ra[i])
-        g = c.gemm_inner(self.ra, self.ra)
-        return float(np.max(np.diag(g)))
+        nrm2 = c.axpy_pairs_norm(-self.lam, self.rp, self.ra)
+        return float(np.max(nrm2))
 
 
 def op_kernels(op, m):

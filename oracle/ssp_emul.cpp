@@ -359,6 +359,7 @@ int ssp_axpy_gram(ssp_ctx* c, const double* cc, double* x, double xs, int store_
                   double* out) {
   if (m < 1 || !cc || !out) return fail(SSP_ERR_ARG, "ssp_axpy_gram: bad arguments");
   const bool st = store_x && xs != 1.0;
+  Led l(c, "axpy_gram", 8.0 * n * ((st ? 2.0 : 1.0) + 2.0 * m));
   if (st)
     trace("axpy_gram", {x}, {x}, nullptr, 0, yy, m);
   else
@@ -374,6 +375,7 @@ int ssp_axpy_gram(ssp_ctx* c, const double* cc, double* x, double xs, int store_
 int ssp_axpy_pairs_norm(ssp_ctx* c, const double* cc, const double* const* xx, const double* xs, double* const* yy,
                         const double* ys, int m, size_t n, double* out) {
   if (m < 0 || (m > 0 && (!cc || !out))) return fail(SSP_ERR_ARG, "ssp_axpy_pairs_norm: bad arguments");
+  Led l(c, "axpy_pairs_norm", 24.0 * n * m);
   trace("axpy_pairs_norm", {}, {}, xx, m, yy, m);
   for (int j = 0; j < m; ++j) {
     const double sx = xs ? xs[j] : 1.0, sy = ys ? ys[j] : 1.0;

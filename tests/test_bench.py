@@ -133,7 +133,7 @@ def test_bench_eight_ranks_emulated():
     assert set(d["ops"]) == {"gemm_inner", "gemm_outer", "fill", "axpy", "dot"}
     # the product's own form of the step, and the sharded whole solve (config C4's shape)
     assert d["product_step"]["bytes_per_step"] == bench.product_step_bytes(n, 8, 48)
-    assert set(d["product_step"]["ops"]) == {"gemm_inner", "gemm_outer_set", "axpy"}
+    assert set(d["product_step"]["ops"]) == {"gemm_inner", "gemm_outer_set", "axpy_pairs_norm"}
     s = d["in_solver"]
     assert s["converged"] and s["iterations"] > 0 and s["n_global"] == n and s["reductions_per_iteration"] > 0
 
