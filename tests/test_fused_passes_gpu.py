@@ -1,0 +1,57 @@
+"""The fused solver passes (hbm_handlers.h, from 2^20 elements: the one-pass self-orthonormalisation
+ssp_axpy_gram, the batched overlap rows, the residuals with their norms ssp_axpy_pairs_norm) against
+the block-by-block call sequence they replace, on the MI355X, at a size where the product selects
+them: the same solves in two processes, SSP_FUSED_MIN_SIZE=0 (fused) and SSP_FUSED_MIN_SIZE huge
+(call by call).  Same steps (iterations, R creations), eigenvalues within 1e-10, the DIIS solution
+within 1e-10 -- the north-star bar between two summation orders of the same algorithm.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(os.path.dirname(HERE), "iterative-solver_amd")
+
+CHILD = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import itsolv_hbm as ih
+import subspace_hip as sh
+n = int(sys.argv[2])
+with sh.Context(0) as ctx:
+    d = ih.davidson_synthetic(ctx, n, 0.1, 8, 1, solutions=False, nroots=8, max_p=16, max_size_qspace=48,
+                              reset_D=8, convergence_threshold=1e-8)
+    c = ih.diis_synthetic(ctx, n, solutions=True, **ih.c5_spec(n), max_size_qspace=6, convergence_threshold=1e-8)
+print(json.dumps({"dav": {k: (v.tolist() if hasattr(v, "tolist") else v) for k, v in d.items()
+                          if k in ("iterations", "r_creations", "converged", "eigenvalues")},
+                  "diis": {"iterations": c["iterations"], "converged": c["converged"],
+                           "x_head": np.asarray(c["x"][:1000]).tolist()}}))
+"""
+
+
+def run(n, min_size):
+    env = dict(os.environ, SSP_FUSED_MIN_SIZE=str(min_size))
+    env.pop("SSP_ORTHO", None)
+    p = subprocess.run([sys.executable, "-c", CHILD, PKG, str(n)], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_fused_passes_take_the_call_by_call_steps():
+    n = 1_500_000
+    fused, plain = run(n, 0), run(n, 10**15)
+    a, b = fused["dav"], plain["dav"]
+    assert a["converged"] and b["converged"]
+    assert a["iterations"] == b["iterations"] and a["r_creations"] == b["r_creations"], (a, b)
+    ea, eb = a["eigenvalues"][:8], b["eigenvalues"][:8]
+    assert all(abs(x - y) <= 1e-10 * abs(y) for x, y in zip(ea, eb)), (ea, eb)
+    c, d = fused["diis"], plain["diis"]
+    assert c["converged"] and d["converged"] and c["iterations"] == d["iterations"], (c["iterations"], d["iterations"])
+    assert max(abs(x - y) for x, y in zip(c["x_head"], d["x_head"])) <= 1e-10
