@@ -188,45 +188,97 @@ def rendezvous_uid(rank, world, timeout=300.0):
         return f.read(), None
 
 
-def cpu_baseline(m, k, seconds):
-    """The oracle (CPU restatement of ArrayHandlerIterable: pairwise gemm, sequential loops) on one
-    host core, same op sequence, bounded sample; then the host-parallel and DRAM-resident figures."""
-    cb = cpu_baseline_core(m, k, seconds)
-    cpu_baseline_extras(cb, m, k, seconds)
-    return cb
+def gpu_c2_solve(ctx, world, n=None):
+    """The same C2 solve on the GPU(s) (sharded at N > 1), for in_solver_cpu's like-for-like ratio."""
+    import itsolv_hbm as ih
+
+    kw = dict(C2_SOLVE, **({"n": int(n)} if n else {}))
+    n, rho, rank, seed = kw.pop("n"), kw.pop("rho"), kw.pop("rank"), kw.pop("seed")
+    ih.davidson_synthetic(ctx, n, rho, rank, seed, n_local=0, solutions=False, **kw)  # warm
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    r = ih.davidson_synthetic(ctx, n, rho, rank, seed, n_local=0, solutions=False, **kw)
+    ctx.synchronize()
+    return {"wall_s": round(time.perf_counter() - t0, 4), "iterations": r["iterations"],
+            "r_creations": r["r_creations"], "eigenvalues": [round(float(e), 12) for e in r["eigenvalues"][:4]]}
 
 
-def cpu_baseline_core(m, k, seconds):
-    """The 1-core leg of cpu_baseline (bench.py runs it beside the GPU's sustained phase)."""
+def pin_this_thread():
+    """Pins the calling thread (only it: Linux sched_setaffinity of tid 0) to one host core -- the
+    last one this process may use, away from the thread that drives the GPU -- and returns it."""
+    try:
+        core = max(os.sched_getaffinity(0))
+        os.sched_setaffinity(0, {core})
+        return core
+    except (AttributeError, OSError):
+        return None
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+CPU_N = 10_000_000  # BASELINE.md §3: N in {1e7, 1e8}; 112 vectors of 80 MB, far beyond the host caches
+
+
+def cpu_baseline_core(m, k, seconds, n=CPU_N):
+    """The 1-core leg of cpu_baseline: the reference loops (oracle_ops.c: sequential dot / axpy,
+    pairwise gemm_inner_default / gemm_outer_default, ArrayHandlerIterable.h:65-82, gemm.h:257-279)
+    running the headline step's op sequence on DRAM-resident operands at N = 1e7, on one pinned core.
+    Whole steps only: at least one, until `seconds` have passed."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
 
-    n = 1_000_000
+    core = pin_this_thread()
+    runner = oracle.CpuUpdateStep(n, m, k, SEED)
     t0 = time.perf_counter()
     steps = 0
-    runner = oracle.CpuUpdateStep(n, m, k, SEED)
     while True:
         runner.step()
         steps += 1
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    cpu = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    del runner
     return {
         "value": step_bytes(n, m, k) * steps / dt / 1e9,
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{steps} step(s) of the same op sequence at N=1e6 (m={m}, k={k}) on 1 core of "
-                  f"{cpu} (nproc={os.cpu_count()}), {dt:.1f} s, oracle/oracle_ops.c (reference loops)",
+        "sample": f"{steps} step(s) of the headline op sequence at N={n:.0e} (m={m}, k={k}; {2 * (m + k)} vectors, "
+                  f"{16 * (m + k) * n / 1e9:.1f} GB, DRAM-resident) on 1 core (pinned: cpu {core}) of {cpu_model()} (nproc={os.cpu_count()}), "
+                  f"{dt:.1f} s, oracle/oracle_ops.c (reference loops: sequential dot/axpy, pairwise gemm)",
     }
+
+
+# BASELINE.md §3 "In-solver": a whole LinearEigensystemDavidson on the rank-one H = diag(1 + i) + rho 1 1^T
+# (rho = 0.1, test_rayleigh_quotient.cpp:37-42) at BASELINE config C2's size (N = 1e7, 4 roots); the
+# committed CPU-path trace of the same solve is traces.json C2_rank1
+C2_SOLVE = dict(n=10_000_000, rho=0.1, rank=1, seed=1, nroots=4, max_p=0, max_size_qspace=24, reset_D=8,
+                convergence_threshold=1e-8)
+
+
+def cpu_solve_core(n=None):
+    """The in-solver CPU baseline: the oracle's C2 solve (the reference's Davidson over its CPU
+    handlers, the same restated solver headers) on one pinned core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg only
+
+    core = pin_this_thread()
+    kw = dict(C2_SOLVE, **({"n": int(n)} if n else {}))
+    n, rho, rank, seed = kw.pop("n"), kw.pop("rho"), kw.pop("rank"), kw.pop("seed")
+    t0 = time.perf_counter()
+    r = oracle.davidson_synthetic(n, rho, rank, seed, solutions=False, **kw)
+    dt = time.perf_counter() - t0
+    return {"wall_s": round(dt, 3), "iterations": r["iterations"], "r_creations": r["r_creations"],
+            "converged": bool(r["converged"]), "cores": 1, "pinned_core": core, "kind": "port",
+            "eigenvalues": [round(float(e), 12) for e in r["eigenvalues"][:4]]}
 
 
 def cpu_baseline_extras(cb, m, k, seconds):
@@ -368,6 +420,8 @@ def main():
     ap.add_argument("--qsize", type=int, default=48)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-n", type=float, default=CPU_N, help="vector length of the 1-core CPU baseline step")
+    ap.add_argument("--cpu-solve-n", type=float, default=C2_SOLVE["n"], help="length of the in-solver C2 solve")
     ap.add_argument("--ledger-steps", type=int, default=3,
                     help="with --no-timed-ledger: extra steps under the HIP-event ledger after the timed region")
     ap.add_argument("--no-timed-ledger", action="store_true",
@@ -481,27 +535,34 @@ def main():
         "ops": {op: {"calls_per_step": v["calls"], "avg_us": round(1e3 * v["ms"] / v["calls"], 2),
                      "GBs": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)} for op, v in pled.items()},
     }
-    # Sustained phase (rank 0 of a 1-GPU run): the headline step repeated on the GPU for as long as
-    # the 1-core CPU baseline runs on another host core -- the GPU's long-run rate over ~15 s beside the
-    # 0.8-8 s timed region.  The GPU thread only enqueues kernels and waits on reductions; the CPU leg
-    # streams host DRAM on its own core.  host-parallel (all host threads) runs later, GPU idle.
-    sustained, cb = None, None
+    # CPU baselines (rank 0 of a 1-GPU run) on ONE pinned host core, in a thread beside the GPU work
+    # that follows (the reference loops release the GIL inside their C calls): the headline step's op
+    # sequence at N = 1e7, DRAM-resident, then the C2 Davidson solve (BASELINE.md §3's "In-solver"
+    # row).  Meanwhile the sustained phase repeats the headline step on the GPU for ~cpu_seconds -- its
+    # long-run rate beside the timed region -- and the GPU solves run; host-parallel (all host threads)
+    # and the DRAM-resident single calls come last, GPU idle.
+    sustained, cb, th, box = None, None, None, {}
     run_cpu = world == 1 and not args.no_cpu_baseline
     if run_cpu:
-        log("timing CPU baseline (oracle, 1 core) beside the GPU's sustained phase...")
-        box = {}
-        th = threading.Thread(target=lambda: box.update(cb=cpu_baseline_core(m, k, args.cpu_seconds)))
+        log("CPU baselines (oracle, 1 pinned core) in a thread beside the GPU work...")
+
+        def cpu_leg():
+            try:
+                box["cb"] = cpu_baseline_core(m, k, args.cpu_seconds, int(args.cpu_n))
+                box["solve"] = cpu_solve_core(args.cpu_solve_n)
+            except Exception as e:  # noqa: BLE001 - reported in the JSON line, never fatal to the bench
+                box["error"] = repr(e)
+
+        th = threading.Thread(target=cpu_leg, daemon=True)
         ctx.synchronize()
         ts = time.perf_counter()
         th.start()
         n_sus = 0
-        while th.is_alive() or n_sus < 5:
+        while n_sus < 5 or time.perf_counter() - ts < args.cpu_seconds:
             wl.step()
             n_sus += 1
         ctx.synchronize()
         ts = time.perf_counter() - ts
-        th.join()
-        cb = box["cb"]
         sustained = {"steps": n_sus, "seconds": round(ts, 2), "ms_per_step": round(1e3 * ts / n_sus, 4),
                      "GBs": round(step_bytes(n_global, m, k) * n_sus / ts / 1e9, 2),
                      "note": "headline step repeated while the 1-core CPU baseline runs on another core"}
@@ -528,10 +589,16 @@ def main():
         wls.free()
         small = {"n_global": ns_global, "steps": s_steps, "ms_per_step": round(1e3 * t_s / s_steps, 4),
                  "GBs": round(step_bytes(ns_global, m, k) * s_steps / t_s / 1e9, 2)}
-    solve = solve_diis = None
+    solve = solve_diis = gpu_c2 = None
     if not args.no_in_solver:
         solve = in_solver(ctx, n_global, world, barrier)
         solve_diis = in_solver(ctx, n_global, world, barrier, kind="diis")
+        if run_cpu:
+            gpu_c2 = gpu_c2_solve(ctx, world, args.cpu_solve_n)
+    if th is not None:
+        log("waiting for the CPU baselines...")
+        th.join()
+        cb = box.get("cb")
 
     total_bytes = step_bytes(n_global, m, k) * args.steps
     value = total_bytes / elapsed / 1e9
@@ -604,6 +671,15 @@ def main():
         if cb is not None:
             cpu_baseline_extras(cb, m, k, args.cpu_seconds)
         result["cpu_baseline"] = cb
+        if run_cpu:
+            cs = box.get("solve")
+            result["in_solver_cpu"] = {
+                "config": f"LinearEigensystemDavidson C2 (BASELINE.md §3 In-solver): 4 roots, N={args.cpu_solve_n:.0e}, rank-one "
+                          "H = diag(1+i) + 0.1 1 1^T, max_size_qspace 24, reset_D 8, threshold 1e-8",
+                "cpu": cs, "gpu": gpu_c2, "cpu_path_trace": "tests/golden/traces.json:C2_rank1",
+                "speedup": round(cs["wall_s"] / gpu_c2["wall_s"], 1) if cs and gpu_c2 else None,
+                "same_iterations": bool(cs and gpu_c2 and cs["iterations"] == gpu_c2["iterations"]),
+                "error": box.get("error")}
         result["sustained"] = sustained
         print(json.dumps(result), flush=True)
     barrier()

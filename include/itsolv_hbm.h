@@ -66,6 +66,11 @@ typedef struct {
   int trace_nwork[ITSOLV_TRACE_ITER];
   double trace_eigenvalues[ITSOLV_TRACE_ITER * ITSOLV_TRACE_ROOTS];
   double trace_errors[ITSOLV_TRACE_ITER * ITSOLV_TRACE_ROOTS];
+  /* propose_rspace's screening (extension): new R vectors removed by the redundancy screen and as
+   * null after orthogonalisation, in all, and cumulative after each iteration */
+  int redundant_params;
+  int null_params;
+  int trace_screened[ITSOLV_TRACE_ITER];
 } itsolv_result;
 
 const char* itsolv_last_error(void);

@@ -79,6 +79,20 @@ typedef int (*ssp_host_allreduce_fn)(double* buf, size_t n, void* user);
 typedef int (*ssp_host_allgather_fn)(const void* send, void* recv, size_t bytes, void* user);
 int ssp_ctx_attach_host_comm(ssp_ctx* ctx, int nranks, int rank, ssp_host_allreduce_fn allreduce,
                              ssp_host_allgather_fn allgather, void* user);
+/* Peer-memory communicator (no RCCL): the ranks of ONE node exchange reduction partials through
+ * IPC-shared device memory (push into every rank's inbox, device-side flag wait, fixed rank-order
+ * sum: bit-identical results on every rank) and host data through a POSIX shared-memory segment.
+ * Several ranks may share one device.  `id` (SSP_UNIQUE_ID_BYTES, from ssp_p2p_unique_id on rank 0)
+ * is distributed by the caller.  Collective: returns once every rank has attached.  At most 16 ranks.
+ * Replaces any other communicator. */
+int ssp_p2p_unique_id(char* id_out);
+int ssp_ctx_attach_p2p(ssp_ctx* ctx, int nranks, int rank, const char* id);
+/* Fail fast: every wait that depends on other ranks gives up after `seconds` (default 300, or
+ * SSP_COMM_TIMEOUT_S at context creation), and RCCL's asynchronous errors are polled meanwhile; the
+ * communicator is then aborted (ncclCommAbort / the peer-memory abort word) and the call, and every
+ * later exchange on the context, returns SSP_ERR_COMM naming the operation -- the status-code form of
+ * the reference's abort of the whole job on a distributed error (DistrArray.cpp:16-23). */
+int ssp_ctx_set_comm_timeout(ssp_ctx* ctx, double seconds);
 /* Shard of a global length n owned by `rank` of `nranks` (host only, no context):
  * make_distribution_spread_remainder, reference util/Distribution.h:99-109. */
 int ssp_shard_range(size_t n, int nranks, int rank, size_t* offset, size_t* length);
@@ -265,6 +279,9 @@ int sspx_synthetic_diagonal(ssp_ctx* ctx, double* d, size_t n, size_t offset, do
 /* x[g] = uniform [-1,1) from splitmix64(seed, vec, g): G-independent benchmark data. */
 int sspx_fill_random(ssp_ctx* ctx, double* x, size_t n, size_t offset, unsigned long long seed,
                      unsigned long long vec);
+/* Test harness: occupies the context's stream for `ms` milliseconds (one workgroup spinning on the
+ * device clock; always ends), to exercise the communication deadline. */
+int sspx_debug_stall(ssp_ctx* ctx, double ms);
 /* y = A x for a dense row-major n_global x n_global matrix A in device memory, local rows
  * [offset, offset+n) of y; x must be the full (gathered) vector.  Used for small fixtures. */
 int sspx_dense_action(ssp_ctx* ctx, const double* a, size_t n_global, const double* const* xx, double* const* yy,

@@ -56,7 +56,7 @@ unsigned stream_grid(const ssp_ctx* ctx, size_t work_items, unsigned per_thread,
 int ensure_partial(ssp_ctx* ctx, size_t n) {
   if (n <= ctx->partial_cap) return SSP_OK;
   if (ctx->partial) {
-    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    SSP_TRY(sync_stream(ctx, "reduction workspace growth"));
     SSP_TRY_HIP(hipFree(ctx->partial));
     ctx->partial = nullptr;
   }
@@ -69,7 +69,7 @@ int ensure_partial(ssp_ctx* ctx, size_t n) {
 
 int ensure_result(ssp_ctx* ctx, size_t n) {
   if (n <= ctx->result_cap) return SSP_OK;
-  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  SSP_TRY(sync_stream(ctx, "result staging growth"));
   if (ctx->result_dev) SSP_TRY_HIP(hipFree(ctx->result_dev));
   if (ctx->result_host) SSP_TRY_HIP(hipHostFree(ctx->result_host));
   ctx->result_dev = nullptr;
@@ -92,7 +92,7 @@ int ensure_result(ssp_ctx* ctx, size_t n) {
 int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev) {
   const size_t need = (bytes + 255) & ~size_t(255);
   if (need > ctx->ring_cap) {
-    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    SSP_TRY(sync_stream(ctx, "upload ring growth"));
     if (ctx->ring_dev) SSP_TRY_HIP(hipFree(ctx->ring_dev));
     if (ctx->ring_host) SSP_TRY_HIP(hipHostFree(ctx->ring_host));
     ctx->ring_dev = ctx->ring_host = nullptr;
@@ -105,7 +105,7 @@ int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev) {
   }
   if (ctx->ring_head + need > ctx->ring_cap) {
     // Wrap: every earlier copy out of the ring has completed once the stream drains.
-    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    SSP_TRY(sync_stream(ctx, "upload ring wrap"));
     ctx->ring_head = 0;
   }
   char* h = ctx->ring_host + ctx->ring_head;
@@ -120,16 +120,18 @@ int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev) {
 }
 
 int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n) {
+  SSP_TRY(comm_check(ctx));
   if (n == 0) return SSP_OK;
+  if (ctx->p2p) return p2p_allreduce_dev(ctx, buf, n);
   if (ctx->host_allreduce && ctx->nranks > 1) {
     // Host-callback communicator: stage through the host (test / fallback transport only).
     std::vector<double> h(n);
     SSP_TRY_HIP(hipMemcpyAsync(h.data(), buf, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    SSP_TRY(sync_stream(ctx, "host allreduce"));
     if (ctx->host_allreduce(h.data(), n, ctx->host_user) != 0)
-      return set_error(SSP_ERR_COMM, "host allreduce callback failed");
+      return comm_fail(ctx, "host allreduce callback failed (a peer closed or timed out)");
     SSP_TRY_HIP(hipMemcpyAsync(buf, h.data(), n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    SSP_TRY(sync_stream(ctx, "host allreduce"));
     return SSP_OK;
   }
   if (!ctx->comm) return SSP_OK;
@@ -155,14 +157,21 @@ __global__ __launch_bounds__(256) void k_publish(const double* src, size_t n, do
 // hipStreamSynchronize cuts the host-visible latency of a reduction (tools/sync_probe.hip,
 // profiles/r1/sync_probe.txt).  The stream is queried every few hundred polls so that a failed
 // kernel surfaces as an error instead of a hang.  *seen is false when the stream drained without the
-// flag becoming visible (the writes of a finished kernel are visible all the same).
+// flag becoming visible (the writes of a finished kernel are visible all the same).  With a
+// communicator attached the wait is bounded (comm_poll: SSP_COMM_TIMEOUT_S, RCCL's asynchronous
+// error, the peer-memory transport's abort word), since the flag then depends on other ranks.
 int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen) {
   *seen = true;
+  const bool ranks = comm_attached(ctx);
+  const double t0 = ranks ? now_s() : 0.0;
   for (unsigned spin = 1;; ++spin) {
     if (__atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq) return SSP_OK;
     if ((spin & 255) == 0) {
       const hipError_t e = hipStreamQuery(ctx->stream);
-      if (e == hipErrorNotReady) continue;
+      if (e == hipErrorNotReady) {
+        if (ranks && (spin & 4095) == 0) SSP_TRY(comm_poll(ctx, t0, "reduction"));
+        continue;
+      }
       if (e != hipSuccess) return hip_error(e, "reduction");
       *seen = __atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq;
       return SSP_OK;
@@ -191,12 +200,19 @@ int fetch_result(ssp_ctx* ctx, double* out, size_t n) {
   return SSP_OK;
 }
 
+int reduce_fetch(ssp_ctx* ctx, double* out, size_t n) {
+  if (ctx->p2p) return p2p_allreduce_fetch(ctx, ctx->result_dev, out, n);
+  SSP_TRY(allreduce_dev(ctx, ctx->result_dev, n));
+  return fetch_result(ctx, out, n);
+}
+
 int fold_begin(ssp_ctx* ctx, int nout, FoldTail* t) {
+  SSP_TRY(comm_check(ctx));
   SSP_TRY(ensure_result(ctx, size_t(nout)));
   t->counter = ctx->fold_counter;
   t->nout = nout;
   t->flag = ctx->pub_flag;
-  const bool ranks = ctx->comm || (ctx->host_allreduce && ctx->nranks > 1);
+  const bool ranks = comm_attached(ctx);
   if (ranks) {
     t->out = ctx->result_dev;
     t->host = nullptr;
@@ -210,10 +226,7 @@ int fold_begin(ssp_ctx* ctx, int nout, FoldTail* t) {
 }
 
 int fold_finish(ssp_ctx* ctx, const FoldTail& t, double* out) {
-  if (!t.host) {
-    SSP_TRY(allreduce_dev(ctx, ctx->result_dev, size_t(t.nout)));
-    return fetch_result(ctx, out, size_t(t.nout));
-  }
+  if (!t.host) return reduce_fetch(ctx, out, size_t(t.nout));
   bool seen = true;
   SSP_TRY(wait_flag(ctx, t.seq, &seen));
   std::memcpy(out, ctx->result_host, size_t(t.nout) * sizeof(double));
@@ -345,6 +358,10 @@ int ssp_ctx_create(int device, ssp_ctx** out) {
     ctx->num_cus = prop.multiProcessorCount;
   if (const char* rs = std::getenv("SSP_ROW_SHAPE")) ctx->row_stride = std::string(rs) == "stride";
   if (const char* pc = std::getenv("SSP_PUBLISH")) ctx->publish_copy = std::string(pc) == "copy";
+  if (const char* ct = std::getenv("SSP_COMM_TIMEOUT_S")) {
+    const double v = std::atof(ct);
+    if (v > 0) ctx->comm_timeout_s = v;
+  }
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return ssp::set_error(SSP_ERR_HIP, "hipStreamCreate failed");
@@ -368,8 +385,10 @@ int ssp_ctx_create(int device, ssp_ctx** out) {
 int ssp_ctx_destroy(ssp_ctx* ctx) {
   if (!ctx) return SSP_OK;
   (void)hipSetDevice(ctx->device);
+  (void)ssp::p2p_detach(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
+  if (ctx->dev_err_host) (void)hipHostFree(ctx->dev_err_host);
   for (auto& e : ctx->ledger)
     for (auto& pr : e.pending) {
       (void)hipEventDestroy(pr.first);
@@ -395,8 +414,7 @@ void* ssp_ctx_stream(ssp_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->s
 
 int ssp_synchronize(ssp_ctx* ctx) {
   SSP_CHECK_CTX(ctx);
-  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
-  return SSP_OK;
+  return ssp::sync_stream(ctx, "synchronize");
 }
 
 int ssp_alloc(ssp_ctx* ctx, size_t n, double** out) {
@@ -493,11 +511,14 @@ int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id) {
     ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
   }
+  SSP_TRY(ssp::p2p_detach(ctx));
   ctx->host_allreduce = nullptr;
   ctx->host_allgather = nullptr;
   ctx->host_user = nullptr;
   ctx->nranks = nranks;
   ctx->rank = rank;
+  ctx->comm_failed = false;
+  ctx->comm_fail_msg.clear();
   // A one-rank communicator is created too: its collectives run through RCCL like any other, which
   // is how the RCCL calls are exercised on a one-GPU machine (tests/test_rccl_gpu.py).
   ncclUniqueId uid;
@@ -520,6 +541,9 @@ int ssp_ctx_attach_host_comm(ssp_ctx* ctx, int nranks, int rank, ssp_host_allred
     ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
   }
+  SSP_TRY(ssp::p2p_detach(ctx));
+  ctx->comm_failed = false;
+  ctx->comm_fail_msg.clear();
   ctx->nranks = nranks;
   ctx->rank = rank;
   ctx->host_allreduce = allreduce;
@@ -545,15 +569,16 @@ int ssp_ctx_nranks(ssp_ctx* ctx) { return ctx ? ctx->nranks : 0; }
 int ssp_allreduce_sum(ssp_ctx* ctx, double* buf, size_t n) {
   SSP_CHECK_CTX(ctx);
   SSP_TRY(ssp::allreduce_dev(ctx, buf, n));
-  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
-  return SSP_OK;
+  return ssp::sync_stream(ctx, "allreduce");
 }
 
 int ssp_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes) {
   SSP_CHECK_CTX(ctx);
+  SSP_TRY(ssp::comm_check(ctx));
+  if (ctx->p2p) return ssp::p2p_allgather_host(ctx, send, recv, bytes);
   if (ctx->host_allgather && ctx->nranks > 1) {
     if (ctx->host_allgather(send, recv, bytes, ctx->host_user) != 0)
-      return ssp::set_error(SSP_ERR_COMM, "host allgather callback failed");
+      return ssp::comm_fail(ctx, "host allgather callback failed (a peer closed or timed out)");
     return SSP_OK;
   }
   if (!ctx->comm) {
@@ -569,8 +594,7 @@ int ssp_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes)
   ncclResult_t r = ncclAllGather(dsend, drecv, bytes, ncclChar, ctx->comm, ctx->stream);
   if (r != ncclSuccess) return ssp::set_error(SSP_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
   SSP_TRY_HIP(hipMemcpyAsync(recv, drecv, total, hipMemcpyDeviceToHost, ctx->stream));
-  SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
-  return SSP_OK;
+  return ssp::sync_stream(ctx, "allgather");
 }
 
 }  // extern "C"

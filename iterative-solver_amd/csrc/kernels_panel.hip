@@ -342,7 +342,8 @@ __global__ __launch_bounds__(kBlock) void k_gemm_outer(const OuterArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int j = 0; j < M; ++j) acc[u][j] = sc2<SC>(acc[u][j], scale(a.k + j));
+        for (int j = 0; j < M; ++j)
+          if (j < a.m) acc[u][j] = sc2<SC>(acc[u][j], scale(a.k + j));  // only a.k + a.m scales exist
     }
     int i = 0;
     for (; i + 4 <= a.k; i += 4) {
@@ -1042,8 +1043,7 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
   if (tail.counter) {
     SSP_TRY(ssp::fold_finish(ctx, tail, dst));
   } else {
-    SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, total));
-    SSP_TRY(ssp::fetch_result(ctx, dst, total));
+    SSP_TRY(ssp::reduce_fetch(ctx, dst, total));
   }
   if (!swap) return SSP_OK;
   for (int i = 0; i < m; ++i)
@@ -1178,8 +1178,7 @@ int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* y
     SSP_TRY_HIP(hipGetLastError());
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
-  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, size_t(m)));
-  return ssp::fetch_result(ctx, out, size_t(m));
+  return ssp::reduce_fetch(ctx, out, size_t(m));
 }
 
 int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const* yy, int m, size_t n, double* out) {
@@ -1225,8 +1224,7 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
     SSP_TRY_HIP(hipGetLastError());
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
-  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, 1));
-  return ssp::fetch_result(ctx, out, 1);
+  return ssp::reduce_fetch(ctx, out, 1);
 }
 
 int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store_x, double* const* yy, int m,
@@ -1281,8 +1279,7 @@ int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store
     SSP_TRY_HIP(hipGetLastError());
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
-  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, size_t(m)));
-  return ssp::fetch_result(ctx, out, size_t(m));
+  return ssp::reduce_fetch(ctx, out, size_t(m));
 }
 
 int ssp_axpy_pairs_norm(ssp_ctx* ctx, const double* c, const double* const* xx, const double* xs, double* const* yy,
@@ -1335,8 +1332,7 @@ int ssp_axpy_pairs_norm(ssp_ctx* ctx, const double* c, const double* const* xx, 
     SSP_TRY_HIP(hipGetLastError());
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
-  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, size_t(m)));
-  return ssp::fetch_result(ctx, out, size_t(m));
+  return ssp::reduce_fetch(ctx, out, size_t(m));
 }
 
 int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const* yy, int m, const double* z, size_t n,
@@ -1385,8 +1381,7 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
     }
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
-  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, size_t(m)));
-  return ssp::fetch_result(ctx, out, size_t(m));
+  return ssp::reduce_fetch(ctx, out, size_t(m));
 }
 
 }  // extern "C"

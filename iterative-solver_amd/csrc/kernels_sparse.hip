@@ -245,8 +245,7 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const do
     hipLaunchKernelGGL(k_sparse_inner, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
-  SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, total));
-  return ssp::fetch_result(ctx, out, total);
+  return ssp::reduce_fetch(ctx, out, total);
 }
 
 int ssp_sparse_dot(ssp_ctx* ctx, const double* x, size_t n, size_t offset, const size_t* idx, const double* val,

@@ -389,8 +389,7 @@ int dot_impl(ssp_ctx* ctx, const double* x, double xs, const double* y, double y
   if (n == 0) {
     SSP_TRY(ssp::ensure_result(ctx, 1));
     SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, sizeof(double), ctx->stream));
-    SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, 1));
-    return ssp::fetch_result(ctx, out, 1);
+    return ssp::reduce_fetch(ctx, out, 1);
   }
   const unsigned grid = ssp::win_grid(ctx, n, kDotU, 8);
   SSP_TRY(ssp::ensure_partial(ctx, grid));

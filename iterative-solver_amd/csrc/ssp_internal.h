@@ -23,6 +23,10 @@ struct ssp_ledger_entry_t {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
 };
 
+namespace ssp {
+struct P2PComm;  // comm_p2p.hip
+}
+
 struct ssp_ctx {
   int device = 0;
   bool ledger_on = false;
@@ -79,8 +83,19 @@ struct ssp_ctx {
   ssp_host_allreduce_fn host_allreduce = nullptr;
   ssp_host_allgather_fn host_allgather = nullptr;
   void* host_user = nullptr;
+  // Peer-memory communicator (ssp_ctx_attach_p2p, comm_p2p.hip), used instead of RCCL when set.
+  ssp::P2PComm* p2p = nullptr;
   int nranks = 1;
   int rank = 0;
+  // Fail-fast (comm_p2p.hip): every wait that depends on other ranks gives up after comm_timeout_s
+  // (SSP_COMM_TIMEOUT_S, ssp_ctx_set_comm_timeout); the communicator is then aborted and every later
+  // exchange on this context returns SSP_ERR_COMM with comm_fail_msg (the reference aborts the whole
+  // job, DistrArray.cpp:16-23).
+  double comm_timeout_s = 300.0;
+  bool comm_failed = false;
+  std::string comm_fail_msg;
+  // Coherent host word a device-side exchange sets when it gave up (peer missing / mismatched).
+  int* dev_err_host = nullptr;
 };
 
 namespace ssp {
@@ -106,6 +121,11 @@ int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n);
 // Copies n doubles of ctx->result_dev to host `out` once every operation queued before it has
 // completed (publish kernel + host poll of a sequence flag; see context.hip).
 int fetch_result(ssp_ctx* ctx, double* out, size_t n);
+// Sums ctx->result_dev[0, n) over ranks and delivers it to host `out` (allreduce_dev + fetch_result,
+// or the peer-memory transport's fused exchange-and-publish).
+int reduce_fetch(ssp_ctx* ctx, double* out, size_t n);
+// Waits (host poll) until the publish flag carries seq; bounded when a communicator is attached.
+int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen);
 // Grid size for streaming kernels: enough workgroups to fill 256 CUs, grid-stride beyond.
 // Workgroups for a grid-stride streaming launch: enough for work_items / (kBlock * per_thread),
 // at most blocks_per_cu per CU.
@@ -288,6 +308,29 @@ __device__ inline void fold_tail(const double* partial, const FoldTail& t) {
 // flag, or allreduce + fetch_result).
 int fold_begin(ssp_ctx* ctx, int nout, FoldTail* t);
 int fold_finish(ssp_ctx* ctx, const FoldTail& t, double* out);
+
+// comm_p2p.hip: transport-independent fail-fast helpers and the peer-memory transport.
+// True when reductions/gathers go to other ranks (any transport, including a one-rank RCCL comm).
+inline bool comm_attached(const ssp_ctx* ctx) {
+  return ctx->comm_failed || ctx->comm || ctx->p2p || (ctx->host_allreduce && ctx->nranks > 1);
+}
+// SSP_ERR_COMM with the recorded failure, when the communicator has been aborted.
+int comm_check(ssp_ctx* ctx);
+// Records a communication failure on `what`, aborts the communicator (RCCL: ncclCommAbort; p2p: the
+// shared abort word every rank polls) and returns SSP_ERR_COMM.
+int comm_fail(ssp_ctx* ctx, const std::string& what);
+// Polled once per few hundred spins by every host wait on a rank-dependent result: the deadline
+// and RCCL's asynchronous error.  `t0` is the wait's start (steady clock, seconds).
+int comm_poll(ssp_ctx* ctx, double t0, const char* what);
+double now_s();
+// hipStreamSynchronize, bounded by the deadline when a communicator is attached.
+int sync_stream(ssp_ctx* ctx, const char* what);
+// Peer-memory transport: in-place sum over ranks of n device doubles in fixed rank order (stream
+// ordered), and the fused form that publishes the sum into the coherent host result buffer.
+int p2p_allreduce_dev(ssp_ctx* ctx, double* buf, size_t n);
+int p2p_allreduce_fetch(ssp_ctx* ctx, const double* src, double* out, size_t n);
+int p2p_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes);
+int p2p_detach(ssp_ctx* ctx);
 
 // kernels_stream.hip
 int launch_reduce_partials(ssp_ctx* ctx, const double* partial, int nblocks, int rows, int cols, double* out,

@@ -242,7 +242,7 @@ int ensure_mask(ssp_ctx* ctx, SynthArgs& a, unsigned long long seed) {
     return SSP_OK;
   }
   if (ctx->synth_mask) {
-    SSP_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    SSP_TRY(ssp::sync_stream(ctx, "synthetic mask"));
     SSP_TRY_HIP(hipFree(ctx->synth_mask));
     ctx->synth_mask = nullptr;
   }

@@ -152,6 +152,14 @@ class ArrayHandler {
 
   const Counter& counter() const { return *m_counter; }
   void clear_counter() { *m_counter = Counter{}; }
+  // Extension (not in the reference): a fused call site (e.g. the residuals with
+  // their norms, the block Gram-Schmidt update) records the handler operations its one pass
+  // replaced, so Statistics reads the same operation counts whether or not the pass was fused.
+  void count_replaced(int axpy, int dot, int gemm_outer) {
+    m_counter->axpy += axpy;
+    m_counter->dot += dot;
+    m_counter->gemm_outer += gemm_outer;
+  }
 
   std::string counter_to_string(std::string L, std::string R) {
     std::string s;
@@ -200,13 +208,16 @@ class ArrayHandler {
     template <typename T>
     using ref_wrap = std::reference_wrapper<T>;
 
-    explicit LazyHandle(ArrayHandler<AL, AR>& handler) : m_handler{handler} {}
+    explicit LazyHandle(ArrayHandler<AL, AR>& handler)
+        : m_handler{handler}, m_uncaught_at_creation{std::uncaught_exceptions()} {}
     // As the reference, destruction evaluates what is still registered -- except while an exception
-    // unwinds the stack (a failed eval() or handler call in the caller's scope): then the register
-    // is dropped, so a recoverable device or size error reaches the caller (e.g. the C API's status
-    // codes) instead of std::terminate from a second throw in this destructor.
+    // thrown in this handle's own scope unwinds it (a failed eval() or handler call): then the
+    // register is dropped, so a recoverable device or size error reaches the caller (e.g. the C API's
+    // status codes) instead of std::terminate from a second throw in this destructor.  Scope-guard
+    // rule: only an unwind that began after the handle was made counts, so a handle created and
+    // finished inside a cleanup path of some unrelated unwind still evaluates its operations.
     virtual ~LazyHandle() {
-      if (std::uncaught_exceptions() > 0)
+      if (std::uncaught_exceptions() > m_uncaught_at_creation)
         clear();
       else
         LazyHandle::eval();
@@ -261,6 +272,7 @@ class ArrayHandler {
     util::OperationRegister<ref_wrap<const AL>, ref_wrap<const AR>, ref_wrap<value_type>> m_dot;
     ArrayHandler<AL, AR>& m_handler;
     bool m_invalid = false;
+    int m_uncaught_at_creation = 0;  // std::uncaught_exceptions() when the handle was made
   };
 
   // What lazy_handle() returns (reference :384-414): forwards to the LazyHandle; with off(), every

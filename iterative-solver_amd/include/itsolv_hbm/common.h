@@ -63,6 +63,11 @@ struct Statistics {
   int current_r_creations = 0;
   int line_searches = 0;
   int line_search_steps = 0;
+  // Extension (not in the reference's Statistics): propose_rspace's screening of new R vectors --
+  // parameters the redundancy screen removed (propose_rspace.h:481-512) and null norms after the
+  // Gram-Schmidt step (:450-465) -- the decisions a near-dependent problem exercises.
+  int redundant_params = 0;
+  int null_params = 0;
   std::string rq_ops, qr_ops, rr_ops, qq_ops, rp_ops, qp_ops;
 };
 

@@ -105,6 +105,7 @@ void record_trace(const S& solver, const std::vector<double>& eigenvalues, itsol
   }
   out.trace_nq[it] = int(solver.dimensions().nQ);
   out.trace_nwork[it] = int(solver.working_set().size());
+  out.trace_screened[it] = solver.statistics().redundant_params + solver.statistics().null_params;
   out.eig_trace[it] = eigenvalues.empty() ? 0.0 : eigenvalues.front();
   out.n_eig_trace = it + 1;
 }
@@ -167,6 +168,8 @@ void run_davidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Proble
   out.iterations = st.iterations;
   out.r_creations = st.r_creations;
   out.q_creations = st.q_creations;
+  out.redundant_params = st.redundant_params;
+  out.null_params = st.null_params;
   const auto ev = solver.eigenvalues();
   out.nroots = int(std::min<size_t>(ev.size(), ITSOLV_MAX_ROOTS));
   for (int i = 0; i < out.nroots; ++i) {
@@ -214,6 +217,8 @@ void run_linear_equations(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, cons
   out.iterations = st.iterations;
   out.r_creations = st.r_creations;
   out.q_creations = st.q_creations;
+  out.redundant_params = st.redundant_params;
+  out.null_params = st.null_params;
   out.nroots = int(std::min<size_t>(nwork, ITSOLV_MAX_ROOTS));
   for (int i = 0; i < out.nroots; ++i) {
     out.eigenvalues[i] = 0;
@@ -258,6 +263,8 @@ void run_optimize(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Proble
   out.iterations = st.iterations;
   out.r_creations = st.r_creations;
   out.q_creations = st.q_creations;
+  out.redundant_params = st.redundant_params;
+  out.null_params = st.null_params;
   out.nroots = 1;
   out.errors[0] = solver->errors().empty() ? 0.0 : solver->errors().front();
   out.eigenvalues[0] = solver->value();
@@ -290,6 +297,8 @@ void run_diis(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R,
   out.iterations = st.iterations;
   out.r_creations = st.r_creations;
   out.q_creations = st.q_creations;
+  out.redundant_params = st.redundant_params;
+  out.null_params = st.null_params;
   out.nroots = 1;
   out.errors[0] = solver.errors().empty() ? 0.0 : solver.errors().front();
   out.eigenvalues[0] = 0;

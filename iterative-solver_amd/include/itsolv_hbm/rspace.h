@@ -423,6 +423,9 @@ std::vector<int> block_gram_schmidt(const VecRef<R>& rparams, const Matrix<doubl
     if (!fused_block_update(h.rp(), block(d.oP, d.nP), pp, block(d.oQ, d.nQ + d.nD), qd, rparams)) {
       if (d.nP) h.rp().gemm_outer(block(d.oP, d.nP), pp, rparams);
       if (d.nQ + d.nD) h.rq().gemm_outer(block(d.oQ, d.nQ + d.nD), qd, rparams);
+    } else {  // the handler calls the one pass replaced
+      h.rp().count_replaced(0, 0, d.nP ? 1 : 0);
+      h.rq().count_replaced(0, 0, d.nQ + d.nD ? 1 : 0);
     }
   }
   return orthonormalise_among(rparams, norm_thresh, h.rr());

@@ -552,6 +552,7 @@ class IterativeSolverTemplate {
       std::vector<double> errors(roots.size(), 0);
       if (m_residual_norms2.size() == roots.size()) {  // from a fused construct_residual
         for (size_t i = 0; i < errors.size(); ++i) errors[i] = std::sqrt(std::abs(m_residual_norms2[i]));
+        m_handlers->rr().count_replaced(0, int(roots.size()), 0);  // update_errors' self-dots
       } else {
         detail::update_errors(errors, cwrap(action), m_handlers->rr());
       }
@@ -727,6 +728,8 @@ class DavidsonSolver : public IterativeSolverTemplate<R, Q, P> {
             : detail::modified_gram_schmidt(wres, xs.data.at(EqnData::S), xs.dimensions(), xs.cparamsp(),
                                             xs.cparamsq(), xs.cparamsd(), norm_thresh, h);
     detail::delete_parameters(null_params, wres);
+    this->m_stats->redundant_params += int(redundant.size());
+    this->m_stats->null_params += int(null_params.size());
     detail::normalise(wres, h.rr(), log);
     for (size_t i = 0; i < wres.size(); ++i) h.rr().copy(parameters.at(i), wres.at(i));
     return detail::get_new_working_set(this->working_set(), cwrap(residuals), cwrap(wres));
@@ -784,8 +787,10 @@ class LinearEigensystemDavidson : public DavidsonSolver<R, Q, P> {
     for (size_t i = 0; i < roots.size(); ++i) c[i] = -ev.at(roots[i]);
     using array::fused_residual_norms;
     if (fused_residual_norms(this->m_handlers->rr(), c, params, VecRef<R>(actions.begin(), actions.begin() + long(roots.size())),
-                             this->m_residual_norms2))
+                             this->m_residual_norms2)) {
+      this->m_handlers->rr().count_replaced(int(roots.size()), 0, 0);  // the axpys it replaced
       return;
+    }
     for (size_t i = 0; i < roots.size(); ++i) this->m_handlers->rr().axpy(c[i], params.at(i), actions.at(i));
   }
 

@@ -75,6 +75,9 @@ class Result(C.Structure):
         ("trace_nwork", C.c_int * TRACE_ITER),
         ("trace_eigenvalues", C.c_double * (TRACE_ITER * TRACE_ROOTS)),
         ("trace_errors", C.c_double * (TRACE_ITER * TRACE_ROOTS)),
+        ("redundant_params", C.c_int),
+        ("null_params", C.c_int),
+        ("trace_screened", C.c_int * TRACE_ITER),
     ]
 
     def as_dict(self):
@@ -84,6 +87,8 @@ class Result(C.Structure):
             "iterations": self.iterations,
             "r_creations": self.r_creations,
             "q_creations": self.q_creations,
+            "redundant_params": self.redundant_params,
+            "null_params": self.null_params,
             "eigenvalues": np.array(self.eigenvalues[:k]),
             "errors": np.array(self.errors[:k]),
             "residual_norms": np.array(self.residual_norms[:k]),
@@ -98,7 +103,7 @@ class Result(C.Structure):
         ev = np.array(self.trace_eigenvalues[: it * TRACE_ROOTS]).reshape(it, TRACE_ROOTS)[:, :nr]
         er = np.array(self.trace_errors[: it * TRACE_ROOTS]).reshape(it, TRACE_ROOTS)[:, :nr]
         return {"eigenvalues": ev, "errors": er, "nq": np.array(self.trace_nq[:it]),
-                "nwork": np.array(self.trace_nwork[:it])}
+                "nwork": np.array(self.trace_nwork[:it]), "screened": np.array(self.trace_screened[:it])}
 
 
 def make_options(**kw) -> Options:

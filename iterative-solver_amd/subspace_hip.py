@@ -33,6 +33,7 @@ EXPORTS = [
     "ssp_synchronize", "ssp_alloc", "ssp_free", "ssp_release_cached", "ssp_memory_stats", "ssp_upload",
     "ssp_download", "ssp_comm_unique_id", "ssp_ctx_attach_comm", "ssp_ctx_rank", "ssp_ctx_nranks",
     "ssp_allreduce_sum", "ssp_allgather_host", "ssp_ctx_attach_host_comm", "ssp_shard_range", "ssp_select_merge",
+    "ssp_p2p_unique_id", "ssp_ctx_attach_p2p", "ssp_ctx_set_comm_timeout", "sspx_debug_stall",
     "ssp_ledger_enable", "ssp_ledger_reset", "ssp_ledger_count", "ssp_ledger_reserve",
     "ssp_ledger_entry", "ssp_fill", "ssp_scal", "ssp_copy", "ssp_axpy", "ssp_dot",
     "ssp_gemm_inner", "ssp_gemm_outer", "ssp_gemm_outer_set", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_axpy_gram", "ssp_axpy_pairs_norm", "ssp_precondition", "ssp_select", "ssp_select_max_dot",
@@ -100,6 +101,10 @@ def _declare(lib):
         "ssp_allreduce_sum": (I, [P, P, Z]),
         "ssp_allgather_host": (I, [P, P, P, Z]),
         "ssp_ctx_attach_host_comm": (I, [P, I, I, ALLREDUCE_FN, ALLGATHER_FN, P]),
+        "ssp_p2p_unique_id": (I, [C.c_char_p]),
+        "ssp_ctx_attach_p2p": (I, [P, I, I, C.c_char_p]),
+        "ssp_ctx_set_comm_timeout": (I, [P, D]),
+        "sspx_debug_stall": (I, [P, D]),
         "ssp_shard_range": (I, [Z, I, I, PZ, PZ]),
         "ssp_select_merge": (I, [I, PZ, Z, PZ, PD, Z, I, PZ, PD, PZ]),
         "ssp_ledger_enable": (I, [P, I]),
@@ -431,6 +436,26 @@ class Context:
 
     def attach_comm(self, nranks: int, rank: int, uid: bytes):
         _check(self.lib.ssp_ctx_attach_comm(self.handle, nranks, rank, uid))
+
+    @staticmethod
+    def p2p_unique_id() -> bytes:
+        """Name of a new peer-memory communicator (made on rank 0, distributed by the caller)."""
+        buf = C.create_string_buffer(128)
+        _check(load_library().ssp_p2p_unique_id(buf))
+        return buf.raw
+
+    def attach_p2p(self, nranks: int, rank: int, uid: bytes):
+        """Peer-memory communicator (ssp_ctx_attach_p2p): IPC-shared device inboxes, no RCCL; several
+        ranks may share one device.  Collective."""
+        _check(self.lib.ssp_ctx_attach_p2p(self.handle, nranks, rank, uid))
+
+    def set_comm_timeout(self, seconds: float):
+        """Deadline of every wait that depends on other ranks (SSP_COMM_TIMEOUT_S)."""
+        _check(self.lib.ssp_ctx_set_comm_timeout(self.handle, float(seconds)))
+
+    def debug_stall(self, ms: float):
+        """Test harness: holds the stream for ms milliseconds (sspx_debug_stall)."""
+        _check(self.lib.sspx_debug_stall(self.handle, float(ms)))
 
     def allgather_bytes(self, data: bytes) -> list:
         """Every rank's `data` (equal lengths), rank order, over the attached communicator."""

@@ -217,6 +217,18 @@ int ssp_ctx_attach_host_comm(ssp_ctx* c, int nranks, int rank, ssp_host_allreduc
   c->user = user;
   return SSP_OK;
 }
+int ssp_p2p_unique_id(char* id) {
+  std::memset(id, 0, SSP_UNIQUE_ID_BYTES);
+  std::memcpy(id, "/ssp_emul", 9);
+  return SSP_OK;
+}
+int ssp_ctx_attach_p2p(ssp_ctx*, int nranks, int, const char*) {
+  return nranks == 1 ? SSP_OK : fail(SSP_ERR_UNSUPPORTED, "emul: no device memory to share; use ssp_ctx_attach_host_comm");
+}
+int ssp_ctx_set_comm_timeout(ssp_ctx*, double seconds) {
+  return seconds > 0 ? SSP_OK : fail(SSP_ERR_ARG, "ssp_ctx_set_comm_timeout: seconds must be > 0");
+}
+int sspx_debug_stall(ssp_ctx*, double) { return SSP_OK; }
 int ssp_ctx_rank(ssp_ctx* c) { return c->rank; }
 int ssp_ctx_nranks(ssp_ctx* c) { return c->nranks; }
 int ssp_allreduce_sum(ssp_ctx* c, double* v, size_t n) { return reduce(c, v, n); }

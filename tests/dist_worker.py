@@ -40,6 +40,18 @@ def make_comm(kind):
                       int(os.environ["SSP_HUB_PORT"]))
 
 
+def attach(ctx, comm):
+    """The rank transport under test: the host communicator itself, or (SSP_TEST_TRANSPORT=p2p) the
+    peer-memory communicator, whose id rank 0 makes and the hub distributes."""
+    import subspace_hip as sh
+
+    if os.environ.get("SSP_TEST_TRANSPORT") == "p2p" and comm.nranks > 1:
+        uid = comm.allgather(sh.Context.p2p_unique_id() if comm.rank == 0 else bytes(128))[0]
+        ctx.attach_p2p(comm.nranks, comm.rank, uid)
+    else:
+        attach(ctx, comm)
+
+
 def case_reductions(comm):
     import numpy as np
 
@@ -90,7 +102,7 @@ def case_gpu_ops(comm):
 
     rank, world = comm.rank, comm.nranks
     ctx = sh.Context(0)
-    ctx.attach_host_comm(comm)
+    attach(ctx, comm)
     assert (ctx.lib.ssp_ctx_rank(ctx.handle), ctx.lib.ssp_ctx_nranks(ctx.handle)) == (rank, world)
     for n in (5, 1003, 100_003):
         off, ln = sh.shard_range(n, world, rank)
@@ -136,7 +148,7 @@ def case_gpu_solver(comm):
 
     rank, world = comm.rank, comm.nranks
     ctx = sh.Context(0)
-    ctx.attach_host_comm(comm)
+    attach(ctx, comm)
     n, rho, seed = 100_003, 0.1, 20251015
     _, nl = sh.shard_range(n, world, rank)
     for rk, nroot, np_ in ((1, 4, 0), (4, 4, 8)):
@@ -175,8 +187,8 @@ def case_gpu_traces(comm):
 
     rank, world = comm.rank, comm.nranks
     ctx = sh.Context(0)
-    ctx.attach_host_comm(comm)
-    names = ("C3_n1e7_rank8", "C2_rank8", "C5_n1e7", "C5x_n1e7_traj12")
+    attach(ctx, comm)
+    names = ("C3_n1e7_rank8", "C2_rank8", "C5_n1e7", "C5x_n1e7_traj12", "RS_n2e21_p16", "RS_n2e21_rho1")
     if os.environ.get("SSP_TRACES_FULL"):
         names = FULL_TRACES[os.environ["SSP_TRACES_FULL"]]
     for name in names:
@@ -185,7 +197,7 @@ def case_gpu_traces(comm):
         nl = sh.shard_range(c["n"], world, rank)[1]
         g = run_case(ih, ctx, ref, n_local=nl, solutions=c["kind"] == "diis")
         assert_trace(g, ref, f"{name} on {world} shards")
-        if c["kind"] == "diis" and ref["converged"]:  # x = 1 on every shard
+        if c["kind"] == "diis" and ref["converged"]:  # x = t 1 (t = 1/sqrt(N)) on every shard
             assert np.max(np.abs(g["x"] - solution_target(ref))) <= ref["options"]["convergence_threshold"], name
         if rank == 0:
             print(f"{name} on {world} shards: {g['iterations']} iterations (CPU path {ref['iterations']}), "
@@ -201,20 +213,90 @@ def case_gpu_distr(comm):
     import subspace_hip as sh
 
     ctx = sh.Context(0)
-    ctx.attach_host_comm(comm)
+    attach(ctx, comm)
     distr_cases.check(ctx, sh, comm.rank, comm.nranks)
     ctx.close()
+
+
+def case_gpu_peer_lost(comm):
+    """Fail fast instead of hanging when a rank is lost mid-solve.  Both ranks repeat sharded Davidson
+    solves (C2's shape at N = 1e7).  Host transport: rank 1 dies (os._exit) 1 s in, and rank 0's next
+    reduction must fail with SSP_ERR_COMM at once (the peer's socket closes).  Peer-memory transport:
+    rank 1 stops taking part after its first solve, but stays alive (so no rank frees memory another
+    rank's kernel may still address); rank 0's next exchange must fail within SSP_COMM_TIMEOUT_S with
+    the device-side deadline naming rank 1, and rank 1 must then see the abort too.  Returns True: no
+    closing barrier (the communicator is gone)."""
+    import threading
+    import time
+
+    import itsolv_hbm as ih
+    import subspace_hip as sh
+
+    rank, world = comm.rank, comm.nranks
+    transport = os.environ.get("SSP_TEST_TRANSPORT", "host")
+    timeout = float(os.environ["SSP_COMM_TIMEOUT_S"])
+    ctx = sh.Context(0)
+    attach(ctx, comm)
+    n = 10_000_000
+    nl = sh.shard_range(n, world, rank)[1]
+    kw = dict(nroots=4, max_p=0, convergence_threshold=1e-8, max_size_qspace=24, reset_D=8)
+    solve = lambda: ih.davidson_synthetic(ctx, n, 0.1, 8, 1, n_local=nl, solutions=False, **kw)  # noqa: E731
+    t_lost = None
+    if rank == 1:
+        if transport == "host":
+            threading.Timer(1.0, lambda: os._exit(17)).start()
+            while True:
+                solve()
+        solve()
+        time.sleep(timeout + 8)  # missing from rank 0's next exchange, but alive
+        try:
+            ctx.dot(ctx.alloc(nl), ctx.alloc(nl))
+            raise AssertionError("rank 1: exchange after the abort succeeded")
+        except sh.SspError as e:
+            assert e.code == 5, e
+            print(f"rank 1 sees the abort: {e}", flush=True)
+        ctx.close()
+        return True
+    solve()
+    t_lost = time.time()
+    try:
+        while True:
+            solve()
+            t_lost = time.time()
+    except RuntimeError as e:
+        dt = time.time() - t_lost
+        msg = str(e)
+        print(f"rank 0: error {dt:.2f} s after the last completed solve: {msg}", flush=True)
+        if transport == "host":
+            assert "callback failed" in msg, msg
+            assert dt < 30, dt
+        else:  # the device-side deadline of a reduction, or the host deadline of a gather
+            assert "rank 1 did not arrive" in msg or "no completion within" in msg, msg
+            assert timeout - 1 < dt < timeout + 20, dt
+    # every later exchange fails at once
+    t0 = time.time()
+    try:
+        ctx.dot(ctx.alloc(nl), ctx.alloc(nl))
+        raise AssertionError("rank 0: exchange after the abort succeeded")
+    except sh.SspError as e:
+        assert e.code == 5 and time.time() - t0 < 1.0, e
+    ctx.close()
+    return True
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--comm", choices=["gloo", "hub"], required=True)
-    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver", "gpu_distr", "gpu_traces"],
-                    required=True)
+    ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver", "gpu_distr", "gpu_traces",
+                                       "gpu_peer_lost"], required=True)
     a = ap.parse_args()
     comm = make_comm(a.comm)
-    {"reductions": case_reductions, "gpu_ops": case_gpu_ops, "gpu_solver": case_gpu_solver,
-     "gpu_distr": case_gpu_distr, "gpu_traces": case_gpu_traces}[a.case](comm)
+    no_barrier = {"reductions": case_reductions, "gpu_ops": case_gpu_ops, "gpu_solver": case_gpu_solver,
+                  "gpu_distr": case_gpu_distr, "gpu_traces": case_gpu_traces,
+                  "gpu_peer_lost": case_gpu_peer_lost}[a.case](comm)
+    if no_barrier:
+        print(f"rank {comm.rank}/{comm.nranks} {a.case} OK", flush=True)
+        os._exit(0)  # the hub peer may be gone: no closing collective
     if a.comm == "gloo":
         import torch.distributed as dist
 

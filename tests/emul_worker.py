@@ -193,6 +193,31 @@ def case_c4(gloo=False):
     assert np.allclose(e, ei, rtol=1e-4, atol=0), (e, ei)
 
 
+def case_rs_traces():
+    """The near-dependent trace cases (traces.json RS_*: N = 2^21, the redundancy screen fires) through
+    the product's host code over the emulation: above the 2^20 threshold, so the fused solver passes
+    (one-pass self-orthonormalisation, batched overlap rows, residuals with their norms, block
+    Gram-Schmidt) run, with the emulation's arithmetic set by argv[2] = "sum_order,fma" (0,0: the
+    reference's sequential uncontracted loops; 1,1: 8-lane sums and fma, as a GPU rounds).  Full trace
+    bar against the committed CPU-path traces (tests/trace_check.py)."""
+    import ctypes
+
+    from trace_check import T, assert_trace, run_case
+
+    so, fma = (int(v) for v in sys.argv[2].split(","))
+    lib = ctypes.CDLL(sh.LIB_PATH)
+    assert lib.ssp_emul_set_arith(so, fma) == 0
+    ctx = sh.Context(0)
+    for name in ("RS_n2e21_p16", "RS_n2e21_rho1"):
+        ref = T[name]
+        g = run_case(ih, ctx, ref, solutions=False)
+        assert g["redundant_params"] > 0, name
+        assert_trace(g, ref, f"{name} (emulated device, arith {so},{fma})")
+        np.testing.assert_allclose(g["eigenvalues"], ref["eigenvalues"], rtol=1e-10, atol=0)
+        print(name, g["iterations"], "iterations,", g["redundant_params"], "redundant", flush=True)
+    ctx.close()
+
+
 def case_devsel():
     """The reference C API's instances take the device of the node-local rank the launcher exported
     (iterative_solver_c.cpp default_device) modulo the visible device count; argv[2] = expected."""
@@ -219,5 +244,5 @@ def case_distr():
 
 if __name__ == "__main__":
     {"api": case_api, "spmd": case_spmd, "spmd-gloo": lambda: case_spmd(gloo=True), "c4": case_c4, "distr": case_distr,
-     "devsel": case_devsel}[sys.argv[1]]()
+     "devsel": case_devsel, "rs_traces": case_rs_traces}[sys.argv[1]]()
     print(f"{sys.argv[1]} OK", flush=True)

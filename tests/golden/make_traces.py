@@ -32,6 +32,13 @@ reference's test_rayleigh_quotient.cpp:37-42 matrix at large n), options of §8d
                                               by up to 20 % and the unit-norm solution 1/sqrt(N);
                                               |r_0| = 3.2, 10 steps to the 1e-8 threshold, the last
                                               two errors 2.8x above / 1.5x below it)
+  RS  Davidson  8 roots (+ P 16)   N = 2^21  the redundancy screen's cases (propose_rspace.h:481-512):
+                                              H = diag(1 + g) + rho 1 1^T, whose preconditioned residuals
+                                              (D - lambda)^-1 r all lie close to the span of earlier
+                                              (D - mu)^-1 1, so new R vectors are near-dependent and the
+                                              screen removes 6 (P 16, rho 0.1) and 3 (rho 1) of them; above
+                                              the fused-pass threshold (2^20), so the product runs its
+                                              one-pass orthonormalisation and batched overlap rows on them
   C5x DIIS      max_size_qspace 6   N = 1e7   the round-1 instance (diag(1+g), rank 3, rho 0.01):
                                               |r_0| = 1.9e10, so the threshold lies below its rounding
                                               floor and the count past the 1e-6 plateau is decided by
@@ -70,6 +77,9 @@ CASES = {
                     target=10_000_000 ** -0.5, convergence_threshold=1e-8),
     "C5_n1e8": dict(kind="diis", n=100_000_000, rho=1.0 / 100_000_000, rank=1, seed=3, diag_kind=1, alpha=0.2,
                     target=100_000_000 ** -0.5, convergence_threshold=1e-8),
+    # RS: near-dependent R vectors at 2^21 elements (the redundancy screen fires; fused passes on)
+    "RS_n2e21_p16": dict(kind="davidson", n=2 ** 21, rho=0.1, rank=1, seed=SEED, nroots=8, max_p=16),
+    "RS_n2e21_rho1": dict(kind="davidson", n=2 ** 21, rho=1.0, rank=1, seed=SEED, nroots=8, max_p=0),
     # C5x: the round-1 DIIS problem (profiles/r1/solver_ledger_v10.json: rho 0.01, rank 3, seed 3), chaotic
     "C5x_n1e7_traj12": dict(kind="diis", n=10_000_000, rho=0.01, rank=3, seed=3, max_iter=12,
                             convergence_threshold=1e-14),
@@ -110,7 +120,8 @@ def variant_record(c, r, v):
         "q_creations": v["q_creations"],
         "converged": v["converged"],
         "same_steps": bool(v["iterations"] == r["iterations"] and v["r_creations"] == r["r_creations"]
-                           and list(tv["nq"]) == list(tr["nq"]) and list(tv["nwork"]) == list(tr["nwork"])),
+                           and list(tv["nq"]) == list(tr["nq"]) and list(tv["nwork"]) == list(tr["nwork"])
+                           and list(tv.get("screened", [])) == list(tr.get("screened", []))),
         # per iteration (over the common prefix): max |error_variant - error_reference| over roots
         "error_abs_dev": np.max(np.abs(np.asarray(tv["errors"])[:k] - np.asarray(tr["errors"])[:k]),
                                 axis=1).tolist(),
@@ -153,7 +164,10 @@ def run(name, variants=tuple(VARIANTS), base=None):
             "errors": tr["errors"].tolist(),
             "nq": tr["nq"].tolist(),
             "nwork": tr["nwork"].tolist(),
+            "screened": tr["screened"].tolist(),
         },
+        "redundant_params": r["redundant_params"],
+        "null_params": r["null_params"],
         "cpu_seconds": round(time.time() - t0, 1),
     }
     for key in variants:
@@ -186,7 +200,9 @@ def run_part(name, part):
         "eigenvalues": [float(x) for x in r["eigenvalues"]] if c["kind"] == "davidson" else [],
         "errors": [float(x) for x in r["errors"]],
         "trace": {"eigenvalues": tr["eigenvalues"].tolist() if c["kind"] == "davidson" else [],
-                  "errors": tr["errors"].tolist(), "nq": tr["nq"].tolist(), "nwork": tr["nwork"].tolist()},
+                  "errors": tr["errors"].tolist(), "nq": tr["nq"].tolist(), "nwork": tr["nwork"].tolist(),
+                  "screened": tr["screened"].tolist()},
+        "redundant_params": r["redundant_params"], "null_params": r["null_params"],
         "cpu_seconds": round(time.time() - t0, 1),
     }
 

@@ -65,8 +65,20 @@ def test_mfma_util_lookup():
 
 
 def test_cpu_baseline_leg():
-    cb = bench.cpu_baseline(2, 3, 0.05)
+    # in a thread, as bench.py runs it: the leg pins its own thread to one core (never the caller's)
+    import threading
+
+    box = {}
+    th = threading.Thread(target=lambda: box.update(cb=bench.cpu_baseline_core(2, 3, 0.05, n=200_000),
+                                                    solve=bench.cpu_solve_core(n=20_000)))
+    before = os.sched_getaffinity(0)
+    th.start()
+    th.join()
+    assert os.sched_getaffinity(0) == before
+    cb, cs = box["cb"], box["solve"]
     assert cb["kind"] == "port" and cb["cores"] == 1 and cb["unit"] == "GB/s" and cb["value"] > 0
+    assert "pinned: cpu" in cb["sample"] and cs["cores"] == 1 and cs["converged"] and cs["iterations"] > 0
+    bench.cpu_baseline_extras(cb, 2, 3, 0.05)
     hp = cb["host_parallel"]
     assert hp["kind"] == "host-parallel" and hp["cores"] >= 1 and hp["value"] > 0
 
@@ -85,7 +97,7 @@ def parse(out):
 @pytest.mark.gpu
 def test_bench_single_gpu():
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--n-global", "4e6",
-           "--cpu-seconds", "0.5"]
+           "--cpu-seconds", "0.5", "--cpu-n", "1e6", "--cpu-solve-n", "1e5"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
     d = parse(r.stdout)
@@ -94,6 +106,8 @@ def test_bench_single_gpu():
     # the roofline ledger is the timed region: every op of the 3 steps carries its event pair
     assert d["ledger"].startswith("HIP events around every op") and d["ops"]["gemm_outer"]["calls_per_step"] == 2
     assert d["sustained"]["steps"] >= 5 and d["sustained"]["GBs"] > 0
+    s = d["in_solver_cpu"]
+    assert s["cpu"]["converged"] and s["same_iterations"] and s["speedup"] > 0
 
 
 @pytest.mark.gpu

@@ -43,12 +43,15 @@ def run_torchrun(case, world=WORLD, timeout=300):
     assert r.stdout.count(f"{case} OK") == world, r.stdout[-2000:]
 
 
-def run_hub(case, world=WORLD, timeout=600):
-    """world ranks as plain subprocesses with the stdlib-socket host communicator."""
+def run_hub(case, world=WORLD, timeout=600, transport="host", env_extra=None):
+    """world ranks as plain subprocesses with the stdlib-socket host communicator; transport "p2p"
+    moves the reductions to the peer-memory communicator (ssp_ctx_attach_p2p, its id sent over the
+    hub), the hub then only bootstraps and checks."""
     port = free_port()
     procs = []
     for rank in range(world):
-        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), SSP_HUB_PORT=str(port))
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), SSP_HUB_PORT=str(port),
+                   SSP_TEST_TRANSPORT=transport, **(env_extra or {}))
         procs.append(subprocess.Popen([sys.executable, WORKER, "--comm", "hub", "--case", case], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []

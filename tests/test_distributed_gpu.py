@@ -9,9 +9,14 @@ solver.  The bar is the unsharded reference: select bit-exact, reductions to rou
 sharded Davidson / DIIS runs take the same iterations as the CPU reference path with eigenvalues
 within 1e-10 (tests/dist_worker.py).
 """
+import os
+import subprocess
+import sys
+import time
+
 import pytest
 
-from test_distributed import run_hub
+from test_distributed import WORKER, free_port, run_hub
 
 pytestmark = pytest.mark.gpu
 
@@ -51,6 +56,70 @@ def test_c4_full_size_on_8_shards(monkeypatch):
 def test_c5_full_size_on_8_shards(monkeypatch):
     # BASELINE config C5 at full size (DIIS, N = 1e8) over 8 ranks (8 processes on one MI355X, host
     # communicator): the committed CPU-path trace (traces.json C5_n1e8) step for step -- iterations,
-    # R/Q creations, Q-space and working-set sizes -- and x = 1 on every shard
+    # R/Q creations, Q-space and working-set sizes -- and x = t 1 (t = 1/sqrt(N)) on every shard
     monkeypatch.setenv("SSP_TRACES_FULL", "C5")
     print(run_hub("gpu_traces", world=8, timeout=600)[0])
+
+
+# ---- the peer-memory transport (ssp_ctx_attach_p2p): the multi-rank DEVICE exchange on one MI355X --
+# The same cases with every reduction summed by the ranks' k_p2p_allreduce kernels through IPC-shared
+# inboxes (fixed rank order, bit-identical on every rank) and the select all-gather / barriers through
+# the shared host segment: the code path of a multi-rank device exchange, which RCCL cannot run with
+# several ranks on one GPU.
+
+def test_world2_ops_on_shards_p2p():
+    run_hub("gpu_ops", timeout=600, transport="p2p", env_extra={"SSP_COMM_TIMEOUT_S": "60"})
+
+
+def test_world2_davidson_and_diis_on_shards_p2p():
+    run_hub("gpu_solver", timeout=900, transport="p2p", env_extra={"SSP_COMM_TIMEOUT_S": "60"})
+
+
+def test_world2_reference_distributed_array_known_answers_p2p():
+    run_hub("gpu_distr", timeout=300, transport="p2p", env_extra={"SSP_COMM_TIMEOUT_S": "60"})
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_sharded_traces_match_reference_path_p2p(world):
+    print(run_hub("gpu_traces", world=world, timeout=600, transport="p2p",
+                  env_extra={"SSP_COMM_TIMEOUT_S": "60"})[0])
+
+
+def test_c4_full_size_on_8_shards_p2p():
+    print(run_hub("gpu_traces", world=8, timeout=600, transport="p2p",
+                  env_extra={"SSP_TRACES_FULL": "C4", "SSP_COMM_TIMEOUT_S": "60"})[0])
+
+
+def test_c5_full_size_on_8_shards_p2p():
+    print(run_hub("gpu_traces", world=8, timeout=600, transport="p2p",
+                  env_extra={"SSP_TRACES_FULL": "C5", "SSP_COMM_TIMEOUT_S": "60"})[0])
+
+
+# ---- fail fast: a lost rank ends the survivors' solves with SSP_ERR_COMM, no hang, no process left --
+@pytest.mark.parametrize("transport", ["host", "p2p"])
+def test_lost_rank_fails_fast(transport):
+    timeout_s = 6.0
+    port = free_port()
+    procs = []
+    t0 = time.time()
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", SSP_HUB_PORT=str(port), SSP_TEST_TRANSPORT=transport,
+                   SSP_COMM_TIMEOUT_S=str(timeout_s))
+        procs.append(subprocess.Popen([sys.executable, "-u", WORKER, "--comm", "hub", "--case", "gpu_peer_lost"],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=100)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    print(outs[0][-2000:])
+    assert procs[0].returncode == 0 and "gpu_peer_lost OK" in outs[0], outs[0][-4000:]
+    if transport == "host":
+        assert procs[1].returncode == 17, outs[1][-4000:]  # died mid-solve, as intended
+    else:
+        assert procs[1].returncode == 0 and "sees the abort" in outs[1], outs[1][-4000:]
+    assert all(p.poll() is not None for p in procs)  # nothing left behind
+    assert time.time() - t0 < 90

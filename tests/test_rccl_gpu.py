@@ -75,3 +75,78 @@ def test_davidson_and_diis_through_rccl(pair):
     a, b = both(pair, lambda c: ih.diis_synthetic(c, 100_000, 0.1, 1, 3, **kw))
     assert a["iterations"] == b["iterations"]
     assert np.array_equal(a["x"], b["x"])
+
+
+def test_comm_deadline_aborts_instead_of_hanging():
+    # Fail fast (context.hip wait_flag / comm_p2p.hip comm_poll): with a communicator attached, a
+    # reduction whose result does not arrive within SSP_COMM_TIMEOUT_S returns SSP_ERR_COMM, the
+    # communicator is aborted (ncclCommAbort) and every later exchange fails at once -- the
+    # status-code form of the reference's job abort (DistrArray.cpp:16-23).  The stalled stream (a
+    # bounded device spin standing in for a missing peer) ends on its own.
+    import time
+
+    c = sh.Context(0)
+    c.attach_comm(1, 0, sh.Context.unique_id())
+    c.set_comm_timeout(0.5)
+    x = c.upload(np.ones(1000))
+    assert c.dot(x, x) == 1000.0
+    c.debug_stall(3000)
+    t0 = time.time()
+    with pytest.raises(sh.SspError) as e:
+        c.dot(x, x)
+    dt = time.time() - t0
+    assert e.value.code == 5 and "no completion within 0.5 s" in str(e.value), e.value
+    # the deadline fired at 0.5 s; ncclCommAbort then waits for the stream's work -- a stuck RCCL
+    # kernel is released by the abort, this stand-in spin ends by itself at 3 s
+    assert 0.4 < dt < 4.0, dt
+    t0 = time.time()
+    with pytest.raises(sh.SspError) as e:
+        c.gemm_inner([x], [x])
+    assert e.value.code == 5 and time.time() - t0 < 0.5
+    with pytest.raises(sh.SspError):
+        c.allgather_bytes(b"x")
+    c.close()  # waits for the stall to drain
+
+
+def test_p2p_deadline_aborts_instead_of_hanging():
+    # The same on the peer-memory transport, whose abort only raises the shared abort word (no wait):
+    # the error comes at the host deadline (timeout + min(5 s, timeout)) while the stream is still busy.
+    import time
+
+    c = sh.Context(0)
+    c.attach_p2p(1, 0, sh.Context.p2p_unique_id())
+    c.set_comm_timeout(0.5)
+    x = c.upload(np.ones(1000))
+    assert c.dot(x, x) == 1000.0
+    c.debug_stall(4000)
+    t0 = time.time()
+    with pytest.raises(sh.SspError) as e:
+        c.dot(x, x)
+    dt = time.time() - t0
+    assert e.value.code == 5 and "no completion within 0.5 s" in str(e.value), e.value
+    assert 0.9 < dt < 2.0, dt
+    with pytest.raises(sh.SspError):
+        c.barrier()
+    c.close()
+
+
+@pytest.mark.parametrize("n", [1, 1003, 1_000_003])
+def test_one_rank_p2p_transport_is_the_identity(pair, n):
+    # The peer-memory transport with one rank pushes into its own inbox and sums it: every reduction
+    # bit-identical to the communicator-free context (the multi-rank cases: test_distributed_gpu.py).
+    plain, _ = pair
+    c = sh.Context(0)
+    c.attach_p2p(1, 0, sh.Context.p2p_unique_id())
+    try:
+        r = np.random.default_rng(n)
+        xs = [r.uniform(-1, 1, n) for _ in range(8)]
+        ys = [r.uniform(-1, 1, n) for _ in range(5)]
+        for fn in (lambda k: k.dot(k.upload(xs[0]), k.upload(ys[0])),
+                   lambda k: k.gemm_inner([k.upload(v) for v in xs], [k.upload(v) for v in ys]),
+                   lambda k: k.gemm_inner_sparse([k.upload(v) for v in xs[:3]], [{0: 1.0}, {n - 1: -2.0}]),
+                   lambda k: k.select(k.upload(np.round(xs[1] * 30)), min(16, n))[0].tolist()):
+            assert np.array_equal(fn(plain), fn(c))
+        assert c.allgather_bytes(b"abc") == [b"abc"]
+        c.barrier()
+    finally:
+        c.close()

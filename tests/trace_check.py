@@ -60,6 +60,9 @@ def assert_trace(gpu, ref, name):
         assert gpu["q_creations"] == ref["q_creations"], name
         assert list(g["nq"]) == r["nq"], (name, list(g["nq"]), r["nq"])
         assert list(g["nwork"]) == r["nwork"], name
+        if "screened" in r:  # propose_rspace's redundancy / null screening, iteration by iteration
+            assert list(g["screened"]) == r["screened"], (name, list(g["screened"]), r["screened"])
+            assert (gpu["redundant_params"], gpu["null_params"]) == (ref["redundant_params"], ref["null_params"]), name
     if r["eigenvalues"]:
         re = np.array(r["eigenvalues"])
         de = np.abs(g["eigenvalues"] - re)
