@@ -126,14 +126,13 @@ int sync_stream(ssp_ctx* ctx, const char* what) {
     return SSP_OK;
   }
   SSP_TRY(comm_check(ctx));
-  const double t0 = now_s();
-  for (unsigned spin = 1;; ++spin) {
-    const hipError_t e = hipStreamQuery(ctx->stream);
-    if (e == hipSuccess) return SSP_OK;
-    if (e != hipErrorNotReady) return hip_error(e, what);
-    if ((spin & 63) == 0) SSP_TRY(comm_poll(ctx, t0, what));
-    _mm_pause();
-  }
+  // A stream write of the next sequence number into the coherent host flag, then the bounded host
+  // poll of wait_flag (which also queries the stream every few hundred polls): as fast as the
+  // reduction hand-off, where a hipStreamQuery loop costs a runtime call per poll.
+  const unsigned long long seq = ++ctx->pub_seq;
+  SSP_TRY_HIP(hipStreamWriteValue64(ctx->stream, ctx->pub_flag, seq, 0));
+  bool seen = true;  // a drained stream without the flag visible is synchronised all the same
+  return wait_flag(ctx, seq, &seen, what);
 }
 
 // ---- peer-memory transport ------------------------------------------------------------------

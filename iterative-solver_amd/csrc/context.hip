@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void k_publish(const double* src, size_t n, do
 // flag becoming visible (the writes of a finished kernel are visible all the same).  With a
 // communicator attached the wait is bounded (comm_poll: SSP_COMM_TIMEOUT_S, RCCL's asynchronous
 // error, the peer-memory transport's abort word), since the flag then depends on other ranks.
-int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen) {
+int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen, const char* what) {
   *seen = true;
   const bool ranks = comm_attached(ctx);
   const double t0 = ranks ? now_s() : 0.0;
@@ -169,10 +169,10 @@ int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen) {
     if ((spin & 255) == 0) {
       const hipError_t e = hipStreamQuery(ctx->stream);
       if (e == hipErrorNotReady) {
-        if (ranks && (spin & 4095) == 0) SSP_TRY(comm_poll(ctx, t0, "reduction"));
+        if (ranks && (spin & 4095) == 0) SSP_TRY(comm_poll(ctx, t0, what));
         continue;
       }
-      if (e != hipSuccess) return hip_error(e, "reduction");
+      if (e != hipSuccess) return hip_error(e, what);
       *seen = __atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq;
       return SSP_OK;
     }

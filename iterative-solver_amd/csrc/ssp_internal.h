@@ -125,7 +125,7 @@ int fetch_result(ssp_ctx* ctx, double* out, size_t n);
 // or the peer-memory transport's fused exchange-and-publish).
 int reduce_fetch(ssp_ctx* ctx, double* out, size_t n);
 // Waits (host poll) until the publish flag carries seq; bounded when a communicator is attached.
-int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen);
+int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen, const char* what = "reduction");
 // Grid size for streaming kernels: enough workgroups to fill 256 CUs, grid-stride beyond.
 // Workgroups for a grid-stride streaming launch: enough for work_items / (kBlock * per_thread),
 // at most blocks_per_cu per CU.

@@ -365,7 +365,9 @@ def set_sum_order(order):
     """Summation order of the CPU path's dot / gemm_inner (oracle_ops.c or_set_sum_order): 0 = the
     reference's sequential loop (default), 1 = 8 interleaved partial sums (a vectorised build of the
     same loop), 2 = sequential sums over 1024-element blocks folded pairwise (a blocked / threaded
-    reduction).  Used only to measure the reference algorithm's own rounding sensitivity."""
+    reduction), 100 + P = the reference's distributed build on P MPI ranks (rank-local sequential
+    sums, the P partials added in rank order).  Used only to measure the reference algorithm's own
+    rounding sensitivity."""
     L = itsolv_lib()
     L.or_set_sum_order.argtypes = [C.c_int]
     L.or_set_sum_order.restype = C.c_int

@@ -49,17 +49,33 @@ int or_axpy(double alpha, const double* x, size_t nx, double* y, size_t ny) {
  * how sensitive the REFERENCE algorithm itself is to a valid change of summation order
  * (tests/golden/make_traces.py: the "reordered" runs).  2 = sequential partial sums over consecutive
  * 1024-element blocks, the block sums folded pairwise: the shape of a blocked / threaded reduction
- * (an OpenMP-parallel build of the loop, numpy's pairwise sum) and of the GPU's ("reordered_blocked"). */
+ * (an OpenMP-parallel build of the loop, numpy's pairwise sum) and of the GPU's ("reordered_blocked").
+ * 100 + P (P = 2..64) = the reference's own distributed build on P MPI ranks: the index range split
+ * by make_distribution_spread_remainder (util/Distribution.h:99-109), each rank's local
+ * std::inner_product sequential, the P partials summed in rank order (DistrArray.cpp:124-138, the
+ * MPI_Allreduce of util/gemm.h:179-182) ("mpiP" runs). */
 static int g_sum_order = 0;
 
 int or_set_sum_order(int order) {
-  if (order < 0 || order > 2) return 1;
+  if (order < 0 || (order > 2 && (order < 102 || order > 164))) return 1;
   g_sum_order = order;
   return 0;
 }
 
 int or_dot(const double* x, size_t nx, const double* y, size_t ny, double* out) {
   if (nx > ny) return 1;
+  if (g_sum_order >= 100) {
+    const size_t P = (size_t)(g_sum_order - 100), blk = nx / P, extra = nx % P;
+    double s = 0;
+    for (size_t r = 0; r < P; ++r) {
+      const size_t b = r * blk + (r < extra ? r : extra), e = b + blk + (r < extra ? 1 : 0);
+      double l = 0;
+      for (size_t i = b; i < e; ++i) l = l + x[i] * y[i];
+      s = r ? s + l : l;
+    }
+    *out = s;
+    return 0;
+  }
   if (g_sum_order == 2) {
     const size_t B = 1024;
     size_t nb = (nx + B - 1) / B;

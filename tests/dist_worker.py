@@ -49,7 +49,7 @@ def attach(ctx, comm):
         uid = comm.allgather(sh.Context.p2p_unique_id() if comm.rank == 0 else bytes(128))[0]
         ctx.attach_p2p(comm.nranks, comm.rank, uid)
     else:
-        attach(ctx, comm)
+        ctx.attach_host_comm(comm)
 
 
 def case_reductions(comm):

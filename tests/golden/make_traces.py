@@ -105,7 +105,12 @@ def options(c):
 # The CPU path re-run with its dots summed in other valid orders (oracle_ops.c or_set_sum_order):
 # how far the REFERENCE algorithm itself moves under a change of rounding.
 VARIANTS = {"reordered": 1,          # 8 interleaved partial sums (a vectorising build)
-            "reordered_blocked": 2}  # 1024-element blocks folded pairwise (a blocked / threaded build)
+            "reordered_blocked": 2,  # 1024-element blocks folded pairwise (a blocked / threaded build)
+            # the reference's own distributed build on P MPI ranks (rank-local sequential sums, partials
+            # added in rank order: DistrArray.cpp:124-138 + MPI_Allreduce); generated for the RS cases
+            # (--add-variants), whose residual norms move under them by more than under the two above
+            "mpi2": 102, "mpi3": 103, "mpi4": 104, "mpi8": 108, "mpi16": 116}
+DEFAULT_VARIANTS = ("reordered", "reordered_blocked")
 
 
 def variant_record(c, r, v):
@@ -131,7 +136,7 @@ def variant_record(c, r, v):
     }
 
 
-def run(name, variants=tuple(VARIANTS), base=None):
+def run(name, variants=DEFAULT_VARIANTS, base=None):
     """The reference run of case `name` (or `base`, its committed record) and the given variants."""
     import oracle
 
@@ -251,7 +256,7 @@ def main():
     names = a.only or [n for n in CASES if n != "C3_n1e8_rank8"]
     old = json.load(open(a.out)) if os.path.exists(a.out) else {}
     old = {k: v for k, v in old.items() if k in CASES or k.startswith("_")}
-    variants = tuple(a.add_variants) if a.add_variants else tuple(VARIANTS)
+    variants = tuple(a.add_variants) if a.add_variants else DEFAULT_VARIANTS
 
     def job(n):
         return (n, variants, old[n]) if a.add_variants else (n, variants)

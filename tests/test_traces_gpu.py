@@ -91,3 +91,33 @@ def test_c5x_diis_converges_n1e7_like_reference(ctx):
     assert ref["reordered"]["iterations"] != ref["iterations"]
     print(f"C5x N=1e7: GPU {r['iterations']} iterations, CPU path {ref['iterations']} "
           f"(reordered CPU path {ref['reordered']['iterations']})")
+
+
+RS = sorted(k for k in T if k.startswith("RS_"))
+RS_CHILD = r"""
+import sys
+sys.path[:0] = sys.argv[1:3]
+import itsolv_hbm as ih
+import subspace_hip as sh
+from trace_check import T, assert_trace, run_case
+with sh.Context(0) as ctx:
+    for name in sys.argv[3:]:
+        g = run_case(ih, ctx, T[name], solutions=False)
+        assert_trace(g, T[name], name + " (SSP_ORTHO=two_pass)")
+        print(name, g["iterations"], "iterations", g["redundant_params"], "redundant", flush=True)
+"""
+
+
+def test_rs_traces_with_reference_coefficients():
+    # The near-dependent RS cases with the two-pass self-orthonormalisation (the reference's own
+    # coefficients, SSP_ORTHO=two_pass; the default above 2^20 is one pass): the same bar
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    pkg = os.path.join(os.path.dirname(here), "iterative-solver_amd")
+    r = subprocess.run([sys.executable, "-c", RS_CHILD, pkg, here, *RS], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, SSP_ORTHO="two_pass"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    print(r.stdout)

@@ -26,7 +26,9 @@ DAVIDSON = sorted(k for k, v in T.items() if not k.startswith("_") and v["case"]
 EIG_REL, ERR_REL, ERR_ABS, DEV_FACTOR = 1e-10, 1e-6, 1e-13, 10.0
 
 
-VARIANTS = ("reordered", "reordered_blocked")  # make_traces.py VARIANTS: valid sum orders of the CPU path
+# make_traces.py VARIANTS: valid sum orders of the CPU path -- a vectorising and a blocked build of its
+# loops, and (where generated: the RS cases) the reference's own distributed build on 2..16 MPI ranks
+VARIANTS = ("reordered", "reordered_blocked", "mpi2", "mpi3", "mpi4", "mpi8", "mpi16")
 
 
 def variants(ref):

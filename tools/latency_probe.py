@@ -29,11 +29,16 @@ def main():
     ap.add_argument("--rccl", action="store_true",
                     help="attach a one-rank RCCL communicator: reductions take the multi-rank path "
                          "(fold -> ncclAllReduce -> publish) instead of the fused host publish")
+    ap.add_argument("--p2p", action="store_true",
+                    help="attach a one-rank peer-memory communicator: fold -> k_p2p_allreduce (push, flag "
+                         "wait, rank-order sum, host publish)")
     args = ap.parse_args()
     res = {}
     with sh.Context(0) as ctx:
         if args.rccl:
             ctx.attach_comm(1, 0, sh.Context.unique_id())
+        if args.p2p:
+            ctx.attach_p2p(1, 0, sh.Context.p2p_unique_id())
         for n in (1024, 1_000_000, 12_500_000):
             reps = 2000 if n <= 1_000_000 else 200
             x = [ctx.alloc(n) for _ in range(56)]

@@ -93,10 +93,13 @@ def main():
     ap.add_argument("--configs", default="C2,C2-mgs,C3,C3-mgs,C5")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "solver_ledger.json"))
     ap.add_argument("--rccl", action="store_true", help="attach a one-rank RCCL communicator (multi-rank path)")
+    ap.add_argument("--p2p", action="store_true", help="attach a one-rank peer-memory communicator (multi-rank path)")
     a = ap.parse_args()
     ctx = sh.Context(0)
     if a.rccl:
         ctx.attach_comm(1, 0, sh.Context.unique_id())
+    if a.p2p:
+        ctx.attach_p2p(1, 0, sh.Context.p2p_unique_id())
     res = [run(ctx, c) for c in a.configs.split(",")]
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
