@@ -89,32 +89,41 @@ int ensure_result(ssp_ctx* ctx, size_t n) {
   return SSP_OK;
 }
 
+int flush_uploads(ssp_ctx* ctx) {
+  if (ctx->ring_head > ctx->ring_pending) {
+    const size_t o = ctx->ring_pending;
+    SSP_TRY_HIP(hipMemcpyAsync(ctx->ring_dev + o, ctx->ring_host + o, ctx->ring_head - o, hipMemcpyHostToDevice,
+                               ctx->stream));
+  }
+  ctx->ring_pending = ctx->ring_head;
+  return SSP_OK;
+}
+
 int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev) {
   const size_t need = (bytes + 255) & ~size_t(255);
   if (need > ctx->ring_cap) {
-    SSP_TRY(sync_stream(ctx, "upload ring growth"));
-    if (ctx->ring_dev) SSP_TRY_HIP(hipFree(ctx->ring_dev));
-    if (ctx->ring_host) SSP_TRY_HIP(hipHostFree(ctx->ring_host));
+    // arrays already staged in the old ring keep their addresses: it is retired, not freed
+    SSP_TRY(flush_uploads(ctx));
+    if (ctx->ring_dev || ctx->ring_host) ctx->retired_rings.emplace_back(ctx->ring_dev, ctx->ring_host);
     ctx->ring_dev = ctx->ring_host = nullptr;
     size_t cap = std::max(need * 2, size_t(4) << 20);
     if (hipMalloc(reinterpret_cast<void**>(&ctx->ring_dev), cap) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&ctx->ring_host), cap, hipHostMallocDefault) != hipSuccess)
       return set_error(SSP_ERR_NOMEM, "allocation of upload ring failed");
     ctx->ring_cap = cap;
-    ctx->ring_head = 0;
+    ctx->ring_head = ctx->ring_pending = 0;
   }
   if (ctx->ring_head + need > ctx->ring_cap) {
-    // Wrap: every earlier copy out of the ring has completed once the stream drains.
+    // Wrap: copy what is staged, then every earlier copy out of the ring has completed once the
+    // stream drains.  The staged regions keep their device addresses (the copy lands there).
+    SSP_TRY(flush_uploads(ctx));
     SSP_TRY(sync_stream(ctx, "upload ring wrap"));
-    ctx->ring_head = 0;
+    ctx->ring_head = ctx->ring_pending = 0;
   }
   char* h = ctx->ring_host + ctx->ring_head;
   char* d = ctx->ring_dev + ctx->ring_head;
   ctx->ring_head += need;
-  if (bytes) {
-    std::memcpy(h, host, bytes);
-    SSP_TRY_HIP(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream));
-  }
+  if (bytes) std::memcpy(h, host, bytes);
   *dev = d;
   return SSP_OK;
 }
@@ -405,6 +414,10 @@ int ssp_ctx_destroy(ssp_ctx* ctx) {
   if (ctx->synth_mask) (void)hipFree(ctx->synth_mask);
   if (ctx->ring_dev) (void)hipFree(ctx->ring_dev);
   if (ctx->ring_host) (void)hipHostFree(ctx->ring_host);
+  for (auto& r : ctx->retired_rings) {
+    if (r.first) (void)hipFree(r.first);
+    if (r.second) (void)hipHostFree(r.second);
+  }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return SSP_OK;

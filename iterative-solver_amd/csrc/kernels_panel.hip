@@ -1109,6 +1109,7 @@ int gemm_outer_impl(ssp_ctx* ctx, const double* alphas, const double* const* xx,
         SSP_TRY(ssp::upload_small(ctx, block.data(), block.size() * sizeof(double), &p));
         a.alpha_dev = static_cast<const double*>(p);
       }
+      SSP_TRY(ssp::flush_uploads(ctx));
       SSP_TRY(launch_outer(ctx, a));
     }
   }

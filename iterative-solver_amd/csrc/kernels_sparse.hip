@@ -177,6 +177,7 @@ int ssp_sparse_copy(ssp_ctx* ctx, double* x, size_t n, size_t offset, const size
   SSP_TRY(upload_entries(ctx, ptr, li, lv, &dptr, &dli, &dv));
   ssp::LedgerScope ls(ctx, "sparse_copy", 16.0 * li.size());
   const unsigned grid = unsigned(std::min<size_t>((li.size() + kBlock - 1) / kBlock, 1024));
+  SSP_TRY(ssp::flush_uploads(ctx));
   hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), 1.0, 0);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
@@ -198,6 +199,7 @@ int ssp_sparse_axpy(ssp_ctx* ctx, double alpha, const size_t* idx, const double*
   ssp::LedgerScope ls(ctx, "sparse_axpy", 24.0 * li.size());
   // Distinct map keys never collide, so entries can be applied in parallel.
   const unsigned grid = unsigned(std::min<size_t>((li.size() + kBlock - 1) / kBlock, 1024));
+  SSP_TRY(ssp::flush_uploads(ctx));
   hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), alpha, 1);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
@@ -242,6 +244,7 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const do
     a.v = dv;
     a.out = ctx->result_dev + size_t(i0) * k;
     const int outs = a.m * a.k;
+    SSP_TRY(ssp::flush_uploads(ctx));
     hipLaunchKernelGGL(k_sparse_inner, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
@@ -287,6 +290,7 @@ int ssp_gemm_outer_sparse(ssp_ctx* ctx, const double* alphas, const size_t* ptr,
     a.ptr = dptr;
     a.li = dli;
     a.v = dv;
+    SSP_TRY(ssp::flush_uploads(ctx));
     hipLaunchKernelGGL(k_sparse_outer, dim3(1), dim3(64), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
@@ -325,6 +329,7 @@ int solution_impl(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const 
     SSP_TRY(ssp::upload_small(ctx, uidx.data(), uidx.size() * sizeof(unsigned long long), &p));
     const size_t cnt = uidx.size() * size_t(m);
     SSP_TRY(ssp::ensure_partial(ctx, cnt));
+    SSP_TRY(ssp::flush_uploads(ctx));
     hipLaunchKernelGGL(k_gather_touched, dim3(unsigned((cnt + 255) / 256)), dim3(256), 0, ctx->stream,
                        static_cast<const unsigned long long*>(p), uidx.size(), m, ydev, ctx->partial);
     SSP_TRY_HIP(hipGetLastError());
@@ -375,6 +380,7 @@ int solution_impl(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const 
   ssp::LedgerScope ls(ctx, rmw ? "block_update_sparse" : "construct_solution_sparse",
                       8.0 * a.nu * m * (2.0 + k + (rmw ? 1.0 : 0.0)));
   const size_t threads = a.nu * size_t(m);
+  SSP_TRY(ssp::flush_uploads(ctx));
   hipLaunchKernelGGL(k_construct_fixup, dim3(unsigned((threads + 255) / 256)), dim3(256), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;

@@ -64,11 +64,17 @@ struct ssp_ctx {
   unsigned* fold_counter = nullptr;
 
   // Upload ring: pinned host + device mirror for small per-call operand arrays (sparse index
-  // lists).  Regions are reused only after a stream synchronisation at wrap-around.
+  // lists).  Regions are reused only after a stream synchronisation at wrap-around.  The arrays one
+  // op stages are copied by ONE hipMemcpyAsync (flush_uploads, before the op's first launch that
+  // reads them): [ring_pending, ring_head) is staged but not yet copied.
   char* ring_host = nullptr;
   char* ring_dev = nullptr;
   size_t ring_cap = 0;
   size_t ring_head = 0;
+  size_t ring_pending = 0;
+  // Rings replaced by a larger one: arrays staged in them may still be read by queued launches, so
+  // they are freed with the context.
+  std::vector<std::pair<char*, char*>> retired_rings;
 
   // Synthetic test problem (synthetic.hip): the per-element sign masks of u_1..u_{rank-1}, computed
   // once per (seed, rank, shard) and reused by every action of a solve.
@@ -114,8 +120,11 @@ int hip_error(hipError_t e, const char* what);
 int use_device(ssp_ctx* ctx);
 int ensure_partial(ssp_ctx* ctx, size_t n_doubles);
 int ensure_result(ssp_ctx* ctx, size_t n_doubles);
-// Copies `bytes` from host into the upload ring and returns the device address.
+// Stages `bytes` from host into the upload ring and returns the device address the data will have;
+// the copy itself is issued by flush_uploads, which every launch that reads staged data is preceded by.
 int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev);
+// One host-to-device copy of everything staged since the last flush (no-op when nothing is staged).
+int flush_uploads(ssp_ctx* ctx);
 // Sums the rank-local device results over ranks (no-op for one rank).
 int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n);
 // Copies n doubles of ctx->result_dev to host `out` once every operation queued before it has

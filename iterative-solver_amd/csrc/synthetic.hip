@@ -358,13 +358,9 @@ int sspx_synth_action_scaled(ssp_ctx* ctx, const sspx_synth* spec, const double*
       SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, nc * sizeof(double), ctx->stream));
     }
     SSP_TRY(ssp::allreduce_dev(ctx, ctx->result_dev, nc));
-    // The coefficients are consumed on the device; copy them aside so the next reduction can reuse
-    // the result staging buffer.
-    void* coeff;
-    std::vector<double> zeros(nc, 0.0);
-    SSP_TRY(ssp::upload_small(ctx, zeros.data(), nc * sizeof(double), &coeff));
-    SSP_TRY_HIP(hipMemcpyAsync(coeff, ctx->result_dev, nc * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
-    a.coeff = static_cast<const double*>(coeff);
+    // The coefficients are consumed on the device straight from the result staging buffer: the next
+    // reduction that rewrites it is queued after the apply kernel on the same stream.
+    a.coeff = ctx->result_dev;
     if (n > 0) {
       synth_apply<false>(ssp::stream_grid(ctx, n, 1), ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
@@ -397,6 +393,7 @@ int sspx_synth_add_lowrank(ssp_ctx* ctx, const sspx_synth* spec, double* const* 
     void* coeff;
     SSP_TRY(ssp::upload_small(ctx, w + size_t(v0) * rank, size_t(a.nvec) * rank * sizeof(double), &coeff));
     a.coeff = static_cast<const double*>(coeff);
+    SSP_TRY(ssp::flush_uploads(ctx));
     synth_apply<true>(ssp::stream_grid(ctx, n, 1), ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }

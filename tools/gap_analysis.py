@@ -17,8 +17,9 @@ from collections import defaultdict
 
 
 def short(name):
+    name = re.sub(r"^void ", "", name).replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)
-    return name[:60]
+    return name[:60] or "?"
 
 
 def main():

@@ -23,12 +23,14 @@ import subspace_hip as sh  # noqa: E402
 from solver_ledger import CONFIGS, REDUCING  # noqa: E402
 
 
-def solve(ctx, name):
+def solve(ctx, name, ledger):
+    """One solve; with ledger=False the wall time carries no HIP-event records (each op's two
+    hipEventRecord calls are host work on the path between a reduction and the next launch)."""
     solver, n, kw = CONFIGS[name]
     kw = dict(kw)
     rho, rank, seed = kw.pop("rho"), kw.pop("rank"), kw.pop("seed")
     ctx.ledger_reset()
-    ctx.ledger_enable(True)
+    ctx.ledger_enable(ledger)
     ctx.synchronize()
     t0 = time.perf_counter()
     fn = ih.davidson_synthetic if solver == "davidson" else ih.diis_synthetic
@@ -52,19 +54,25 @@ def main():
     ctxs["rccl"].attach_comm(1, 0, sh.Context.unique_id())
     ctxs["p2p"].attach_p2p(1, 0, sh.Context.p2p_unique_id())
     runs = {k: [] for k in ctxs}
+    led = {k: [] for k in ctxs}
     for k, c in ctxs.items():  # warm: arena and code objects
-        solve(c, a.config)
+        solve(c, a.config, True)
     for rep in range(a.reps):
         for k, c in ctxs.items():
-            runs[k].append(solve(c, a.config))
-    out = {"config": a.config, "reps": a.reps}
+            runs[k].append(solve(c, a.config, False))
+            led[k].append(solve(c, a.config, True))
+    out = {"config": a.config, "reps": a.reps,
+           "note": "wall: ledger-off solves; kernel: HIP-event ledger of ledger-on solves of the same problem"}
     for k, rs in runs.items():
-        med = {f: statistics.median(r[f] for r in rs) for f in ("wall_ms", "kernel_ms")}
-        out[k] = {"wall_ms": round(med["wall_ms"], 2), "kernel_ms": round(med["kernel_ms"], 2),
-                  "idle_ms": round(med["wall_ms"] - med["kernel_ms"], 2),
+        wall = statistics.median(r["wall_ms"] for r in rs)
+        wall_led = statistics.median(r["wall_ms"] for r in led[k])
+        kern = statistics.median(r["kernel_ms"] for r in led[k])
+        red = led[k][0]["reductions"]
+        out[k] = {"wall_ms": round(wall, 2), "wall_ms_ledger_on": round(wall_led, 2), "kernel_ms": round(kern, 2),
+                  "idle_ms": round(wall - kern, 2), "idle_frac_of_wall": round((wall - kern) / wall, 4),
                   "wall_ms_all": [round(r["wall_ms"], 2) for r in rs],
-                  "iterations": rs[0]["iterations"], "reductions": rs[0]["reductions"],
-                  "idle_us_per_reduction": round(1e3 * (med["wall_ms"] - med["kernel_ms"]) / max(1, rs[0]["reductions"]), 1)}
+                  "iterations": rs[0]["iterations"], "reductions": red,
+                  "idle_us_per_reduction": round(1e3 * (wall - kern) / max(1, red), 1)}
         print(k, json.dumps(out[k]), flush=True)
     for c in ctxs.values():
         c.close()
