@@ -166,15 +166,16 @@ def mfma_util(path, kernel_prefix="k_gemm_inner<2, 12"):
     return None, None
 
 
-def rendezvous_uid(rank, world, timeout=300.0):
-    """RCCL unique id from rank 0 to every rank of this node through a file keyed by the launcher
-    (MASTER_ADDR/PORT and the parent pid all local ranks share).  No torch in this process: it
-    would bring a second HIP runtime next to libsubspace_hip.so's."""
+def rendezvous_uid(rank, world, timeout=300.0, kind="rccl"):
+    """A communicator id (RCCL unique id, or kind "p2p": the peer-memory communicator's name) from
+    rank 0 to every rank of this node through a file keyed by the launcher (MASTER_ADDR/PORT and the
+    parent pid all local ranks share).  No torch in this process: it would bring a second HIP runtime
+    next to libsubspace_hip.so's."""
     tag = "{}_{}_{}".format(os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"),
                             os.getppid())
-    path = os.path.join(tempfile.gettempdir(), f"ssp_bench_uid_{tag}")
+    path = os.path.join(tempfile.gettempdir(), f"ssp_bench_{kind}_uid_{tag}")
     if rank == 0:
-        uid = sh.Context.unique_id()
+        uid = sh.Context.p2p_unique_id() if kind == "p2p" else sh.Context.unique_id()
         with open(path + ".tmp", "wb") as f:
             f.write(uid)
         os.replace(path + ".tmp", path)
@@ -289,8 +290,7 @@ def cpu_baseline_extras(cb, m, k, seconds):
     cb["host_parallel"] = host_parallel(m, k, max(1.0, seconds / 3))
     dram = {op: {kk: (round(v, 4) if isinstance(v, float) else v) for kk, v in d.items()}
             for op, d in oracle.dram_resident_sample(SEED).items()}
-    cb["dram_resident"] = dict(dram, note="one call each on 1 core, operands far beyond the host caches "
-                                          "(the N=1e6 step above is partly cache-resident)")
+    cb["dram_resident"] = dict(dram, note="one call each on 1 core, operands far beyond the host caches")
 
 
 def host_parallel(m, k, seconds):
@@ -432,9 +432,10 @@ def main():
                          "extra steps); for measuring the events' cost")
     ap.add_argument("--no-in-solver", action="store_true", help="skip the whole-solve block")
     ap.add_argument("--no-small", action="store_true", help="skip the headline step at N / 10")
-    ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
-                    help="rank transport at N > 1: RCCL (the product path) or the host socket hub, which "
-                         "lets tests run several ranks on ONE device (RCCL refuses duplicate GPUs)")
+    ap.add_argument("--comm", choices=("rccl", "p2p", "auto", "host"), default="rccl",
+                    help="rank transport at N > 1: RCCL; the peer-memory communicator (p2p: IPC-shared device "
+                         "inboxes, rank-order sums); auto = p2p when its attach self-test passes on every rank, "
+                         "else RCCL; or the host socket hub (tests: several ranks on ONE device)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r3", "pmc_traffic_n1e8.json"),
                     help="rocprofv3 --pmc summary of this workload (roofline.traffic)")
     ap.add_argument("--mfma-json", default=os.path.join(ROOT, "profiles", "r3", "mfma_util_n1e8.json"),
@@ -454,13 +455,26 @@ def main():
             port = int(os.environ.get("MASTER_PORT", "29500")) + 1
             ctx.attach_host_comm(sh.HubComm(rank, world, os.environ.get("MASTER_ADDR", "127.0.0.1"), port))
     else:
-        uid, uid_path = rendezvous_uid(rank, world) if world > 1 else (None, None)
         # one GPU per rank; a launcher that narrows HIP_VISIBLE_DEVICES per rank leaves one visible
         ctx = sh.Context(local_rank % max(1, sh.device_count()))
-        if world > 1:
+        transport = "rccl"
+        if world > 1 and args.comm in ("p2p", "auto"):
+            uid, uid_path = rendezvous_uid(rank, world, kind="p2p")
+            try:
+                ctx.attach_p2p(world, rank, uid)  # collective, self-tested, the verdict agreed by all ranks
+                transport = "p2p"
+            except sh.SspError as e:
+                if args.comm == "p2p":
+                    raise
+                log(f"rank {rank}: peer-memory transport unavailable ({e}); using RCCL")
+            if uid_path:  # attach returned on rank 0: every rank has read the id
+                os.remove(uid_path)
+        if world > 1 and transport == "rccl":
+            uid, uid_path = rendezvous_uid(rank, world)
             ctx.attach_comm(world, rank, uid)  # collective: returns once every rank has joined
             if uid_path:
                 os.remove(uid_path)
+        args.comm_used = transport
 
     ctx.synchronize()
     ctx_create_s = time.perf_counter() - t_ctx
@@ -635,7 +649,8 @@ def main():
                 "roots": m,
                 "qspace": k,
                 "parallelism": f"index-range shards x{world} ("
-                               + ("RCCL" if args.comm == "rccl" else "host-hub") + " allreduce for reductions)",
+                               + {"rccl": "RCCL", "p2p": "peer-memory", "host": "host-hub"}[getattr(args, "comm_used", args.comm)]
+                               + " allreduce for reductions)",
                 "bytes_per_step": step_bytes(n_global, m, k),
             },
             "roofline": {

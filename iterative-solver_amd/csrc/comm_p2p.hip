@@ -56,6 +56,7 @@ struct P2PShm {
   std::atomic<unsigned> attached[kP2PMaxRanks];
   std::atomic<int> abort_plus1;  // 0: running; q + 1: rank q gave up
   std::atomic<unsigned long long> host_seq[kP2PMaxRanks];
+  std::atomic<int> vote[kP2PMaxRanks];  // attach self-test: 1 passed, 2 failed
   hipIpcMemHandle_t handle[kP2PMaxRanks];
   char gather[2][kP2PMaxRanks][kP2PGather];
 };
@@ -126,6 +127,9 @@ int sync_stream(ssp_ctx* ctx, const char* what) {
     return SSP_OK;
   }
   SSP_TRY(comm_check(ctx));
+  const hipError_t q = hipStreamQuery(ctx->stream);  // an idle stream: nothing to wait for
+  if (q == hipSuccess) return SSP_OK;
+  if (q != hipErrorNotReady) return hip_error(q, what);
   // A stream write of the next sequence number into the coherent host flag, then the bounded host
   // poll of wait_flag (which also queries the stream every few hundred polls): as fast as the
   // reduction hand-off, where a hipStreamQuery loop costs a runtime call per poll.
@@ -463,6 +467,30 @@ int ssp_ctx_attach_p2p(ssp_ctx* ctx, int nranks, int rank, const char* id) {
   const int s = p2p_allgather_host(ctx, nullptr, nullptr, 0);
   if (s != SSP_OK) return fail(s, ssp_last_error());
   if (rank == 0) (void)shm_unlink(p->name.c_str());
+  // Self-test: one device exchange of known values (deadline at most 30 s), then a vote through the
+  // shared segment -- which needs no device path -- so that every rank reaches the same verdict
+  // and a caller can fall back to another transport consistently (bench.py --comm auto).
+  const double keep = ctx->comm_timeout_s;
+  SSP_TRY(ssp_ctx_set_comm_timeout(ctx, std::min(keep, 30.0)));
+  constexpr int kTest = 5;
+  double vals[kTest], got[kTest];
+  for (int i = 0; i < kTest; ++i) vals[i] = double(rank + 1 + i);
+  bool ok = hipMemcpy(ctx->result_dev, vals, sizeof(vals), hipMemcpyHostToDevice) == hipSuccess &&
+            p2p_allreduce_fetch(ctx, ctx->result_dev, got, kTest) == SSP_OK;
+  for (int i = 0; ok && i < kTest; ++i) ok = got[i] == double(nranks) * (nranks + 1) / 2 + double(nranks) * i;
+  p->shm->vote[rank].store(ok ? 1 : 2, std::memory_order_release);
+  bool all = true;
+  const double tv = now_s();
+  for (int q = 0; q < nranks; ++q) {
+    int v;
+    while ((v = p->shm->vote[q].load(std::memory_order_acquire)) == 0) {
+      if (now_s() - tv > ctx->comm_timeout_s + 10) return fail(SSP_ERR_COMM, "self-test vote timed out");
+      usleep(50);
+    }
+    all = all && v == 1;
+  }
+  if (!all) return fail(SSP_ERR_COMM, "self-test exchange failed on some rank (device path unusable)");
+  SSP_TRY(ssp_ctx_set_comm_timeout(ctx, keep));
   return SSP_OK;
 }
 

@@ -125,6 +125,24 @@ def test_bench_two_ranks_host_hub():
     assert d["config"]["n_local_rank0"] == 2_000_001  # spread-remainder: rank 0 takes the extra element
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("comm", ["p2p", "auto"])
+def test_bench_two_ranks_peer_memory(comm):
+    # the driver's launch with the peer-memory transport (two ranks on the one device): the attach
+    # self-test passes, the reductions run through k_p2p_allreduce, one JSON line
+    env = dict(os.environ)
+    for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--n-global", "4000001", "--comm", comm]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = parse(r.stdout)
+    assert d["n_gpus"] == 2 and "peer-memory" in d["config"]["parallelism"]
+    assert d["in_solver"]["converged"] and d["in_solver"].get("same_steps_as_cpu_path") is not False
+
+
 def test_bench_eight_ranks_emulated():
     """The driver's 8-GPU launch rehearsed on CPU: 8 ranks under torch.distributed.run over the host
     emulation of the device ABI (--comm host): shard sizes, barriers, max-over-ranks time, ledger and
