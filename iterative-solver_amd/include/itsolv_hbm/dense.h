@@ -51,7 +51,7 @@ inline void sym_eigen(size_t n, const std::vector<double>& a, std::vector<double
   std::vector<double> Z(n * n);
   for (size_t i = 0; i < n; ++i)
     for (size_t j = 0; j < n; ++j) Z[i * n + j] = 0.5 * (a[i * n + j] + a[j * n + i]);
-  std::vector<double> d(n, 0.0), e(n, 0.0);
+  std::vector<double> d(n, 0.0), e(n, 0.0), gacc_t(n, 0.0);
   if (n == 0) {
     evals.clear();
     evecs.clear();
@@ -76,13 +76,25 @@ inline void sym_eigen(size_t n, const std::vector<double>& a, std::vector<double
         h -= f * g;
         Z[i * n + l] = f - g;
         f = 0;
+        // gg_j = sum_{k<=j} Z[j][k] z_k, then + Z[k][j] z_k for k = j+1..l, in that order (the
+        // symmetric product with the lower triangle, z = row i).  The second part is accumulated
+        // row k at a time (unit stride) -- each gg_j still receives its terms in increasing k.
+        // Column i, written here, is read by none of these sums (they read columns <= l < i).
+        const double* zi = &Z[i * n];
         for (size_t j = 0; j <= l; ++j) {
-          Z[j * n + i] = Z[i * n + j] / h;
+          Z[j * n + i] = zi[j] / h;
           double gg = 0;
-          for (size_t k = 0; k <= j; ++k) gg += Z[j * n + k] * Z[i * n + k];
-          for (size_t k = j + 1; k <= l; ++k) gg += Z[k * n + j] * Z[i * n + k];
-          e[j] = gg / h;
-          f += e[j] * Z[i * n + j];
+          for (size_t k = 0; k <= j; ++k) gg += Z[j * n + k] * zi[k];
+          gacc_t[j] = gg;
+        }
+        for (size_t k = 1; k <= l; ++k) {
+          const double zk = zi[k];
+          const double* rk = &Z[k * n];
+          for (size_t j = 0; j < k; ++j) gacc_t[j] += rk[j] * zk;
+        }
+        for (size_t j = 0; j <= l; ++j) {
+          e[j] = gacc_t[j] / h;
+          f += e[j] * zi[j];
         }
         const double hh = f / (h + h);
         for (size_t j = 0; j <= l; ++j) {
@@ -99,13 +111,23 @@ inline void sym_eigen(size_t n, const std::vector<double>& a, std::vector<double
   }
   d[0] = 0;
   e[0] = 0;
-  // Accumulate the transformations.
+  // Accumulate the transformations.  For row i, g_j = sum_k Z[i][k] Z[k][j] (k = 0..i-1 in order)
+  // reads row i and column j only, and the update of column j touches neither row i nor any other
+  // column, so all g_j are formed first and the columns updated after -- the same operations on
+  // every element in the same order as the column-at-a-time loop, with unit-stride inner loops.
+  std::vector<double> gacc(n);
   for (size_t i = 0; i < n; ++i) {
     if (d[i] != 0) {
-      for (size_t j = 0; j < i; ++j) {
-        double g = 0;
-        for (size_t k = 0; k < i; ++k) g += Z[i * n + k] * Z[k * n + j];
-        for (size_t k = 0; k < i; ++k) Z[k * n + j] -= g * Z[k * n + i];
+      std::fill(gacc.begin(), gacc.begin() + long(i), 0.0);
+      for (size_t k = 0; k < i; ++k) {
+        const double zik = Z[i * n + k];
+        const double* zk = &Z[k * n];
+        for (size_t j = 0; j < i; ++j) gacc[j] += zik * zk[j];
+      }
+      for (size_t k = 0; k < i; ++k) {
+        const double zki = Z[k * n + i];
+        double* zk = &Z[k * n];
+        for (size_t j = 0; j < i; ++j) zk[j] -= gacc[j] * zki;
       }
     }
     d[i] = Z[i * n + i];
@@ -463,21 +485,31 @@ inline void eigenproblem(std::vector<double>& eigenvectors, std::vector<double>&
   }
   std::vector<double> svmh(rank);
   for (size_t k = 0; k < rank; ++k) svmh[k] = sing[k] > 1e-14 ? 1 / std::sqrt(sing[k]) : 0;
-  // Hbar = diag(svmh) U_r^T H V_r diag(svmh)  (rank x rank, column-major)
+  // Hbar = diag(svmh) U_r^T H V_r diag(svmh)  (rank x rank, column-major).  HV[i,j] accumulates
+  // H[i,l] V[l,j] over l = 0..n-1 in order for every i at once (unit stride in i).
   std::vector<double> HV(n * rank, 0.0);
-  for (size_t j = 0; j < rank; ++j)
-    for (size_t i = 0; i < n; ++i) {
-      double s = 0;
-      for (size_t l = 0; l < n; ++l) s += H[i + n * l] * V[l + n * j];
-      HV[i + n * j] = s;
+  for (size_t j = 0; j < rank; ++j) {
+    double* hv = &HV[n * j];
+    for (size_t l = 0; l < n; ++l) {
+      const double vlj = V[l + n * j];
+      const double* hl = &H[n * l];
+      for (size_t i = 0; i < n; ++i) hv[i] += hl[i] * vlj;
     }
-  std::vector<double> Hbar(rank * rank, 0.0);
-  for (size_t j = 0; j < rank; ++j)
-    for (size_t i = 0; i < rank; ++i) {
-      double s = 0;
-      for (size_t l = 0; l < n; ++l) s += U[l + n * i] * HV[l + n * j];
-      Hbar[i + rank * j] = svmh[i] * s * svmh[j];
+  }
+  // Hbar[i,j] = svmh[i] (sum_l U[l,i] HV[l,j], l in order) svmh[j]: U_r transposed once so that the
+  // sums of one column j advance together over l (unit stride in i).
+  std::vector<double> Hbar(rank * rank, 0.0), Ut(n * rank), acc(rank);
+  for (size_t i = 0; i < rank; ++i)
+    for (size_t l = 0; l < n; ++l) Ut[l * rank + i] = U[l + n * i];
+  for (size_t j = 0; j < rank; ++j) {
+    std::fill(acc.begin(), acc.end(), 0.0);
+    for (size_t l = 0; l < n; ++l) {
+      const double hv = HV[l + n * j];
+      const double* ul = &Ut[l * rank];
+      for (size_t i = 0; i < rank; ++i) acc[i] += ul[i] * hv;
     }
+    for (size_t i = 0; i < rank; ++i) Hbar[i + rank * j] = svmh[i] * acc[i] * svmh[j];
+  }
   std::vector<cd> evals_c(rank), y(rank * rank);
   if (hermitian) {
     std::vector<double> ev, vec;
@@ -508,23 +540,38 @@ inline void eigenproblem(std::vector<double>& eigenvectors, std::vector<double>&
       }
     }
   }
-  // Back-transform: X = V_r diag(svmh) Y  (n x rank)
+  // Back-transform: X = V_r diag(svmh) Y  (n x rank), each X[i,k] summed over l = 0..rank-1 in order.
+  // Hermitian: Y is real, and (V svmh) * (y + 0i) accumulated in complex arithmetic has exactly
+  // these real parts (and zero imaginary parts), so the real loop, unit stride in i, is used.
   std::vector<cd> X(n * rank, cd(0));
-  for (size_t k = 0; k < rank; ++k)
-    for (size_t i = 0; i < n; ++i) {
-      cd s = 0;
-      for (size_t l = 0; l < rank; ++l) s += V[i + n * l] * svmh[l] * y[l + rank * k];
-      X[i + n * k] = s;
+  if (hermitian) {
+    std::vector<double> Xr(n);
+    for (size_t k = 0; k < rank; ++k) {
+      std::fill(Xr.begin(), Xr.end(), 0.0);
+      for (size_t l = 0; l < rank; ++l) {
+        const double ylk = y[l + rank * k].real(), sl = svmh[l];
+        const double* vl = &V[n * l];
+        for (size_t i = 0; i < n; ++i) Xr[i] += vl[i] * sl * ylk;
+      }
+      for (size_t i = 0; i < n; ++i) X[i + n * k] = Xr[i];
     }
+  } else {
+    for (size_t k = 0; k < rank; ++k)
+      for (size_t i = 0; i < n; ++i) {
+        cd s = 0;
+        for (size_t l = 0; l < rank; ++l) s += V[i + n * l] * svmh[l] * y[l + rank * k];
+        X[i + n * k] = s;
+      }
+  }
   // Selection sort ascending by real part (first minimum wins), sign fix on the largest component.
-  std::vector<size_t> used;
+  std::vector<char> used(rank, 0);
   std::vector<cd> sv(rank), sX(n * rank);
   for (size_t k = 0; k < rank; ++k) {
     size_t ll = 0;
-    while (std::count(used.begin(), used.end(), ll)) ++ll;
+    while (used[ll]) ++ll;
     for (size_t l = 0; l < rank; ++l)
-      if (!std::count(used.begin(), used.end(), l) && evals_c[l].real() < evals_c[ll].real()) ll = l;
-    used.push_back(ll);
+      if (!used[l] && evals_c[l].real() < evals_c[ll].real()) ll = l;
+    used[ll] = 1;
     sv[k] = evals_c[ll];
     for (size_t i = 0; i < n; ++i) sX[i + n * k] = X[i + n * ll];
     // (the reference scans the first `rank` components for the largest)
