@@ -29,6 +29,27 @@ __global__ void k_scatter(double* __restrict__ x, const unsigned long long* __re
   }
 }
 
+// Few local entries (the P vectors are mostly unit vectors, IterativeSolverTemplate.h:340-368): the
+// entries travel in the kernel argument block, so the op needs no staging copy and no second launch.
+constexpr int kInlineEntries = 64;
+struct ScatterInline {
+  double* x;
+  double alpha;
+  int add;
+  int nnz;
+  unsigned long long li[kInlineEntries];
+  double v[kInlineEntries];
+};
+
+__global__ void k_scatter_inline(const ScatterInline a) {
+  const int e = int(threadIdx.x);
+  if (e >= a.nnz) return;
+  if (a.add)
+    a.x[a.li[e]] += a.alpha * a.v[e];
+  else
+    a.x[a.li[e]] = a.v[e];
+}
+
 // out[i*k + j] = sum over entries e of p_j (in order) of x_i[li_e] * v_e.
 struct SparseInnerArgs {
   const double* x[64];
@@ -41,19 +62,36 @@ struct SparseInnerArgs {
   const double* v;
   double* out;
 };
+// The same with k <= 32 vectors of at most kInlineEntries local entries in all carried inline.
+struct SparseInnerInline {
+  const double* x[64];
+  double xs[64];
+  int sc;
+  int m;
+  int k;
+  unsigned short ptr[33];
+  unsigned long long li[kInlineEntries];
+  double v[kInlineEntries];
+  double* out;
+};
+static_assert(sizeof(SparseInnerInline) <= 4000, "kernel argument block too large");
 
-__global__ void k_sparse_inner(const SparseInnerArgs a) {
+template <class A>
+__device__ __forceinline__ void sparse_inner_body(const A& a, const unsigned long long* li, const double* v) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= a.m * a.k) return;
   const int i = o / a.k, j = o % a.k;
   double s = 0;
   const double xs = a.xs[i];
   for (unsigned long long e = a.ptr[j]; e < a.ptr[j + 1]; ++e) {
-    const double xv = a.sc ? a.x[i][a.li[e]] * xs : a.x[i][a.li[e]];
-    s += xv * a.v[e];
+    const double xv = a.sc ? a.x[i][li[e]] * xs : a.x[i][li[e]];
+    s += xv * v[e];
   }
   a.out[o] = s;
 }
+
+__global__ void k_sparse_inner(const SparseInnerArgs a) { sparse_inner_body(a, a.li, a.v); }
+__global__ void k_sparse_inner_inline(const SparseInnerInline a) { sparse_inner_body(a, a.li, a.v); }
 
 // yy[j][li_e] += alpha(i,j) * v_e for sources i in order, then entries in order; one lane per
 // destination, so colliding indices accumulate in the reference's order.
@@ -153,6 +191,22 @@ int upload_entries(ssp_ctx* ctx, const std::vector<unsigned long long>& ptr, con
   return SSP_OK;
 }
 
+int launch_scatter_inline(ssp_ctx* ctx, double* x, const std::vector<unsigned long long>& li,
+                          const std::vector<double>& lv, double alpha, int add) {
+  ScatterInline a{};
+  a.x = x;
+  a.alpha = alpha;
+  a.add = add;
+  a.nnz = int(li.size());
+  for (size_t e = 0; e < li.size(); ++e) {
+    a.li[e] = li[e];
+    a.v[e] = lv[e];
+  }
+  hipLaunchKernelGGL(k_scatter_inline, dim3(1), dim3(kInlineEntries), 0, ctx->stream, a);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
 int check_entries(const size_t* idx, const double* val, size_t nnz, const char* what) {
   if (nnz && (!idx || !val)) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null entries");
   return SSP_OK;
@@ -171,6 +225,10 @@ int ssp_sparse_copy(ssp_ctx* ctx, double* x, size_t n, size_t offset, const size
   std::vector<double> lv;
   filter_local(idx, val, nnz, n, offset, li, lv);
   if (li.empty()) return SSP_OK;
+  if (li.size() <= size_t(kInlineEntries)) {
+    ssp::LedgerScope ls(ctx, "sparse_copy", 16.0 * li.size());
+    return launch_scatter_inline(ctx, x, li, lv, 1.0, 0);
+  }
   std::vector<unsigned long long> ptr{0, li.size()};
   unsigned long long *dptr, *dli;
   double* dv;
@@ -192,6 +250,10 @@ int ssp_sparse_axpy(ssp_ctx* ctx, double alpha, const size_t* idx, const double*
   filter_local(idx, val, nnz, n, offset, li, lv);
   if (li.empty()) return SSP_OK;
   if (!x) return ssp::set_error(SSP_ERR_ARG, "ssp_sparse_axpy: null vector");
+  if (li.size() <= size_t(kInlineEntries)) {
+    ssp::LedgerScope ls(ctx, "sparse_axpy", 24.0 * li.size());
+    return launch_scatter_inline(ctx, x, li, lv, alpha, 1);
+  }
   std::vector<unsigned long long> ptr{0, li.size()};
   unsigned long long *dptr, *dli;
   double* dv;
@@ -226,6 +288,29 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const do
   }
   const size_t total = size_t(m) * k;
   SSP_TRY(ssp::ensure_result(ctx, total));
+  if (k <= 32 && li.size() <= size_t(kInlineEntries)) {
+    ssp::LedgerScope ls(ctx, "gemm_inner_sparse", 16.0 * li.size() * m);
+    for (int i0 = 0; i0 < m; i0 += 64) {
+      SparseInnerInline a{};
+      a.m = std::min(64, m - i0);
+      a.k = k;
+      for (int i = 0; i < a.m; ++i) {
+        a.x[i] = xx[i0 + i];
+        a.xs[i] = xs ? xs[i0 + i] : 1.0;
+        if (a.xs[i] != 1.0) a.sc = 1;
+      }
+      for (int j = 0; j <= k; ++j) a.ptr[j] = (unsigned short)lptr[size_t(j)];
+      for (size_t e = 0; e < li.size(); ++e) {
+        a.li[e] = li[e];
+        a.v[e] = lv[e];
+      }
+      a.out = ctx->result_dev + size_t(i0) * k;
+      const int outs = a.m * a.k;
+      hipLaunchKernelGGL(k_sparse_inner_inline, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a);
+      SSP_TRY_HIP(hipGetLastError());
+    }
+    return ssp::reduce_fetch(ctx, out, total);
+  }
   unsigned long long *dptr, *dli;
   double* dv;
   SSP_TRY(upload_entries(ctx, lptr, li, lv, &dptr, &dli, &dv));
