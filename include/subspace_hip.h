@@ -93,6 +93,13 @@ int ssp_ctx_attach_p2p(ssp_ctx* ctx, int nranks, int rank, const char* id);
  * later exchange on the context, returns SSP_ERR_COMM naming the operation -- the status-code form of
  * the reference's abort of the whole job on a distributed error (DistrArray.cpp:16-23). */
 int ssp_ctx_set_comm_timeout(ssp_ctx* ctx, double seconds);
+/* Vectors of at most n local elements (default 16384, or SSP_EXACT_MAX at context creation; 0 turns
+ * it off) are computed in the reference's own arithmetic: every dot a sequential sum in index order
+ * (std::inner_product, ArrayHandlerIterable.h:76-82) and every y = alpha x + y rounded twice (no fused
+ * multiply-add, ArrayHandlerIterable.h:65-74), gemm_inner / gemm_outer pairwise in the reference's loop
+ * order (util/gemm.h:257-279), fused entry points as their documented unfused sequence.  Results on
+ * such vectors are the reference CPU path's bit for bit; longer vectors use the bandwidth kernels. */
+int ssp_ctx_set_exact_max(ssp_ctx* ctx, size_t n);
 /* Shard of a global length n owned by `rank` of `nranks` (host only, no context):
  * make_distribution_spread_remainder, reference util/Distribution.h:99-109. */
 int ssp_shard_range(size_t n, int nranks, int rank, size_t* offset, size_t* length);
@@ -221,6 +228,10 @@ int ssp_sparse_copy(ssp_ctx* ctx, double* x, size_t n, size_t offset, const size
 /* x[idx-offset] += alpha * val */
 int ssp_sparse_axpy(ssp_ctx* ctx, double alpha, const size_t* idx, const double* val, size_t nnz, double* x,
                     size_t n, size_t offset);
+/* xx[k][idx-offset] += val over the entries [ptr[k], ptr[k+1]) of each of nvec sparse vectors (one
+ * ssp_sparse_axpy(1.0) per vector, in one launch when the entries fit the argument block). */
+int ssp_sparse_axpy_batch(ssp_ctx* ctx, int nvec, const size_t* ptr, const size_t* idx, const double* val,
+                          double* const* xx, size_t n, size_t offset);
 /* *out = sum_ranks sum_e x[idx_e-offset] * val_e */
 int ssp_sparse_dot(ssp_ctx* ctx, const double* x, size_t n, size_t offset, const size_t* idx, const double* val,
                    size_t nnz, double* out);

@@ -1,0 +1,154 @@
+// The reference's own arithmetic for short vectors (ssp_ctx_set_exact_max / SSP_EXACT_MAX, default
+// 16384 local elements): every reduction a sequential sum in index order and every multiply-add
+// rounded twice, exactly the reference's ArrayHandlerIterable loops (std::inner_product,
+// ArrayHandlerIterable.h:76-82; y = alpha * x + y, :65-74) and its pairwise gemm_inner_default /
+// gemm_outer_default (util/gemm.h:257-279).  A solve on such vectors is then the reference CPU path bit
+// for bit (on one rank; on several, the reference's distributed build: rank-local sums added in rank
+// order by the peer-memory and host transports).  The short vectors are the reference's own test
+// problems (its matrices have 4 to 784 rows): there every kernel is latency-bound, so the fixed order
+// costs nothing measurable, while the parallel kernels' other -- equally valid -- summation order and
+// fused multiply-adds let last-bit differences decide knife-edge steps of those tests.
+#include <algorithm>
+#include <vector>
+
+#include "ssp_internal.h"
+
+// Products rounded before they are added, as in the reference's x86-64 build.
+#pragma clang fp contract(off)
+
+namespace {
+
+using ssp::kBlock;
+
+struct ExactInnerArgs {
+  const double* const* x;  // m vectors (device array of pointers)
+  const double* const* y;  // k vectors
+  const double* xs;        // m deferred scales
+  const double* ys;        // k deferred scales
+  int m, k;
+  int pairs;               // 1: out[j] = <x_j, y_j> (m == k); 0: out[i * k + j] = <x_i, y_j>
+  size_t n;
+  double* out;             // device
+};
+
+// One workgroup per output: the sequential std::inner_product of the (stored-equivalent) operands.
+// The workgroup forms a chunk of products in LDS (each product rounded alone, whichever lane forms
+// it), then lane 0 adds them in index order; the next chunk follows.
+constexpr int kExactChunk = 4 * kBlock;
+__global__ __launch_bounds__(kBlock) void k_exact_inner(const ExactInnerArgs a) {
+  __shared__ double prod[kExactChunk];
+  const int o = int(blockIdx.x);
+  const int i = a.pairs ? o : o / a.k, j = a.pairs ? o : o % a.k;
+  const double* x = a.x[i];
+  const double* y = a.y[j];
+  const double xs = a.xs[i], ys = a.ys[j];
+  double s = 0;
+  for (size_t c0 = 0; c0 < a.n; c0 += kExactChunk) {
+    const int len = int(a.n - c0 < size_t(kExactChunk) ? a.n - c0 : size_t(kExactChunk));
+    for (int t = int(threadIdx.x); t < len; t += kBlock) prod[t] = (x[c0 + t] * xs) * (y[c0 + t] * ys);
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int t = 0; t < len; ++t) s = s + prod[t];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.out[o] = s;
+}
+
+struct ExactOuterArgs {
+  const double* const* x;  // k sources
+  double* const* y;        // m destinations
+  const double* xs;        // k source scales
+  const double* ys;        // m destination scales (applied to the values read)
+  const double* alpha;     // alpha[i * m + j]
+  int m, k, set;
+  size_t n;
+};
+
+// One thread per (element, destination): y_j[e] = y_j[e] + alpha(i, j) x_i[e] for i = 0..k-1 in order,
+// each product rounded -- the pairwise axpy loop of gemm_outer_default, element by element.
+__global__ __launch_bounds__(kBlock) void k_exact_outer(const ExactOuterArgs a) {
+  const size_t total = a.n * size_t(a.m);
+  for (size_t t = size_t(blockIdx.x) * kBlock + threadIdx.x; t < total; t += size_t(gridDim.x) * kBlock) {
+    const int j = int(t / a.n);
+    const size_t e = t % a.n;
+    double v = a.set ? 0.0 : a.y[j][e] * a.ys[j];
+    for (int i = 0; i < a.k; ++i) v = v + a.alpha[size_t(i) * a.m + j] * (a.x[i][e] * a.xs[i]);
+    a.y[j][e] = v;
+  }
+}
+
+template <class T>
+int stage(ssp_ctx* ctx, const T* host, size_t count, const T** dev) {
+  void* p;
+  SSP_TRY(ssp::upload_small(ctx, host, count * sizeof(T), &p));
+  *dev = static_cast<const T*>(p);
+  return SSP_OK;
+}
+
+}  // namespace
+
+namespace ssp {
+
+bool exact_mode(const ssp_ctx* ctx, size_t n) { return n > 0 && n <= ctx->exact_max; }
+
+int exact_inner(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, const double* const* yy,
+                const double* ys, int k, size_t n, bool pairs) {
+  const int nout = pairs ? m : m * k;
+  SSP_TRY(ensure_result(ctx, size_t(nout)));
+  if (nout == 0) return SSP_OK;
+  std::vector<double> one(size_t(std::max(m, k)), 1.0);
+  ExactInnerArgs a{};
+  SSP_TRY(stage(ctx, xx, size_t(m), &a.x));
+  SSP_TRY(stage(ctx, yy, size_t(k), &a.y));
+  SSP_TRY(stage(ctx, xs ? xs : one.data(), size_t(m), &a.xs));
+  SSP_TRY(stage(ctx, ys ? ys : one.data(), size_t(k), &a.ys));
+  a.m = m;
+  a.k = k;
+  a.pairs = pairs ? 1 : 0;
+  a.n = n;
+  a.out = ctx->result_dev;
+  SSP_TRY(flush_uploads(ctx));
+  hipLaunchKernelGGL(k_exact_inner, dim3(unsigned(nout)), dim3(kBlock), 0, ctx->stream, a);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+int exact_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, const double* xs, int k,
+                double* const* yy, const double* ys, int m, size_t n, bool set) {
+  if (m == 0 || n == 0) return SSP_OK;
+  std::vector<double> one(size_t(std::max(m, k)), 1.0);
+  std::vector<double> al(size_t(std::max(1, k * m)), 0.0);
+  if (k > 0) std::copy(alphas, alphas + size_t(k) * m, al.begin());
+  ExactOuterArgs a{};
+  std::vector<const double*> xp(size_t(std::max(k, 1)), nullptr);
+  for (int i = 0; i < k; ++i) xp[size_t(i)] = xx[i];
+  SSP_TRY(stage(ctx, xp.data(), xp.size(), &a.x));
+  void* py;
+  SSP_TRY(upload_small(ctx, yy, size_t(m) * sizeof(double*), &py));
+  a.y = static_cast<double* const*>(py);
+  SSP_TRY(stage(ctx, xs && k > 0 ? xs : one.data(), size_t(std::max(k, 1)), &a.xs));
+  SSP_TRY(stage(ctx, ys && !set ? ys : one.data(), size_t(m), &a.ys));
+  SSP_TRY(stage(ctx, al.data(), al.size(), &a.alpha));
+  a.m = m;
+  a.k = k;
+  a.set = set ? 1 : 0;
+  a.n = n;
+  SSP_TRY(flush_uploads(ctx));
+  const size_t total = n * size_t(m);
+  const unsigned grid = unsigned(std::min<size_t>((total + kBlock - 1) / kBlock, size_t(ctx->num_cus) * 4));
+  hipLaunchKernelGGL(k_exact_outer, dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+}  // namespace ssp
+
+extern "C" {
+
+int ssp_ctx_set_exact_max(ssp_ctx* ctx, size_t n) {
+  SSP_CHECK_CTX(ctx);
+  ctx->exact_max = n;
+  return SSP_OK;
+}
+
+}  // extern "C"

@@ -953,6 +953,18 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
   for (int j = 0; j < k; ++j) (swap ? rs : cs)[size_t(j)] = ys ? ys[j] : 1.0;
   const bool sc = any_scaled(rs.data(), R) || any_scaled(cs.data(), C);
   const size_t total = size_t(R) * C;
+  if (ssp::exact_mode(ctx, n)) {  // the reference's sequential dots, m x k in the caller's layout
+    SSP_TRY(ssp::comm_check(ctx));
+    {
+      std::vector<const double*> distinct(xx, xx + m);
+      distinct.insert(distinct.end(), yy, yy + k);
+      std::sort(distinct.begin(), distinct.end());
+      const double nvec = double(std::unique(distinct.begin(), distinct.end()) - distinct.begin());
+      ssp::LedgerScope ls(ctx, "gemm_inner", 8.0 * n * nvec);
+      SSP_TRY(ssp::exact_inner(ctx, xx, xs, m, yy, ys, k, n, false));
+    }
+    return ssp::reduce_fetch(ctx, out, total);
+  }
   SSP_TRY(ssp::ensure_result(ctx, total));
   ssp::FoldTail tail{};
   if (n == 0) {
@@ -1077,6 +1089,7 @@ int gemm_outer_impl(ssp_ctx* ctx, const double* alphas, const double* const* xx,
   // Destinations are independent; sources are applied in increasing order, in groups that fit
   // the kernel argument block, so each destination sees the reference's summation order.
   ssp::LedgerScope ls(ctx, set ? "gemm_outer_set" : "gemm_outer", 8.0 * n * (k + (set ? 1.0 : 2.0) * m));
+  if (ssp::exact_mode(ctx, n)) return ssp::exact_outer(ctx, alphas, xx, xs, k, yy, ys, m, n, set);
   for (int j0 = 0; j0 < m; j0 += ssp::kOuterDst) {
     const int mm = std::min(ssp::kOuterDst, m - j0);
     // Up to kOuterSrc sources per launch; their alphas ride in the argument block when they fit,
@@ -1147,7 +1160,8 @@ int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* y
   SSP_TRY(check_ptrs(yy, m, n, "ssp_scal_inner"));
   for (int j = 0; j < m; ++j)
     if (yy[j] == x) return ssp::set_error(SSP_ERR_ARG, "ssp_scal_inner: a vector of yy aliases x");
-  if (m == 0 || m > ssp::kOuterDst) {  // no dots, or more than one launch: the unfused pair
+  // no dots, more than one launch, or the reference's arithmetic (short vectors): the unfused pair
+  if (m == 0 || m > ssp::kOuterDst || ssp::exact_mode(ctx, n)) {
     SSP_TRY(ssp_scal(ctx, alpha, x, n));
     return m == 0 ? SSP_OK : ssp_gemm_inner(ctx, const_cast<const double* const*>(&x), 1, yy, m, n, out);
   }
@@ -1190,7 +1204,7 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
   SSP_TRY(check_ptrs(const_cast<const double* const*>(yy), m, n, "ssp_axpy_norm"));
   for (int j = 0; j < m; ++j)
     if (yy[j] == x) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_norm: a destination aliases x");
-  if (m > ssp::kOuterDst) {  // more than one launch: the unfused pair
+  if (m > ssp::kOuterDst || ssp::exact_mode(ctx, n)) {  // more than one launch / short vectors: the unfused pair
     std::vector<double> alpha(c, c + m);
     SSP_TRY(ssp_gemm_outer(ctx, alpha.data(), &x, 1, yy, m, n));
     return ssp_dot(ctx, yy[0], yy[0], n, out);
@@ -1240,7 +1254,7 @@ int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store
     for (int i = 0; i < j; ++i)
       if (yy[i] == yy[j]) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_gram: repeated destination");
   }
-  if (m > ssp::kOuterDst) {  // more than one launch: the unfused sequence, same values
+  if (m > ssp::kOuterDst || ssp::exact_mode(ctx, n)) {  // more than one launch / short vectors: unfused
     const double* xp = x;
     SSP_TRY(ssp_gemm_outer_scaled(ctx, c, &xp, &xs, 1, yy, nullptr, m, n));
     if (store_x && xs != 1.0) SSP_TRY(ssp_scal(ctx, xs, x, n));
@@ -1295,6 +1309,17 @@ int ssp_axpy_pairs_norm(ssp_ctx* ctx, const double* c, const double* const* xx, 
     for (int i = 0; i < m; ++i)
       if (yy[j] == xx[i] || (i < j && yy[i] == yy[j]))
         return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_pairs_norm: a destination aliases another operand");
+  if (ssp::exact_mode(ctx, n)) {  // short vectors: the reference's arithmetic, one reduction
+    SSP_TRY(ssp::comm_check(ctx));
+    {
+      ssp::LedgerScope ls(ctx, "axpy_pairs_norm", 24.0 * n * m);
+      for (int j = 0; j < m; ++j)
+        SSP_TRY(ssp::exact_outer(ctx, c + j, xx + j, xs ? xs + j : nullptr, 1, yy + j, ys ? ys + j : nullptr, 1, n, false));
+      SSP_TRY(ssp::exact_inner(ctx, const_cast<const double* const*>(yy), nullptr, m,
+                               const_cast<const double* const*>(yy), nullptr, m, n, true));
+    }
+    return ssp::reduce_fetch(ctx, out, size_t(m));
+  }
   if (m > ssp::kOuterDst) {  // more than one launch: the unfused sequence, same values
     for (int j = 0; j < m; ++j)
       SSP_TRY(ssp_axpy_scaled(ctx, c[j], xx[j], xs ? xs[j] : 1.0, yy[j], ys ? ys[j] : 1.0, n));
@@ -1347,6 +1372,15 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
   SSP_TRY(check_ptrs(const_cast<const double* const*>(yy), m, n, "ssp_axpy_inner"));
   for (int j = 0; j < m; ++j)
     if (yy[j] == x || yy[j] == z) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_inner: a destination aliases x or z");
+  if (ssp::exact_mode(ctx, n)) {  // short vectors: the reference's arithmetic, one reduction
+    SSP_TRY(ssp::comm_check(ctx));
+    {
+      ssp::LedgerScope ls(ctx, "axpy_inner", 8.0 * n * (2.0 + 2.0 * m));
+      SSP_TRY(ssp::exact_outer(ctx, c, &x, nullptr, 1, yy, nullptr, m, n, false));
+      SSP_TRY(ssp::exact_inner(ctx, const_cast<const double* const*>(yy), nullptr, m, &z, nullptr, 1, n, false));
+    }
+    return ssp::reduce_fetch(ctx, out, size_t(m));
+  }
   SSP_TRY(ssp::ensure_result(ctx, size_t(m)));
   ssp::FoldTail tail{};
   if (n == 0) {

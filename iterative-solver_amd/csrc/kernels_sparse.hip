@@ -50,6 +50,21 @@ __global__ void k_scatter_inline(const ScatterInline a) {
     a.x[a.li[e]] = a.v[e];
 }
 
+// The same for up to 16 destinations at once (ssp_sparse_axpy_batch): entry e goes to x[dst[e]].
+struct ScatterBatchInline {
+  double* x[16];
+  int nnz;
+  unsigned char dst[kInlineEntries];
+  unsigned long long li[kInlineEntries];
+  double v[kInlineEntries];
+};
+
+__global__ void k_scatter_batch_inline(const ScatterBatchInline a) {
+  const int e = int(threadIdx.x);
+  if (e >= a.nnz) return;
+  a.x[a.dst[e]][a.li[e]] += a.v[e];
+}
+
 // out[i*k + j] = sum over entries e of p_j (in order) of x_i[li_e] * v_e.
 struct SparseInnerArgs {
   const double* x[64];
@@ -127,6 +142,7 @@ struct ConstructFixArgs {
   const double* ys;                // rmw: m destination scales
   const double* xs;                // k source scales or null
   int rmw;
+  int exact;                       // the reference's arithmetic (kernels_exact.hip): no fma below
   const unsigned long long* uidx;  // distinct local indices touched by P
   size_t nu;
   int m;
@@ -154,9 +170,21 @@ __global__ void k_construct_fixup(const ConstructFixArgs a) {
     for (unsigned long long e = a.ptr[i]; e < a.ptr[i + 1]; ++e)
       if (a.li[e] == g) v += al * a.v[e];
   }
-  for (int s = 0; s < a.k; ++s) {
-    const double xv = a.xs ? a.x[s][g] * a.xs[s] : a.x[s][g];
-    v = fma(a.alpha[size_t(s) * a.m + j], xv, v);
+  // the dense sources in groups of 8: the group's loads are issued together, then the chain of adds
+  constexpr int G = 8;
+  for (int s0 = 0; s0 < a.k; s0 += G) {
+    double xv[G], al[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int s = s0 + u;
+      if (s < a.k) {
+        xv[u] = a.xs ? a.x[s][g] * a.xs[s] : a.x[s][g];
+        al[u] = a.alpha[size_t(s) * a.m + j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+      if (s0 + u < a.k) v = a.exact ? v + al[u] * xv[u] : fma(al[u], xv[u], v);
   }
   a.y[j][g] = v;
 }
@@ -263,6 +291,42 @@ int ssp_sparse_axpy(ssp_ctx* ctx, double alpha, const size_t* idx, const double*
   const unsigned grid = unsigned(std::min<size_t>((li.size() + kBlock - 1) / kBlock, 1024));
   SSP_TRY(ssp::flush_uploads(ctx));
   hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), alpha, 1);
+  SSP_TRY_HIP(hipGetLastError());
+  return SSP_OK;
+}
+
+int ssp_sparse_axpy_batch(ssp_ctx* ctx, int nvec, const size_t* ptr, const size_t* idx, const double* val,
+                          double* const* xx, size_t n, size_t offset) {
+  SSP_CHECK_CTX(ctx);
+  if (nvec < 0 || (nvec > 0 && (!ptr || !xx))) return ssp::set_error(SSP_ERR_ARG, "ssp_sparse_axpy_batch: bad arguments");
+  ScatterBatchInline a{};
+  bool inl = nvec <= 16;
+  for (int k = 0; k < nvec && inl; ++k) {
+    SSP_TRY(check_entries(idx + ptr[k], val + ptr[k], ptr[k + 1] - ptr[k], "ssp_sparse_axpy_batch"));
+    std::vector<unsigned long long> li;
+    std::vector<double> lv;
+    filter_local(idx + ptr[k], val + ptr[k], ptr[k + 1] - ptr[k], n, offset, li, lv);
+    if (li.empty()) continue;
+    if (!xx[k]) return ssp::set_error(SSP_ERR_ARG, "ssp_sparse_axpy_batch: null vector");
+    if (a.nnz + li.size() > size_t(kInlineEntries)) {
+      inl = false;
+      break;
+    }
+    a.x[k] = xx[k];
+    for (size_t e = 0; e < li.size(); ++e) {
+      a.dst[a.nnz] = static_cast<unsigned char>(k);
+      a.li[a.nnz] = li[e];
+      a.v[a.nnz++] = lv[e];
+    }
+  }
+  if (!inl) {  // more entries than one argument block carries: one launch per vector
+    for (int k = 0; k < nvec; ++k)
+      SSP_TRY(ssp_sparse_axpy(ctx, 1.0, idx + ptr[k], val + ptr[k], ptr[k + 1] - ptr[k], xx[k], n, offset));
+    return SSP_OK;
+  }
+  if (a.nnz == 0) return SSP_OK;
+  ssp::LedgerScope ls(ctx, "sparse_axpy", 24.0 * a.nnz);
+  hipLaunchKernelGGL(k_scatter_batch_inline, dim3(1), dim3(kInlineEntries), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -459,6 +523,7 @@ int solution_impl(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const 
     a.rmw = 1;
   }
   a.nu = uidx.size();
+  a.exact = ssp::exact_mode(ctx, n) ? 1 : 0;
   a.m = m;
   a.kp = kp;
   a.k = k;

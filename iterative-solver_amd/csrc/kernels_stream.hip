@@ -367,6 +367,7 @@ int axpy_impl(ssp_ctx* ctx, double alpha, const double* x, double xs, double* y,
   if (n == 0) return SSP_OK;
   const bool sc = xs != 1.0 || ys != 1.0;
   ssp::LedgerScope ls(ctx, "axpy", 24.0 * n);
+  if (ssp::exact_mode(ctx, n)) return ssp::exact_outer(ctx, &alpha, &x, &xs, 1, &y, &ys, 1, n, false);
   if (n >= kWinMin) {
     const dim3 g(ssp::win_grid(ctx, n, kWinU, 16));
     if (sc) hipLaunchKernelGGL(k_axpy_win<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
@@ -389,6 +390,14 @@ int dot_impl(ssp_ctx* ctx, const double* x, double xs, const double* y, double y
   if (n == 0) {
     SSP_TRY(ssp::ensure_result(ctx, 1));
     SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, sizeof(double), ctx->stream));
+    return ssp::reduce_fetch(ctx, out, 1);
+  }
+  if (ssp::exact_mode(ctx, n)) {
+    SSP_TRY(ssp::comm_check(ctx));
+    {
+      ssp::LedgerScope ls(ctx, "dot", (x == y && xs == ys ? 8.0 : 16.0) * n);
+      SSP_TRY(ssp::exact_inner(ctx, &x, &xs, 1, &y, &ys, 1, n, false));
+    }
     return ssp::reduce_fetch(ctx, out, 1);
   }
   const unsigned grid = ssp::win_grid(ctx, n, kDotU, 8);

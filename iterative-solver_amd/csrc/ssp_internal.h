@@ -98,6 +98,9 @@ struct ssp_ctx {
   // exchange on this context returns SSP_ERR_COMM with comm_fail_msg (the reference aborts the whole
   // job, DistrArray.cpp:16-23).
   double comm_timeout_s = 300.0;
+  // Vectors of at most this many local elements take the reference's own arithmetic
+  // (kernels_exact.hip: sequential sums, no fused multiply-adds); SSP_EXACT_MAX / ssp_ctx_set_exact_max.
+  size_t exact_max = 16384;
   bool comm_failed = false;
   std::string comm_fail_msg;
   // Coherent host word a device-side exchange sets when it gave up (peer missing / mismatched).
@@ -340,6 +343,14 @@ int p2p_allreduce_dev(ssp_ctx* ctx, double* buf, size_t n);
 int p2p_allreduce_fetch(ssp_ctx* ctx, const double* src, double* out, size_t n);
 int p2p_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes);
 int p2p_detach(ssp_ctx* ctx);
+
+// kernels_exact.hip: the reference's arithmetic for short vectors.  exact_inner writes the m x k (or,
+// pairs, the m) dots into result_dev; exact_outer updates (set: writes) the destinations.
+bool exact_mode(const ssp_ctx* ctx, size_t n);
+int exact_inner(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, const double* const* yy,
+                const double* ys, int k, size_t n, bool pairs);
+int exact_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, const double* xs, int k,
+                double* const* yy, const double* ys, int m, size_t n, bool set);
 
 // kernels_stream.hip
 int launch_reduce_partials(ssp_ctx* ctx, const double* partial, int nblocks, int rows, int cols, double* out,

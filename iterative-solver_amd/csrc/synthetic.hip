@@ -73,6 +73,7 @@ struct SynthArgs {
   double rho;
   double* partial;      // [grid][nvec*rank]
   const double* coeff;  // [nvec*rank] global u_l . x_v
+  int exact;            // the reference's arithmetic (ssp_ctx_set_exact_max): products rounded alone
 };
 
 template <int R>
@@ -145,6 +146,40 @@ __global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a) {
   }
 }
 
+// Short vectors (ssp_ctx_set_exact_max): the coefficients as sequential sums in index order, as the
+// host restatement's loop (one workgroup per vector: a chunk of scaled values and masks in LDS, then
+// lane l adds the chunk for coefficient l in order).  out[v * R + l], v < nvec.
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_synth_coeff_exact(const SynthArgs a, double* out) {
+  constexpr int kChunk = 4 * kBlock;
+  __shared__ double xv[kChunk];
+  __shared__ unsigned short mk[kChunk];
+  const int v = int(blockIdx.x);
+  double s = 0;
+  for (size_t c0 = 0; c0 < a.n; c0 += kChunk) {
+    const int len = int(a.n - c0 < size_t(kChunk) ? a.n - c0 : size_t(kChunk));
+    for (int t = int(threadIdx.x); t < len; t += kBlock) {
+      xv[t] = a.x[v][c0 + t] * a.xs[v];
+      mk[t] = a.mask[c0 + t];
+    }
+    __syncthreads();
+    if (int(threadIdx.x) < R)
+      for (int t = 0; t < len; ++t) s = s + flip(mk[t], int(threadIdx.x), xv[t]);
+    __syncthreads();
+  }
+  if (int(threadIdx.x) < R) out[v * R + int(threadIdx.x)] = s;
+}
+
+// d x + rho s and y + rho s with every product rounded alone (the reference's arithmetic).
+__device__ __forceinline__ double mul_add_mul(double a, double b, double c, double d) {
+#pragma clang fp contract(off)
+  return a * b + c * d;
+}
+__device__ __forceinline__ double add_mul(double y, double c, double d) {
+#pragma clang fp contract(off)
+  return y + c * d;
+}
+
 template <int R>
 __device__ __forceinline__ double lowrank(unsigned mm, const double* c) {
   double s = 0;
@@ -168,10 +203,12 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
       double2 out;
       if (ADD) {
         const double2 y = *reinterpret_cast<const double2*>(a.y[v] + 2 * i);
-        out = make_double2(fma(a.rho, s0, y.x), fma(a.rho, s1, y.y));
+        out = a.exact ? make_double2(add_mul(y.x, a.rho, s0), add_mul(y.y, a.rho, s1))
+                      : make_double2(fma(a.rho, s0, y.x), fma(a.rho, s1, y.y));
       } else {
         const double2 x = ld2nt(a.x[v] + 2 * i);
-        out = make_double2(fma(d0, x.x * a.xs[v], a.rho * s0), fma(d1, x.y * a.xs[v], a.rho * s1));
+        out = a.exact ? make_double2(mul_add_mul(d0, x.x * a.xs[v], a.rho, s0), mul_add_mul(d1, x.y * a.xs[v], a.rho, s1))
+                      : make_double2(fma(d0, x.x * a.xs[v], a.rho * s0), fma(d1, x.y * a.xs[v], a.rho * s1));
       }
       ssp::st2nt(a.y[v] + 2 * i, out);
     }
@@ -182,7 +219,10 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
     const double d = synth_d(a.diag_kind, a.offset + e);
     for (int v = 0; v < a.nvec; ++v) {
       const double s = lowrank<R>(mm, a.coeff + v * R);
-      a.y[v][e] = ADD ? fma(a.rho, s, a.y[v][e]) : fma(d, a.x[v][e] * a.xs[v], a.rho * s);
+      if (a.exact)
+        a.y[v][e] = ADD ? add_mul(a.y[v][e], a.rho, s) : mul_add_mul(d, a.x[v][e] * a.xs[v], a.rho, s);
+      else
+        a.y[v][e] = ADD ? fma(a.rho, s, a.y[v][e]) : fma(d, a.x[v][e] * a.xs[v], a.rho * s);
     }
   }
 }
@@ -203,6 +243,17 @@ void synth_coeff(unsigned grid, hipStream_t st, const SynthArgs& a) {
 #define F(r) \
   case r:    \
     launch_coeff<r>(grid, st, a); \
+    break;
+    SSP_RANK_CASES(F)
+#undef F
+  }
+}
+
+void synth_coeff_exact(hipStream_t st, const SynthArgs& a, double* out) {
+  switch (a.rank) {
+#define F(r)                                                                                          \
+  case r:                                                                                             \
+    hipLaunchKernelGGL((k_synth_coeff_exact<r>), dim3(unsigned(a.nvec)), dim3(kBlock), 0, st, a, out); \
     break;
     SSP_RANK_CASES(F)
 #undef F
@@ -294,7 +345,10 @@ struct DenseArgs {
   size_t offset;
 };
 
+// The fixture problems' H x: row sums in column order with every product rounded alone (the
+// reference's test drivers' loop on x86-64), so that the parity fixtures see the same actions.
 __global__ void k_dense_action(const DenseArgs p) {
+#pragma clang fp contract(off)
   const size_t r = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (r >= p.n) return;
   const double* row = p.a + (p.offset + r) * p.ng;
@@ -350,7 +404,11 @@ int sspx_synth_action_scaled(ssp_ctx* ctx, const sspx_synth* spec, const double*
     SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * nc));
     SSP_TRY(ssp::ensure_result(ctx, nc));
     a.partial = ctx->partial;
-    if (n > 0) {
+    a.exact = ssp::exact_mode(ctx, n) ? 1 : 0;
+    if (a.exact) {
+      synth_coeff_exact(ctx->stream, a, ctx->result_dev);
+      SSP_TRY_HIP(hipGetLastError());
+    } else if (n > 0) {
       synth_coeff(grid, ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
       SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, nc, ctx->result_dev, nc, 0, 0));
@@ -393,6 +451,7 @@ int sspx_synth_add_lowrank(ssp_ctx* ctx, const sspx_synth* spec, double* const* 
     void* coeff;
     SSP_TRY(ssp::upload_small(ctx, w + size_t(v0) * rank, size_t(a.nvec) * rank * sizeof(double), &coeff));
     a.coeff = static_cast<const double*>(coeff);
+    a.exact = ssp::exact_mode(ctx, n) ? 1 : 0;
     SSP_TRY(ssp::flush_uploads(ctx));
     synth_apply<true>(ssp::stream_grid(ctx, n, 1), ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());

@@ -91,7 +91,7 @@ class SyntheticProblem : public Problem<Vec, SparseP> {
       for (size_t j : idx) m.push_back(m_s.h(i, j));
     return m;
   }
-  // actions[k] += sum_p c[k][p] H e_{i_p}: diagonal part as a sparse axpy per action, then the
+  // actions[k] += sum_p c[k][p] H e_{i_p}: diagonal part as one batched sparse axpy, then the
   // low-rank part of every action in one device pass (the sign table read once for all of them;
   // per element the same two updates in the same order as action by action).
   void p_action(const std::vector<std::vector<double>>& c, const CVecRef<SparseP>& pp,
@@ -100,10 +100,10 @@ class SyntheticProblem : public Problem<Vec, SparseP> {
     const size_t rank = size_t(m_s.rank);
     std::vector<double> w(c.size() * rank, 0.0);
     std::vector<double*> yp;
+    std::vector<size_t> ptr{0}, idx;
+    std::vector<double> val;
     for (size_t k = 0; k < c.size(); ++k) {
       auto& a = actions[k].get();
-      std::vector<size_t> idx;
-      std::vector<double> val;
       for (size_t p = 0; p < pp.size(); ++p) {
         for (auto& [i, coef] : pp[p].get()) {
           idx.push_back(i);
@@ -111,11 +111,13 @@ class SyntheticProblem : public Problem<Vec, SparseP> {
           for (size_t l = 0; l < rank; ++l) w[k * rank + l] += c[k][p] * coef * m_s.u(int(l), i);
         }
       }
-      check(ssp_sparse_axpy(ctx(), 1.0, idx.data(), val.data(), idx.size(), a.data_rw(), a.local_size(), a.offset()),
-            "ssp_sparse_axpy");
+      ptr.push_back(idx.size());
       yp.push_back(a.data_rw());
     }
     const auto& a0 = actions.front().get();
+    check(ssp_sparse_axpy_batch(ctx(), int(yp.size()), ptr.data(), idx.data(), val.data(), yp.data(), a0.local_size(),
+                                a0.offset()),
+          "ssp_sparse_axpy_batch");
     check(sspx_synth_add_lowrank(ctx(), &m_c, yp.data(), int(yp.size()), a0.local_size(), a0.offset(), w.data()),
           "sspx_synth_add_lowrank");
   }
@@ -171,15 +173,18 @@ class DenseProblem : public Problem<Vec, SparseP> {
   }
   void p_action(const std::vector<std::vector<double>>& c, const CVecRef<SparseP>& pp,
                 const VecRef<Vec>& actions) const override {
+    // one column term at a time, added into the action as the reference's test drivers do
+    // (a_j += H_ji coef c), so that the parity fixtures see the same sums
+    Vec t(m_dev, m_n);
+    std::vector<double> col(m_n);
     for (size_t k = 0; k < c.size(); ++k) {
-      std::vector<double> add(m_n, 0.0);
-      for (size_t p = 0; p < pp.size(); ++p)
-        for (auto& [i, coef] : pp[p].get())
-          for (size_t j = 0; j < m_n; ++j) add[j] += m_h[j * m_n + i] * coef * c[k][p];
-      Vec t(m_dev, m_n);
-      t.set_local_values(add);
       auto& a = actions[k].get();
-      check(ssp_axpy(ctx(), 1.0, t.data(), a.data_rw(), m_n), "ssp_axpy");
+      for (size_t p = 0; p < pp.size(); ++p)
+        for (auto& [i, coef] : pp[p].get()) {
+          for (size_t j = 0; j < m_n; ++j) col[j] = m_h[j * m_n + i] * coef * c[k][p];
+          t.set_local_values(col);
+          check(ssp_axpy(ctx(), 1.0, t.data(), a.data_rw(), m_n), "ssp_axpy");
+        }
     }
   }
 

@@ -332,9 +332,12 @@ template <class T>
 struct batched_symmetric_overlap : std::false_type {};
 
 //  * block_gram_schmidt_default: whether Davidson solvers over this R type orthogonalise new R
-//    vectors by block Gram-Schmidt (rspace.h block_gram_schmidt) unless the option says otherwise.
+//    vectors by block Gram-Schmidt (rspace.h block_gram_schmidt) unless the option says otherwise;
+//    for_length(n): the same for vectors of global length n.
 template <class T>
-struct block_gram_schmidt_default : std::false_type {};
+struct block_gram_schmidt_default : std::false_type {
+  static bool for_length(size_t) { return false; }
+};
 
 // Fused MGS step hook: y_j += c_j x for all j, then dots_j = <y_j, z>, in one pass; returns false
 // when the handler has no fused form (the caller then issues gemm_outer + gemm_inner).  Found by

@@ -303,12 +303,16 @@ namespace molpro::linalg::array {
 // HBM handlers form symmetric overlaps with one gemm_inner (reads each vector once).
 template <>
 struct batched_symmetric_overlap<hbm::Vec> : std::true_type {};
-// Davidson over HBM vectors orthogonalises new R vectors by block Gram-Schmidt (rspace.h) unless the
-// option BLOCK_GRAM_SCHMIDT=false selects the reference's sequential MGS: it passes the same parity
-// bar as the sequential sweep on every GPU test (traces at the BASELINE sizes step for step, the
-// reference's reverse-communication loops, fixtures, linear equations), removes one
-// gemm_inner + gemm_outer per Q / D vector and iteration (C3: 0.85 -> 0.59 s) and a third of the
-// reductions (C3: 57 -> 39 per iteration, the latency that bounds the sharded C4 solve).
+// Davidson over HBM vectors orthogonalises new R vectors by block Gram-Schmidt (rspace.h) from
+// fused_min_size() (as the other fused solver passes) unless the option BLOCK_GRAM_SCHMIDT selects
+// otherwise: it passes the same parity bar as the sequential sweep on every GPU test (traces at the
+// BASELINE sizes step for step), removes one gemm_inner + gemm_outer per Q / D vector
+// and iteration (C3: 0.85 -> 0.59 s) and a third of the reductions (C3: 57 -> 39 per iteration, the
+// latency that bounds the sharded C4 solve).  Shorter vectors keep the reference's sequential MGS,
+// so that with the reference's arithmetic there (ssp_ctx_set_exact_max) a solve on the reference's
+// own test problems is its CPU path bit for bit.
 template <>
-struct block_gram_schmidt_default<hbm::Vec> : std::true_type {};
+struct block_gram_schmidt_default<hbm::Vec> : std::true_type {
+  static bool for_length(size_t n) { return n >= hbm::fused_min_size(); }
+};
 }  // namespace molpro::linalg::array

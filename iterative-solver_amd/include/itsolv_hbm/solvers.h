@@ -692,7 +692,8 @@ class DavidsonSolver : public IterativeSolverTemplate<R, Q, P> {
 
  public:
   void set_block_gram_schmidt(bool on) { m_block_gram_schmidt = on; }
-  bool block_gram_schmidt() const { return m_block_gram_schmidt; }
+  //! The option as set (unset: the R type's default for the vectors' length, block_gram_schmidt_default).
+  std::optional<bool> block_gram_schmidt() const { return m_block_gram_schmidt; }
 
  protected:
   // reference propose_rspace.h:553-624
@@ -721,8 +722,10 @@ class DavidsonSolver : public IterativeSolverTemplate<R, Q, P> {
     std::iota(rows.begin(), rows.end(), xs.dimensions().nX);
     detail::delete_parameters(redundant, wres);
     detail::delete_parameters(redundant, rows);
+    const bool block_gs = m_block_gram_schmidt.value_or(
+        array::block_gram_schmidt_default<R>::for_length(wres.empty() ? 0 : wres.front().get().size()));
     auto null_params =
-        m_block_gram_schmidt
+        block_gs
             ? detail::block_gram_schmidt(wres, full, rows, xs.dimensions(), xs.cparamsp(), xs.cparamsq(),
                                          xs.cparamsd(), norm_thresh, h)
             : detail::modified_gram_schmidt(wres, xs.data.at(EqnData::S), xs.dimensions(), xs.cparamsp(),
@@ -739,7 +742,7 @@ class DavidsonSolver : public IterativeSolverTemplate<R, Q, P> {
   detail::DSpaceResetter<Q> m_resetter;
   bool m_hermiticity = false;
   bool m_resetting = false;
-  bool m_block_gram_schmidt = array::block_gram_schmidt_default<R>::value;
+  std::optional<bool> m_block_gram_schmidt;
 };
 
 template <class R, class Q = R, class P = std::map<size_t, typename R::value_type>>

@@ -34,10 +34,11 @@ EXPORTS = [
     "ssp_download", "ssp_comm_unique_id", "ssp_ctx_attach_comm", "ssp_ctx_rank", "ssp_ctx_nranks",
     "ssp_allreduce_sum", "ssp_allgather_host", "ssp_ctx_attach_host_comm", "ssp_shard_range", "ssp_select_merge",
     "ssp_p2p_unique_id", "ssp_ctx_attach_p2p", "ssp_ctx_set_comm_timeout", "sspx_debug_stall",
+    "ssp_ctx_set_exact_max",
     "ssp_ledger_enable", "ssp_ledger_reset", "ssp_ledger_count", "ssp_ledger_reserve",
     "ssp_ledger_entry", "ssp_fill", "ssp_scal", "ssp_copy", "ssp_axpy", "ssp_dot",
     "ssp_gemm_inner", "ssp_gemm_outer", "ssp_gemm_outer_set", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_axpy_gram", "ssp_axpy_pairs_norm", "ssp_precondition", "ssp_select", "ssp_select_max_dot",
-    "ssp_sparse_copy", "ssp_sparse_axpy", "ssp_sparse_dot", "ssp_gemm_inner_sparse", "ssp_gemm_outer_sparse",
+    "ssp_sparse_copy", "ssp_sparse_axpy", "ssp_sparse_axpy_batch", "ssp_sparse_dot", "ssp_gemm_inner_sparse", "ssp_gemm_outer_sparse",
     "ssp_construct_solution",
     "sspx_synthetic_action", "sspx_synthetic_add_lowrank", "sspx_synthetic_diagonal", "sspx_fill_random", "sspx_dense_action",
     "sspx_synth_action", "sspx_synth_add_lowrank", "sspx_synth_diagonal",
@@ -105,6 +106,7 @@ def _declare(lib):
         "ssp_ctx_attach_p2p": (I, [P, I, I, C.c_char_p]),
         "ssp_ctx_set_comm_timeout": (I, [P, D]),
         "sspx_debug_stall": (I, [P, D]),
+        "ssp_ctx_set_exact_max": (I, [P, Z]),
         "ssp_shard_range": (I, [Z, I, I, PZ, PZ]),
         "ssp_select_merge": (I, [I, PZ, Z, PZ, PD, Z, I, PZ, PD, PZ]),
         "ssp_ledger_enable": (I, [P, I]),
@@ -130,6 +132,7 @@ def _declare(lib):
         "ssp_select_max_dot": (I, [P, P, P, Z, Z, Z, PZ, PD, PZ]),
         "ssp_sparse_copy": (I, [P, P, Z, Z, PZ, PD, Z]),
         "ssp_sparse_axpy": (I, [P, D, PZ, PD, Z, P, Z, Z]),
+        "ssp_sparse_axpy_batch": (I, [P, I, PZ, PZ, PD, P, Z, Z]),
         "ssp_sparse_dot": (I, [P, P, Z, Z, PZ, PD, Z, PD]),
         "ssp_gemm_inner_sparse": (I, [P, P, I, Z, Z, PZ, PZ, PD, I, PD]),
         "ssp_gemm_outer_sparse": (I, [P, PD, PZ, PZ, PD, I, P, I, Z, Z]),
@@ -453,6 +456,11 @@ class Context:
         """Deadline of every wait that depends on other ranks (SSP_COMM_TIMEOUT_S)."""
         _check(self.lib.ssp_ctx_set_comm_timeout(self.handle, float(seconds)))
 
+    def set_exact_max(self, n: int):
+        """Vectors of at most n local elements use the reference's arithmetic bit for bit: sequential
+        dots, no fused multiply-adds (ssp_ctx_set_exact_max; default 16384, 0 = off)."""
+        _check(self.lib.ssp_ctx_set_exact_max(self.handle, int(n)))
+
     def debug_stall(self, ms: float):
         """Test harness: holds the stream for ms milliseconds (sspx_debug_stall)."""
         _check(self.lib.sspx_debug_stall(self.handle, float(ms)))
@@ -610,6 +618,13 @@ class Context:
         idx = np.ascontiguousarray(idx, dtype=np.uint64)
         val = np.ascontiguousarray(val, dtype=np.float64)
         _check(self.lib.ssp_sparse_axpy(self.handle, alpha, _zptr(idx), _dptr(val), idx.size, x.ptr, x.n, offset))
+
+    def sparse_axpy_batch(self, ps: Sequence[dict], xx: Sequence[DeviceVector], offset: int = 0):
+        """xx[k] += p_k for each sparse vector p_k (ssp_sparse_axpy_batch: one launch)."""
+        ptr, idx, val = self._pack_sparse(ps)
+        n = xx[0].n if xx else 0
+        _check(self.lib.ssp_sparse_axpy_batch(self.handle, len(ps), _zptr(ptr), _zptr(idx), _dptr(val), _ptrs(xx), n,
+                                              offset))
 
     def sparse_dot(self, x: DeviceVector, idx, val, offset: int = 0) -> float:
         idx = np.ascontiguousarray(idx, dtype=np.uint64)

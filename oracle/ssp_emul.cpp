@@ -229,6 +229,7 @@ int ssp_ctx_set_comm_timeout(ssp_ctx*, double seconds) {
   return seconds > 0 ? SSP_OK : fail(SSP_ERR_ARG, "ssp_ctx_set_comm_timeout: seconds must be > 0");
 }
 int sspx_debug_stall(ssp_ctx*, double) { return SSP_OK; }
+int ssp_ctx_set_exact_max(ssp_ctx*, size_t) { return SSP_OK; }
 int ssp_ctx_rank(ssp_ctx* c) { return c->rank; }
 int ssp_ctx_nranks(ssp_ctx* c) { return c->nranks; }
 int ssp_allreduce_sum(ssp_ctx* c, double* v, size_t n) { return reduce(c, v, n); }
@@ -488,6 +489,11 @@ int ssp_sparse_axpy(ssp_ctx*, double a, const size_t* idx, const double* val, si
   std::vector<double> lv;
   filter(idx, val, nnz, n, off, li, lv);
   for (size_t e = 0; e < li.size(); ++e) x[li[e]] += a * lv[e];
+  return SSP_OK;
+}
+int ssp_sparse_axpy_batch(ssp_ctx* c, int nvec, const size_t* ptr, const size_t* idx, const double* val,
+                          double* const* xx, size_t n, size_t off) {
+  for (int k = 0; k < nvec; ++k) ssp_sparse_axpy(c, 1.0, idx + ptr[k], val + ptr[k], ptr[k + 1] - ptr[k], xx[k], n, off);
   return SSP_OK;
 }
 int ssp_gemm_inner_sparse(ssp_ctx* c, const double* const* xx, int m, size_t n, size_t off, const size_t* ptr,

@@ -17,6 +17,15 @@ EPS = np.finfo(np.float64).eps
 SIZES = [0, 1, 2, 7, 64, 1003, 100_003, (1 << 20) + 5]
 
 
+@pytest.fixture(autouse=True)
+def bandwidth_kernels(ctx):
+    """These tests hold the bandwidth kernels (tree-ordered sums, fused multiply-adds) to the oracle at
+    every size: the reference-arithmetic path for short vectors is off here (tests/test_exact_gpu.py)."""
+    ctx.set_exact_max(0)
+    yield
+    ctx.set_exact_max(16384)
+
+
 def rng(seed=1):
     return np.random.default_rng(seed)
 
@@ -414,6 +423,24 @@ def test_sparse_ops_with_shard_offset(ctx):
     np.testing.assert_allclose(dx.numpy(), oracle.sparse_axpy(-0.5, li, lv, x), rtol=2 * EPS, atol=0)
     ctx.sparse_copy(dx, idx, val, offset=off)
     assert np.array_equal(dx.numpy(), oracle.sparse_copy(n, li, lv))
+
+
+@pytest.mark.parametrize("nvec,per", [(1, 1), (8, 1), (8, 8), (16, 4), (5, 20), (17, 1)])
+def test_sparse_axpy_batch_is_one_sparse_axpy_per_vector(ctx, nvec, per):
+    # one launch while the entries fit the argument block (<= 64, <= 16 vectors), else one per vector;
+    # entries outside the shard are dropped as by ssp_sparse_axpy
+    n, off = 1000, 3000
+    r = rng(nvec * 100 + per)
+    ps = [{int(i): float(v) for i, v in zip(r.choice(np.arange(off - 50, off + n + 50), per, replace=False),
+                                            r.uniform(-1, 1, per))} for _ in range(nvec)]
+    xs = [r.uniform(-1, 1, n) for _ in range(nvec)]
+    dx = [ctx.upload(v) for v in xs]
+    ctx.sparse_axpy_batch(ps, dx, offset=off)
+    for p, x, d in zip(ps, xs, dx):
+        idx = np.array(list(p.keys()), dtype=np.uint64)
+        ins = (idx >= off) & (idx < off + n)
+        want = oracle.sparse_axpy(1.0, (idx[ins] - off).astype(np.int64), np.array(list(p.values()))[ins], x)
+        assert np.array_equal(d.numpy(), want)
 
 
 def test_sparse_gemm(ctx):

@@ -17,6 +17,16 @@ import subspace_hip as sh
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def bandwidth_kernels(ctx):
+    """These tests hold the bandwidth kernels (tree-ordered sums, fused multiply-adds) to the oracle at
+    every size: the reference-arithmetic path for short vectors is off here (tests/test_exact_gpu.py)."""
+    ctx.set_exact_max(0)
+    yield
+    ctx.set_exact_max(16384)
+
+
 N_SMALL = 100_003
 N_WIN = (1 << 24) + 5  # the window shape of the element-wise kernels
 
