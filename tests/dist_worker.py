@@ -207,6 +207,47 @@ def case_gpu_traces(comm):
     ctx.close()
 
 
+def case_gpu_exact_mpi(comm):
+    """The reference's own distributed build, bit for bit: on shards of at most ssp_ctx_set_exact_max
+    elements every rank computes in the reference's arithmetic and the transport adds the ranks'
+    partials in rank order (peer memory, host), so a sharded solve over P ranks must reproduce the CPU
+    path run with the dots of P MPI ranks (tests/golden/mpi_traces.json, make_traces.py --mpi-golden)
+    -- every iteration count, trace value, eigenvalue and residual norm to the last bit, including the
+    DIIS case whose step count the reference itself changes with the rank count (13, 13, 32, 12, 56)."""
+    import json
+
+    import numpy as np
+
+    import itsolv_hbm as ih
+    import subspace_hip as sh
+
+    rank, world = comm.rank, comm.nranks
+    gold = json.load(open(os.path.join(HERE, "golden", "mpi_traces.json")))
+    ctx = sh.Context(0)
+    attach(ctx, comm)
+    for name, rec in gold.items():
+        if name.startswith("_"):
+            continue
+        c, ref = rec["case"], rec[f"mpi{world}"]
+        nl = sh.shard_range(c["n"], world, rank)[1]
+        fn = ih.davidson_synthetic if c["kind"] == "davidson" else ih.diis_synthetic
+        g = fn(ctx, c["n"], c["rho"], c["rank"], c["seed"], n_local=nl, solutions=False, **rec["options"])
+        head = f"{name} on {world} shards"
+        assert (g["iterations"], g["converged"]) == (ref["iterations"], ref["converged"]), (head, g["iterations"])
+        assert (g["r_creations"], g["q_creations"]) == (ref["r_creations"], ref["q_creations"]), head
+        # (residual_norms: a post-solve diagnostic of the harness, summed sequentially by the oracle
+        # whatever the order of its dots; not compared here)
+        for f in ("eigenvalues", "errors"):
+            if ref[f]:
+                assert np.array_equal(np.asarray(g[f]), np.asarray(ref[f])), (head, f, g[f], ref[f])
+        for f in ("eigenvalues", "errors", "nq", "nwork", "screened"):
+            if len(ref["trace"][f]):
+                assert np.array_equal(np.asarray(g["trace"][f]), np.asarray(ref["trace"][f])), (head, "trace", f)
+        if rank == 0:
+            print(f"{head}: {g['iterations']} iterations, bit-identical to the {world}-rank CPU path", flush=True)
+    ctx.close()
+
+
 def case_gpu_distr(comm):
     """The reference's distributed-array known answers (tests/distr_cases.py) on HBM shards."""
     import distr_cases
@@ -288,12 +329,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--comm", choices=["gloo", "hub"], required=True)
     ap.add_argument("--case", choices=["reductions", "gpu_ops", "gpu_solver", "gpu_distr", "gpu_traces",
-                                       "gpu_peer_lost"], required=True)
+                                       "gpu_peer_lost", "gpu_exact_mpi"], required=True)
     a = ap.parse_args()
     comm = make_comm(a.comm)
     no_barrier = {"reductions": case_reductions, "gpu_ops": case_gpu_ops, "gpu_solver": case_gpu_solver,
                   "gpu_distr": case_gpu_distr, "gpu_traces": case_gpu_traces,
-                  "gpu_peer_lost": case_gpu_peer_lost}[a.case](comm)
+                  "gpu_peer_lost": case_gpu_peer_lost, "gpu_exact_mpi": case_gpu_exact_mpi}[a.case](comm)
     if no_barrier:
         print(f"rank {comm.rank}/{comm.nranks} {a.case} OK", flush=True)
         os._exit(0)  # the hub peer may be gone: no closing collective

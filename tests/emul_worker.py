@@ -242,7 +242,20 @@ def case_distr():
     comm.close()
 
 
+def case_exact_mpi():
+    """The bit-for-bit check of the reference's MPI build that the GPU runs (dist_worker
+    case_gpu_exact_mpi), through the product's host code over the emulation: sequential sums on each
+    rank, the partials added in rank order by the socket host communicator."""
+    import dist_worker
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    comm = sh.HubComm(rank, world, "127.0.0.1", int(os.environ["SSP_HUB_PORT"]))
+    dist_worker.case_gpu_exact_mpi(comm)
+    comm.barrier()
+    comm.close()
+
+
 if __name__ == "__main__":
     {"api": case_api, "spmd": case_spmd, "spmd-gloo": lambda: case_spmd(gloo=True), "c4": case_c4, "distr": case_distr,
-     "devsel": case_devsel, "rs_traces": case_rs_traces}[sys.argv[1]]()
+     "devsel": case_devsel, "rs_traces": case_rs_traces, "exact_mpi": case_exact_mpi}[sys.argv[1]]()
     print(f"{sys.argv[1]} OK", flush=True)

@@ -226,8 +226,56 @@ def merge_parts(parts):
     return base["case"], out
 
 
+# Short-vector cases for the reference's own distributed build (tests/golden/mpi_traces.json): the
+# whole solve record -- every trace value -- of the CPU path with its dots summed as on P MPI ranks
+# (rank-local sequential sums added in rank order), P = 1 (sequential), 2, 3, 4, 8.  On shards of at
+# most ssp_ctx_set_exact_max elements the HIP path over a rank-order transport (peer memory, host)
+# must reproduce them bit for bit (tests/dist_worker.py case gpu_exact_mpi).
+MPI_CASES = {
+    "C1_rank1": CASES["C1_rank1"],
+    "C1_rank8": CASES["C1_rank8"],
+    "S_p8": {"kind": "davidson", "n": 10007, "rho": 0.1, "rank": 4, "seed": 20251015, "nroots": 4, "max_p": 8},
+    "D_1000": {"kind": "diis", "n": 1000, "rho": 0.1, "rank": 1, "seed": 3},
+}
+MPI_ORDERS = {"mpi1": 0, "mpi2": 102, "mpi3": 103, "mpi4": 104, "mpi8": 108}
+
+
+def mpi_options(c):
+    if c["kind"] == "diis":
+        return {"convergence_threshold": 1e-8, "max_size_qspace": 6}
+    return {"nroots": c["nroots"], "max_p": c["max_p"], "convergence_threshold": 1e-8,
+            "max_size_qspace": 6 * c["nroots"], "reset_D": 8}
+
+
+def mpi_golden(out_path):
+    import numpy as np
+
+    import oracle
+
+    out = {"_generator": "tests/golden/make_traces.py --mpi-golden: oracle (reference CPU path restated, "
+                         "-ffp-contract=off), dots in the rank order of P MPI ranks"}
+    for name, c in MPI_CASES.items():
+        fn = oracle.davidson_synthetic if c["kind"] == "davidson" else oracle.diis_synthetic
+        rec = {"case": c, "options": mpi_options(c)}
+        for key, order in MPI_ORDERS.items():
+            oracle.set_sum_order(order)
+            r = fn(c["n"], c["rho"], c["rank"], c["seed"], solutions=False, **mpi_options(c))
+            tr = r["trace"]
+            rec[key] = {"converged": r["converged"], "iterations": r["iterations"], "r_creations": r["r_creations"],
+                        "q_creations": r["q_creations"], "eigenvalues": [float(x) for x in r["eigenvalues"]],
+                        "errors": [float(x) for x in r["errors"]],
+                        "residual_norms": [float(x) for x in r["residual_norms"]],
+                        "trace": {k: np.asarray(tr[k]).tolist() for k in ("eigenvalues", "errors", "nq", "nwork",
+                                                                          "screened")}}
+            print(name, key, r["iterations"], r["r_creations"], flush=True)
+        oracle.set_sum_order(0)
+        out[name] = rec
+    json.dump(out, open(out_path, "w"), indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--mpi-golden", action="store_true", help="write tests/golden/mpi_traces.json")
     ap.add_argument("--only", nargs="*")
     ap.add_argument("--jobs", type=int, default=3)
     ap.add_argument("--out", default=os.path.join(HERE, "traces.json"))
@@ -238,6 +286,9 @@ def main():
     ap.add_argument("--part", choices=PARTS, help="one run of the single --only case, written to --out as is")
     ap.add_argument("--merge", nargs="*", help="--part outputs of one case to merge into --out")
     a = ap.parse_args()
+    if a.mpi_golden:
+        mpi_golden(os.path.join(HERE, "mpi_traces.json"))
+        return
     if a.omp:
         os.environ["ORACLE_OMP"] = "1"
     if a.part:

@@ -95,6 +95,15 @@ def test_c5_full_size_on_8_shards_p2p():
                   env_extra={"SSP_TRACES_FULL": "C5", "SSP_COMM_TIMEOUT_S": "60"})[0])
 
 
+# ---- the reference's own distributed build, bit for bit (short vectors, rank-order transports) --------
+@pytest.mark.parametrize("transport", ["host", "p2p"])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_sharded_short_solves_are_the_reference_mpi_build(world, transport):
+    out = run_hub("gpu_exact_mpi", world=world, timeout=600, transport=transport,
+                  env_extra={"SSP_COMM_TIMEOUT_S": "60"})[0]
+    print(out)
+
+
 # ---- fail fast: a lost rank ends the survivors' solves with SSP_ERR_COMM, no hang, no process left --
 @pytest.mark.parametrize("transport", ["host", "p2p"])
 def test_lost_rank_fails_fast(transport):

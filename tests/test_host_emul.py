@@ -95,6 +95,21 @@ def test_reference_distributed_array_known_answers(world):
         assert p.returncode == 0 and "distr OK" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_short_solves_reproduce_the_reference_mpi_build(world):
+    # tests/golden/mpi_traces.json (make_traces.py --mpi-golden): the CPU path with the dots of P MPI
+    # ranks; the product's host code over the emulation on P shards, partials added in rank order,
+    # must reproduce every record bit for bit (the GPU twin: test_distributed_gpu.py)
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, WORKER, "exact_mpi"],
+                              env=dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), SSP_HUB_PORT=str(port),
+                                       OMP_NUM_THREADS="1"),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    outs = [p.communicate(timeout=600)[0] for p in procs]
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0 and "exact_mpi OK" in out, out[-3000:]
+
+
 LAUNCHER_VARS = ("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "SLURM_LOCALID", "HIP_VISIBLE_DEVICES",
                  "SSP_EMUL_DEVICES")
 
