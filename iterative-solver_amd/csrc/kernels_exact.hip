@@ -20,49 +20,121 @@ namespace {
 
 using ssp::kBlock;
 
+// Operands ride in the argument block when there are at most kInl of each (no staging copy).
+constexpr int kInl = 64;
 struct ExactInnerArgs {
-  const double* const* x;  // m vectors (device array of pointers)
+  const double* const* x;  // m vectors (device array of pointers; null: inline below)
   const double* const* y;  // k vectors
   const double* xs;        // m deferred scales
   const double* ys;        // k deferred scales
+  const double* xi[kInl];
+  const double* yi[kInl];
+  double xsi[kInl], ysi[kInl];
   int m, k;
   int pairs;               // 1: out[j] = <x_j, y_j> (m == k); 0: out[i * k + j] = <x_i, y_j>
   size_t n;
   double* out;             // device
 };
 
+// s + buf[0] + buf[1] + ... + buf[len-1], added in that order.  The chain of dependent adds is the
+// cost; the LDS reads are issued 16 values ahead of the adds that consume them, so their latency
+// (≈ 50 cycles) hides behind the previous 16 adds.
+__device__ __forceinline__ double add_in_order(const double* buf, int len, double s) {
+  const double2* b2 = reinterpret_cast<const double2*>(buf);
+  int t = 0;
+  if (len >= 16) {
+    double2 cur[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) cur[u] = b2[u];
+    for (t = 16; t + 16 <= len; t += 16) {
+      double2 nxt[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) nxt[u] = b2[t / 2 + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s = s + cur[u].x;
+        s = s + cur[u].y;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s = s + cur[u].x;
+      s = s + cur[u].y;
+    }
+  }
+  for (; t < len; ++t) s = s + buf[t];
+  return s;
+}
+
 // One workgroup per output: the sequential std::inner_product of the (stored-equivalent) operands.
-// The workgroup forms a chunk of products in LDS (each product rounded alone, whichever lane forms
-// it), then lane 0 adds them in index order; the next chunk follows.
-constexpr int kExactChunk = 4 * kBlock;
+// Waves 1..3 form the products of the next chunk in LDS (each product rounded alone, whichever lane
+// forms it) while lane 0 of wave 0 adds the current chunk in index order (double-buffered chunks).
+constexpr int kExactChunk = 2048;
 __global__ __launch_bounds__(kBlock) void k_exact_inner(const ExactInnerArgs a) {
-  __shared__ double prod[kExactChunk];
+  __shared__ __attribute__((aligned(16))) double prod[2][kExactChunk];
   const int o = int(blockIdx.x);
   const int i = a.pairs ? o : o / a.k, j = a.pairs ? o : o % a.k;
-  const double* x = a.x[i];
-  const double* y = a.y[j];
-  const double xs = a.xs[i], ys = a.ys[j];
-  double s = 0;
-  for (size_t c0 = 0; c0 < a.n; c0 += kExactChunk) {
+  const double* x = a.x ? a.x[i] : a.xi[i];
+  const double* y = a.x ? a.y[j] : a.yi[j];
+  const double xs = a.x ? a.xs[i] : a.xsi[i], ys = a.x ? a.ys[j] : a.ysi[j];
+  const int fill_lane = int(threadIdx.x) - 64, fill_lanes = kBlock - 64;
+  const int nchunk = int((a.n + kExactChunk - 1) / kExactChunk);
+  auto fill = [&](int c) {
+    const size_t c0 = size_t(c) * kExactChunk;
     const int len = int(a.n - c0 < size_t(kExactChunk) ? a.n - c0 : size_t(kExactChunk));
-    for (int t = int(threadIdx.x); t < len; t += kBlock) prod[t] = (x[c0 + t] * xs) * (y[c0 + t] * ys);
-    __syncthreads();
-    if (threadIdx.x == 0)
-      for (int t = 0; t < len; ++t) s = s + prod[t];
+    // 4 elements' loads in flight per lane before the products are formed
+    for (int t0 = fill_lane; t0 < len; t0 += 4 * fill_lanes) {
+      double xv[4], yv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u * fill_lanes;
+        if (t < len) {
+          xv[u] = x[c0 + t];
+          yv[u] = y[c0 + t];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u * fill_lanes;
+        if (t < len) prod[c & 1][t] = (xv[u] * xs) * (yv[u] * ys);
+      }
+    }
+  };
+  if (fill_lane >= 0) fill(0);
+  __syncthreads();
+  double s = 0;
+  for (int c = 0; c < nchunk; ++c) {
+    if (fill_lane >= 0) {
+      if (c + 1 < nchunk) fill(c + 1);
+    } else if (threadIdx.x == 0) {
+      const size_t c0 = size_t(c) * kExactChunk;
+      const int len = int(a.n - c0 < size_t(kExactChunk) ? a.n - c0 : size_t(kExactChunk));
+      s = add_in_order(prod[c & 1], len, s);
+    }
     __syncthreads();
   }
   if (threadIdx.x == 0) a.out[o] = s;
 }
 
+static_assert(sizeof(ExactInnerArgs) <= 4000, "kernel argument block too large");
+
+// Inline operands: at most kOutSrc sources, kOutDst destinations and kOutAl coefficients.
+constexpr int kOutSrc = 32, kOutDst = 16, kOutAl = 128;
 struct ExactOuterArgs {
-  const double* const* x;  // k sources
+  const double* const* x;  // k sources (device array; null: inline below)
   double* const* y;        // m destinations
   const double* xs;        // k source scales
   const double* ys;        // m destination scales (applied to the values read)
   const double* alpha;     // alpha[i * m + j]
+  const double* xi[kOutSrc];
+  double* yi[kOutDst];
+  double xsi[kOutSrc], ysi[kOutDst], ali[kOutAl];
   int m, k, set;
   size_t n;
 };
+static_assert(sizeof(ExactOuterArgs) <= 4000, "kernel argument block too large");
 
 // One thread per (element, destination): y_j[e] = y_j[e] + alpha(i, j) x_i[e] for i = 0..k-1 in order,
 // each product rounded -- the pairwise axpy loop of gemm_outer_default, element by element.
@@ -71,9 +143,15 @@ __global__ __launch_bounds__(kBlock) void k_exact_outer(const ExactOuterArgs a) 
   for (size_t t = size_t(blockIdx.x) * kBlock + threadIdx.x; t < total; t += size_t(gridDim.x) * kBlock) {
     const int j = int(t / a.n);
     const size_t e = t % a.n;
-    double v = a.set ? 0.0 : a.y[j][e] * a.ys[j];
-    for (int i = 0; i < a.k; ++i) v = v + a.alpha[size_t(i) * a.m + j] * (a.x[i][e] * a.xs[i]);
-    a.y[j][e] = v;
+    if (a.x) {
+      double v = a.set ? 0.0 : a.y[j][e] * a.ys[j];
+      for (int i = 0; i < a.k; ++i) v = v + a.alpha[size_t(i) * a.m + j] * (a.x[i][e] * a.xs[i]);
+      a.y[j][e] = v;
+    } else {
+      double v = a.set ? 0.0 : a.yi[j][e] * a.ysi[j];
+      for (int i = 0; i < a.k; ++i) v = v + a.ali[i * a.m + j] * (a.xi[i][e] * a.xsi[i]);
+      a.yi[j][e] = v;
+    }
   }
 }
 
@@ -98,10 +176,21 @@ int exact_inner(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, 
   if (nout == 0) return SSP_OK;
   std::vector<double> one(size_t(std::max(m, k)), 1.0);
   ExactInnerArgs a{};
-  SSP_TRY(stage(ctx, xx, size_t(m), &a.x));
-  SSP_TRY(stage(ctx, yy, size_t(k), &a.y));
-  SSP_TRY(stage(ctx, xs ? xs : one.data(), size_t(m), &a.xs));
-  SSP_TRY(stage(ctx, ys ? ys : one.data(), size_t(k), &a.ys));
+  if (m <= kInl && k <= kInl) {
+    for (int i = 0; i < m; ++i) {
+      a.xi[i] = xx[i];
+      a.xsi[i] = xs ? xs[i] : 1.0;
+    }
+    for (int j = 0; j < k; ++j) {
+      a.yi[j] = yy[j];
+      a.ysi[j] = ys ? ys[j] : 1.0;
+    }
+  } else {
+    SSP_TRY(stage(ctx, xx, size_t(m), &a.x));
+    SSP_TRY(stage(ctx, yy, size_t(k), &a.y));
+    SSP_TRY(stage(ctx, xs ? xs : one.data(), size_t(m), &a.xs));
+    SSP_TRY(stage(ctx, ys ? ys : one.data(), size_t(k), &a.ys));
+  }
   a.m = m;
   a.k = k;
   a.pairs = pairs ? 1 : 0;
@@ -116,10 +205,30 @@ int exact_inner(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, 
 int exact_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, const double* xs, int k,
                 double* const* yy, const double* ys, int m, size_t n, bool set) {
   if (m == 0 || n == 0) return SSP_OK;
+  ExactOuterArgs a{};
+  if (k <= kOutSrc && m <= kOutDst && k * m <= kOutAl) {
+    for (int i = 0; i < k; ++i) {
+      a.xi[i] = xx[i];
+      a.xsi[i] = xs ? xs[i] : 1.0;
+    }
+    for (int j = 0; j < m; ++j) {
+      a.yi[j] = yy[j];
+      a.ysi[j] = ys && !set ? ys[j] : 1.0;
+    }
+    for (int q = 0; q < k * m; ++q) a.ali[q] = alphas[q];
+    a.m = m;
+    a.k = k;
+    a.set = set ? 1 : 0;
+    a.n = n;
+    const size_t total = n * size_t(m);
+    const unsigned grid = unsigned(std::min<size_t>((total + kBlock - 1) / kBlock, size_t(ctx->num_cus) * 4));
+    hipLaunchKernelGGL(k_exact_outer, dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_TRY_HIP(hipGetLastError());
+    return SSP_OK;
+  }
   std::vector<double> one(size_t(std::max(m, k)), 1.0);
   std::vector<double> al(size_t(std::max(1, k * m)), 0.0);
   if (k > 0) std::copy(alphas, alphas + size_t(k) * m, al.begin());
-  ExactOuterArgs a{};
   std::vector<const double*> xp(size_t(std::max(k, 1)), nullptr);
   for (int i = 0; i < k; ++i) xp[size_t(i)] = xx[i];
   SSP_TRY(stage(ctx, xp.data(), xp.size(), &a.x));

@@ -147,27 +147,71 @@ __global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a) {
 }
 
 // Short vectors (ssp_ctx_set_exact_max): the coefficients as sequential sums in index order, as the
-// host restatement's loop (one workgroup per vector: a chunk of scaled values and masks in LDS, then
-// lane l adds the chunk for coefficient l in order).  out[v * R + l], v < nvec.
+// host restatement's loop.  One workgroup per vector: waves 1..3 stage the next chunk of scaled
+// values and sign masks in LDS while lanes l < R of wave 0 add the current chunk for coefficient l in
+// order (double-buffered; the LDS reads run 8 values ahead of the adds).  out[v * R + l], v < nvec.
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_synth_coeff_exact(const SynthArgs a, double* out) {
-  constexpr int kChunk = 4 * kBlock;
-  __shared__ double xv[kChunk];
-  __shared__ unsigned short mk[kChunk];
-  const int v = int(blockIdx.x);
-  double s = 0;
-  for (size_t c0 = 0; c0 < a.n; c0 += kChunk) {
+  constexpr int kChunk = 2048;
+  __shared__ __attribute__((aligned(16))) double xv[2][kChunk];
+  __shared__ __attribute__((aligned(16))) unsigned short mk[2][kChunk];
+  const int v = int(blockIdx.x), l = int(threadIdx.x);
+  const int fill_lane = int(threadIdx.x) - 64, fill_lanes = kBlock - 64;
+  const int nchunk = int((a.n + kChunk - 1) / kChunk);
+  auto fill = [&](int c) {
+    const size_t c0 = size_t(c) * kChunk;
     const int len = int(a.n - c0 < size_t(kChunk) ? a.n - c0 : size_t(kChunk));
-    for (int t = int(threadIdx.x); t < len; t += kBlock) {
-      xv[t] = a.x[v][c0 + t] * a.xs[v];
-      mk[t] = a.mask[c0 + t];
+    const double* x = a.x[v];
+    const double xs = a.xs[v];
+    for (int t0 = fill_lane; t0 < len; t0 += 4 * fill_lanes) {  // 4 elements' loads in flight per lane
+      double x4[4];
+      unsigned short m4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u * fill_lanes;
+        if (t < len) {
+          x4[u] = x[c0 + t];
+          m4[u] = a.mask[c0 + t];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u * fill_lanes;
+        if (t < len) {
+          xv[c & 1][t] = x4[u] * xs;
+          mk[c & 1][t] = m4[u];
+        }
+      }
+    }
+  };
+  if (fill_lane >= 0) fill(0);
+  __syncthreads();
+  double s = 0;
+  for (int c = 0; c < nchunk; ++c) {
+    if (fill_lane >= 0) {
+      if (c + 1 < nchunk) fill(c + 1);
+    } else if (l < R) {
+      const size_t c0 = size_t(c) * kChunk;
+      const int len = int(a.n - c0 < size_t(kChunk) ? a.n - c0 : size_t(kChunk));
+      const double* xb = xv[c & 1];
+      const unsigned short* mb = mk[c & 1];
+      int t = 0;
+      for (; t + 8 <= len; t += 8) {
+        double x8[8];
+        unsigned short m8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          x8[u] = xb[t + u];
+          m8[u] = mb[t + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s = s + flip(m8[u], l, x8[u]);
+      }
+      for (; t < len; ++t) s = s + flip(mb[t], l, xb[t]);
     }
     __syncthreads();
-    if (int(threadIdx.x) < R)
-      for (int t = 0; t < len; ++t) s = s + flip(mk[t], int(threadIdx.x), xv[t]);
-    __syncthreads();
   }
-  if (int(threadIdx.x) < R) out[v * R + int(threadIdx.x)] = s;
+  if (l < R) out[v * R + l] = s;
 }
 
 // d x + rho s and y + rho s with every product rounded alone (the reference's arithmetic).
