@@ -93,7 +93,7 @@ int ssp_ctx_attach_p2p(ssp_ctx* ctx, int nranks, int rank, const char* id);
  * later exchange on the context, returns SSP_ERR_COMM naming the operation -- the status-code form of
  * the reference's abort of the whole job on a distributed error (DistrArray.cpp:16-23). */
 int ssp_ctx_set_comm_timeout(ssp_ctx* ctx, double seconds);
-/* Vectors of at most n local elements (default 16384, or SSP_EXACT_MAX at context creation; 0 turns
+/* Vectors of at most n local elements (default 2048, or SSP_EXACT_MAX at context creation; 0 turns
  * it off) are computed in the reference's own arithmetic: every dot a sequential sum in index order
  * (std::inner_product, ArrayHandlerIterable.h:76-82) and every y = alpha x + y rounded twice (no fused
  * multiply-add, ArrayHandlerIterable.h:65-74), gemm_inner / gemm_outer pairwise in the reference's loop

@@ -1,13 +1,16 @@
 // The reference's own arithmetic for short vectors (ssp_ctx_set_exact_max / SSP_EXACT_MAX, default
-// 16384 local elements): every reduction a sequential sum in index order and every multiply-add
+// 2048 local elements): every reduction a sequential sum in index order and every multiply-add
 // rounded twice, exactly the reference's ArrayHandlerIterable loops (std::inner_product,
 // ArrayHandlerIterable.h:76-82; y = alpha * x + y, :65-74) and its pairwise gemm_inner_default /
 // gemm_outer_default (util/gemm.h:257-279).  A solve on such vectors is then the reference CPU path bit
 // for bit (on one rank; on several, the reference's distributed build: rank-local sums added in rank
 // order by the peer-memory and host transports).  The short vectors are the reference's own test
-// problems (its matrices have 4 to 784 rows): there every kernel is latency-bound, so the fixed order
-// costs nothing measurable, while the parallel kernels' other -- equally valid -- summation order and
-// fused multiply-adds let last-bit differences decide knife-edge steps of those tests.
+// problems (its matrices have 4 to 1000 rows): there every kernel is latency-bound, while the parallel
+// kernels' other -- equally valid -- summation order and fused multiply-adds let last-bit differences
+// decide knife-edge steps of those tests.  The cost is the chain of dependent adds, ≈ 7 ns per element
+// on gfx950 (tools/exact_cost.py): 2048 elements add ≈ 14 µs to a reduction, about a bandwidth
+// kernel's whole launch-and-fetch time; at 16384 a dot takes 131 µs against 14 µs, so longer vectors
+// default to the bandwidth kernels (the knob raises the limit; tests/test_exact_gpu.py runs to 16384).
 #include <algorithm>
 #include <vector>
 

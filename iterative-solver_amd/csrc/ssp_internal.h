@@ -100,7 +100,7 @@ struct ssp_ctx {
   double comm_timeout_s = 300.0;
   // Vectors of at most this many local elements take the reference's own arithmetic
   // (kernels_exact.hip: sequential sums, no fused multiply-adds); SSP_EXACT_MAX / ssp_ctx_set_exact_max.
-  size_t exact_max = 16384;
+  size_t exact_max = 2048;
   bool comm_failed = false;
   std::string comm_fail_msg;
   // Coherent host word a device-side exchange sets when it gave up (peer missing / mismatched).

@@ -100,48 +100,78 @@ __device__ __forceinline__ double block_sum(double v, double* wsum) {
 // of an odd-length shard is folded in by the thread that owns pair n/2).
 __device__ __forceinline__ double2 ld2nt(const double* p) { return ssp::ld2nt(p); }
 
-// Per-block partial sums of u_l . x_v, vectors in groups of G (R x G accumulators per thread).
-template <int R, int G>
-__global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a) {
+// Per-block partial sums of u_l . x_v for the NV vectors v0 .. v0+NV-1 (R x NV accumulators per
+// thread).  NV is a compile-time count, so every vector's loads of a visit are issued together, and two
+// visits (i, i + stride) are in flight per lane; each accumulator still adds its terms in the order
+// i, i + stride, i + 2 stride, ...
+template <int R, int NV>
+__device__ __forceinline__ void coeff_visit(double (&s)[NV][R], unsigned mm, const double2 (&xv)[NV]) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int l = 0; l < R; ++l) s[v][l] += flip(mm, l, xv[v].x) + flip(mm >> 16, l, xv[v].y);
+}
+
+template <int R, int NV>
+__global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a, int v0) {
   __shared__ double wsum[kBlock / 64];
   const size_t stride = size_t(gridDim.x) * kBlock, n2 = a.n >> 1;
   const unsigned* mask2 = reinterpret_cast<const unsigned*>(a.mask);
-  for (int v0 = 0; v0 < a.nvec; v0 += G) {
-    double s[G][R];
+  const double* xp[NV];
+  double xs[NV];
 #pragma unroll
-    for (int v = 0; v < G; ++v)
+  for (int v = 0; v < NV; ++v) {
+    xp[v] = a.x[v0 + v];
+    xs[v] = a.xs[v0 + v];
+  }
+  double s[NV][R];
 #pragma unroll
-      for (int l = 0; l < R; ++l) s[v][l] = 0;
-    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += stride) {
-      const unsigned mm = mask2[i];
+  for (int v = 0; v < NV; ++v)
 #pragma unroll
-      for (int v = 0; v < G; ++v) {
-        if (v0 + v < a.nvec) {
-          double2 xv = ld2nt(a.x[v0 + v] + 2 * i);
-          xv.x *= a.xs[v0 + v];
-          xv.y *= a.xs[v0 + v];
+    for (int l = 0; l < R; ++l) s[v][l] = 0;
+  size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + stride < n2; i += 2 * stride) {
+    const unsigned m0 = mask2[i], m1 = mask2[i + stride];
+    double2 x0[NV], x1[NV];
 #pragma unroll
-          for (int l = 0; l < R; ++l) s[v][l] += flip(mm, l, xv.x) + flip(mm >> 16, l, xv.y);
-        }
-      }
-    }
-    if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-      const unsigned mm = a.mask[a.n - 1];
-#pragma unroll
-      for (int v = 0; v < G; ++v)
-        if (v0 + v < a.nvec)
-#pragma unroll
-          for (int l = 0; l < R; ++l) s[v][l] += flip(mm, l, a.x[v0 + v][a.n - 1] * a.xs[v0 + v]);
+    for (int v = 0; v < NV; ++v) {
+      x0[v] = ld2nt(xp[v] + 2 * i);
+      x1[v] = ld2nt(xp[v] + 2 * (i + stride));
     }
 #pragma unroll
-    for (int v = 0; v < G; ++v) {
-      if (v0 + v < a.nvec) {
+    for (int v = 0; v < NV; ++v) {
+      x0[v].x *= xs[v];
+      x0[v].y *= xs[v];
+      x1[v].x *= xs[v];
+      x1[v].y *= xs[v];
+    }
+    coeff_visit<R, NV>(s, m0, x0);
+    coeff_visit<R, NV>(s, m1, x1);
+  }
+  if (i < n2) {
+    const unsigned m0 = mask2[i];
+    double2 x0[NV];
 #pragma unroll
-        for (int l = 0; l < R; ++l) {
-          const double t = block_sum(s[v][l], wsum);
-          if (threadIdx.x == 0) a.partial[size_t(blockIdx.x) * a.nvec * R + (v0 + v) * R + l] = t;
-        }
-      }
+    for (int v = 0; v < NV; ++v) {
+      x0[v] = ld2nt(xp[v] + 2 * i);
+      x0[v].x *= xs[v];
+      x0[v].y *= xs[v];
+    }
+    coeff_visit<R, NV>(s, m0, x0);
+  }
+  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const unsigned mm = a.mask[a.n - 1];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int l = 0; l < R; ++l) s[v][l] += flip(mm, l, xp[v][a.n - 1] * xs[v]);
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+#pragma unroll
+    for (int l = 0; l < R; ++l) {
+      const double t = block_sum(s[v][l], wsum);
+      if (threadIdx.x == 0) a.partial[size_t(blockIdx.x) * a.nvec * R + (v0 + v) * R + l] = t;
     }
   }
 }
@@ -225,7 +255,7 @@ __device__ __forceinline__ double add_mul(double y, double c, double d) {
 }
 
 template <int R>
-__device__ __forceinline__ double lowrank(unsigned mm, const double* c) {
+__device__ __forceinline__ double lowrank(unsigned mm, const double (&c)[R]) {
   double s = 0;
 #pragma unroll
   for (int l = 0; l < R; ++l) s += flip(mm, l, c[l]);
@@ -234,49 +264,92 @@ __device__ __forceinline__ double lowrank(unsigned mm, const double* c) {
 
 // y_v = d x_v + rho sum_l u_l coeff[v][l]   (ADD = false)
 // y_v += rho sum_l u_l coeff[v][l]          (ADD = true, the P-space low-rank term)
-template <int R, bool ADD>
-__global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a) {
+// for the NV vectors v0 .. v0+NV-1, coefficients in registers.  The next visit's mask and operands
+// are loaded before this visit's stores are issued: vector-memory operations retire in order on
+// gfx9, so a load issued after a store cannot be waited for without waiting for the store.
+// EX: the reference's arithmetic (short vectors, kernels_exact.hip): products rounded alone.
+template <int R, bool ADD, int NV, bool EX>
+__global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a, int v0) {
   const size_t stride = size_t(gridDim.x) * kBlock, n2 = a.n >> 1;
   const unsigned* mask2 = reinterpret_cast<const unsigned*>(a.mask);
-  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += stride) {
-    const unsigned mm = mask2[i];
-    const size_t g = a.offset + 2 * i;
-    const double d0 = synth_d(a.diag_kind, g), d1 = synth_d(a.diag_kind, g + 1);
-    for (int v = 0; v < a.nvec; ++v) {
-      const double s0 = lowrank<R>(mm, a.coeff + v * R), s1 = lowrank<R>(mm >> 16, a.coeff + v * R);
-      double2 out;
-      if (ADD) {
-        const double2 y = *reinterpret_cast<const double2*>(a.y[v] + 2 * i);
-        out = a.exact ? make_double2(add_mul(y.x, a.rho, s0), add_mul(y.y, a.rho, s1))
-                      : make_double2(fma(a.rho, s0, y.x), fma(a.rho, s1, y.y));
-      } else {
-        const double2 x = ld2nt(a.x[v] + 2 * i);
-        out = a.exact ? make_double2(mul_add_mul(d0, x.x * a.xs[v], a.rho, s0), mul_add_mul(d1, x.y * a.xs[v], a.rho, s1))
-                      : make_double2(fma(d0, x.x * a.xs[v], a.rho * s0), fma(d1, x.y * a.xs[v], a.rho * s1));
+  double c[NV][R];
+  const double* xp[NV];
+  double* yp[NV];
+  double xs[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+#pragma unroll
+    for (int l = 0; l < R; ++l) c[v][l] = a.coeff[(v0 + v) * R + l];
+    xp[v] = ADD ? a.y[v0 + v] : a.x[v0 + v];
+    yp[v] = a.y[v0 + v];
+    xs[v] = ADD ? 1.0 : a.xs[v0 + v];
+  }
+  size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n2) {
+    unsigned mm = mask2[i];
+    double2 in[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) in[v] = ld2nt(xp[v] + 2 * i);
+    for (; i < n2; i += stride) {
+      const size_t ip = i + stride < n2 ? i + stride : i;  // the next visit (or this one again)
+      const unsigned mnext = mask2[ip];
+      double2 nxt[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) nxt[v] = ld2nt(xp[v] + 2 * ip);
+      const size_t g = a.offset + 2 * i;
+      const double d0 = synth_d(a.diag_kind, g), d1 = synth_d(a.diag_kind, g + 1);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const double s0 = lowrank<R>(mm, c[v]), s1 = lowrank<R>(mm >> 16, c[v]);
+        double2 out;
+        if (ADD) {
+          const double2 y = in[v];
+          out = EX ? make_double2(add_mul(y.x, a.rho, s0), add_mul(y.y, a.rho, s1))
+                   : make_double2(fma(a.rho, s0, y.x), fma(a.rho, s1, y.y));
+        } else {
+          const double2 x = in[v];
+          out = EX ? make_double2(mul_add_mul(d0, x.x * xs[v], a.rho, s0), mul_add_mul(d1, x.y * xs[v], a.rho, s1))
+                   : make_double2(fma(d0, x.x * xs[v], a.rho * s0), fma(d1, x.y * xs[v], a.rho * s1));
+        }
+        ssp::st2nt(yp[v] + 2 * i, out);
       }
-      ssp::st2nt(a.y[v] + 2 * i, out);
+      mm = mnext;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) in[v] = nxt[v];
     }
   }
   if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
     const size_t e = a.n - 1;
     const unsigned mm = a.mask[e];
     const double d = synth_d(a.diag_kind, a.offset + e);
-    for (int v = 0; v < a.nvec; ++v) {
-      const double s = lowrank<R>(mm, a.coeff + v * R);
-      if (a.exact)
-        a.y[v][e] = ADD ? add_mul(a.y[v][e], a.rho, s) : mul_add_mul(d, a.x[v][e] * a.xs[v], a.rho, s);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const double s = lowrank<R>(mm, c[v]);
+      if (EX)
+        yp[v][e] = ADD ? add_mul(yp[v][e], a.rho, s) : mul_add_mul(d, xp[v][e] * xs[v], a.rho, s);
       else
-        a.y[v][e] = ADD ? fma(a.rho, s, a.y[v][e]) : fma(d, a.x[v][e] * a.xs[v], a.rho * s);
+        yp[v][e] = ADD ? fma(a.rho, s, yp[v][e]) : fma(d, xp[v][e] * xs[v], a.rho * s);
     }
   }
 }
 
+// Vectors in groups of NV = 4 (2 from rank 9 on, where R x NV accumulators would crowd the
+// registers), one launch per group; the last group's NV is the remainder.
+template <int R>
+constexpr int coeff_group() {
+  return R > 8 ? 2 : 4;
+}
+
 template <int R>
 void launch_coeff(unsigned grid, hipStream_t st, const SynthArgs& a) {
-  if (a.nvec <= 2 || R > 8)
-    hipLaunchKernelGGL((k_synth_coeff<R, 2>), dim3(grid), dim3(kBlock), 0, st, a);
-  else
-    hipLaunchKernelGGL((k_synth_coeff<R, 4>), dim3(grid), dim3(kBlock), 0, st, a);
+  constexpr int G = coeff_group<R>();
+  for (int v0 = 0; v0 < a.nvec; v0 += G) {
+    const int nv = std::min(G, a.nvec - v0);
+    if (nv == 4) hipLaunchKernelGGL((k_synth_coeff<R, (G >= 4 ? 4 : 1)>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    else if (nv == 3) hipLaunchKernelGGL((k_synth_coeff<R, (G >= 4 ? 3 : 1)>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    else if (nv == 2) hipLaunchKernelGGL((k_synth_coeff<R, 2>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    else hipLaunchKernelGGL((k_synth_coeff<R, 1>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+  }
 }
 
 #define SSP_RANK_CASES(F) \
@@ -304,12 +377,30 @@ void synth_coeff_exact(hipStream_t st, const SynthArgs& a, double* out) {
   }
 }
 
+template <int R, bool ADD, bool EX>
+void launch_apply_ex(unsigned grid, hipStream_t st, const SynthArgs& a) {
+  constexpr int G = coeff_group<R>();
+  for (int v0 = 0; v0 < a.nvec; v0 += G) {
+    const int nv = std::min(G, a.nvec - v0);
+    if (nv == 4) hipLaunchKernelGGL((k_synth_apply<R, ADD, (G >= 4 ? 4 : 1), EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    else if (nv == 3) hipLaunchKernelGGL((k_synth_apply<R, ADD, (G >= 4 ? 3 : 1), EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    else if (nv == 2) hipLaunchKernelGGL((k_synth_apply<R, ADD, 2, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    else hipLaunchKernelGGL((k_synth_apply<R, ADD, 1, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+  }
+}
+
+template <int R, bool ADD>
+void launch_apply(unsigned grid, hipStream_t st, const SynthArgs& a) {
+  if (a.exact) launch_apply_ex<R, ADD, true>(grid, st, a);
+  else launch_apply_ex<R, ADD, false>(grid, st, a);
+}
+
 template <bool ADD>
 void synth_apply(unsigned grid, hipStream_t st, const SynthArgs& a) {
   switch (a.rank) {
-#define F(r)                                                                       \
-  case r:                                                                          \
-    hipLaunchKernelGGL((k_synth_apply<r, ADD>), dim3(grid), dim3(kBlock), 0, st, a); \
+#define F(r)                            \
+  case r:                               \
+    launch_apply<r, ADD>(grid, st, a); \
     break;
     SSP_RANK_CASES(F)
 #undef F

@@ -458,7 +458,7 @@ class Context:
 
     def set_exact_max(self, n: int):
         """Vectors of at most n local elements use the reference's arithmetic bit for bit: sequential
-        dots, no fused multiply-adds (ssp_ctx_set_exact_max; default 16384, 0 = off)."""
+        dots, no fused multiply-adds (ssp_ctx_set_exact_max; default 2048, 0 = off)."""
         _check(self.lib.ssp_ctx_set_exact_max(self.handle, int(n)))
 
     def debug_stall(self, ms: float):

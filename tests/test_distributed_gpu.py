@@ -99,8 +99,9 @@ def test_c5_full_size_on_8_shards_p2p():
 @pytest.mark.parametrize("transport", ["host", "p2p"])
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_sharded_short_solves_are_the_reference_mpi_build(world, transport):
+    # C1's shards (N = 1e4 over P ranks) and S_p8's exceed the 2048-element default on 2 ranks
     out = run_hub("gpu_exact_mpi", world=world, timeout=600, transport=transport,
-                  env_extra={"SSP_COMM_TIMEOUT_S": "60"})[0]
+                  env_extra={"SSP_COMM_TIMEOUT_S": "60", "SSP_EXACT_MAX": "16384"})[0]
     print(out)
 
 

@@ -1,5 +1,5 @@
-"""The reference's own arithmetic on short vectors (ssp_ctx_set_exact_max, kernels_exact.hip): at most
-16384 local elements by default, every dot a sequential sum in index order and every y = alpha x + y
+"""The reference's own arithmetic on short vectors (ssp_ctx_set_exact_max, kernels_exact.hip; 2048 local
+elements by default, raised to 16384 here): every dot a sequential sum in index order and every y = alpha x + y
 rounded twice, so each entry point is the oracle's restated loop (ArrayHandlerIterable.h:65-82,
 util/gemm.h:257-279) BIT FOR BIT, and a whole solve on the reference's own test problems -- with the
 reference's sequential MGS, which the HBM handlers keep below fused_min_size() -- is the reference
@@ -29,7 +29,7 @@ def same(a, b):
 def exact(ctx):
     ctx.set_exact_max(16384)
     yield ctx
-    ctx.set_exact_max(16384)
+    ctx.set_exact_max(2048)  # the default (include/subspace_hip.h)
 
 
 @pytest.mark.parametrize("n", SIZES)

@@ -15,6 +15,7 @@ import oracle
 pytestmark = pytest.mark.gpu
 EPS = np.finfo(np.float64).eps
 SIZES = [0, 1, 2, 7, 64, 1003, 100_003, (1 << 20) + 5]
+EXACT_MAX_DEFAULT = 2048  # ssp_ctx_set_exact_max default (include/subspace_hip.h)
 
 
 @pytest.fixture(autouse=True)
@@ -23,7 +24,7 @@ def bandwidth_kernels(ctx):
     every size: the reference-arithmetic path for short vectors is off here (tests/test_exact_gpu.py)."""
     ctx.set_exact_max(0)
     yield
-    ctx.set_exact_max(16384)
+    ctx.set_exact_max(EXACT_MAX_DEFAULT)
 
 
 def rng(seed=1):

@@ -16,6 +16,7 @@ import itsolv_hbm as ih
 import subspace_hip as sh
 
 pytestmark = pytest.mark.gpu
+EXACT_MAX_DEFAULT = 2048  # ssp_ctx_set_exact_max default (include/subspace_hip.h)
 
 
 @pytest.fixture(autouse=True)
@@ -24,7 +25,7 @@ def bandwidth_kernels(ctx):
     every size: the reference-arithmetic path for short vectors is off here (tests/test_exact_gpu.py)."""
     ctx.set_exact_max(0)
     yield
-    ctx.set_exact_max(16384)
+    ctx.set_exact_max(EXACT_MAX_DEFAULT)
 
 
 N_SMALL = 100_003

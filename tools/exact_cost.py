@@ -65,7 +65,7 @@ def main():
             row[mode] = {"wall_ms": 1e3 * (time.perf_counter() - t0), "iterations": g["iterations"]}
         out["solves"][name] = row
         print(name, json.dumps(row), flush=True)
-    ctx.set_exact_max(16384)
+    ctx.set_exact_max(2048)
     ctx.close()
     if a.out:
         json.dump(out, open(a.out, "w"), indent=1)
