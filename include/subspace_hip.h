@@ -229,7 +229,7 @@ int ssp_sparse_copy(ssp_ctx* ctx, double* x, size_t n, size_t offset, const size
 int ssp_sparse_axpy(ssp_ctx* ctx, double alpha, const size_t* idx, const double* val, size_t nnz, double* x,
                     size_t n, size_t offset);
 /* xx[k][idx-offset] += val over the entries [ptr[k], ptr[k+1]) of each of nvec sparse vectors (one
- * ssp_sparse_axpy(1.0) per vector, in one launch when the entries fit the argument block). */
+ * ssp_sparse_axpy(1.0) per vector, in one launch for up to 16 vectors and 256 local entries). */
 int ssp_sparse_axpy_batch(ssp_ctx* ctx, int nvec, const size_t* ptr, const size_t* idx, const double* val,
                           double* const* xx, size_t n, size_t offset);
 /* *out = sum_ranks sum_e x[idx_e-offset] * val_e */

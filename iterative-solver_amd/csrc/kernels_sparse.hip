@@ -50,14 +50,17 @@ __global__ void k_scatter_inline(const ScatterInline a) {
     a.x[a.li[e]] = a.v[e];
 }
 
-// The same for up to 16 destinations at once (ssp_sparse_axpy_batch): entry e goes to x[dst[e]].
+// The same for up to 16 destinations at once (ssp_sparse_axpy_batch): entry e goes to x[dst[e]]; up to
+// 256 entries with 32-bit local indices (a P-space action's terms: 16 P vectors x 8 roots = 128).
+constexpr int kBatchEntries = 256;
 struct ScatterBatchInline {
   double* x[16];
   int nnz;
-  unsigned char dst[kInlineEntries];
-  unsigned long long li[kInlineEntries];
-  double v[kInlineEntries];
+  unsigned char dst[kBatchEntries];
+  unsigned li[kBatchEntries];
+  double v[kBatchEntries];
 };
+static_assert(sizeof(ScatterBatchInline) <= 4000, "kernel argument block too large");
 
 __global__ void k_scatter_batch_inline(const ScatterBatchInline a) {
   const int e = int(threadIdx.x);
@@ -308,14 +311,14 @@ int ssp_sparse_axpy_batch(ssp_ctx* ctx, int nvec, const size_t* ptr, const size_
     filter_local(idx + ptr[k], val + ptr[k], ptr[k + 1] - ptr[k], n, offset, li, lv);
     if (li.empty()) continue;
     if (!xx[k]) return ssp::set_error(SSP_ERR_ARG, "ssp_sparse_axpy_batch: null vector");
-    if (a.nnz + li.size() > size_t(kInlineEntries)) {
+    if (a.nnz + li.size() > size_t(kBatchEntries) || n > 0xffffffffull) {
       inl = false;
       break;
     }
     a.x[k] = xx[k];
     for (size_t e = 0; e < li.size(); ++e) {
       a.dst[a.nnz] = static_cast<unsigned char>(k);
-      a.li[a.nnz] = li[e];
+      a.li[a.nnz] = static_cast<unsigned>(li[e]);
       a.v[a.nnz++] = lv[e];
     }
   }
@@ -326,7 +329,7 @@ int ssp_sparse_axpy_batch(ssp_ctx* ctx, int nvec, const size_t* ptr, const size_
   }
   if (a.nnz == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "sparse_axpy", 24.0 * a.nnz);
-  hipLaunchKernelGGL(k_scatter_batch_inline, dim3(1), dim3(kInlineEntries), 0, ctx->stream, a);
+  hipLaunchKernelGGL(k_scatter_batch_inline, dim3(1), dim3(kBatchEntries), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }

@@ -426,9 +426,9 @@ def test_sparse_ops_with_shard_offset(ctx):
     assert np.array_equal(dx.numpy(), oracle.sparse_copy(n, li, lv))
 
 
-@pytest.mark.parametrize("nvec,per", [(1, 1), (8, 1), (8, 8), (16, 4), (5, 20), (17, 1)])
+@pytest.mark.parametrize("nvec,per", [(1, 1), (8, 1), (8, 16), (16, 16), (5, 60), (17, 1)])
 def test_sparse_axpy_batch_is_one_sparse_axpy_per_vector(ctx, nvec, per):
-    # one launch while the entries fit the argument block (<= 64, <= 16 vectors), else one per vector;
+    # one launch while the entries fit the argument block (<= 256, <= 16 vectors), else one per vector;
     # entries outside the shard are dropped as by ssp_sparse_axpy
     n, off = 1000, 3000
     r = rng(nvec * 100 + per)
