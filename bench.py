@@ -606,10 +606,15 @@ def main():
         wls.free()
         small = {"n_global": ns_global, "steps": s_steps, "ms_per_step": round(1e3 * t_s / s_steps, 4),
                  "GBs": round(step_bytes(ns_global, m, k) * s_steps / t_s / 1e9, 2)}
-    solve = solve_diis = gpu_c2 = None
+    solve = solve_diis = gpu_c2 = shard = None
     if not args.no_in_solver:
         solve = in_solver(ctx, n_global, world, barrier)
         solve_diis = in_solver(ctx, n_global, world, barrier, kind="diis")
+        if world == 1 and n_global >= 8:
+            # one rank's share of C4 (N / 8 elements, the same subspace work): the solve whose wall
+            # against its kernel time bounds the 8-GPU C4 solve
+            shard = in_solver(ctx, n_global // 8, world, barrier)
+            shard["config"] = "C4, one rank's share on one GPU: " + shard["config"].split(": ", 1)[1]
         if run_cpu:
             gpu_c2 = gpu_c2_solve(ctx, world, args.cpu_solve_n)
     if th is not None:
@@ -672,6 +677,7 @@ def main():
             "headline_step_at_n_div_10": small,
             "in_solver": solve,
             "in_solver_diis": solve_diis,
+            "in_solver_c4_shard": shard,
             "startup": {"ctx_create_s": round(ctx_create_s, 3),
                         "first_solve_wall_s": solve["wall_s_cold"] if solve else None,
                         "warm_solve_wall_s": solve["wall_s"] if solve else None},

@@ -108,6 +108,8 @@ def test_bench_single_gpu():
     assert d["sustained"]["steps"] >= 5 and d["sustained"]["GBs"] > 0
     s = d["in_solver_cpu"]
     assert s["cpu"]["converged"] and s["same_iterations"] and s["speedup"] > 0
+    c4 = d["in_solver_c4_shard"]  # one rank's share of C4 (N / 8)
+    assert c4["n_global"] == 500_000 and c4["converged"] and c4["config"].startswith("C4, one rank's share")
 
 
 @pytest.mark.gpu
