@@ -114,6 +114,10 @@ def test_diis_synthetic_rounding_sensitive_case(ctx):
     assert gpu["converged"] and cpu["converged"]
     np.testing.assert_allclose(gpu["x"], np.ones(n), atol=1e-8)
     np.testing.assert_allclose(gpu["x"], cpu["x"], atol=2e-8)
+    # At 1000 elements the GPU computes in the reference's own arithmetic by default (<= 2048,
+    # ssp_ctx_set_exact_max): it then takes the CPU path's 13 steps to the last bit.
+    assert gpu["iterations"] == cpu["iterations"] == 13
+    assert np.array_equal(gpu["x"], cpu["x"])
     # The first iterations agree to rounding.
     kw8 = dict(convergence_threshold=1e-12, max_size_qspace=6, max_iter=5)
     g8, c8 = ih.diis_synthetic(ctx, n, rho, rank, seed, **kw8), oracle.diis_synthetic(n, rho, rank, seed, **kw8)
