@@ -37,7 +37,7 @@ def main():
     ctx = sh.Context(0)
     r = np.random.default_rng(1)
     out = {"unit": "us per call (host wall, synchronised)", "ops": {}, "solves": {}}
-    for n in (1000, 4096, 16384):
+    for n in (1000, 2048, 4096, 16384):
         xs = [ctx.upload(r.uniform(-1, 1, n)) for _ in range(48)]
         ys = [ctx.upload(r.uniform(-1, 1, n)) for _ in range(8)]
         al = r.uniform(-1, 1, (48, 8))

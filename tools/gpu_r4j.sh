@@ -8,6 +8,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -n 3 "$OUT/$name.log"; if [ $rc -gt 1 ]; then return $rc; fi; return 0; }
 step tests 600 python -u -m pytest tests/test_ops_gpu.py tests/test_solver_gpu.py tests/test_traces_gpu.py -q -x --timeout 200 --timeout-method thread -rf -k "sparse or synthetic or davidson or trace" || exit $?
+step exact_cost 300 python -u tools/exact_cost.py --out "$OUT/exact_cost.json" || exit $?
 step transport_ab 600 python -u tools/transport_ab.py --config C4-shard --reps 5 --out "$OUT/transport_ab_c4shard.json" || exit $?
 step ledger 600 python -u tools/solver_ledger.py --configs C3,C4-shard --out "$OUT/solver_ledger.json" || exit $?
 rm -rf "$OUT/trace"
