@@ -825,7 +825,7 @@ constexpr int ng_max(int) { return 16; }
 unsigned inner_grid(const ssp_ctx* ctx, size_t n) {
   const size_t chunks = n / 32 + 1;
   const size_t blocks = (chunks + 3) / 4;
-  const size_t cap = size_t(ctx->num_cus) * 4;
+  const size_t cap = size_t(ctx->num_cus) * size_t(ctx->inner_per_cu);
   return unsigned(std::max<size_t>(1, std::min(blocks, cap)));
 }
 
