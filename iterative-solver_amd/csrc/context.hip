@@ -369,6 +369,7 @@ int ssp_ctx_create(int device, ssp_ctx** out) {
   if (const char* pc = std::getenv("SSP_PUBLISH")) ctx->publish_copy = std::string(pc) == "copy";
   if (const char* ex = std::getenv("SSP_EXACT_MAX")) ctx->exact_max = size_t(std::strtoull(ex, nullptr, 10));
   if (const char* ip = std::getenv("SSP_INNER_PER_CU")) ctx->inner_per_cu = std::max(1, std::atoi(ip));
+  if (const char* ss = std::getenv("SSP_SYNTH_SHAPE")) ctx->synth_stride = std::string(ss) == "stride";
   if (const char* ct = std::getenv("SSP_COMM_TIMEOUT_S")) {
     const double v = std::atof(ct);
     if (v > 0) ctx->comm_timeout_s = v;

@@ -33,7 +33,8 @@ struct ssp_ctx {
   std::vector<ssp_ledger_entry_t> ledger;
   std::vector<hipEvent_t> event_pool;
   int num_cus = 256;
-  int inner_per_cu = 4;  // gemm_inner workgroups per CU (SSP_INNER_PER_CU: the A/B knob of tools/ab_inner.py)
+  int inner_per_cu = 4;
+  bool synth_stride = false;  // SSP_SYNTH_SHAPE=stride: the synthetic apply kernel grid-strided (A/B)  // gemm_inner workgroups per CU (SSP_INNER_PER_CU: the A/B knob of tools/ab_inner.py)
   // Shape of the 1 x 1 / 1 x 2 gemm_inner row kernel: window (default) or, with SSP_ROW_SHAPE=stride
   // in the environment at context creation, the round-2 grid-stride shape (A/B: tools/row_shape_ab.py).
   bool row_stride = false;

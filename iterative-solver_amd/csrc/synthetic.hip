@@ -17,6 +17,7 @@ namespace {
 using ssp::kBlock;
 constexpr int kMaxVec = 16;
 constexpr int kMaxRank = 16;
+constexpr int kSynthU = 2;  // window of the apply kernel: kSynthU x 64 pairs of each vector per wave visit
 
 __host__ __device__ inline unsigned long long splitmix64(unsigned long long z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -264,12 +265,88 @@ __device__ __forceinline__ double lowrank(unsigned mm, const double (&c)[R]) {
 
 // y_v = d x_v + rho sum_l u_l coeff[v][l]   (ADD = false)
 // y_v += rho sum_l u_l coeff[v][l]          (ADD = true, the P-space low-rank term)
+// for the NV vectors v0 .. v0+NV-1, coefficients in registers, in the window shape of the streaming
+// kernels (ssp::for_windows: each wave owns U x 64 consecutive pairs of every vector per visit, all of
+// the visit's masks and operands loaded before its stores).  Element for element the same operations
+// as one pair at a time.
+// EX: the reference's arithmetic (short vectors, kernels_exact.hip): products rounded alone.
+template <int R, bool ADD, int NV, bool EX>
+__global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a, int v0) {
+  constexpr int U = kSynthU;
+  const unsigned* mask2 = reinterpret_cast<const unsigned*>(a.mask);
+  double c[NV][R];
+  const double* xp[NV];
+  double* yp[NV];
+  double xs[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+#pragma unroll
+    for (int l = 0; l < R; ++l) c[v][l] = a.coeff[(v0 + v) * R + l];
+    xp[v] = ADD ? a.y[v0 + v] : a.x[v0 + v];
+    yp[v] = a.y[v0 + v];
+    xs[v] = ADD ? 1.0 : a.xs[v0 + v];
+  }
+  // y at pair i from its mask and operands
+  auto pair = [&](size_t i, unsigned mm, const double2 (&in)[NV]) {
+    const size_t g = a.offset + 2 * i;
+    const double d0 = synth_d(a.diag_kind, g), d1 = synth_d(a.diag_kind, g + 1);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const double s0 = lowrank<R>(mm, c[v]), s1 = lowrank<R>(mm >> 16, c[v]);
+      double2 out;
+      if (ADD) {
+        const double2 y = in[v];
+        out = EX ? make_double2(add_mul(y.x, a.rho, s0), add_mul(y.y, a.rho, s1))
+                 : make_double2(fma(a.rho, s0, y.x), fma(a.rho, s1, y.y));
+      } else {
+        const double2 x = in[v];
+        out = EX ? make_double2(mul_add_mul(d0, x.x * xs[v], a.rho, s0), mul_add_mul(d1, x.y * xs[v], a.rho, s1))
+                 : make_double2(fma(d0, x.x * xs[v], a.rho * s0), fma(d1, x.y * xs[v], a.rho * s1));
+      }
+      ssp::st2nt(yp[v] + 2 * i, out);
+    }
+  };
+  ssp::for_windows<U>(
+      a.n,
+      [&](size_t p0) {
+        unsigned mm[U];
+        double2 in[U][NV];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          mm[u] = mask2[p0 + 64 * u];
+#pragma unroll
+          for (int v = 0; v < NV; ++v) in[u][v] = ld2nt(xp[v] + 2 * (p0 + 64 * u));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) pair(p0 + 64 * u, mm[u], in[u]);
+      },
+      [&](size_t i) {
+        double2 in[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) in[v] = ld2nt(xp[v] + 2 * i);
+        pair(i, mask2[i], in);
+      },
+      [&](size_t e) {
+        const unsigned mm = a.mask[e];
+        const double d = synth_d(a.diag_kind, a.offset + e);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const double s = lowrank<R>(mm, c[v]);
+          if (EX)
+            yp[v][e] = ADD ? add_mul(yp[v][e], a.rho, s) : mul_add_mul(d, xp[v][e] * xs[v], a.rho, s);
+          else
+            yp[v][e] = ADD ? fma(a.rho, s, yp[v][e]) : fma(d, xp[v][e] * xs[v], a.rho * s);
+        }
+      });
+}
+
+// The same, grid-strided one pair per lane and visit (SSP_SYNTH_SHAPE=stride, the A/B of the window shape).
 // for the NV vectors v0 .. v0+NV-1, coefficients in registers.  The next visit's mask and operands
 // are loaded before this visit's stores are issued: vector-memory operations retire in order on
 // gfx9, so a load issued after a store cannot be waited for without waiting for the store.
 // EX: the reference's arithmetic (short vectors, kernels_exact.hip): products rounded alone.
 template <int R, bool ADD, int NV, bool EX>
-__global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a, int v0) {
+__global__ __launch_bounds__(kBlock) void k_synth_apply_pipe(const SynthArgs a, int v0) {
   const size_t stride = size_t(gridDim.x) * kBlock, n2 = a.n >> 1;
   const unsigned* mask2 = reinterpret_cast<const unsigned*>(a.mask);
   double c[NV][R];
@@ -377,30 +454,41 @@ void synth_coeff_exact(hipStream_t st, const SynthArgs& a, double* out) {
   }
 }
 
-template <int R, bool ADD, bool EX>
-void launch_apply_ex(unsigned grid, hipStream_t st, const SynthArgs& a) {
+template <int R, bool ADD, bool EX, bool WIN>
+void launch_apply_ex(const ssp_ctx* ctx, hipStream_t st, const SynthArgs& a) {
   constexpr int G = coeff_group<R>();
+  const unsigned grid = WIN ? ssp::win_grid(ctx, a.n, kSynthU, 16) : ssp::stream_grid(ctx, a.n, 1);
   for (int v0 = 0; v0 < a.nvec; v0 += G) {
     const int nv = std::min(G, a.nvec - v0);
-    if (nv == 4) hipLaunchKernelGGL((k_synth_apply<R, ADD, (G >= 4 ? 4 : 1), EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
-    else if (nv == 3) hipLaunchKernelGGL((k_synth_apply<R, ADD, (G >= 4 ? 3 : 1), EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
-    else if (nv == 2) hipLaunchKernelGGL((k_synth_apply<R, ADD, 2, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
-    else hipLaunchKernelGGL((k_synth_apply<R, ADD, 1, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+#define SSP_APPLY(NV)                                                                                   \
+  if (WIN) hipLaunchKernelGGL((k_synth_apply<R, ADD, NV, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0); \
+  else hipLaunchKernelGGL((k_synth_apply_pipe<R, ADD, NV, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    if (nv == 4) { SSP_APPLY((G >= 4 ? 4 : 1)) }
+    else if (nv == 3) { SSP_APPLY((G >= 4 ? 3 : 1)) }
+    else if (nv == 2) { SSP_APPLY(2) }
+    else { SSP_APPLY(1) }
+#undef SSP_APPLY
   }
 }
 
+// Shape (tools/gpu_r4n.sh, profiles/r4/synth_shape_ab/): the window shape moves the P-space low-rank
+// update (ADD) at every size measured (C3's 1e8: 18.6-18.8 against 19.9-22.3 ms per solve; C4's shard:
+// 2.26 against 2.34-2.59 ms) and the action from 2^24 elements (C3: 24.9 against 25.4-28.2 ms), while
+// at C4's shard the action's grid-strided pipelined form is ahead (3.33-3.40 against 3.61 ms: the
+// window kernel holds 256 registers per lane).  SSP_SYNTH_SHAPE=stride forces the strided form.
 template <int R, bool ADD>
-void launch_apply(unsigned grid, hipStream_t st, const SynthArgs& a) {
-  if (a.exact) launch_apply_ex<R, ADD, true>(grid, st, a);
-  else launch_apply_ex<R, ADD, false>(grid, st, a);
+void launch_apply(const ssp_ctx* ctx, hipStream_t st, const SynthArgs& a) {
+  const bool win = !ctx->synth_stride && (ADD || a.n >= (size_t(1) << 24));
+  if (a.exact) win ? launch_apply_ex<R, ADD, true, true>(ctx, st, a) : launch_apply_ex<R, ADD, true, false>(ctx, st, a);
+  else win ? launch_apply_ex<R, ADD, false, true>(ctx, st, a) : launch_apply_ex<R, ADD, false, false>(ctx, st, a);
 }
 
 template <bool ADD>
-void synth_apply(unsigned grid, hipStream_t st, const SynthArgs& a) {
+void synth_apply(const ssp_ctx* ctx, hipStream_t st, const SynthArgs& a) {
   switch (a.rank) {
-#define F(r)                            \
-  case r:                               \
-    launch_apply<r, ADD>(grid, st, a); \
+#define F(r)                           \
+  case r:                              \
+    launch_apply<r, ADD>(ctx, st, a); \
     break;
     SSP_RANK_CASES(F)
 #undef F
@@ -555,7 +643,7 @@ int sspx_synth_action_scaled(ssp_ctx* ctx, const sspx_synth* spec, const double*
     // reduction that rewrites it is queued after the apply kernel on the same stream.
     a.coeff = ctx->result_dev;
     if (n > 0) {
-      synth_apply<false>(ssp::stream_grid(ctx, n, 1), ctx->stream, a);
+      synth_apply<false>(ctx, ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
     }
   }
@@ -588,7 +676,7 @@ int sspx_synth_add_lowrank(ssp_ctx* ctx, const sspx_synth* spec, double* const* 
     a.coeff = static_cast<const double*>(coeff);
     a.exact = ssp::exact_mode(ctx, n) ? 1 : 0;
     SSP_TRY(ssp::flush_uploads(ctx));
-    synth_apply<true>(ssp::stream_grid(ctx, n, 1), ctx->stream, a);
+    synth_apply<true>(ctx, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
   return SSP_OK;
