@@ -242,3 +242,27 @@ def test_c1_traces_are_the_committed_reference_trace(exact, name):
     assert same(g["eigenvalues"], ref["eigenvalues"]) and same(g["errors"], ref["errors"])
     for key in ("eigenvalues", "errors", "nq", "nwork"):
         assert np.array_equal(np.asarray(g["trace"][key]), np.asarray(ref["trace"][key])), key
+
+
+@pytest.mark.parametrize("n", [7, 1003])
+def test_block_update_is_the_reference_sequence(exact, n):
+    # yy[j] = ys[j] yy[j] (the eager scal), then the sparse gemm_outer over P, then the dense gemm_outer
+    # over the scaled sources: bit for bit (the block Gram-Schmidt update's arithmetic on short vectors)
+    ctx = exact
+    r = np.random.default_rng(n + 1)
+    k, m = 3, 4
+    xs = [r.uniform(-1, 1, n) for _ in range(k)]
+    ys = [r.uniform(-1, 1, n) for _ in range(m)]
+    ps = [{0: 1.0}, {n - 1: -0.5, 2 % n: 0.25}]
+    pa, al = r.uniform(-1, 1, (len(ps), m)), r.uniform(-1, 1, (k, m))
+    sx, sy = r.uniform(0.5, 2, k), r.uniform(0.5, 2, m)
+    dx, dy = [ctx.upload(v) for v in xs], [ctx.upload(v) for v in ys]
+    ctx.block_update(pa, ps, al, dx, sx, dy, sy)
+    want = [oracle.scal(sy[j], ys[j]) for j in range(m)]
+    for i, p in enumerate(ps):
+        idx, val = np.array(list(p.keys()), dtype=np.uint64), np.array(list(p.values()))
+        for j in range(m):
+            want[j] = oracle.sparse_axpy(pa[i, j], idx, val, want[j])
+    want = oracle.gemm_outer(al, [oracle.scal(s, v) for s, v in zip(sx, xs)], want)
+    for v, w in zip(dy, want):
+        assert same(v.numpy(), w)
