@@ -39,6 +39,11 @@ def main():
     for m, k in ((8, 48), (8, 1), (1, 6), (1, 48), (4, 24), (16, 64), (48, 8), (1, 1), (1, 2), (2, 2), (1, 3)):
         cases.append((f"gemm_inner {m}x{k}", "gemm_inner",
                       lambda m=m, k=k: ctx.gemm_inner(pool[:m], pool[m:m + k])))
+    # the same 8 x 48 panel on other vector sets: rows from the last-allocated vectors, and rows and
+    # columns exchanged (role against placement)
+    cases.append(("gemm_inner 8x48 rows=pool[48:56]", "gemm_inner", lambda: ctx.gemm_inner(pool[48:56], pool[0:48])))
+    cases.append(("gemm_inner 8x48 rows=pool[8:16]", "gemm_inner", lambda: ctx.gemm_inner(pool[8:16], pool[16:64])))
+    cases.append(("gemm_inner 8x48 rows=pool[0:8] again", "gemm_inner", lambda: ctx.gemm_inner(pool[:8], pool[8:56])))
     for k, m in ((48, 8), (1, 8), (6, 1), (8, 8), (24, 4), (64, 16)):
         al = rng.uniform(-0.1, 0.1, (k, m))
         cases.append((f"gemm_outer {k}->{m}", "gemm_outer",
