@@ -6,7 +6,8 @@ CPU: the reference CPU path (oracle.RcSolver: the restated solvers over the CPU 
 GPU: the same loops through the C API on the HIP handlers (iterative_solver package) take the
      same steps as the CPU path -- identical per-iteration return values and iteration counts,
      parameters within 1e-10 (1e-6 mid-trajectory on Rosenbrock) -- and satisfy the same
-     assertions.
+     assertions.  At these sizes the HIP path computes in the reference's arithmetic by default
+     (ssp_ctx_set_exact_max), and the *_bit_for_bit tests hold every loop to the CPU path exactly.
 """
 import numpy as np
 import pytest
@@ -511,3 +512,55 @@ def test_rspt_dense_2000_gpu():
         np.testing.assert_allclose(a[-1], b[-1], rtol=0, atol=1e-12 * max(1e-300, np.max(np.abs(b[-1]))))
     np.testing.assert_allclose(rspt_series(trace, h, h0), rspt_series(ref, h, h0), rtol=1e-14, atol=0)
     g.finalize()
+
+
+# ---- the reference's arithmetic: every reverse-communication loop bit for bit ------------------------
+# These problems have at most 1000 elements, where the HIP path computes as the reference's loops do by
+# default (sequential sums, no fused multiply-adds; ssp_ctx_set_exact_max): the GPU then
+# takes the CPU path's steps with bit-identical parameters and values in every case -- including the
+# cases above whose steps the CPU path itself changes under a 2^-50 perturbation, and n_eigen.
+@pytest.mark.gpu
+@pytest.mark.parametrize("family", list(EIGEN_FAMILIES))
+def test_eigen_gpu_is_the_cpu_path_bit_for_bit(family):
+    import iterative_solver
+
+    for h in EIGEN_FAMILIES[family]():
+        hermitian = bool(np.linalg.norm(h - h.T) < 1e-10)
+        for nroot, np_ in rp.eigen_cases(h.shape[0], hermitian):
+            tag = f"{family} n={h.shape[0]} nroot={nroot} np={np_}"
+            c, ctrace, _, _ = run_eigen(cpu_eigen, h, nroot, np_)
+            cst = c.stats()
+            g, gtrace, _, _ = run_eigen(gpu_eigen, h, nroot, np_)
+            st = iterative_solver.statistics()
+            assert gtrace == ctrace, tag
+            assert st["iterations"] == cst["iterations"], tag
+            assert np.array_equal(np.asarray(g.eigenvalues), np.asarray(cst["eigenvalues"])), tag
+            g.finalize()
+
+
+@pytest.mark.gpu
+def test_optimizer_and_diis_loops_gpu_are_the_cpu_path_bit_for_bit():
+    for n in (2, 11, 20, 29):
+        for alg in ("BFGS", "SD"):
+            h = rp.quadratic_matrix(n, 10.0)
+            ref = rp.loop_quadratic(cpu("Optimize", n, alg), h, optimize=True)
+            g = gpu("Optimize", n, alg)
+            same_trace(rp.loop_quadratic(g, h, optimize=True)[0], ref[0], xtol=0)
+            g.finalize()
+    for n in (2, 7, 20, 50):
+        h = rp.quadratic_matrix(n, 10.0)
+        ref = rp.loop_quadratic(cpu("NonLinearEquations", n), h, optimize=False)
+        g = gpu("NonLinearEquations", n)
+        same_trace(rp.loop_quadratic(g, h, optimize=False)[0], ref[0], xtol=0)
+        g.finalize()
+    for n in (2, 3, 4, 5, 6):  # Rosenbrock: above, 1e-6 mid-trajectory with the bandwidth kernels
+        ref, _ = rp.loop_rosenbrock(cpu("Optimize", n, "BFGS"), n)
+        g = gpu("Optimize", n, "BFGS")
+        same_trace(rp.loop_rosenbrock(g, n)[0], ref, xtol=0)
+        g.finalize()
+    opts = "convergence_threshold=1e-8,max_size_qspace=5"
+    for n in (1, 2):
+        ref, _ = rp.loop_trig(cpu("NonLinearEquations", n, options=opts), n)
+        g = gpu("NonLinearEquations", n, options=opts)
+        same_trace(rp.loop_trig(g, n)[0], ref, xtol=0)
+        g.finalize()
