@@ -242,6 +242,16 @@ def case_distr():
     comm.close()
 
 
+def case_api_record():
+    """tests/api_cases.py on the CPU path (the product's host code over the emulation, the reference's
+    arithmetic), written to argv[2] as JSON for tests/test_python_api_gpu.py to compare bit for bit."""
+    import json
+
+    import api_cases
+
+    json.dump(api_cases.run_all(iterative_solver), open(sys.argv[2], "w"))
+
+
 def case_exact_mpi():
     """The bit-for-bit check of the reference's MPI build that the GPU runs (dist_worker
     case_gpu_exact_mpi), through the product's host code over the emulation: sequential sums on each
@@ -257,5 +267,5 @@ def case_exact_mpi():
 
 if __name__ == "__main__":
     {"api": case_api, "spmd": case_spmd, "spmd-gloo": lambda: case_spmd(gloo=True), "c4": case_c4, "distr": case_distr,
-     "devsel": case_devsel, "rs_traces": case_rs_traces, "exact_mpi": case_exact_mpi}[sys.argv[1]]()
+     "devsel": case_devsel, "rs_traces": case_rs_traces, "exact_mpi": case_exact_mpi, "api_record": case_api_record}[sys.argv[1]]()
     print(f"{sys.argv[1]} OK", flush=True)

@@ -281,3 +281,25 @@ def test_solver_factory_dispatch():
     # C API method names through the SolverFactory restatement (reference SolverFactory.h:114-185):
     # unknown methods raise "Unimplemented method <m>"; Davidson/RSPT/DIIS/BFGS/SD construct
     check_factory_dispatch()
+
+
+def test_python_api_is_the_cpu_path_bit_for_bit(tmp_path):
+    """The reference's Python tests and the dense C-API loops (tests/api_cases.py) on the HIP path
+    against the CPU path -- the same host code over the host emulation of the device ABI, in a process
+    of its own (tests/emul_worker.py api_record) -- every eigenvalue, error, solution and residual
+    element and every iteration count bit for bit: at these sizes the HIP path computes in the
+    reference's arithmetic (ssp_ctx_set_exact_max)."""
+    import subprocess
+    import sys
+
+    import api_cases
+
+    out = tmp_path / "api_emul.json"
+    worker = os.path.join(os.path.dirname(__file__), "emul_worker.py")
+    subprocess.run([sys.executable, worker, "api_record", str(out)], check=True, timeout=600, capture_output=True)
+    cpu = json.load(open(out))
+    gpu = json.loads(json.dumps(api_cases.run_all(iterative_solver)))
+    assert gpu.keys() == cpu.keys()
+    for key in cpu:
+        for field, value in cpu[key].items():
+            assert np.array_equal(np.asarray(gpu[key][field]), np.asarray(value)), (key, field)
