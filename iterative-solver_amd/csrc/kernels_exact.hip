@@ -37,6 +37,7 @@ struct ExactInnerArgs {
   int pairs;               // 1: out[j] = <x_j, y_j> (m == k); 0: out[i * k + j] = <x_i, y_j>
   size_t n;
   double* out;             // device
+  ssp::FoldTail tail;      // tail.host: the last workgroup publishes every output to the host
 };
 
 // s + buf[0] + buf[1] + ... + buf[len-1], added in that order.  The chain of dependent adds is the
@@ -118,7 +119,33 @@ __global__ __launch_bounds__(kBlock) void k_exact_inner(const ExactInnerArgs a) 
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) a.out[o] = s;
+  if (!a.tail.host) {  // a communicator is attached: the results stay on the device for the exchange
+    if (threadIdx.x == 0) a.out[o] = s;
+    return;
+  }
+  // One rank: each workgroup hands its output over write-through (the hand-off of ssp::fold_tail,
+  // checked in the emitted assembly by tests/test_fold_tail_isa.py), and the last to arrive publishes
+  // all of them into coherent host memory, then the sequence flag -- no second kernel, no copy.
+  const int nout = a.pairs ? a.m : a.m * a.k;
+  unsigned* top = a.tail.counter + ssp::kFoldLine * ssp::kFoldShards;
+  __shared__ unsigned s_last;
+  if (threadIdx.x == 0) {
+    ssp::store_partial(a.out + o, s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == unsigned(nout) - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the loads are sc1
+  for (int q = int(threadIdx.x); q < nout; q += kBlock)
+    __hip_atomic_store(a.tail.host + q, __hip_atomic_load(a.out + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's results have reached host memory
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.tail.flag, a.tail.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 static_assert(sizeof(ExactInnerArgs) <= 4000, "kernel argument block too large");
@@ -173,7 +200,7 @@ namespace ssp {
 bool exact_mode(const ssp_ctx* ctx, size_t n) { return n > 0 && n <= ctx->exact_max; }
 
 int exact_inner(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, const double* const* yy,
-                const double* ys, int k, size_t n, bool pairs) {
+                const double* ys, int k, size_t n, bool pairs, const FoldTail& tail) {
   const int nout = pairs ? m : m * k;
   SSP_TRY(ensure_result(ctx, size_t(nout)));
   if (nout == 0) return SSP_OK;
@@ -199,6 +226,7 @@ int exact_inner(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, 
   a.pairs = pairs ? 1 : 0;
   a.n = n;
   a.out = ctx->result_dev;
+  a.tail = tail;
   SSP_TRY(flush_uploads(ctx));
   hipLaunchKernelGGL(k_exact_inner, dim3(unsigned(nout)), dim3(kBlock), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());

@@ -954,16 +954,17 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
   const bool sc = any_scaled(rs.data(), R) || any_scaled(cs.data(), C);
   const size_t total = size_t(R) * C;
   if (ssp::exact_mode(ctx, n)) {  // the reference's sequential dots, m x k in the caller's layout
-    SSP_TRY(ssp::comm_check(ctx));
+    ssp::FoldTail tail{};
+    SSP_TRY(ssp::fold_begin(ctx, int(total), &tail));
     {
       std::vector<const double*> distinct(xx, xx + m);
       distinct.insert(distinct.end(), yy, yy + k);
       std::sort(distinct.begin(), distinct.end());
       const double nvec = double(std::unique(distinct.begin(), distinct.end()) - distinct.begin());
       ssp::LedgerScope ls(ctx, "gemm_inner", 8.0 * n * nvec);
-      SSP_TRY(ssp::exact_inner(ctx, xx, xs, m, yy, ys, k, n, false));
+      SSP_TRY(ssp::exact_inner(ctx, xx, xs, m, yy, ys, k, n, false, tail));
     }
-    return ssp::reduce_fetch(ctx, out, total);
+    return ssp::fold_finish(ctx, tail, out);
   }
   SSP_TRY(ssp::ensure_result(ctx, total));
   ssp::FoldTail tail{};
@@ -1310,15 +1311,16 @@ int ssp_axpy_pairs_norm(ssp_ctx* ctx, const double* c, const double* const* xx, 
       if (yy[j] == xx[i] || (i < j && yy[i] == yy[j]))
         return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_pairs_norm: a destination aliases another operand");
   if (ssp::exact_mode(ctx, n)) {  // short vectors: the reference's arithmetic, one reduction
-    SSP_TRY(ssp::comm_check(ctx));
+    ssp::FoldTail tail{};
+    SSP_TRY(ssp::fold_begin(ctx, m, &tail));
     {
       ssp::LedgerScope ls(ctx, "axpy_pairs_norm", 24.0 * n * m);
       for (int j = 0; j < m; ++j)
         SSP_TRY(ssp::exact_outer(ctx, c + j, xx + j, xs ? xs + j : nullptr, 1, yy + j, ys ? ys + j : nullptr, 1, n, false));
       SSP_TRY(ssp::exact_inner(ctx, const_cast<const double* const*>(yy), nullptr, m,
-                               const_cast<const double* const*>(yy), nullptr, m, n, true));
+                               const_cast<const double* const*>(yy), nullptr, m, n, true, tail));
     }
-    return ssp::reduce_fetch(ctx, out, size_t(m));
+    return ssp::fold_finish(ctx, tail, out);
   }
   if (m > ssp::kOuterDst) {  // more than one launch: the unfused sequence, same values
     for (int j = 0; j < m; ++j)
@@ -1373,13 +1375,14 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
   for (int j = 0; j < m; ++j)
     if (yy[j] == x || yy[j] == z) return ssp::set_error(SSP_ERR_ARG, "ssp_axpy_inner: a destination aliases x or z");
   if (ssp::exact_mode(ctx, n)) {  // short vectors: the reference's arithmetic, one reduction
-    SSP_TRY(ssp::comm_check(ctx));
+    ssp::FoldTail tail{};
+    SSP_TRY(ssp::fold_begin(ctx, m, &tail));
     {
       ssp::LedgerScope ls(ctx, "axpy_inner", 8.0 * n * (2.0 + 2.0 * m));
       SSP_TRY(ssp::exact_outer(ctx, c, &x, nullptr, 1, yy, nullptr, m, n, false));
-      SSP_TRY(ssp::exact_inner(ctx, const_cast<const double* const*>(yy), nullptr, m, &z, nullptr, 1, n, false));
+      SSP_TRY(ssp::exact_inner(ctx, const_cast<const double* const*>(yy), nullptr, m, &z, nullptr, 1, n, false, tail));
     }
-    return ssp::reduce_fetch(ctx, out, size_t(m));
+    return ssp::fold_finish(ctx, tail, out);
   }
   SSP_TRY(ssp::ensure_result(ctx, size_t(m)));
   ssp::FoldTail tail{};

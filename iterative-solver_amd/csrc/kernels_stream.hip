@@ -393,12 +393,13 @@ int dot_impl(ssp_ctx* ctx, const double* x, double xs, const double* y, double y
     return ssp::reduce_fetch(ctx, out, 1);
   }
   if (ssp::exact_mode(ctx, n)) {
-    SSP_TRY(ssp::comm_check(ctx));
+    ssp::FoldTail tail{};
+    SSP_TRY(ssp::fold_begin(ctx, 1, &tail));
     {
       ssp::LedgerScope ls(ctx, "dot", (x == y && xs == ys ? 8.0 : 16.0) * n);
-      SSP_TRY(ssp::exact_inner(ctx, &x, &xs, 1, &y, &ys, 1, n, false));
+      SSP_TRY(ssp::exact_inner(ctx, &x, &xs, 1, &y, &ys, 1, n, false, tail));
     }
-    return ssp::reduce_fetch(ctx, out, 1);
+    return ssp::fold_finish(ctx, tail, out);
   }
   const unsigned grid = ssp::win_grid(ctx, n, kDotU, 8);
   SSP_TRY(ssp::ensure_partial(ctx, grid));

@@ -346,11 +346,13 @@ int p2p_allreduce_fetch(ssp_ctx* ctx, const double* src, double* out, size_t n);
 int p2p_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes);
 int p2p_detach(ssp_ctx* ctx);
 
-// kernels_exact.hip: the reference's arithmetic for short vectors.  exact_inner writes the m x k (or,
-// pairs, the m) dots into result_dev; exact_outer updates (set: writes) the destinations.
+// kernels_exact.hip: the reference's arithmetic for short vectors.  exact_inner forms the m x k (or,
+// pairs, the m) dots for the tail of fold_begin (in result_dev for an exchange, or published to the
+// host by the last workgroup; fold_finish delivers them); exact_outer updates (set: writes) the
+// destinations.
 bool exact_mode(const ssp_ctx* ctx, size_t n);
 int exact_inner(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, const double* const* yy,
-                const double* ys, int k, size_t n, bool pairs);
+                const double* ys, int k, size_t n, bool pairs, const FoldTail& tail);
 int exact_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, const double* xs, int k,
                 double* const* yy, const double* ys, int m, size_t n, bool set);
 
