@@ -92,12 +92,10 @@ struct SparseInnerInline {
   double v[kInlineEntries];
   double* out;
 };
-static_assert(sizeof(SparseInnerInline) <= 4000, "kernel argument block too large");
+static_assert(sizeof(SparseInnerInline) + sizeof(ssp::FoldTail) <= 4000, "kernel argument block too large");
 
 template <class A>
-__device__ __forceinline__ void sparse_inner_body(const A& a, const unsigned long long* li, const double* v) {
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= a.m * a.k) return;
+__device__ __forceinline__ double sparse_inner_value(const A& a, const unsigned long long* li, const double* v, int o) {
   const int i = o / a.k, j = o % a.k;
   double s = 0;
   const double xs = a.xs[i];
@@ -105,11 +103,45 @@ __device__ __forceinline__ void sparse_inner_body(const A& a, const unsigned lon
     const double xv = a.sc ? a.x[i][li[e]] * xs : a.x[i][li[e]];
     s += xv * v[e];
   }
-  a.out[o] = s;
+  return s;
 }
 
-__global__ void k_sparse_inner(const SparseInnerArgs a) { sparse_inner_body(a, a.li, a.v); }
-__global__ void k_sparse_inner_inline(const SparseInnerInline a) { sparse_inner_body(a, a.li, a.v); }
+__global__ void k_sparse_inner(const SparseInnerArgs a) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o < a.m * a.k) a.out[o] = sparse_inner_value(a, a.li, a.v, o);
+}
+
+// Inline entries; with tail.host (one launch, no communicator) the last workgroup to arrive also
+// publishes all m x k results to coherent host memory and sets the sequence flag -- the hand-off of
+// ssp::fold_tail (write-through stores, vmcnt(0) drain, agent-scope arrival, sc1 loads; checked in
+// the emitted assembly by tests/test_fold_tail_isa.py), so no publish kernel follows.
+__global__ void k_sparse_inner_inline(const SparseInnerInline a, const ssp::FoldTail tail) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nout = a.m * a.k;
+  if (!tail.host) {
+    if (o < nout) a.out[o] = sparse_inner_value(a, a.li, a.v, o);
+    return;
+  }
+  if (o < nout) ssp::store_partial(a.out + o, sparse_inner_value(a, a.li, a.v, o));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's result has completed
+  __syncthreads();
+  unsigned* top = tail.counter + ssp::kFoldLine * ssp::kFoldShards;
+  __shared__ unsigned s_last;
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the loads are sc1
+  for (int q = int(threadIdx.x); q < nout; q += int(blockDim.x))
+    __hip_atomic_store(tail.host + q, __hip_atomic_load(a.out + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's results have reached host memory
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(tail.flag, tail.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 
 // yy[j][li_e] += alpha(i,j) * v_e for sources i in order, then entries in order; one lane per
 // destination, so colliding indices accumulate in the reference's order.
@@ -356,9 +388,42 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const do
   const size_t total = size_t(m) * k;
   SSP_TRY(ssp::ensure_result(ctx, total));
   if (k <= 32 && li.size() <= size_t(kInlineEntries)) {
+    // One launch (m <= 64) publishes its results itself; more launches leave them for reduce_fetch.
+    const bool one = m <= 64;
+    ssp::FoldTail tail{};
+    if (one) SSP_TRY(ssp::fold_begin(ctx, int(total), &tail));
+    {
+      ssp::LedgerScope ls(ctx, "gemm_inner_sparse", 16.0 * li.size() * m);
+      for (int i0 = 0; i0 < m; i0 += 64) {
+        SparseInnerInline a{};
+        a.m = std::min(64, m - i0);
+        a.k = k;
+        for (int i = 0; i < a.m; ++i) {
+          a.x[i] = xx[i0 + i];
+          a.xs[i] = xs ? xs[i0 + i] : 1.0;
+          if (a.xs[i] != 1.0) a.sc = 1;
+        }
+        for (int j = 0; j <= k; ++j) a.ptr[j] = (unsigned short)lptr[size_t(j)];
+        for (size_t e = 0; e < li.size(); ++e) {
+          a.li[e] = li[e];
+          a.v[e] = lv[e];
+        }
+        a.out = ctx->result_dev + size_t(i0) * k;
+        const int outs = a.m * a.k;
+        hipLaunchKernelGGL(k_sparse_inner_inline, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a,
+                           tail);
+        SSP_TRY_HIP(hipGetLastError());
+      }
+    }
+    return one ? ssp::fold_finish(ctx, tail, out) : ssp::reduce_fetch(ctx, out, total);
+  }
+  unsigned long long *dptr, *dli;
+  double* dv;
+  SSP_TRY(upload_entries(ctx, lptr, li, lv, &dptr, &dli, &dv));
+  {
     ssp::LedgerScope ls(ctx, "gemm_inner_sparse", 16.0 * li.size() * m);
     for (int i0 = 0; i0 < m; i0 += 64) {
-      SparseInnerInline a{};
+      SparseInnerArgs a{};
       a.m = std::min(64, m - i0);
       a.k = k;
       for (int i = 0; i < a.m; ++i) {
@@ -366,39 +431,15 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const do
         a.xs[i] = xs ? xs[i0 + i] : 1.0;
         if (a.xs[i] != 1.0) a.sc = 1;
       }
-      for (int j = 0; j <= k; ++j) a.ptr[j] = (unsigned short)lptr[size_t(j)];
-      for (size_t e = 0; e < li.size(); ++e) {
-        a.li[e] = li[e];
-        a.v[e] = lv[e];
-      }
+      a.ptr = dptr;
+      a.li = dli;
+      a.v = dv;
       a.out = ctx->result_dev + size_t(i0) * k;
       const int outs = a.m * a.k;
-      hipLaunchKernelGGL(k_sparse_inner_inline, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a);
+      SSP_TRY(ssp::flush_uploads(ctx));
+      hipLaunchKernelGGL(k_sparse_inner, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
     }
-    return ssp::reduce_fetch(ctx, out, total);
-  }
-  unsigned long long *dptr, *dli;
-  double* dv;
-  SSP_TRY(upload_entries(ctx, lptr, li, lv, &dptr, &dli, &dv));
-  ssp::LedgerScope ls(ctx, "gemm_inner_sparse", 16.0 * li.size() * m);
-  for (int i0 = 0; i0 < m; i0 += 64) {
-    SparseInnerArgs a{};
-    a.m = std::min(64, m - i0);
-    a.k = k;
-    for (int i = 0; i < a.m; ++i) {
-      a.x[i] = xx[i0 + i];
-      a.xs[i] = xs ? xs[i0 + i] : 1.0;
-      if (a.xs[i] != 1.0) a.sc = 1;
-    }
-    a.ptr = dptr;
-    a.li = dli;
-    a.v = dv;
-    a.out = ctx->result_dev + size_t(i0) * k;
-    const int outs = a.m * a.k;
-    SSP_TRY(ssp::flush_uploads(ctx));
-    hipLaunchKernelGGL(k_sparse_inner, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a);
-    SSP_TRY_HIP(hipGetLastError());
   }
   return ssp::reduce_fetch(ctx, out, total);
 }

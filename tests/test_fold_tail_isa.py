@@ -126,7 +126,7 @@ def fold_tail_violations(ins):
 def test_fold_tail_handoff_is_write_through_in_the_isa():
     found, names = 0, []
     with tempfile.TemporaryDirectory() as d:
-        for src in ("kernels_stream.hip", "kernels_panel.hip", "kernels_exact.hip"):
+        for src in ("kernels_stream.hip", "kernels_panel.hip", "kernels_exact.hip", "kernels_sparse.hip"):
             out = os.path.join(d, src + ".s")
             r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
                                 "-I" + CSRC, "--cuda-device-only", "-S", os.path.join(CSRC, src), "-o", out],
@@ -140,9 +140,11 @@ def test_fold_tail_handoff_is_write_through_in_the_isa():
                 names.append(name)
                 assert not bad, (name, bad)
     # k_dot_partial<x==y / x!=y>, k_gemm_inner_row<1,2>, k_scal_inner / k_axpy_inner / k_axpy_norm x4,
-    # and the short-vector dot kernel's publish tail (kernels_exact.hip)
-    assert found >= 17, found
-    assert any("k_exact_inner" in nm for nm in names), names
+    # and the publish tails of the short-vector dot (kernels_exact.hip) and the inline sparse inner
+    # products (kernels_sparse.hip)
+    assert found >= 18, found
+    for kernel in ("k_exact_inner", "k_sparse_inner_inline"):
+        assert any(kernel in nm for nm in names), (kernel, names)
 
 
 
