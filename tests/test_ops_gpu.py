@@ -463,6 +463,24 @@ def test_sparse_gemm(ctx):
         np.testing.assert_allclose(dy[j].numpy(), e, rtol=2 * EPS, atol=0)
 
 
+@pytest.mark.parametrize("m,k,per", [(1, 1, 3), (8, 16, 2), (64, 32, 2), (65, 3, 4), (130, 2, 3), (5, 33, 1),
+                                     (6, 4, 40)])
+def test_sparse_gemm_inner_shapes(ctx, m, k, per):
+    # One launch with inline entries (m <= 64, k <= 32, <= 64 entries) publishes from its last
+    # workgroup -- one workgroup, or up to 8 (64 x 32 outputs); m > 64 takes several launches and
+    # k > 32 or more entries the staged form, both fetched by reduce_fetch.  Bit for bit, calls repeated
+    # so the arrival counter is seen reset between launches.
+    n = 2000
+    r = rng(m * 1000 + k * 10 + per)
+    xs = [r.uniform(-1, 1, n) for _ in range(m)]
+    ps = [{int(i): float(v) for i, v in zip(r.choice(n, per, replace=False), r.uniform(-1, 1, per))} for _ in range(k)]
+    dx = [ctx.upload(v) for v in xs]
+    # entries in index order, as the reference's std::map holds them (and the binding packs them)
+    ref = np.array([[oracle.sparse_dot(x, sorted(p), [p[i] for i in sorted(p)]) for p in ps] for x in xs])
+    for _ in range(3):
+        assert np.array_equal(ctx.gemm_inner_sparse(dx, ps), ref)
+
+
 @pytest.mark.parametrize("rank", [1, 4])
 def test_synthetic_action(ctx, rank):
     n, rho, seed = 10_007, 0.1, 99
