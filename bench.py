@@ -412,6 +412,43 @@ def in_solver(ctx, n_global, world, barrier, repeat=3, kind="davidson"):
     }
 
 
+def setup_context(args, world, rank, local_rank):
+    """This rank's context on its device, with the rank transport attached at N > 1.  Every wait on
+    the other ranks -- RCCL's join included (non-blocking init, polled; csrc/context.hip) -- is bounded
+    by SSP_COMM_TIMEOUT_S (120 s here unless set), so a rank that never arrives ends the run with an
+    error record (main) instead of a hang."""
+    ctx = sh.Context(local_rank % max(1, sh.device_count()))
+    if world > 1:
+        ctx.set_comm_timeout(float(os.environ.get("SSP_COMM_TIMEOUT_S", "120")))
+    if args.comm == "host":
+        if world > 1:
+            port = int(os.environ.get("MASTER_PORT", "29500")) + 1
+            ctx.attach_host_comm(sh.HubComm(rank, world, os.environ.get("MASTER_ADDR", "127.0.0.1"), port))
+        return ctx
+    # one GPU per rank; a launcher that narrows HIP_VISIBLE_DEVICES per rank leaves one visible
+    transport = "rccl"
+    if world > 1 and args.comm in ("p2p", "auto"):
+        uid, uid_path = rendezvous_uid(rank, world, kind="p2p")
+        try:
+            ctx.attach_p2p(world, rank, uid)  # collective, self-tested, the verdict agreed by all ranks
+            transport = "p2p"
+        except sh.SspError as e:
+            if args.comm == "p2p":
+                raise
+            log(f"rank {rank}: peer-memory transport unavailable ({e}); using RCCL")
+        if uid_path:  # attach returned on rank 0: every rank has read the id
+            os.remove(uid_path)
+    if world > 1 and transport == "rccl":
+        uid, uid_path = rendezvous_uid(rank, world, timeout=float(os.environ.get("SSP_COMM_TIMEOUT_S", "120")))
+        try:
+            ctx.attach_comm(world, rank, uid)  # collective: returns once every rank has joined, or fails
+        finally:
+            if uid_path:
+                os.remove(uid_path)
+    args.comm_used = transport
+    return ctx
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -449,32 +486,13 @@ def main():
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
     t_ctx = time.perf_counter()
-    if args.comm == "host":
-        ctx = sh.Context(local_rank % max(1, sh.device_count()))
-        if world > 1:
-            port = int(os.environ.get("MASTER_PORT", "29500")) + 1
-            ctx.attach_host_comm(sh.HubComm(rank, world, os.environ.get("MASTER_ADDR", "127.0.0.1"), port))
-    else:
-        # one GPU per rank; a launcher that narrows HIP_VISIBLE_DEVICES per rank leaves one visible
-        ctx = sh.Context(local_rank % max(1, sh.device_count()))
-        transport = "rccl"
-        if world > 1 and args.comm in ("p2p", "auto"):
-            uid, uid_path = rendezvous_uid(rank, world, kind="p2p")
-            try:
-                ctx.attach_p2p(world, rank, uid)  # collective, self-tested, the verdict agreed by all ranks
-                transport = "p2p"
-            except sh.SspError as e:
-                if args.comm == "p2p":
-                    raise
-                log(f"rank {rank}: peer-memory transport unavailable ({e}); using RCCL")
-            if uid_path:  # attach returned on rank 0: every rank has read the id
-                os.remove(uid_path)
-        if world > 1 and transport == "rccl":
-            uid, uid_path = rendezvous_uid(rank, world)
-            ctx.attach_comm(world, rank, uid)  # collective: returns once every rank has joined
-            if uid_path:
-                os.remove(uid_path)
-        args.comm_used = transport
+    try:
+        ctx = setup_context(args, world, rank, local_rank)
+    except Exception as e:  # noqa: BLE001 - a communicator that does not form ends the run with a record
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "higher_is_better": True, "rank": rank,
+                          "error": f"communicator setup failed on rank {rank}: {e}"}), flush=True)
+        sys.exit(3)
 
     ctx.synchronize()
     ctx_create_s = time.perf_counter() - t_ctx

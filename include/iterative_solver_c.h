@@ -13,11 +13,19 @@
  *  - the solver instances form a stack; only the top one is active (as in the reference).
  *
  * Differences:
- *  - `fcomm` (a Fortran MPI communicator) is ignored: ranks and the device are taken from the
- *    context set by IterativeSolverHbmSetContext (an ssp_ctx with an RCCL or host communicator
- *    attached), or a single-rank context is created on the device of the node-local rank the
- *    launcher exports (LOCAL_RANK, OMPI_COMM_WORLD_LOCAL_RANK, MPI_LOCALRANKID or SLURM_LOCALID,
- *    first one set, modulo the visible device count; device 0 without any of them).
+ *  - `fcomm` (a Fortran MPI communicator, reference IterativeSolverCMPI.cpp:169 MPI_Comm_f2c(fcomm))
+ *    is bridged at run time to the MPI library the calling process has loaded and initialised
+ *    (libitsolv_hbm.so does not link MPI; iterative-solver_amd/host/mpi_bridge.h).  With more than
+ *    one rank the instance's vectors are sharded over the communicator's ranks exactly as the
+ *    reference distributes them (make_distribution_spread_remainder, :79-105), each rank's shard in
+ *    the HBM of the device matching its place among the communicator's ranks on its node, and the
+ *    reductions / sync gathers run over the transport ITSOLV_HBM_COMM names: "mpi" (default:
+ *    MPI_Allreduce / MPI_Allgather on the communicator, the reference's own collectives), "p2p"
+ *    (peer-memory device exchange, one node) or "rccl" (RCCL over xGMI, one rank per device).
+ *    Precedence: a context set by IterativeSolverHbmSetContext; else fcomm when MPI is initialised in
+ *    the process and fcomm names a communicator; else a single-rank context on the device of the
+ *    node-local rank the launcher exports (LOCAL_RANK, OMPI_COMM_WORLD_LOCAL_RANK, MPI_LOCALRANKID or
+ *    SLURM_LOCALID, first one set, modulo the visible device count; device 0 without any of them).
  *  - Supported algorithms: LinearEigensystem and LinearEquations "Davidson" (or ""),
  *    NonLinearEquations "DIIS" (or ""), Optimize "BFGS" (or "") and "SD"; `minimize` is ignored,
  *    as in the reference (IterativeSolverCMPI.cpp:250-268).
@@ -86,9 +94,12 @@ int64_t mpicomm_self(void);
 int64_t mpicomm_global(void);
 int64_t IterativeSolver_mpicomm_global(void);
 int64_t IterativeSolver_mpicomm_self(void);
-/* IterativeSolverCMPI.cpp:516-534; size and rank of the context set by IterativeSolverHbmSetContext
- * (1 and 0 without one); init/finalize return 0.  The _mpi_size_/_mpi_rank_ spellings are the
- * names the reference's Fortran module binds (IterativeSolverF.F90:50-57). */
+/* IterativeSolverCMPI.cpp:481-534 through the caller's MPI library when it has one: the Fortran
+ * handles of MPI_COMM_WORLD / MPI_COMM_SELF (0 without MPI), the world's size and rank (without MPI:
+ * those of the context set by IterativeSolverHbmSetContext, else 1 and 0), MPI_Init when MPI is
+ * loaded but not initialised, and MPI_Finalize of an MPI initialised that way (0 otherwise).  The
+ * _mpi_size_/_mpi_rank_ spellings are the names the reference's Fortran module binds
+ * (IterativeSolverF.F90:50-57). */
 int64_t IterativeSolver_mpisize_global(void);
 int64_t IterativeSolver_mpirank_global(void);
 int64_t IterativeSolver_mpi_size_global(void);
@@ -113,6 +124,14 @@ uint64_t IterativeSolverHbmInstanceId(void);
  * is destroyed after a newer one was created must not pop the newer one, which
  * IterativeSolverFinalize would).  Returns 0, or 1 when no instance has that id. */
 int IterativeSolverHbmFinalizeInstance(uint64_t id);
+/* 1 when the process has an MPI library loaded and initialised (MPI_Init done, MPI_Finalize not),
+ * i.e. when the *Initialize calls bridge `fcomm`; 0 otherwise. */
+int IterativeSolverHbmMpiActive(void);
+/* Attaches `ctx` to the ranks of the Fortran MPI communicator `fcomm` over `transport` ("mpi", "p2p",
+ * "rccl"; NULL or "" -> ITSOLV_HBM_COMM, else "mpi") -- the attach the *Initialize calls perform for
+ * their own contexts, for callers that drive ssp contexts directly.  Collective over fcomm.  Returns
+ * 0, or 1 (IterativeSolverHbmLastError) in no-throw mode. */
+int IterativeSolverHbmMpiAttach(ssp_ctx* ctx, int64_t fcomm, const char* transport);
 /* Number of roots of the top instance (0 when there is none): the length of the arrays
  * IterativeSolverErrors / IterativeSolverEigenvalues fill (used by the Fortran module). */
 size_t IterativeSolverHbmNRoots(void);

@@ -94,11 +94,16 @@ int ssp_ctx_attach_p2p(ssp_ctx* ctx, int nranks, int rank, const char* id);
  * the reference's abort of the whole job on a distributed error (DistrArray.cpp:16-23). */
 int ssp_ctx_set_comm_timeout(ssp_ctx* ctx, double seconds);
 /* Vectors of at most n local elements (default 2048, or SSP_EXACT_MAX at context creation; 0 turns
- * it off) are computed in the reference's own arithmetic: every dot a sequential sum in index order
+ * it off; attaching a communicator gives every rank the smallest value among the ranks, and a later
+ * call must pass the same n on every rank) are computed in the reference's own arithmetic: every dot a sequential sum in index order
  * (std::inner_product, ArrayHandlerIterable.h:76-82) and every y = alpha x + y rounded twice (no fused
  * multiply-add, ArrayHandlerIterable.h:65-74), gemm_inner / gemm_outer pairwise in the reference's loop
  * order (util/gemm.h:257-279), fused entry points as their documented unfused sequence.  Results on
- * such vectors are the reference CPU path's bit for bit; longer vectors use the bandwidth kernels. */
+ * such vectors are the reference CPU path's bit for bit; longer vectors use the bandwidth kernels.
+ * Sharded, the choice is each rank's on its own shard length: when the global length puts the
+ * longer shards (make_distribution_spread_remainder lengths differ by one) just above n and the
+ * shorter ones at n, the ranks' partials come from both arithmetics -- in the same result layout,
+ * summed as always, every rank receiving the same sums -- and the bit-for-bit claim is then void. */
 int ssp_ctx_set_exact_max(ssp_ctx* ctx, size_t n);
 /* Shard of a global length n owned by `rank` of `nranks` (host only, no context):
  * make_distribution_spread_remainder, reference util/Distribution.h:99-109. */

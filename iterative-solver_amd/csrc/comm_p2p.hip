@@ -128,7 +128,7 @@ int sync_stream(ssp_ctx* ctx, const char* what) {
   }
   SSP_TRY(comm_check(ctx));
   const hipError_t q = hipStreamQuery(ctx->stream);  // an idle stream: nothing to wait for
-  if (q == hipSuccess) return SSP_OK;
+  if (q == hipSuccess) return ctx->p2p ? device_exchange_error(ctx, what) : SSP_OK;
   if (q != hipErrorNotReady) return hip_error(q, what);
   // A stream write of the next sequence number into the coherent host flag, then the bounded host
   // poll of wait_flag (which also queries the stream every few hundred polls): as fast as the
@@ -136,7 +136,9 @@ int sync_stream(ssp_ctx* ctx, const char* what) {
   const unsigned long long seq = ++ctx->pub_seq;
   SSP_TRY_HIP(hipStreamWriteValue64(ctx->stream, ctx->pub_flag, seq, 0));
   bool seen = true;  // a drained stream without the flag visible is synchronised all the same
-  return wait_flag(ctx, seq, &seen, what);
+  SSP_TRY(wait_flag(ctx, seq, &seen, what));
+  // a peer-memory exchange queued before this point that gave up left NaN and its error word
+  return ctx->p2p ? device_exchange_error(ctx, what) : SSP_OK;
 }
 
 // ---- peer-memory transport ------------------------------------------------------------------
@@ -206,6 +208,15 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const P2PArgs a) {
   }
   __syncthreads();
   if (s_err) {
+    // No sum: the destination gets NaN, so that a consumer on the device cannot take this rank's
+    // partials alone for the result; the host finds the error word at its next wait on the stream.
+    const double nan = __builtin_nan("");
+    for (unsigned i = threadIdx.x; i < a.n; i += blockDim.x) {
+      if (a.host_dst)
+        __hip_atomic_store(a.host_dst + i, nan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else
+        a.dst[i] = nan;
+    }
     if (threadIdx.x == 0) __hip_atomic_store(a.err, s_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   } else {
     for (unsigned i = threadIdx.x; i < a.n; i += blockDim.x) {
@@ -248,7 +259,10 @@ P2PArgs p2p_args(ssp_ctx* ctx, const double* src, unsigned n) {
   return a;
 }
 
+}  // namespace
+
 int device_exchange_error(ssp_ctx* ctx, const char* what) {
+  if (!ctx->dev_err_host) return SSP_OK;
   const int e = __atomic_load_n(ctx->dev_err_host, __ATOMIC_ACQUIRE);
   if (!e) return SSP_OK;
   char t[64];
@@ -259,7 +273,6 @@ int device_exchange_error(ssp_ctx* ctx, const char* what) {
   return comm_fail(ctx, std::string(what) + ": rank " + std::to_string(e - 1000) + " did not arrive within " + t +
                             " s (SSP_COMM_TIMEOUT_S)");
 }
-}  // namespace
 
 int p2p_allreduce_dev(ssp_ctx* ctx, double* buf, size_t n) {
   SSP_TRY(comm_check(ctx));
@@ -491,7 +504,7 @@ int ssp_ctx_attach_p2p(ssp_ctx* ctx, int nranks, int rank, const char* id) {
   }
   if (!all) return fail(SSP_ERR_COMM, "self-test exchange failed on some rank (device path unusable)");
   SSP_TRY(ssp_ctx_set_comm_timeout(ctx, keep));
-  return SSP_OK;
+  return agree_exact_max(ctx);
 }
 
 }  // extern "C"

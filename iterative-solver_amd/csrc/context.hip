@@ -6,7 +6,10 @@
 // the compute stream.
 #include <immintrin.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -144,8 +147,33 @@ int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n) {
     return SSP_OK;
   }
   if (!ctx->comm) return SSP_OK;
-  ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream);
-  if (r != ncclSuccess) return set_error(SSP_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  return rccl_settle(ctx, ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream), "ncclAllReduce");
+}
+
+// Every rank of a new communicator takes the smallest exact_max among them (SSP_EXACT_MAX is read per
+// process), so that equal shard lengths choose the same arithmetic on every rank.
+int agree_exact_max(ssp_ctx* ctx) {
+  if (ctx->nranks <= 1) return SSP_OK;
+  const unsigned long long mine = ctx->exact_max;
+  std::vector<unsigned long long> all(size_t(ctx->nranks));
+  SSP_TRY(ssp_allgather_host(ctx, &mine, all.data(), sizeof(mine)));
+  ctx->exact_max = size_t(*std::min_element(all.begin(), all.end()));
+  return SSP_OK;
+}
+
+// The outcome of an RCCL call on the (non-blocking) communicator: ncclInProgress is waited out by
+// polling the communicator's state under the deadline; an error aborts the communicator.
+int rccl_settle(ssp_ctx* ctx, ncclResult_t r, const char* what) {
+  if (r == ncclSuccess) return SSP_OK;
+  if (r != ncclInProgress) return comm_fail(ctx, std::string(what) + ": " + ncclGetErrorString(r));
+  const double t0 = now_s();
+  ncclResult_t state = ncclInProgress;
+  while (ncclCommGetAsyncError(ctx->comm, &state) == ncclSuccess && state == ncclInProgress) {
+    if (now_s() - t0 > ctx->comm_timeout_s)
+      return comm_fail(ctx, std::string(what) + ": still in progress after SSP_COMM_TIMEOUT_S");
+    _mm_pause();
+  }
+  if (state != ncclSuccess) return comm_fail(ctx, std::string(what) + ": " + ncclGetErrorString(state));
   return SSP_OK;
 }
 
@@ -537,14 +565,46 @@ int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id) {
   ctx->comm_fail_msg.clear();
   // A one-rank communicator is created too: its collectives run through RCCL like any other, which
   // is how the RCCL calls are exercised on a one-GPU machine (tests/test_rccl_gpu.py).
+  //
+  // Non-blocking initialisation (config.blocking = 0), polled under the communication deadline: a rank
+  // that never joins ends the join of the others with SSP_ERR_COMM after ctx->comm_timeout_s
+  // (SSP_COMM_TIMEOUT_S) -- ncclCommAbort, no process left waiting -- where the blocking
+  // ncclCommInitRank would wait for ever.  The reference aborts the job on such an error
+  // (DistrArray.cpp:16-23).  Collectives on the non-blocking communicator may return ncclInProgress;
+  // rccl_settle waits for those under the same deadline.
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
-  ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, uid, rank);
-  if (r != ncclSuccess) {
+  ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+  config.blocking = 0;
+  ncclResult_t r = ncclCommInitRankConfig(&ctx->comm, nranks, uid, rank, &config);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (ctx->comm) ncclCommAbort(ctx->comm);
     ctx->comm = nullptr;
-    return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
   }
-  return SSP_OK;
+  const double t0 = ssp::now_s();
+  ncclResult_t state = ncclInProgress;
+  while (true) {
+    r = ncclCommGetAsyncError(ctx->comm, &state);
+    if (r != ncclSuccess || state != ncclInProgress) break;
+    if (ssp::now_s() - t0 > ctx->comm_timeout_s) {
+      ncclCommAbort(ctx->comm);
+      ctx->comm = nullptr;
+      char t[64];
+      std::snprintf(t, sizeof(t), "%g", ctx->comm_timeout_s);
+      return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRankConfig: rank ") + std::to_string(rank) + " of " +
+                                              std::to_string(nranks) + ": the communicator did not form within " + t +
+                                              " s (SSP_COMM_TIMEOUT_S): another rank is missing");
+    }
+    usleep(1000);
+  }
+  if (r != ncclSuccess || state != ncclSuccess) {
+    ncclCommAbort(ctx->comm);
+    ctx->comm = nullptr;
+    return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRankConfig: ") +
+                                            ncclGetErrorString(r != ncclSuccess ? r : state));
+  }
+  return ssp::agree_exact_max(ctx);
 }
 
 int ssp_ctx_attach_host_comm(ssp_ctx* ctx, int nranks, int rank, ssp_host_allreduce_fn allreduce,
@@ -565,7 +625,7 @@ int ssp_ctx_attach_host_comm(ssp_ctx* ctx, int nranks, int rank, ssp_host_allred
   ctx->host_allreduce = allreduce;
   ctx->host_allgather = allgather;
   ctx->host_user = user;
-  return SSP_OK;
+  return ssp::agree_exact_max(ctx);
 }
 
 int ssp_shard_range(size_t n, int nranks, int rank, size_t* offset, size_t* length) {
@@ -607,8 +667,7 @@ int ssp_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes)
   char* dsend = reinterpret_cast<char*>(ctx->result_dev + dbl + 1);
   char* drecv = reinterpret_cast<char*>(ctx->result_dev);
   SSP_TRY_HIP(hipMemcpyAsync(dsend, send, bytes, hipMemcpyHostToDevice, ctx->stream));
-  ncclResult_t r = ncclAllGather(dsend, drecv, bytes, ncclChar, ctx->comm, ctx->stream);
-  if (r != ncclSuccess) return ssp::set_error(SSP_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  SSP_TRY(ssp::rccl_settle(ctx, ncclAllGather(dsend, drecv, bytes, ncclChar, ctx->comm, ctx->stream), "ncclAllGather"));
   SSP_TRY_HIP(hipMemcpyAsync(recv, drecv, total, hipMemcpyDeviceToHost, ctx->stream));
   return ssp::sync_stream(ctx, "allgather");
 }

@@ -953,101 +953,103 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
   for (int j = 0; j < k; ++j) (swap ? rs : cs)[size_t(j)] = ys ? ys[j] : 1.0;
   const bool sc = any_scaled(rs.data(), R) || any_scaled(cs.data(), C);
   const size_t total = size_t(R) * C;
-  if (ssp::exact_mode(ctx, n)) {  // the reference's sequential dots, m x k in the caller's layout
-    ssp::FoldTail tail{};
-    SSP_TRY(ssp::fold_begin(ctx, int(total), &tail));
-    {
-      std::vector<const double*> distinct(xx, xx + m);
-      distinct.insert(distinct.end(), yy, yy + k);
-      std::sort(distinct.begin(), distinct.end());
-      const double nvec = double(std::unique(distinct.begin(), distinct.end()) - distinct.begin());
-      ssp::LedgerScope ls(ctx, "gemm_inner", 8.0 * n * nvec);
-      SSP_TRY(ssp::exact_inner(ctx, xx, xs, m, yy, ys, k, n, false, tail));
-    }
-    return ssp::fold_finish(ctx, tail, out);
-  }
-  SSP_TRY(ssp::ensure_result(ctx, total));
   ssp::FoldTail tail{};
-  if (n == 0) {
-    SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, total * sizeof(double), ctx->stream));
-  } else {
-    // Algorithmic bytes: every DISTINCT vector of the panel read once (8 N (m + k) when disjoint).
+  if (ssp::exact_mode(ctx, n)) {
+    // The reference's sequential dots (each the same number whichever operand is the row), in the
+    // R x C layout of the bandwidth kernels below: with a communicator attached the ranks' results are
+    // summed element for element, and a rank whose shard is one element longer may take the other
+    // branch (shards of spread_remainder differ by one; ssp_ctx_set_exact_max).
+    SSP_TRY(ssp::fold_begin(ctx, int(total), &tail));
     std::vector<const double*> distinct(xx, xx + m);
     distinct.insert(distinct.end(), yy, yy + k);
     std::sort(distinct.begin(), distinct.end());
     const double nvec = double(std::unique(distinct.begin(), distinct.end()) - distinct.begin());
     ssp::LedgerScope ls(ctx, "gemm_inner", 8.0 * n * nvec);
-    // 1 x 1 and 1 x 2 panels (rows = the shorter side): VALU row kernel.
-    if (R == 1 && C <= 2) {
-      InnerArgs a{};
-      a.m = 1;
-      a.k = C;
-      a.n = n;
-      a.x[0] = rows[0];
-      a.xs[0] = rs[0];
-      for (int j = 0; j < C; ++j) {
-        a.y[j] = cols[j];
-        a.ys[j] = cs[size_t(j)];
-      }
-      const bool stride = ctx->row_stride;
-      const unsigned grid = stride ? ssp::stream_grid(ctx, n / 2 + 1, 4) : ssp::win_grid(ctx, n, 4, 8);
-      SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * C));
-      a.partial = ctx->partial;
-      SSP_TRY(ssp::fold_begin(ctx, C, &tail));
-      a.tail = tail;
-      const dim3 g(grid), b(kBlock);
-      if (stride) {
-        if (C == 1 && sc) hipLaunchKernelGGL((k_gemm_inner_row<1, true>), g, b, 0, ctx->stream, a);
-        else if (C == 1) hipLaunchKernelGGL((k_gemm_inner_row<1>), g, b, 0, ctx->stream, a);
-        else if (sc) hipLaunchKernelGGL((k_gemm_inner_row<2, true>), g, b, 0, ctx->stream, a);
-        else hipLaunchKernelGGL((k_gemm_inner_row<2>), g, b, 0, ctx->stream, a);
-      } else {
-        if (C == 1 && sc) hipLaunchKernelGGL((k_gemm_inner_row_win<1, true>), g, b, 0, ctx->stream, a);
-        else if (C == 1) hipLaunchKernelGGL((k_gemm_inner_row_win<1>), g, b, 0, ctx->stream, a);
-        else if (sc) hipLaunchKernelGGL((k_gemm_inner_row_win<2, true>), g, b, 0, ctx->stream, a);
-        else hipLaunchKernelGGL((k_gemm_inner_row_win<2>), g, b, 0, ctx->stream, a);
-      }
-      SSP_TRY_HIP(hipGetLastError());
-    }
-    // A symmetric overlap <xx_i, xx_j> of up to 16 vectors: one panel that loads each vector once.
-    bool sym = m == k && m <= ssp::kInnerRows && !(R == 1 && C <= 2);
-    for (int i = 0; sym && i < m; ++i) sym = xx[i] == yy[i] && rs[size_t(i)] == cs[size_t(i)];
-    if (sym) {
-      InnerArgs a{};
-      a.m = a.k = m;
-      a.n = n;
-      for (int i = 0; i < m; ++i) {
-        a.x[i] = a.y[i] = xx[i];
-        a.xs[i] = a.ys[i] = rs[size_t(i)];
-      }
-      const unsigned grid = inner_grid(ctx, n);
-      SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * m * m));
-      a.partial = ctx->partial;
-      SSP_TRY(launch_inner_sym(ctx, a, grid, sc));
-      SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), m, m, ctx->result_dev, m, 0, 0));
-    }
-    for (int r0 = 0; !sym && !(R == 1 && C <= 2) && r0 < R; r0 += ssp::kInnerRows) {
-      const int mr = std::min(ssp::kInnerRows, R - r0);
-      const int cols_per_launch = 4 * ng_max((mr + 3) / 4);
-      for (int c0 = 0; c0 < C; c0 += cols_per_launch) {
+    SSP_TRY(ssp::exact_inner(ctx, rows, rs.data(), R, cols, cs.data(), C, n, false, tail));
+  } else {
+    SSP_TRY(ssp::ensure_result(ctx, total));
+    if (n == 0) {
+      SSP_TRY_HIP(hipMemsetAsync(ctx->result_dev, 0, total * sizeof(double), ctx->stream));
+    } else {
+      // Algorithmic bytes: every DISTINCT vector of the panel read once (8 N (m + k) when disjoint).
+      std::vector<const double*> distinct(xx, xx + m);
+      distinct.insert(distinct.end(), yy, yy + k);
+      std::sort(distinct.begin(), distinct.end());
+      const double nvec = double(std::unique(distinct.begin(), distinct.end()) - distinct.begin());
+      ssp::LedgerScope ls(ctx, "gemm_inner", 8.0 * n * nvec);
+      // 1 x 1 and 1 x 2 panels (rows = the shorter side): VALU row kernel.
+      if (R == 1 && C <= 2) {
         InnerArgs a{};
-        a.m = mr;
-        a.k = std::min(cols_per_launch, C - c0);
+        a.m = 1;
+        a.k = C;
         a.n = n;
-        for (int i = 0; i < a.m; ++i) {
-          a.x[i] = rows[r0 + i];
-          a.xs[i] = rs[size_t(r0 + i)];
+        a.x[0] = rows[0];
+        a.xs[0] = rs[0];
+        for (int j = 0; j < C; ++j) {
+          a.y[j] = cols[j];
+          a.ys[j] = cs[size_t(j)];
         }
-        for (int j = 0; j < a.k; ++j) {
-          a.y[j] = cols[c0 + j];
-          a.ys[j] = cs[size_t(c0 + j)];
-        }
-        const bool sc_launch = any_scaled(a.xs, a.m) || any_scaled(a.ys, a.k);
-        const unsigned grid = inner_grid(ctx, n);
-        SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * a.m * a.k));
+        const bool stride = ctx->row_stride;
+        const unsigned grid = stride ? ssp::stream_grid(ctx, n / 2 + 1, 4) : ssp::win_grid(ctx, n, 4, 8);
+        SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * C));
         a.partial = ctx->partial;
-        SSP_TRY(launch_inner(ctx, a, grid, sc_launch));
-        SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), a.m, a.k, ctx->result_dev, C, r0, c0));
+        SSP_TRY(ssp::fold_begin(ctx, C, &tail));
+        a.tail = tail;
+        const dim3 g(grid), b(kBlock);
+        if (stride) {
+          if (C == 1 && sc) hipLaunchKernelGGL((k_gemm_inner_row<1, true>), g, b, 0, ctx->stream, a);
+          else if (C == 1) hipLaunchKernelGGL((k_gemm_inner_row<1>), g, b, 0, ctx->stream, a);
+          else if (sc) hipLaunchKernelGGL((k_gemm_inner_row<2, true>), g, b, 0, ctx->stream, a);
+          else hipLaunchKernelGGL((k_gemm_inner_row<2>), g, b, 0, ctx->stream, a);
+        } else {
+          if (C == 1 && sc) hipLaunchKernelGGL((k_gemm_inner_row_win<1, true>), g, b, 0, ctx->stream, a);
+          else if (C == 1) hipLaunchKernelGGL((k_gemm_inner_row_win<1>), g, b, 0, ctx->stream, a);
+          else if (sc) hipLaunchKernelGGL((k_gemm_inner_row_win<2, true>), g, b, 0, ctx->stream, a);
+          else hipLaunchKernelGGL((k_gemm_inner_row_win<2>), g, b, 0, ctx->stream, a);
+        }
+        SSP_TRY_HIP(hipGetLastError());
+      }
+      // A symmetric overlap <xx_i, xx_j> of up to 16 vectors: one panel that loads each vector once.
+      bool sym = m == k && m <= ssp::kInnerRows && !(R == 1 && C <= 2);
+      for (int i = 0; sym && i < m; ++i) sym = xx[i] == yy[i] && rs[size_t(i)] == cs[size_t(i)];
+      if (sym) {
+        InnerArgs a{};
+        a.m = a.k = m;
+        a.n = n;
+        for (int i = 0; i < m; ++i) {
+          a.x[i] = a.y[i] = xx[i];
+          a.xs[i] = a.ys[i] = rs[size_t(i)];
+        }
+        const unsigned grid = inner_grid(ctx, n);
+        SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * m * m));
+        a.partial = ctx->partial;
+        SSP_TRY(launch_inner_sym(ctx, a, grid, sc));
+        SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), m, m, ctx->result_dev, m, 0, 0));
+      }
+      for (int r0 = 0; !sym && !(R == 1 && C <= 2) && r0 < R; r0 += ssp::kInnerRows) {
+        const int mr = std::min(ssp::kInnerRows, R - r0);
+        const int cols_per_launch = 4 * ng_max((mr + 3) / 4);
+        for (int c0 = 0; c0 < C; c0 += cols_per_launch) {
+          InnerArgs a{};
+          a.m = mr;
+          a.k = std::min(cols_per_launch, C - c0);
+          a.n = n;
+          for (int i = 0; i < a.m; ++i) {
+            a.x[i] = rows[r0 + i];
+            a.xs[i] = rs[size_t(r0 + i)];
+          }
+          for (int j = 0; j < a.k; ++j) {
+            a.y[j] = cols[c0 + j];
+            a.ys[j] = cs[size_t(c0 + j)];
+          }
+          const bool sc_launch = any_scaled(a.xs, a.m) || any_scaled(a.ys, a.k);
+          const unsigned grid = inner_grid(ctx, n);
+          SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * a.m * a.k));
+          a.partial = ctx->partial;
+          SSP_TRY(launch_inner(ctx, a, grid, sc_launch));
+          SSP_TRY(
+              ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), a.m, a.k, ctx->result_dev, C, r0, c0));
+        }
       }
     }
   }

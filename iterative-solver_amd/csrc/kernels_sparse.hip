@@ -7,6 +7,7 @@
 // one lane in the reference's entry order, so the per-rank results are bitwise those of the
 // reference loop; cross-rank sums are RCCL allreduces.
 #include <algorithm>
+#include <map>
 #include <vector>
 
 #include "ssp_internal.h"
@@ -355,14 +356,47 @@ int ssp_sparse_axpy_batch(ssp_ctx* ctx, int nvec, const size_t* ptr, const size_
     }
   }
   if (!inl) {  // more entries than one argument block carries: one launch per vector
-    for (int k = 0; k < nvec; ++k)
-      SSP_TRY(ssp_sparse_axpy(ctx, 1.0, idx + ptr[k], val + ptr[k], ptr[k + 1] - ptr[k], xx[k], n, offset));
+    for (int k = 0; k < nvec; ++k) {
+      const size_t b = ptr[k], e = ptr[k + 1];
+      std::vector<size_t> sorted(idx + b, idx + e);
+      std::sort(sorted.begin(), sorted.end());
+      if (std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end()) {
+        SSP_TRY(ssp_sparse_axpy(ctx, 1.0, idx + b, val + b, e - b, xx[k], n, offset));
+      } else {  // a repeated index: the entries one at a time, in order
+        for (size_t q = b; q < e; ++q) SSP_TRY(ssp_sparse_axpy(ctx, 1.0, idx + q, val + q, 1, xx[k], n, offset));
+      }
+    }
     return SSP_OK;
   }
   if (a.nnz == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "sparse_axpy", 24.0 * a.nnz);
-  hipLaunchKernelGGL(k_scatter_batch_inline, dim3(1), dim3(kBatchEntries), 0, ctx->stream, a);
-  SSP_TRY_HIP(hipGetLastError());
+  // One vector's slice may hold an index more than once (a P-space action concatenates the entries of
+  // all P vectors, which may share indices).  Entry e's generation is the number of earlier entries
+  // with its (vector, index); each generation is one launch, in order, so no two lanes of a launch add
+  // to one element and every element takes its adds in entry order -- ssp_sparse_axpy's per vector.
+  std::vector<int> gen(size_t(a.nnz), 0);
+  int ngen = 1;
+  {
+    std::map<std::pair<int, unsigned>, int> seen;
+    for (int e = 0; e < a.nnz; ++e) {
+      gen[size_t(e)] = seen[{a.dst[e], a.li[e]}]++;
+      ngen = std::max(ngen, gen[size_t(e)] + 1);
+    }
+  }
+  for (int g = 0; g < ngen; ++g) {
+    ScatterBatchInline b = a;
+    if (ngen > 1) {
+      b.nnz = 0;
+      for (int e = 0; e < a.nnz; ++e)
+        if (gen[size_t(e)] == g) {
+          b.dst[b.nnz] = a.dst[e];
+          b.li[b.nnz] = a.li[e];
+          b.v[b.nnz++] = a.v[e];
+        }
+    }
+    hipLaunchKernelGGL(k_scatter_batch_inline, dim3(1), dim3(kBatchEntries), 0, ctx->stream, b);
+    SSP_TRY_HIP(hipGetLastError());
+  }
   return SSP_OK;
 }
 

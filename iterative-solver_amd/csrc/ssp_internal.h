@@ -33,8 +33,8 @@ struct ssp_ctx {
   std::vector<ssp_ledger_entry_t> ledger;
   std::vector<hipEvent_t> event_pool;
   int num_cus = 256;
-  int inner_per_cu = 4;
-  bool synth_stride = false;  // SSP_SYNTH_SHAPE=stride: the synthetic apply kernel grid-strided (A/B)  // gemm_inner workgroups per CU (SSP_INNER_PER_CU: the A/B knob of tools/ab_inner.py)
+  int inner_per_cu = 4;        // gemm_inner workgroups per CU (SSP_INNER_PER_CU: the A/B knob of tools/ab_inner.py)
+  bool synth_stride = false;  // SSP_SYNTH_SHAPE=stride: the synthetic apply kernel grid-strided (A/B)
   // Shape of the 1 x 1 / 1 x 2 gemm_inner row kernel: window (default) or, with SSP_ROW_SHAPE=stride
   // in the environment at context creation, the round-2 grid-stride shape (A/B: tools/row_shape_ab.py).
   bool row_stride = false;
@@ -132,6 +132,11 @@ int upload_small(ssp_ctx* ctx, const void* host, size_t bytes, void** dev);
 int flush_uploads(ssp_ctx* ctx);
 // Sums the rank-local device results over ranks (no-op for one rank).
 int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n);
+// After an attach: every rank takes the smallest exact_max of the communicator's ranks.
+int agree_exact_max(ssp_ctx* ctx);
+// The outcome of an RCCL call on the context's non-blocking communicator (ncclInProgress waited out
+// under the deadline; an error aborts the communicator and returns SSP_ERR_COMM).
+int rccl_settle(ssp_ctx* ctx, ncclResult_t r, const char* what);
 // Copies n doubles of ctx->result_dev to host `out` once every operation queued before it has
 // completed (publish kernel + host poll of a sequence flag; see context.hip).
 int fetch_result(ssp_ctx* ctx, double* out, size_t n);
@@ -345,6 +350,9 @@ int p2p_allreduce_dev(ssp_ctx* ctx, double* buf, size_t n);
 int p2p_allreduce_fetch(ssp_ctx* ctx, const double* src, double* out, size_t n);
 int p2p_allgather_host(ssp_ctx* ctx, const void* send, void* recv, size_t bytes);
 int p2p_detach(ssp_ctx* ctx);
+// SSP_ERR_COMM (the communicator aborted) when a peer-memory exchange kernel gave up -- a peer missing
+// past the deadline or a mismatched length -- as recorded in the coherent error word; else SSP_OK.
+int device_exchange_error(ssp_ctx* ctx, const char* what);
 
 // kernels_exact.hip: the reference's arithmetic for short vectors.  exact_inner forms the m x k (or,
 // pairs, the m) dots for the tail of fold_begin (in result_dev for an exchange, or published to the

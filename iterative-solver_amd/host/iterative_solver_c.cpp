@@ -8,6 +8,7 @@
 #include <cstring>
 #include <iostream>
 #include <limits>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -18,6 +19,7 @@
 #include "itsolv_hbm/hbm_handlers.h"
 #include "itsolv_hbm/solver_factory.h"
 #include "itsolv_hbm/solvers.h"
+#include "mpi_bridge.h"
 
 using molpro::linalg::hbm::check;
 using molpro::linalg::hbm::Device;
@@ -80,8 +82,38 @@ int default_device() {
   return 0;
 }
 
-std::shared_ptr<Device> make_device() {
+// A context attached to the ranks of an MPI communicator (mpi_bridge.h), with the transport's state.
+class BridgedDevice : public Device {
+ public:
+  BridgedDevice(int device, int64_t fcomm) : Device(device) {
+    m_link = molpro::linalg::hbm::mpi::attach(ctx(), fcomm, nullptr);
+  }
+
+ private:
+  std::shared_ptr<void> m_link;
+};
+// One bridged context per communicator, shared by the instances that use it and released with the
+// last of them (every rank creates and finalizes instances in the same order, so the collective
+// attach happens on all ranks together).
+std::map<int64_t, std::weak_ptr<Device>> g_bridged;
+
+// The instance's device and ranks.  In order:
+//  - the context set by IterativeSolverHbmSetContext;
+//  - the communicator fcomm names, when the process has an initialised MPI library (reference
+//    IterativeSolverCMPI.cpp:169, :205, :234, :254 -- MPI_Comm_f2c(fcomm)): a context attached to its
+//    ranks, on the device of the rank's place among them on its node (one rank: a private context);
+//  - otherwise a private single-rank context on the node-local rank's device.
+std::shared_ptr<Device> make_device(int64_t fcomm) {
+  namespace mpi = molpro::linalg::hbm::mpi;
   if (g_user_ctx) return std::make_shared<Device>(g_user_ctx, true);
+  mpi::Bridge* b = mpi::bridge();
+  if (b && b->active() && b->valid(fcomm)) {
+    if (b->size(fcomm) <= 1) return std::make_shared<Device>(mpi::device_for(fcomm));
+    if (auto d = g_bridged[fcomm].lock()) return d;
+    auto d = std::make_shared<BridgedDevice>(mpi::device_for(fcomm), fcomm);
+    g_bridged[fcomm] = d;
+    return d;
+  }
   return std::make_shared<Device>(default_device());
 }
 
@@ -152,6 +184,11 @@ auto guarded(F&& f) -> decltype(f()) {
   if constexpr (!std::is_void_v<T>) return T{};
 }
 
+molpro::linalg::hbm::mpi::Bridge* active_mpi() {
+  auto* b = molpro::linalg::hbm::mpi::bridge();
+  return b && b->active() ? b : nullptr;
+}
+
 }  // namespace
 
 extern "C" {
@@ -183,9 +220,8 @@ void IterativeSolverLinearEigensystemInitialize(size_t nQ, size_t nroot, size_t*
                                                 const char* options) {
   guarded([&] {
     (void)fname;
-    (void)fcomm;
     Instance in;
-    in.dev = make_device();
+    in.dev = make_device(fcomm);
     // method dispatch and option parsing as the reference's create_LinearEigensystem (SolverFactory.h:114-125)
     auto solver = it::create_LinearEigensystem(algorithm ? algorithm : "", options ? options : "",
                                                molpro::linalg::hbm::make_handlers());
@@ -207,12 +243,11 @@ void IterativeSolverLinearEquationsInitialize(size_t n, size_t nroot, size_t* ra
                                               const char* algorithm, const char* options) {
   guarded([&] {
     (void)fname;
-    (void)fcomm;
     auto made = it::create_LinearEquations(algorithm ? algorithm : "", options ? options : "",
                                            molpro::linalg::hbm::make_handlers());
     std::unique_ptr<LinEq> solver(static_cast<LinEq*>(made.release()));
     Instance in;
-    in.dev = make_device();
+    in.dev = make_device(fcomm);
     setup(in, n, range_begin, range_end);
     // reference IterativeSolverCMPI.cpp:199-225: rhs as R vectors, then options
     std::vector<Vec> b;
@@ -237,9 +272,8 @@ void IterativeSolverNonLinearEquationsInitialize(size_t n, size_t* range_begin, 
                                                  const char* algorithm, const char* options) {
   guarded([&] {
     (void)fname;
-    (void)fcomm;
     Instance in;
-    in.dev = make_device();
+    in.dev = make_device(fcomm);
     auto solver = it::create_NonLinearEquations(algorithm ? algorithm : "", options ? options : "",
                                                 molpro::linalg::hbm::make_handlers());
     solver->set_convergence_threshold(thresh);
@@ -255,10 +289,9 @@ void IterativeSolverOptimizeInitialize(size_t n, size_t* range_begin, size_t* ra
                                        int64_t fcomm, const char* algorithm, const char* options) {
   guarded([&] {
     (void)fname;
-    (void)fcomm;
     (void)minimize;  // ignored, as the reference does (IterativeSolverCMPI.cpp:250-268)
     Instance in;
-    in.dev = make_device();
+    in.dev = make_device(fcomm);
     auto solver = it::create_Optimize(algorithm ? algorithm : "", options ? options : "",
                                       molpro::linalg::hbm::make_handlers());
     // reference IterativeSolverCMPI.cpp:245-264
@@ -515,22 +548,50 @@ size_t IterativeSolverHbmNRoots(void) {
   return instances.empty() ? 0 : instances.back()->solver->n_roots();
 }
 
-// No MPI on this back end: ranks come from the ssp_ctx communicator (IterativeSolverHbmSetContext).
-int64_t mpicomm_self(void) { return 0; }
-int64_t mpicomm_global(void) { return 0; }
-int64_t IterativeSolver_mpicomm_global(void) { return 0; }
-int64_t IterativeSolver_mpicomm_self(void) { return 0; }
-// reference IterativeSolverCMPI.cpp:516-534 (mpi::size_global / rank_global / init / finalize), for
-// the Fortran module.  Size and rank are those of the context the next instance will use; init
-// and finalize have nothing to start or stop (the launcher owns the processes, the caller the
-// communicator) and return 0 as MPI_SUCCESS.  The reference's Fortran module binds the size/rank
-// functions as IterativeSolver_mpi_size_global / _mpi_rank_global (IterativeSolverF.F90:50-57)
+// reference IterativeSolverCMPI.cpp:481-534 (mpi::comm_global / comm_self / size_global /
+// rank_global / init / finalize), through the caller's MPI library when the process has one
+// (mpi_bridge.h).  Without MPI the handles are 0 and size and rank are those of the context the next
+// instance will use.  init calls MPI_Init when MPI is loaded but not initialised, and finalize undoes
+// only that; both return 0 (MPI_SUCCESS) without MPI.  The reference's Fortran module binds the
+// size/rank functions as IterativeSolver_mpi_size_global / _mpi_rank_global (IterativeSolverF.F90:50-57)
 // while its C++ defines IterativeSolver_mpisize_global / _mpirank_global: both spellings exist here.
-int64_t IterativeSolver_mpisize_global(void) { return g_user_ctx ? ssp_ctx_nranks(g_user_ctx) : 1; }
-int64_t IterativeSolver_mpirank_global(void) { return g_user_ctx ? ssp_ctx_rank(g_user_ctx) : 0; }
+int64_t IterativeSolver_mpicomm_global(void) { return active_mpi() ? active_mpi()->world() : 0; }
+int64_t IterativeSolver_mpicomm_self(void) { return active_mpi() ? active_mpi()->self() : 0; }
+int64_t mpicomm_global(void) { return IterativeSolver_mpicomm_global(); }
+int64_t mpicomm_self(void) { return IterativeSolver_mpicomm_self(); }
+int64_t IterativeSolver_mpisize_global(void) {
+  if (g_user_ctx) return ssp_ctx_nranks(g_user_ctx);
+  auto* b = active_mpi();
+  return b ? b->size(b->world()) : 1;
+}
+int64_t IterativeSolver_mpirank_global(void) {
+  if (g_user_ctx) return ssp_ctx_rank(g_user_ctx);
+  auto* b = active_mpi();
+  return b ? b->rank(b->world()) : 0;
+}
 int64_t IterativeSolver_mpi_size_global(void) { return IterativeSolver_mpisize_global(); }
 int64_t IterativeSolver_mpi_rank_global(void) { return IterativeSolver_mpirank_global(); }
-int IterativeSolver_mpi_init(void) { return 0; }
-int IterativeSolver_mpi_finalize(void) { return 0; }
+int IterativeSolver_mpi_init(void) {
+  auto* b = molpro::linalg::hbm::mpi::bridge();
+  return b ? b->init() : 0;
+}
+int IterativeSolver_mpi_finalize(void) {
+  auto* b = molpro::linalg::hbm::mpi::bridge();
+  return b ? b->finalize() : 0;
+}
+
+int IterativeSolverHbmMpiActive(void) { return active_mpi() ? 1 : 0; }
+
+int IterativeSolverHbmMpiAttach(ssp_ctx* ctx, int64_t fcomm, const char* transport) {
+  return guarded([&] {
+    if (!ctx) throw std::invalid_argument("IterativeSolverHbmMpiAttach: null context");
+    auto link = molpro::linalg::hbm::mpi::attach(ctx, fcomm, transport);
+    // The caller owns ctx and detaches it by destroying it; the transport's callback state stays
+    // with the process (a few bytes per attach).
+    static std::vector<std::shared_ptr<void>> keep;
+    if (link) keep.push_back(std::move(link));
+    return 0;
+  }) == 0 && g_error.empty() ? 0 : 1;
+}
 
 }  // extern "C"

@@ -71,6 +71,8 @@ def _load():
             "IterativeSolverHbmLastError": (C.c_char_p, []),
             "IterativeSolverHbmInstanceId": (C.c_uint64, []),
             "IterativeSolverHbmFinalizeInstance": (I, [C.c_uint64]),
+            "IterativeSolverHbmMpiActive": (I, []),
+            "IterativeSolverHbmMpiAttach": (I, [P, C.c_int64, C.c_char_p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -144,9 +146,11 @@ class IterativeSolver:
             pass
 
     def mpicomm_compute(self):
-        """The communicator handle of the reference (IterativeSolver_mpicomm_global); on the HBM back
-        end ranks communicate through the context's RCCL communicator and this is 0."""
-        return int(_call("IterativeSolver_mpicomm_global"))
+        """The communicator the instances use by default, as in the reference
+        (iterative_solver_extension.pyx:27-31): IterativeSolver_mpicomm_global(), the Fortran handle of
+        MPI_COMM_WORLD when the process has initialised MPI (the C layer then shards the vectors over its
+        ranks), else 0 (no communicator: one rank, or the context set by use_context)."""
+        return _mpicomm_compute()
 
     def finalize(self):
         if getattr(self, "_active", False):
@@ -294,6 +298,20 @@ class IterativeSolver:
                 break
 
 
+_m_mpicomm_compute = None
+
+
+def _mpicomm_compute():
+    global _m_mpicomm_compute
+    if _m_mpicomm_compute is None:
+        _m_mpicomm_compute = int(_call("IterativeSolver_mpicomm_global"))
+    return _m_mpicomm_compute
+
+
+def _comm(mpicomm):
+    return int(mpicomm) if mpicomm is not None else _mpicomm_compute()
+
+
 def _range_arrays(range):
     rb = C.c_size_t(range[0] if range is not None else 0)
     re = C.c_size_t(range[1] if range is not None else 0)
@@ -306,7 +324,7 @@ class LinearEigensystem(IterativeSolver):
         super().__init__(n, nroot)
         rb, re = _range_arrays(range)
         _call("IterativeSolverLinearEigensystemInitialize", n, nroot, C.byref(rb), C.byref(re), thresh, thresh_value,
-              1 if hermitian else 0, verbosity, pname.encode(), int(mpicomm or 0), algorithm.encode(),
+              1 if hermitian else 0, verbosity, pname.encode(), _comm(mpicomm), algorithm.encode(),
               options.encode())
         self._register()
         if range is not None:
@@ -325,7 +343,7 @@ class NonLinearEquations(IterativeSolver):
         super().__init__(n)
         rb, re = _range_arrays(range)
         _call("IterativeSolverNonLinearEquationsInitialize", n, C.byref(rb), C.byref(re), thresh, verbosity,
-              pname.encode(), int(mpicomm or 0), algorithm.encode(), options.encode())
+              pname.encode(), _comm(mpicomm), algorithm.encode(), options.encode())
         self._register()
         if range is not None:
             range[0], range[1] = rb.value, re.value
@@ -340,7 +358,7 @@ class LinearEquations(IterativeSolver):
         rb, re = _range_arrays(range)
         r = np.ascontiguousarray(rhs, dtype=np.float64)
         _call("IterativeSolverLinearEquationsInitialize", n, nroot, C.byref(rb), C.byref(re), _d(r), aughes, thresh,
-              thresh_value, 1 if hermitian else 0, verbosity, pname.encode(), int(mpicomm or 0), algorithm.encode(),
+              thresh_value, 1 if hermitian else 0, verbosity, pname.encode(), _comm(mpicomm), algorithm.encode(),
               options.encode())
         self._register()
 
@@ -351,5 +369,5 @@ class Optimize(IterativeSolver):
         super().__init__(n)
         rb, re = _range_arrays(range)
         _call("IterativeSolverOptimizeInitialize", n, C.byref(rb), C.byref(re), thresh, thresh_value, verbosity,
-              1 if minimize else 0, pname.encode(), int(mpicomm or 0), algorithm.encode(), options.encode())
+              1 if minimize else 0, pname.encode(), _comm(mpicomm), algorithm.encode(), options.encode())
         self._register()

@@ -53,17 +53,50 @@ int or_axpy(double alpha, const double* x, size_t nx, double* y, size_t ny) {
  * 100 + P (P = 2..64) = the reference's own distributed build on P MPI ranks: the index range split
  * by make_distribution_spread_remainder (util/Distribution.h:99-109), each rank's local
  * std::inner_product sequential, the P partials summed in rank order (DistrArray.cpp:124-138, the
- * MPI_Allreduce of util/gemm.h:179-182) ("mpiP" runs). */
+ * MPI_Allreduce of util/gemm.h:179-182) ("mpiP" runs) -- one valid association of MPI_Allreduce.
+ * 200 + P = the same rank partials combined in the association MPICH's MPI_Allreduce(MPI_SUM) of doubles
+ * gives them on one node: with pof2 the largest power of two <= P and rem = P - pof2, ranks 2i and
+ * 2i+1 (i < rem) first add their partials, and the pof2 values left are combined pairwise at distance
+ * 1, 2, 4, ... (the recursive-doubling / reduce-scatter tree MPICH 3.3 uses for buffers over 2048
+ * bytes).  Buffers of at most 2048 bytes MPICH reduces along a binomial tree ((p0 + p1) + (p2 + p3)) +
+ * p4 ...; the two trees are the same association for P = 2, 3, 4, 6, 7, 8 (and every power of two),
+ * so there the model holds for every buffer length (measured: /opt/conda MPICH 3.3.2, random
+ * partials, tests/test_mpi_bridge.py::test_mpich_allreduce_association).  For P = 2 and 3 it is the
+ * rank order, for P = 4 (p0 + p1) + (p2 + p3).  Pinned against MPICH's own MPI_Allreduce by the C-API
+ * loops of tests/mpi_worker.py ("mpichP" runs). */
 static int g_sum_order = 0;
 
 int or_set_sum_order(int order) {
-  if (order < 0 || (order > 2 && (order < 102 || order > 164))) return 1;
+  if (order < 0 || (order > 2 && (order < 102 || order > 164) && (order < 202 || order > 264))) return 1;
   g_sum_order = order;
   return 0;
 }
 
 int or_dot(const double* x, size_t nx, const double* y, size_t ny, double* out) {
   if (nx > ny) return 1;
+  if (g_sum_order >= 200) {
+    const size_t P = (size_t)(g_sum_order - 200), blk = nx / P, extra = nx % P;
+    double v[64];
+    size_t pof2 = 1;
+    while (2 * pof2 <= P) pof2 *= 2;
+    const size_t rem = P - pof2;
+    for (size_t r = 0; r < P; ++r) {
+      const size_t b = r * blk + (r < extra ? r : extra), e = b + blk + (r < extra ? 1 : 0);
+      double l = 0;
+      for (size_t i = b; i < e; ++i) l = l + x[i] * y[i];
+      /* new rank of r: i for the pair (2i, 2i+1), i < rem; r - rem above the pairs */
+      if (r < 2 * rem) {
+        if (r & 1) v[r / 2] = v[r / 2] + l;
+        else v[r / 2] = l;
+      } else {
+        v[r - rem] = l;
+      }
+    }
+    for (size_t mask = 1; mask < pof2; mask *= 2)
+      for (size_t i = 0; i < pof2; i += 2 * mask) v[i] = v[i] + v[i + mask];
+    *out = v[0];
+    return 0;
+  }
   if (g_sum_order >= 100) {
     const size_t P = (size_t)(g_sum_order - 100), blk = nx / P, extra = nx % P;
     double s = 0;

@@ -104,7 +104,9 @@ def case_gpu_ops(comm):
     ctx = sh.Context(0)
     attach(ctx, comm)
     assert (ctx.lib.ssp_ctx_rank(ctx.handle), ctx.lib.ssp_ctx_nranks(ctx.handle)) == (rank, world)
-    for n in (5, 1003, 100_003):
+    # 4097 on 2 ranks: shards of 2049 and 2048 elements, either side of the default exact_max -- one rank
+    # takes the bandwidth kernels, the other the reference's arithmetic, in the same result layout
+    for n in (5, 1003, 4097, 100_003):
         off, ln = sh.shard_range(n, world, rank)
         rng = np.random.default_rng(n)
         X = rng.uniform(-1, 1, (6, n))
@@ -116,6 +118,11 @@ def case_gpu_ops(comm):
         M = ctx.gemm_inner(xs[:2], xs[2:])
         terms = np.abs(X[:2]) @ np.abs(X[2:]).T
         assert np.all(np.abs(M - oracle.gemm_inner(list(X[:2]), list(X[2:]))) <= tol(terms))
+        # m > k: the bandwidth kernels put the shorter side on the rows (a transposed result)
+        M = ctx.gemm_inner(xs[:4], xs[4:])
+        terms = np.abs(X[:4]) @ np.abs(X[4:]).T
+        assert np.all(np.abs(M - oracle.gemm_inner(list(X[:4]), list(X[4:]))) <= tol(terms)), (n, M)
+        assert len(set(ctx.allgather_bytes(M.tobytes()))) == 1  # every rank received the same sums
         for mx, ig in ((False, False), (True, False), (False, True)):
             nsel = min(7, n)
             gi, gv = ctx.select(xs[3], nsel, max=mx, ignore_sign=ig, offset=off)

@@ -186,9 +186,12 @@ def loop_eigen(solver, h, nroot, np_, max_iter=100):
         pp = h[np.ix_(pidx, pidx)].copy()
 
         def apply_p(pc, gl, ranges):
+            # adds to this rank's range [r0, r1) of each action row, rows n apart (the reference's
+            # apply_on_p_c contract, IterativeSolverCMPI.cpp:141-157; one rank: the whole row)
             for i in range(pc.shape[0]):
+                r0, r1 = int(ranges[i, 0]), int(ranges[i, 1])
                 for pi, k in enumerate(pidx):
-                    gl[i * n:(i + 1) * n] += h[:, k] * pc[i, pi]
+                    gl[i * n:i * n + r1 - r0] += h[r0:r1, k] * pc[i, pi]
 
         nwork = solver.add_p(pspace, pp, x, g, apply_p)
         trace.append(("p", nwork))

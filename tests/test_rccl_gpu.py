@@ -150,3 +150,40 @@ def test_one_rank_p2p_transport_is_the_identity(pair, n):
         c.barrier()
     finally:
         c.close()
+
+
+RCCL_ALONE = r"""
+import sys, time
+sys.path[:0] = [sys.argv[1]]
+import subspace_hip as sh
+c = sh.Context(0)
+c.set_comm_timeout(float(sys.argv[2]))
+t0 = time.time()
+try:
+    c.attach_comm(2, 0, sh.Context.unique_id())  # rank 1 never joins
+    print("ATTACHED")
+except sh.SspError as e:
+    print(f"FAILED {e.code} {time.time() - t0:.2f} {e}")
+c.close()
+"""
+
+
+def test_rccl_join_without_the_other_rank_fails_within_the_deadline():
+    # The driver's N > 1 bench joins an RCCL communicator; a rank that never arrives must end the join
+    # of the others with SSP_ERR_COMM after SSP_COMM_TIMEOUT_S (non-blocking ncclCommInitRankConfig,
+    # polled, ncclCommAbort) instead of waiting for ever -- and leave no process behind.
+    import os
+    import subprocess
+    import sys
+    import time
+
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "iterative-solver_amd")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", RCCL_ALONE, pkg, "8"], capture_output=True, text=True, timeout=90)
+    wall = time.time() - t0
+    print(r.stdout[-1500:], r.stderr[-1500:])
+    assert r.returncode == 0 and "FAILED 5" in r.stdout, r.stdout + r.stderr
+    took = float(r.stdout.split("FAILED 5 ")[1].split()[0])
+    assert 7.5 < took < 20, took
+    assert "did not form within 8 s" in r.stdout
+    assert wall < 80

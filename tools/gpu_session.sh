@@ -1,83 +1,89 @@
 #!/bin/bash
-# One GPU-box session: GPU tests, bench, kernel-trace profile.  Each GPU step has its own time limit;
-# a fault / abort / timeout ends the session (no retries).  Outputs land in gpurun_out/.
-# Usage: tools/gpu_session.sh [tests|bench|prof|pmc|mfma|ledger|all] [extra bench args...]
-set -u
+# One GPU-box session: any of the GPU tests, smoke, bench, kernel-trace profile, PMC passes, ledgers.
+#
+#   tools/gpu_session.sh STEPS [args...]      STEPS: comma-separated, run in order, e.g. tests,smoke,bench
+#     tests   [pytest args]   python -m pytest tests -m gpu -v (every test named as it starts and ends)
+#     smoke                    __graft_entry__.smoke()
+#     bench   [bench args]     python bench.py
+#     prof    [bench args]     rocprofv3 --kernel-trace --stats of a short bench run
+#     pmc     [bench args]     HBM traffic counters (FETCH_SIZE, WRITE_SIZE), one --pmc pass each
+#     mfma    [bench args]     matrix-core counters of the bench step and of the per-shape bench
+#     ledger                   tools/shapes_bench.py and tools/solver_ledger.py
+#   Outputs: gpurun_out/${SESSION:-session}/<step>.log (+ bench.json, prof/, pmc_*/).
+#
+# Every step streams its output to stdout (tee) as well as to its log, and a heartbeat line goes to
+# stdout every 50 s: the pool takes a command that is silent on stdout / stderr / gpurun_out for 180 s
+# as hung and kills it, and a single long test (the 8-process full-size solves) prints nothing while it
+# runs.  Each step has its own time limit; a fault, abort or timeout ends the session (no retries).
+set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-OUT=$ROOT/gpurun_out
+OUT=$ROOT/gpurun_out/${SESSION:-session}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-what=${1:-all}
+steps=${1:-tests,smoke,bench,prof}
 shift || true
 
-step() {  # step <name> <seconds> <cmd...>; returns the command's status
+(while sleep 50; do echo "[heartbeat $(date +%T)]"; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+
+step() {  # step <name> <seconds> <cmd...>: the command's status; output to stdout and $OUT/<name>.log
   local name=$1 t=$2
   shift 2
   echo "== $name (limit ${t}s): $*"
-  timeout -k 10 "$t" "$@" >"$OUT/$name.log" 2>&1
+  timeout -k 10 "$t" "$@" 2>&1 | tee "$OUT/$name.log"
   local rc=$?
   echo "== $name rc=$rc"
-  tail -n 5 "$OUT/$name.log"
   return $rc
 }
 
-fatal() {  # statuses after which nothing else may use the GPU in this call
-  case $1 in 0 | 1) return 1 ;; *) return 0 ;; esac
-}
-
-if [ "$what" = tests ] || [ "$what" = all ]; then
-  step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -rf --timeout 120 --timeout-method thread
-  rc=$?
-  if fatal $rc; then exit $rc; fi
-fi
-if [ "$what" = bench ] || [ "$what" = all ]; then
-  step bench 900 python bench.py "$@"
-  rc=$?
-  if [ $rc -ne 0 ]; then exit $rc; fi
-  grep '^{' "$OUT/bench.log" >"$OUT/bench.json" || true
-fi
-if [ "$what" = prof ] || [ "$what" = all ]; then
-  rm -rf "$OUT/prof"
-  step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-in-solver --no-small "$@"
-  rc=$?
-  if [ $rc -ne 0 ]; then exit $rc; fi
-  # The bench line of the profiled process itself: its HIP-event ledger and the kernel statistics
-  # below come from the same allocation (placement moves gemm_outer by up to 8 % between processes).
-  grep '^{' "$OUT/rocprof.log" >"$OUT/bench_rocprof.json" || true
-fi
-if [ "$what" = pmc ] || [ "$what" = all ]; then
-  # HBM traffic counters, one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass);
-  # kernel trace only, no runtime/API tracing alongside --pmc.
-  for c in FETCH_SIZE WRITE_SIZE; do
-    rm -rf "$OUT/pmc_$c"
-    step "pmc_$c" 600 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- \
-      python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 --no-cpu-baseline --no-in-solver --no-small "$@"
-    rc=$?
-    if [ $rc -ne 0 ]; then exit $rc; fi
-  done
-fi
-if [ "$what" = mfma ] || [ "$what" = all ]; then
-  # Matrix-core activity (MfmaUtil, MfmaFlopsF64): the bench step, then the per-shape bench
-  # (gemm_inner 16x64 is the densest panel), one --pmc pass each.
-  rm -rf "$OUT/pmc_mfma" "$OUT/pmc_mfma_shapes"
-  step pmc_mfma 600 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 --kernel-trace -d "$OUT/pmc_mfma" \
-    -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 --no-cpu-baseline --no-in-solver --no-small "$@"
-  rc=$?
-  if [ $rc -ne 0 ]; then exit $rc; fi
-  step pmc_mfma_shapes 600 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 --kernel-trace \
-    -d "$OUT/pmc_mfma_shapes" -o run --output-format csv -- python3 tools/shapes_bench.py --reps 1 \
-    --out "$OUT/shapes_pmc.json"
-  rc=$?
-  if [ $rc -ne 0 ]; then exit $rc; fi
-fi
-if [ "$what" = ledger ] || [ "$what" = all ]; then
-  step shapes 600 python tools/shapes_bench.py --out "$OUT/shapes.json"
-  rc=$?
-  if [ $rc -ne 0 ]; then exit $rc; fi
-  step solver_ledger 900 python tools/solver_ledger.py --out "$OUT/solver_ledger.json"
-  rc=$?
-  if [ $rc -ne 0 ]; then exit $rc; fi
-fi
+for s in ${steps//,/ }; do
+  case $s in
+    tests)
+      step pytest_gpu 2400 python -u -m pytest tests -m gpu -v -x -rf --durations=15 --timeout 600 \
+        --timeout-method thread "$@" || exit $?
+      ;;
+    smoke)
+      step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $?
+      ;;
+    bench)
+      step bench 900 python -u bench.py "$@" || exit $?
+      grep '^{' "$OUT/bench.log" >"$OUT/bench.json" || true
+      ;;
+    prof)
+      rm -rf "$OUT/prof"
+      step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+        python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline "$@" || exit $?
+      # the bench line of the profiled process itself: its ledger and the kernel statistics come
+      # from the same allocation
+      grep '^{' "$OUT/rocprof.log" >"$OUT/bench_rocprof.json" || true
+      ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        rm -rf "$OUT/pmc_$c"
+        step "pmc_$c" 600 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- \
+          python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 --no-cpu-baseline --no-in-solver --no-small \
+          "$@" || exit $?
+      done
+      ;;
+    mfma)
+      rm -rf "$OUT/pmc_mfma" "$OUT/pmc_mfma_shapes"
+      step pmc_mfma 600 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 --kernel-trace \
+        -d "$OUT/pmc_mfma" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 \
+        --no-cpu-baseline --no-in-solver --no-small "$@" || exit $?
+      step pmc_mfma_shapes 600 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 --kernel-trace \
+        -d "$OUT/pmc_mfma_shapes" -o run --output-format csv -- python3 tools/shapes_bench.py --reps 1 \
+        --out "$OUT/shapes_pmc.json" || exit $?
+      ;;
+    ledger)
+      step shapes 600 python -u tools/shapes_bench.py --out "$OUT/shapes.json" || exit $?
+      step solver_ledger 900 python -u tools/solver_ledger.py --out "$OUT/solver_ledger.json" || exit $?
+      ;;
+    *)
+      echo "unknown step $s"
+      exit 2
+      ;;
+  esac
+done
 echo "session done"
