@@ -65,6 +65,8 @@ int ssp_download(ssp_ctx* ctx, double* dst_host, const double* src_dev, size_t n
  * by rank 0 with ssp_comm_unique_id and distributed by the caller (e.g. torch.distributed). */
 #define SSP_UNIQUE_ID_BYTES 128
 int ssp_comm_unique_id(char* id_out);
+/* Collective: returns once every rank has joined, or SSP_ERR_COMM when the communicator has not formed
+ * within the communication deadline (ssp_ctx_set_comm_timeout; a rank is missing). */
 int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id);
 int ssp_ctx_rank(ssp_ctx* ctx);
 int ssp_ctx_nranks(ssp_ctx* ctx);

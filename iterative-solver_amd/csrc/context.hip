@@ -9,10 +9,14 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <thread>
 
 #include "ssp_internal.h"
 
@@ -161,8 +165,8 @@ int agree_exact_max(ssp_ctx* ctx) {
   return SSP_OK;
 }
 
-// The outcome of an RCCL call on the (non-blocking) communicator: ncclInProgress is waited out by
-// polling the communicator's state under the deadline; an error aborts the communicator.
+// The outcome of an RCCL call on the context's communicator: an error aborts it (every later exchange
+// fails at once); ncclInProgress (a non-blocking communicator's answer) is waited out under the deadline.
 int rccl_settle(ssp_ctx* ctx, ncclResult_t r, const char* what) {
   if (r == ncclSuccess) return SSP_OK;
   if (r != ncclInProgress) return comm_fail(ctx, std::string(what) + ": " + ncclGetErrorString(r));
@@ -566,44 +570,66 @@ int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id) {
   // A one-rank communicator is created too: its collectives run through RCCL like any other, which
   // is how the RCCL calls are exercised on a one-GPU machine (tests/test_rccl_gpu.py).
   //
-  // Non-blocking initialisation (config.blocking = 0), polled under the communication deadline: a rank
-  // that never joins ends the join of the others with SSP_ERR_COMM after ctx->comm_timeout_s
-  // (SSP_COMM_TIMEOUT_S) -- ncclCommAbort, no process left waiting -- where the blocking
-  // ncclCommInitRank would wait for ever.  The reference aborts the job on such an error
-  // (DistrArray.cpp:16-23).  Collectives on the non-blocking communicator may return ncclInProgress;
-  // rccl_settle waits for those under the same deadline.
-  ncclUniqueId uid;
-  std::memcpy(&uid, id, sizeof(uid));
-  ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
-  config.blocking = 0;
-  ncclResult_t r = ncclCommInitRankConfig(&ctx->comm, nranks, uid, rank, &config);
-  if (r != ncclSuccess && r != ncclInProgress) {
-    if (ctx->comm) ncclCommAbort(ctx->comm);
-    ctx->comm = nullptr;
-    return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+  // The join runs on a helper thread and this thread waits for it under the communication deadline
+  // (ctx->comm_timeout_s, SSP_COMM_TIMEOUT_S): a rank that never arrives ends the join of the others
+  // with SSP_ERR_COMM instead of a wait for ever (the reference aborts the job on a distributed error,
+  // DistrArray.cpp:16-23).  RCCL's init blocks in its bootstrap until every rank has checked in, and
+  // its non-blocking form (ncclConfig_t blocking = 0) does too (measured on the MI355X boxes:
+  // tools/rccl_alone_probe.py, profiles/r5/rccl_alone_probe.txt), so the deadline cannot be polled from
+  // inside RCCL.  The abandoned helper keeps the join's state alive on the heap; if the missing ranks
+  // ever arrive it aborts the late communicator itself.  A process whose join failed should end
+  // (bench.py: an error record, then os._exit).
+  struct Join {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclSuccess;
+    ncclUniqueId uid;
+    int nranks = 0, rank = 0, device = 0;
+  };
+  static const bool trace = std::getenv("SSP_COMM_TRACE") != nullptr;  // stage lines on stderr
+  auto say = [&](const char* what) {
+    if (trace) std::fprintf(stderr, "[ssp comm rank %d/%d %.3f] %s\n", rank, nranks, ssp::now_s(), what);
+  };
+  auto job = std::make_shared<Join>();
+  std::memcpy(&job->uid, id, sizeof(job->uid));
+  job->nranks = nranks;
+  job->rank = rank;
+  job->device = ctx->device;
+  say("ncclCommInitRank (helper thread)");
+  try {
+    std::thread([job] {
+      ncclComm_t c = nullptr;
+      ncclResult_t r = hipSetDevice(job->device) == hipSuccess ? ncclCommInitRank(&c, job->nranks, job->uid, job->rank)
+                                                                : ncclInvalidUsage;
+      std::lock_guard<std::mutex> lk(job->m);
+      job->comm = c;
+      job->r = r;
+      job->done = true;
+      if (job->abandoned && c) ncclCommAbort(c);
+      job->cv.notify_all();
+    }).detach();
+  } catch (const std::exception& e) {
+    return ssp::set_error(SSP_ERR_COMM, std::string("ssp_ctx_attach_comm: no helper thread: ") + e.what());
   }
-  const double t0 = ssp::now_s();
-  ncclResult_t state = ncclInProgress;
-  while (true) {
-    r = ncclCommGetAsyncError(ctx->comm, &state);
-    if (r != ncclSuccess || state != ncclInProgress) break;
-    if (ssp::now_s() - t0 > ctx->comm_timeout_s) {
-      ncclCommAbort(ctx->comm);
-      ctx->comm = nullptr;
-      char t[64];
-      std::snprintf(t, sizeof(t), "%g", ctx->comm_timeout_s);
-      return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRankConfig: rank ") + std::to_string(rank) + " of " +
-                                              std::to_string(nranks) + ": the communicator did not form within " + t +
-                                              " s (SSP_COMM_TIMEOUT_S): another rank is missing");
-    }
-    usleep(1000);
+  std::unique_lock<std::mutex> lk(job->m);
+  const auto limit = std::chrono::duration<double>(ctx->comm_timeout_s);
+  if (!job->cv.wait_for(lk, limit, [&] { return job->done; })) {
+    job->abandoned = true;
+    say("deadline: join abandoned");
+    char t[64];
+    std::snprintf(t, sizeof(t), "%g", ctx->comm_timeout_s);
+    return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRank: rank ") + std::to_string(rank) + " of " +
+                                            std::to_string(nranks) + ": the communicator did not form within " + t +
+                                            " s (SSP_COMM_TIMEOUT_S): another rank is missing");
   }
-  if (r != ncclSuccess || state != ncclSuccess) {
-    ncclCommAbort(ctx->comm);
-    ctx->comm = nullptr;
-    return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRankConfig: ") +
-                                            ncclGetErrorString(r != ncclSuccess ? r : state));
+  say("joined");
+  if (job->r != ncclSuccess) {
+    if (job->comm) ncclCommAbort(job->comm);
+    return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(job->r));
   }
+  ctx->comm = job->comm;
   return ssp::agree_exact_max(ctx);
 }
 

@@ -134,8 +134,8 @@ int flush_uploads(ssp_ctx* ctx);
 int allreduce_dev(ssp_ctx* ctx, double* buf, size_t n);
 // After an attach: every rank takes the smallest exact_max of the communicator's ranks.
 int agree_exact_max(ssp_ctx* ctx);
-// The outcome of an RCCL call on the context's non-blocking communicator (ncclInProgress waited out
-// under the deadline; an error aborts the communicator and returns SSP_ERR_COMM).
+// The outcome of an RCCL call on the context's communicator (an error aborts it and returns
+// SSP_ERR_COMM; ncclInProgress is waited out under the deadline).
 int rccl_settle(ssp_ctx* ctx, ncclResult_t r, const char* what);
 // Copies n doubles of ctx->result_dev to host `out` once every operation queued before it has
 // completed (publish kernel + host poll of a sequence flag; see context.hip).

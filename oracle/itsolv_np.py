@@ -225,7 +225,8 @@ class Davidson:
         self.action_dot_action = False
         self.hermitian = True
         self.record_eigenvalues = True
-        self.trace = {"eigenvalues": [], "errors": [], "nq": [], "nwork": []}
+        self.screened = 0  # new R vectors removed by the redundancy screen and as null, in all
+        self.trace = {"eigenvalues": [], "errors": [], "nq": [], "nwork": [], "screened": []}
 
     # -- dimensions
     @property
@@ -541,6 +542,7 @@ class Davidson:
                 null.append(a)
         for k in sorted(null, reverse=True):
             del idx[k]
+        self.screened += len(redundant) + len(null)
         for i in idx:
             nrm = np.sqrt(abs(residuals[i] @ residuals[i]))
             if nrm > 1e-14:
@@ -639,6 +641,7 @@ class Davidson:
             self.trace["errors"].append(list(self.errors))
             self.trace["nq"].append(self.nQ)
             self.trace["nwork"].append(len(self.working_set))
+            self.trace["screened"].append(self.screened)
         converged = nwork == 0 and max(self.errors) <= self.thresh
         return {"converged": converged, "iterations": self.iterations, "r_creations": self.r_creations,
                 "eigenvalues": list(self.eigvals), "errors": list(self.errors), "trace": self.trace}

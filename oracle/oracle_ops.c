@@ -50,7 +50,7 @@ int or_axpy(double alpha, const double* x, size_t nx, double* y, size_t ny) {
  * (tests/golden/make_traces.py: the "reordered" runs).  2 = sequential partial sums over consecutive
  * 1024-element blocks, the block sums folded pairwise: the shape of a blocked / threaded reduction
  * (an OpenMP-parallel build of the loop, numpy's pairwise sum) and of the GPU's ("reordered_blocked").
- * 100 + P (P = 2..64) = the reference's own distributed build on P MPI ranks: the index range split
+ * 100 + P (P = 2..64) = the reference's distributed build on P MPI ranks with rank-order sums: the index range split
  * by make_distribution_spread_remainder (util/Distribution.h:99-109), each rank's local
  * std::inner_product sequential, the P partials summed in rank order (DistrArray.cpp:124-138, the
  * MPI_Allreduce of util/gemm.h:179-182) ("mpiP" runs) -- one valid association of MPI_Allreduce.

@@ -12,6 +12,16 @@ for p in (ROOT, PKG, os.path.join(ROOT, "oracle")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
+    config.addinivalue_line("markers", "slow: minutes of CPU work at the configs' sizes; run with ITSOLV_SLOW=1")
+
+
+def pytest_collection_modifyitems(config, items):
+    if os.environ.get("ITSOLV_SLOW"):
+        return
+    skip = pytest.mark.skip(reason="slow (minutes of CPU work at the configs' sizes): set ITSOLV_SLOW=1")
+    for item in items:
+        if "slow" in item.keywords:
+            item.add_marker(skip)
 
 
 @pytest.fixture(scope="session")

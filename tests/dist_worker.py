@@ -215,12 +215,14 @@ def case_gpu_traces(comm):
 
 
 def case_gpu_exact_mpi(comm):
-    """The reference's own distributed build, bit for bit: on shards of at most ssp_ctx_set_exact_max
-    elements every rank computes in the reference's arithmetic and the transport adds the ranks'
-    partials in rank order (peer memory, host), so a sharded solve over P ranks must reproduce the CPU
-    path run with the dots of P MPI ranks (tests/golden/mpi_traces.json, make_traces.py --mpi-golden)
-    -- every iteration count, trace value, eigenvalue and residual norm to the last bit, including the
-    DIIS case whose step count the reference itself changes with the rank count (13, 13, 32, 12, 56)."""
+    """Rank-order sums, bit for bit: on shards of at most ssp_ctx_set_exact_max elements every rank
+    computes in the reference's arithmetic and the transport adds the ranks' partials in rank order
+    (peer memory, host hub) -- one valid association of the reference's MPI_Allreduce -- so a sharded
+    solve over P ranks must reproduce the CPU path run with its dots summed that way
+    (tests/golden/mpi_traces.json, make_traces.py --mpi-golden): every iteration count, trace value,
+    eigenvalue and error to the last bit, including the DIIS case whose step count the reference
+    itself changes with the association (rank order: 13, 13, 32, 12, 56 steps at P = 1, 2, 3, 4, 8;
+    MPICH's: 13, 13, 32, 46, 32 -- tests/golden/mpich_traces.json, tests/test_mpi_bridge*.py)."""
     import json
 
     import numpy as np
@@ -251,7 +253,8 @@ def case_gpu_exact_mpi(comm):
             if len(ref["trace"][f]):
                 assert np.array_equal(np.asarray(g["trace"][f]), np.asarray(ref["trace"][f])), (head, "trace", f)
         if rank == 0:
-            print(f"{head}: {g['iterations']} iterations, bit-identical to the {world}-rank CPU path", flush=True)
+            print(f"{head}: {g['iterations']} iterations, bit-identical to the CPU path with {world}-rank rank-order sums",
+                  flush=True)
     ctx.close()
 
 

@@ -253,9 +253,9 @@ def case_api_record():
 
 
 def case_exact_mpi():
-    """The bit-for-bit check of the reference's MPI build that the GPU runs (dist_worker
-    case_gpu_exact_mpi), through the product's host code over the emulation: sequential sums on each
-    rank, the partials added in rank order by the socket host communicator."""
+    """The bit-for-bit check of rank-order sums that the GPU runs (dist_worker case_gpu_exact_mpi),
+    through the product's host code over the emulation: sequential sums on each rank, the partials
+    added in rank order by the socket host communicator."""
     import dist_worker
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])

@@ -106,7 +106,7 @@ def options(c):
 # how far the REFERENCE algorithm itself moves under a change of rounding.
 VARIANTS = {"reordered": 1,          # 8 interleaved partial sums (a vectorising build)
             "reordered_blocked": 2,  # 1024-element blocks folded pairwise (a blocked / threaded build)
-            # the reference's own distributed build on P MPI ranks (rank-local sequential sums, partials
+            # the reference's distributed build on P MPI ranks with rank-order sums (rank-local sequential sums, partials
             # added in rank order: DistrArray.cpp:124-138 + MPI_Allreduce); generated for the RS cases
             # (--add-variants), whose residual norms move under them by more than under the two above
             "mpi2": 102, "mpi3": 103, "mpi4": 104, "mpi8": 108, "mpi16": 116}
@@ -226,11 +226,12 @@ def merge_parts(parts):
     return base["case"], out
 
 
-# Short-vector cases for the reference's own distributed build (tests/golden/mpi_traces.json): the
-# whole solve record -- every trace value -- of the CPU path with its dots summed as on P MPI ranks
-# (rank-local sequential sums added in rank order), P = 1 (sequential), 2, 3, 4, 8.  On shards of at
-# most ssp_ctx_set_exact_max elements the HIP path over a rank-order transport (peer memory, host)
-# must reproduce them bit for bit (tests/dist_worker.py case gpu_exact_mpi).
+# Short-vector cases for rank-order sums (tests/golden/mpi_traces.json): the whole solve record -- every
+# trace value -- of the CPU path with its dots summed as P ranks' partials added in rank order (one
+# valid MPI_Allreduce association), P = 1 (sequential), 2, 3, 4, 8.  On shards of at most
+# ssp_ctx_set_exact_max elements the HIP path over a rank-order transport (peer memory, host hub) must
+# reproduce them bit for bit (tests/dist_worker.py case gpu_exact_mpi).  MPICH's own association of the
+# same cases: tests/golden/make_mpi_traces.py -> mpich_traces.json.
 MPI_CASES = {
     "C1_rank1": CASES["C1_rank1"],
     "C1_rank8": CASES["C1_rank8"],

@@ -441,3 +441,60 @@ def test_gpu_optimize_same_steps_as_independent_restatement(ctx, mat, alg, q):
     assert first_divergence(gpu["trace"], ind["trace"]) >= k, (mat, alg, q)
     assert gpu["iterations"] <= ind["iterations"] + 3, (gpu["iterations"], ind["iterations"])
     _assert_opt_prefix(gpu, ind, k, (mat, alg, q))
+
+
+# ---- the host layer pinned at the BASELINE configs' sizes ------------------------------------------
+# The committed traces of C2 (N = 1e7), C3's shape at N = 1e7, C5 at N = 1e7 and the near-dependent
+# RS cases (N = 2^21, where the redundancy screen fires) come from the C++ oracle, which compiles the
+# product's own solvers.h / rspace.h / subspace.h over CPU handlers.  Here the numpy restatement, which
+# shares no code with them, runs the same problems at the same sizes -- above the 2^20 elements where
+# the product switches its fused passes on -- and is held to the same bar as the GPU runs
+# (tests/trace_check.py): convergence, iteration and R-creation counts, Q-space / working-set sizes and
+# the screening counts after every iteration, eigenvalues within 1e-10 relative after every iteration,
+# errors within the reordering tolerance.  About 9 minutes and 10 GB of CPU work (ITSOLV_SLOW=1; the
+# last run's output: profiles/r5/independent_config_traces.txt).
+CONFIG_TRACES = ("RS_n2e21_p16", "RS_n2e21_rho1", "C5_n1e7", "C2_rank8", "C3_n1e7_rank8")
+
+
+def independent_run(ref):
+    import trace_check as tc
+
+    c, o = ref["case"], ref["options"]
+    problem = dn.SyntheticProblem(c["n"], c["rho"], c["rank"], c["seed"], **tc.problem_kw(c))
+    if c["kind"] == "diis":
+        return dn.DIIS(o["convergence_threshold"], max_size_qspace=o["max_size_qspace"],
+                       **({"max_iter": o["max_iter"]} if "max_iter" in o else {})).solve(problem)
+    return dn.Davidson(o["nroots"], o["convergence_threshold"], max_size_qspace=o["max_size_qspace"],
+                       reset_D=o["reset_D"], max_p=o["max_p"]).solve(problem)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", CONFIG_TRACES)
+def test_independent_restatement_takes_the_config_traces(name):
+    import trace_check as tc
+
+    ref = tc.T[name]
+    ind = independent_run(ref)
+    g = {"converged": ind["converged"], "iterations": ind["iterations"], "trace": {
+        "eigenvalues": np.array(ind["trace"]["eigenvalues"]) if ind["trace"]["eigenvalues"] else np.zeros(0),
+        "errors": np.array(ind["trace"]["errors"])}}
+    assert g["converged"] == ref["converged"], name
+    assert g["iterations"] == ref["iterations"], (name, g["iterations"], ref["iterations"])
+    r = ref["trace"]
+    if tc.same_steps(ref):
+        assert ind["r_creations"] == ref["r_creations"], (name, ind["r_creations"], ref["r_creations"])
+        assert ind["trace"]["nq"] == r["nq"], (name, ind["trace"]["nq"], r["nq"])
+        assert ind["trace"]["nwork"] == r["nwork"], name
+        if "screened" in r:
+            assert ind["trace"]["screened"] == r["screened"], (name, ind["trace"]["screened"], r["screened"])
+    if r["eigenvalues"]:
+        re_ = np.array(r["eigenvalues"])
+        ge = np.array([row[:re_.shape[1]] for row in ind["trace"]["eigenvalues"]])
+        de = np.abs(ge - re_)
+        assert np.all(de <= tc.EIG_REL * np.maximum(np.abs(re_), 1.0)), (name, de.max())
+    rr = np.array(r["errors"])
+    gr = np.array([row[:rr.shape[1]] for row in ind["trace"]["errors"]])
+    tol = tc.error_tolerance(ref)
+    assert np.all(np.abs(gr - rr) <= tol), (name, float(np.max(np.abs(gr - rr) / tol)))
+    print(f"{name}: {g['iterations']} iterations, worst error deviation "
+          f"{float(np.max(np.abs(gr - rr) / tol)):.3g} of the tolerance")

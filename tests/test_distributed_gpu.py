@@ -95,10 +95,12 @@ def test_c5_full_size_on_8_shards_p2p():
                   env_extra={"SSP_TRACES_FULL": "C5", "SSP_COMM_TIMEOUT_S": "60"})[0])
 
 
-# ---- the reference's own distributed build, bit for bit (short vectors, rank-order transports) --------
+# ---- rank-order sums, bit for bit (short vectors, rank-order transports) ------------------------------
+# The CPU path with its dots summed as P ranks' partials added in rank order (mpi_traces.json) -- one
+# valid MPI_Allreduce association; MPICH's own, through the "mpi" transport, is test_mpi_bridge_gpu.py.
 @pytest.mark.parametrize("transport", ["host", "p2p"])
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_sharded_short_solves_are_the_reference_mpi_build(world, transport):
+def test_sharded_short_solves_rank_order_sums(world, transport):
     # C1's shards (N = 1e4 over P ranks) and S_p8's exceed the 2048-element default on 2 ranks
     out = run_hub("gpu_exact_mpi", world=world, timeout=600, transport=transport,
                   env_extra={"SSP_COMM_TIMEOUT_S": "60", "SSP_EXACT_MAX": "16384"})[0]

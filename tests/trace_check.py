@@ -27,7 +27,8 @@ EIG_REL, ERR_REL, ERR_ABS, DEV_FACTOR = 1e-10, 1e-6, 1e-13, 10.0
 
 
 # make_traces.py VARIANTS: valid sum orders of the CPU path -- a vectorising and a blocked build of its
-# loops, and (where generated: the RS cases) the reference's own distributed build on 2..16 MPI ranks
+# loops, and (where generated: the RS cases) the reference's distributed build on 2..16 MPI ranks with rank-order
+# sums (one valid MPI_Allreduce association)
 VARIANTS = ("reordered", "reordered_blocked", "mpi2", "mpi3", "mpi4", "mpi8", "mpi16")
 
 
