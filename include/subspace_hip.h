@@ -169,6 +169,15 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
  *                    bit-identical)                                           bytes 8N(1 + store + 2m) */
 int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store_x, double* const* yy, int m,
                   size_t n, double* out);
+/* Block transform of m vectors in place (the block self-orthonormalisation of the new R vectors,
+ * itsolv_hbm/hbm_handlers.h): x_j <- sum_{i<m} t[i*m + j] (xs_i x_i) for j < m, the outputs of each
+ * element formed from its loaded inputs before any is stored (the destinations are the sources), the
+ * sum by fused multiply-adds in order i = 0..m-1 (on vectors of at most exact_max elements each
+ * product rounded before its add).  With gram != NULL also gram[i*m + j] = <x_i', x_j'> of the new
+ * vectors (m x m, symmetric), summed over ranks, in the same pass.  1 <= m <= 8; xs may be null (all 1).
+ *                                                                          bytes 16 N m */
+int ssp_transform_gram(ssp_ctx* ctx, const double* t, double* const* xx, const double* xs, int m, size_t n,
+                       double* gram);
 /* Residuals and their norms (construct_residual + update_errors, reference
  * LinearEigensystemDavidson.h:186-192, IterativeSolverTemplate.h:95-102) in one pass:
  *   yy[j] = ys[j] yy[j] + c[j] (xs[j] xx[j])  (= ssp_axpy_scaled per pair, yy bit-identical),

@@ -735,6 +735,142 @@ __global__ __launch_bounds__(kBlock) void k_axpy_gram(const AxpyGramArgs a) {
   if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
 }
 
+// Block transform in place (the block self-orthonormalisation of the new R vectors,
+// itsolv_hbm/hbm_handlers.h fused_orthonormalise): x_j <- sum_{i<m} t(i,j) (s_i x_i), every output of a
+// position formed from that position's loaded inputs before any is stored, so the destinations are
+// the sources.  FMA: the sum by fused multiply-adds in order i = 0..m-1; without, each product rounded
+// before its add (the short-vector arithmetic).  GRAM: the M(M+1)/2 dots <x_a', x_b'> (a <= b, row by
+// row) of the stored outputs, folded per launch.
+struct TransformArgs {
+  double* x[ssp::kOuterDst];
+  double s[ssp::kOuterDst];                     // deferred input scales
+  double t[ssp::kOuterDst * ssp::kOuterDst];    // t[i * m + j]
+  int m;
+  size_t n;
+  double* partial;     // [gridDim.x][M (M + 1) / 2]
+  ssp::FoldTail tail;  // GRAM: fused fold
+};
+static_assert(sizeof(TransformArgs) <= 4000, "kernel argument block too large");
+
+template <bool FMA>
+__device__ __forceinline__ double tmul(double t, double x, double acc) {
+#pragma clang fp contract(off)
+  if constexpr (FMA) return fma(t, x, acc);
+  return acc + t * x;  // the product rounded before the add
+}
+
+// M = m exactly (instantiated for m = 1..8): no per-vector branch in the streaming loop.
+template <int M, bool GRAM, bool FMA>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_transform(const TransformArgs a) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  constexpr int NP = M * (M + 1) / 2;
+  constexpr int U = GRAM ? 1 : (M <= 4 ? 4 : 2);  // GRAM keeps every output of the window for the pair dots
+  double acc[GRAM ? NP : 1];
+#pragma unroll
+  for (int q = 0; q < (GRAM ? NP : 1); ++q) acc[q] = 0;
+  auto pairs = [&](const double (&y)[M]) {
+    if constexpr (GRAM) {
+      int q = 0;
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int j = i; j < M; ++j) {
+          acc[q] = fma(y[i], y[j], acc[q]);
+          ++q;
+        }
+    }
+  };
+  // Each output is stored as soon as it is formed (the GRAM instance keeps the window's outputs for
+  // the pair dots): far fewer live registers than forming all outputs first (tools/mb_transform.hip).
+  ssp::for_windows<U>(
+      a.n,
+      [&](size_t p0) {
+        double2 xv[U][M];
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+#pragma unroll
+          for (int u = 0; u < U; ++u) xv[u][i] = sc2<true>(ld2nt(a.x[i] + 2 * (p0 + 64 * u)), a.s[i]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          double ylo[M], yhi[M];
+#pragma unroll
+          for (int j = 0; j < M; ++j) {
+            double vl = 0, vh = 0;
+#pragma unroll
+            for (int i = 0; i < M; ++i) {
+              vl = tmul<FMA>(a.t[i * M + j], xv[u][i].x, vl);
+              vh = tmul<FMA>(a.t[i * M + j], xv[u][i].y, vh);
+            }
+            st2nt(a.x[j] + 2 * (p0 + 64 * u), make_double2(vl, vh));
+            ylo[j] = vl;
+            yhi[j] = vh;
+          }
+          pairs(ylo);
+          pairs(yhi);
+        }
+      },
+      [&](size_t p) {
+        double2 xv[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i) xv[i] = sc2<true>(ld2(a.x[i] + 2 * p), a.s[i]);
+        double ylo[M], yhi[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          double vl = 0, vh = 0;
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            vl = tmul<FMA>(a.t[i * M + j], xv[i].x, vl);
+            vh = tmul<FMA>(a.t[i * M + j], xv[i].y, vh);
+          }
+          *reinterpret_cast<double2*>(a.x[j] + 2 * p) = make_double2(vl, vh);
+          ylo[j] = vl;
+          yhi[j] = vh;
+        }
+        pairs(ylo);
+        pairs(yhi);
+      },
+      [&](size_t e) {
+        double x1[M], y1[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i) x1[i] = a.x[i][e] * a.s[i];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          double v = 0;
+#pragma unroll
+          for (int i = 0; i < M; ++i) v = tmul<FMA>(a.t[i * M + j], x1[i], v);
+          a.x[j][e] = v;
+          y1[j] = v;
+        }
+        pairs(y1);
+      });
+  if constexpr (GRAM) {
+    block_partials<NP>(acc, NP, a.partial);
+    if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+  }
+}
+
+template <int M>
+void launch_transform_m(ssp_ctx* ctx, unsigned grid, const TransformArgs& a, bool gram, bool exact) {
+  const dim3 g(grid), b(kBlock);
+  if (exact) hipLaunchKernelGGL((k_transform<M, false, false>), g, b, 0, ctx->stream, a);
+  else if (gram) hipLaunchKernelGGL((k_transform<M, true, true>), g, b, 0, ctx->stream, a);
+  else hipLaunchKernelGGL((k_transform<M, false, true>), g, b, 0, ctx->stream, a);
+}
+
+void launch_transform(ssp_ctx* ctx, int m, unsigned grid, const TransformArgs& a, bool gram, bool exact) {
+  switch (m) {
+    case 1: return launch_transform_m<1>(ctx, grid, a, gram, exact);
+    case 2: return launch_transform_m<2>(ctx, grid, a, gram, exact);
+    case 3: return launch_transform_m<3>(ctx, grid, a, gram, exact);
+    case 4: return launch_transform_m<4>(ctx, grid, a, gram, exact);
+    case 5: return launch_transform_m<5>(ctx, grid, a, gram, exact);
+    case 6: return launch_transform_m<6>(ctx, grid, a, gram, exact);
+    case 7: return launch_transform_m<7>(ctx, grid, a, gram, exact);
+    default: return launch_transform_m<8>(ctx, grid, a, gram, exact);
+  }
+}
+
 // Residuals and their norms in one pass (construct_residual + update_errors, reference
 // LinearEigensystemDavidson.h:186-192 and IterativeSolverTemplate.h:95-102): y_j = y_j s^y_j +
 // c_j (x_j s^x_j) -- ssp_axpy_scaled's fma, element for element -- then acc_j += y_j^2.
@@ -1422,6 +1558,53 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
   return ssp::reduce_fetch(ctx, out, size_t(m));
+}
+
+int ssp_transform_gram(ssp_ctx* ctx, const double* t, double* const* xx, const double* xs, int m, size_t n,
+                       double* gram) {
+  SSP_CHECK_CTX(ctx);
+  if (m < 1 || m > 8) return ssp::set_error(SSP_ERR_ARG, "ssp_transform_gram: 1 <= m <= 8");
+  if (!t) return ssp::set_error(SSP_ERR_ARG, "ssp_transform_gram: null t");
+  SSP_TRY(check_ptrs(const_cast<const double* const*>(xx), m, n, "ssp_transform_gram"));
+  for (int j = 0; j < m; ++j)
+    for (int i = 0; i < j; ++i)
+      if (xx[i] == xx[j]) return ssp::set_error(SSP_ERR_ARG, "ssp_transform_gram: repeated vector");
+  const bool exact = ssp::exact_mode(ctx, n);
+  TransformArgs a{};
+  a.m = m;
+  a.n = n;
+  for (int i = 0; i < m; ++i) {
+    a.x[i] = xx[i];
+    a.s[i] = xs ? xs[i] : 1.0;
+  }
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < m; ++j) a.t[i * m + j] = t[i * m + j];
+  const int np = m * (m + 1) / 2;
+  // the fused Gram only from the bandwidth kernel; short vectors take the reference's sequential dots
+  const bool fused = gram && !exact && n > 0;
+  ssp::FoldTail tail{};
+  if (n > 0) {
+    ssp::LedgerScope ls(ctx, gram ? "transform_gram" : "transform", 16.0 * n * m);
+    const unsigned grid = ssp::win_grid(ctx, n, fused ? 1 : (m <= 4 ? 4 : 2), 8);
+    if (fused) {
+      SSP_TRY(ssp::fold_begin(ctx, np, &tail));
+      SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * np));
+      a.partial = ctx->partial;
+      a.tail = tail;
+    }
+    launch_transform(ctx, m, grid, a, fused, exact);
+    SSP_TRY_HIP(hipGetLastError());
+  }
+  if (!gram) return SSP_OK;
+  if (!fused) {  // short (or empty) vectors: the Gram of the stored outputs as the reference's dots
+    std::vector<const double*> c(xx, xx + m);
+    return ssp_gemm_inner(ctx, c.data(), m, c.data(), m, n, gram);
+  }
+  std::vector<double> pr(static_cast<size_t>(np));
+  SSP_TRY(ssp::fold_finish(ctx, tail, pr.data()));
+  for (int i = 0, q = 0; i < m; ++i)
+    for (int j = i; j < m; ++j, ++q) gram[size_t(i) * m + j] = gram[size_t(j) * m + i] = pr[size_t(q)];
+  return SSP_OK;
 }
 
 }  // extern "C"

@@ -202,20 +202,24 @@ inline bool fused_residual_norms(array::ArrayHandler<Vec, Vec>&, const std::vect
 // of propose_rspace.h:481-512 fires), whose tolerance includes the reference's own distributed
 // builds on 2..16 ranks: one pass 0.1x, two passes 0.02x of the bar.
 inline bool orthonormalise_two_pass(const itsolv::VecRef<Vec>& rr, double norm_thresh, std::vector<int>& null_params);
+inline bool orthonormalise_block(const itsolv::VecRef<Vec>& rr, double norm_thresh, std::vector<double>& g0);
 
 inline bool fused_orthonormalise(array::ArrayHandler<Vec, Vec>&, const itsolv::VecRef<Vec>& rr, double norm_thresh,
                                  std::vector<int>& null_params) {
   const size_t nR = rr.size();
   if (nR == 0) return true;
-  // SSP_ORTHO=one_pass | two_pass overrides the size rule (A/B runs, tests); the rule looks at the
-  // global length, so every rank of a sharded solve takes the same branch.
+  // SSP_ORTHO=block | one_pass | two_pass overrides the size rule (A/B runs, tests); the rule looks at
+  // the global length, so every rank of a sharded solve takes the same branch.
   static const int forced = [] {
     const char* e = std::getenv("SSP_ORTHO");
     if (!e) return 0;
-    return std::string(e) == "one_pass" ? 1 : std::string(e) == "two_pass" ? 2 : 0;
+    const std::string v(e);
+    return v == "one_pass" ? 1 : v == "two_pass" ? 2 : v == "block" ? 3 : 0;
   }();
   if (forced == 2 || (forced == 0 && rr[0].get().size() < fused_min_size()))
     return orthonormalise_two_pass(rr, norm_thresh, null_params);
+  std::vector<double> g0;  // <r_0, r_j>, when the block form has measured it before declining
+  if (forced != 1 && nR >= 2 && nR <= 8 && orthonormalise_block(rr, norm_thresh, g0)) return true;
   ssp_ctx* ctx = rr[0].get().ctx();
   const size_t n = rr[0].get().local_size();
   // g[j - i] = <r_i, r_j> for j >= i: the Gram row of the vector being normalised.
@@ -227,7 +231,7 @@ inline bool fused_orthonormalise(array::ArrayHandler<Vec, Vec>&, const itsolv::V
     check(ssp_gemm_inner(ctx, &x, 1, y.data(), int(y.size()), n, g.data()), "ssp_gemm_inner");
     return g;
   };
-  std::vector<double> g = gram_row(0);
+  std::vector<double> g = g0.size() == nR ? g0 : gram_row(0);
   for (size_t i = 0; i < nR; ++i) {
     const double nrm = std::sqrt(std::abs(g[0]));
     if (nrm > norm_thresh) {
@@ -251,6 +255,86 @@ inline bool fused_orthonormalise(array::ArrayHandler<Vec, Vec>&, const itsolv::V
       if (i + 1 < nR) g = gram_row(i + 1);
     }
   }
+  return true;
+}
+
+// Upper Cholesky factor u (row-major m x m) of the Gram matrix g of m vectors, column by column:
+// u_jj^2 = g_jj - sum_{k<j} u_kj^2 is the squared norm of vector j after its components along the
+// vectors before it are removed -- the norm the sequential MGS (propose_rspace.h:450-465) computes
+// and tests against norm_thresh.  False, with nothing decided, when such a norm is not resolved with
+// a wide margin from g's rounding: below 1e-8 of g_jj (a relative norm of 1e-4), or within a factor
+// 1e4 of norm_thresh.
+inline bool mgs_cholesky(const std::vector<double>& g, size_t m, double norm_thresh, std::vector<double>& u) {
+  u.assign(m * m, 0.0);
+  for (size_t j = 0; j < m; ++j) {
+    for (size_t k = 0; k < j; ++k) {
+      double v = g[k * m + j];
+      for (size_t l = 0; l < k; ++l) v -= u[l * m + k] * u[l * m + j];
+      u[k * m + j] = v / u[k * m + k];
+    }
+    double d = g[j * m + j];
+    for (size_t k = 0; k < j; ++k) d -= u[k * m + j] * u[k * m + j];
+    if (!(d >= 1e-8 * g[j * m + j]) || !(d > 1e8 * norm_thresh * norm_thresh)) return false;
+    u[j * m + j] = std::sqrt(d);
+  }
+  return true;
+}
+
+// t = u^-1 for an upper-triangular u (row-major m x m), column by column.
+inline std::vector<double> upper_inverse(const std::vector<double>& u, size_t m) {
+  std::vector<double> t(m * m, 0.0);
+  for (size_t j = 0; j < m; ++j) {
+    t[j * m + j] = 1.0 / u[j * m + j];
+    for (size_t i = j; i-- > 0;) {
+      double v = 0;
+      for (size_t k = i + 1; k <= j; ++k) v += u[i * m + k] * t[k * m + j];
+      t[i * m + j] = -v / u[i * m + i];
+    }
+  }
+  return t;
+}
+
+// Block self-orthonormalisation of the new R vectors (extension): the sequential MGS
+// of propose_rspace.h:450-465 as a Cholesky QR, twice.  With G the Gram matrix of R = (r_0 .. r_m-1)
+// and G = U^T U, the MGS result is Q = R U^-1 in exact arithmetic (the QR factorisation with a positive
+// diagonal is unique); the second round, on the Gram matrix of the stored first result, removes what
+// the first left of the rounding (CholeskyQR2: orthonormal to working precision while the vectors are
+// conditioned to well below 1e8).  Passes: the Gram matrix (gemm_inner), the transform with the new
+// Gram matrix in the same pass (ssp_transform_gram), the second transform -- 40 N m bytes and 2
+// reductions for m vectors, against 8 N (m + 3m(m-1)/2 ...) and m reductions for the one-pass MGS (C3,
+// m = 8: 320 N against 624 N bytes, 2 against 8 reductions).  Declines (false) whenever a norm MGS
+// would compute is not resolved with a wide margin (mgs_cholesky) -- near-dependent vectors, a null
+// vector -- leaving the vectors untouched and g0 = <r_0, r_j> for the sequential form, which then
+// decides exactly as before.  The decision comes from reduced (rank-identical) Gram matrices, so every
+// rank of a sharded solve takes the same branch.
+inline bool orthonormalise_block(const itsolv::VecRef<Vec>& rr, double norm_thresh, std::vector<double>& g0) {
+  const size_t m = rr.size();
+  ssp_ctx* ctx = rr[0].get().ctx();
+  const size_t n = rr[0].get().local_size();
+  std::vector<double> g(m * m), u;
+  {
+    itsolv::CVecRef<Vec> c;
+    for (auto& r : rr) c.emplace_back(r.get());
+    std::vector<double> xs;
+    auto xp = detail::deferred_ptrs(c, xs);
+    check(ssp_gemm_inner_scaled(ctx, xp.data(), xs.data(), int(m), xp.data(), xs.data(), int(m), n, g.data()),
+          "ssp_gemm_inner_scaled");
+  }
+  if (!mgs_cholesky(g, m, norm_thresh, u)) {
+    g0.assign(g.begin(), g.begin() + long(m));
+    return false;
+  }
+  std::vector<double> ys;
+  auto yp = detail::rw_deferred_ptrs(rr, ys);
+  std::vector<double> t = upper_inverse(u, m);
+  check(ssp_transform_gram(ctx, t.data(), yp.data(), ys.data(), int(m), n, g.data()), "ssp_transform_gram");
+  detail::scales_applied(rr);
+  if (!mgs_cholesky(g, m, norm_thresh, u)) {  // not expected after the first round: MGS finishes it
+    g0.assign(g.begin(), g.begin() + long(m));
+    return false;
+  }
+  t = upper_inverse(u, m);
+  check(ssp_transform_gram(ctx, t.data(), yp.data(), nullptr, int(m), n, nullptr), "ssp_transform_gram");
   return true;
 }
 

@@ -385,6 +385,26 @@ int ssp_axpy_gram(ssp_ctx* c, const double* cc, double* x, double xs, int store_
   for (int j = 0; j < m; ++j) out[j] = dot_n(yy[0], yy[j], n);
   return reduce(c, out, size_t(m));
 }
+int ssp_transform_gram(ssp_ctx* c, const double* t, double* const* xx, const double* xs, int m, size_t n,
+                       double* gram) {
+  if (m < 1 || m > 8 || !t) return fail(SSP_ERR_ARG, "ssp_transform_gram: bad arguments");
+  Led l(c, gram ? "transform_gram" : "transform", 16.0 * n * m);
+  trace("transform", {}, {}, nullptr, 0, xx, m);
+  // x_j <- sum_i t(i,j) (xs_i x_i), in order i = 0..m-1 (madd: the build's multiply-add), per element
+  std::vector<double> in(static_cast<size_t>(m));
+  for (size_t e = 0; e < n; ++e) {
+    for (int i = 0; i < m; ++i) in[size_t(i)] = xx[i][e] * (xs ? xs[i] : 1.0);
+    for (int j = 0; j < m; ++j) {
+      double v = 0;
+      for (int i = 0; i < m; ++i) v = madd(t[size_t(i) * m + j], in[size_t(i)], v);
+      xx[j][e] = v;
+    }
+  }
+  if (!gram) return SSP_OK;
+  for (int i = 0; i < m; ++i)
+    for (int j = i; j < m; ++j) gram[size_t(i) * m + j] = gram[size_t(j) * m + i] = dot_n(xx[i], xx[j], n);
+  return reduce(c, gram, size_t(m) * m);
+}
 int ssp_axpy_pairs_norm(ssp_ctx* c, const double* cc, const double* const* xx, const double* xs, double* const* yy,
                         const double* ys, int m, size_t n, double* out) {
   if (m < 0 || (m > 0 && (!cc || !out))) return fail(SSP_ERR_ARG, "ssp_axpy_pairs_norm: bad arguments");

@@ -57,3 +57,53 @@ def test_fused_passes_take_the_call_by_call_steps():
     c, d = fused["diis"], plain["diis"]
     assert c["converged"] and d["converged"] and c["iterations"] == d["iterations"], (c["iterations"], d["iterations"])
     assert max(abs(x - y) for x, y in zip(c["x_head"], d["x_head"])) <= 1e-10
+
+
+# ---- ssp_transform_gram: the block self-orthonormalisation's pass (hbm_handlers.h orthonormalise_block)
+@pytest.mark.parametrize("m,n,gram", [(8, 1_000_003, True), (3, 777_777, True), (5, 64, True), (7, 300_001, False),
+                                      (8, 2048, True)])
+def test_transform_gram_in_place(ctx, m, n, gram):
+    import numpy as np
+
+    rng = np.random.default_rng(m * 1000 + n % 997)
+    X = rng.uniform(-1, 1, (m, n))
+    t = np.triu(rng.uniform(-1, 1, (m, m))) + 2 * np.eye(m)
+    s = rng.uniform(0.5, 2.0, m)
+    xs = [ctx.upload(v) for v in X]
+    g = ctx.transform_gram(t, xs, s, gram=gram)
+    got = np.array([ctx.download(v) for v in xs])
+    if n <= 2048:  # the short-vector arithmetic: each product rounded, added in order i = 0..m-1
+        ref = np.zeros_like(X)
+        for i in range(m):
+            ref = ref + t[i][:, None] * (X[i] * s[i])[None, :]
+        assert np.array_equal(got, ref)
+    else:
+        ref = t.T @ (X * s[:, None])
+        assert np.max(np.abs(got - ref)) <= 1e-13 * np.max(np.abs(t).sum(0)) * 2
+    if gram:
+        want = got @ got.T
+        assert np.all(np.abs(g - want) <= 1e-12 * n), np.max(np.abs(g - want))
+        assert np.array_equal(g, g.T)
+
+
+def test_block_orthonormalisation_is_mgs_in_exact_arithmetic(ctx):
+    # CholeskyQR2 of 8 well-conditioned vectors (what orthonormalise_block runs): orthonormal to
+    # working precision, and the same vectors as the sequential MGS up to rounding
+    import numpy as np
+
+    m, n = 8, 2_000_003
+    rng = np.random.default_rng(11)
+    X = rng.uniform(-1, 1, (m, n)) + 0.3 * rng.uniform(-1, 1, n)[None, :]  # correlated columns
+    xs = [ctx.upload(v) for v in X]
+    G = np.array([[ctx.dot(a, b) for b in xs] for a in xs])
+    for _ in range(2):
+        U = np.linalg.cholesky(G).T
+        G = ctx.transform_gram(np.linalg.inv(U), xs)
+    Q = np.array([ctx.download(v) for v in xs])
+    assert np.max(np.abs(Q @ Q.T - np.eye(m))) < 1e-13
+    mgs = X.copy()
+    for i in range(m):
+        mgs[i] /= np.linalg.norm(mgs[i])
+        for j in range(i + 1, m):
+            mgs[j] -= (mgs[i] @ mgs[j]) * mgs[i]
+    assert np.max(np.abs(Q - mgs)) < 1e-10

@@ -37,13 +37,14 @@ def test_single_rank_api_and_loop_parity(ortho):
     assert r.returncode == 0 and "api OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
 
 
-@pytest.mark.parametrize("ortho", ["one_pass", "two_pass"])
+@pytest.mark.parametrize("ortho", ["block", "one_pass", "two_pass"])
 @pytest.mark.parametrize("arith", ["0,0", "1,1"])
 def test_fused_passes_hold_the_redundancy_screen_traces(arith, ortho):
     # traces.json RS_* (N = 2^21, near-dependent R vectors: the redundancy screen removes 6 and 3 of
     # them): the product's fused numerics, which switch on from 2^20 elements, take the reference CPU
     # path's steps -- screened counts, Q sizes, working sets -- in the reference's arithmetic and in
-    # a GPU-like one (8-lane sums, fma), with either self-orthonormalisation form
+    # a GPU-like one (8-lane sums, fma), with each self-orthonormalisation form (the block
+    # form declines on most of these near-dependent sets and hands them to the sequential one)
     r = subprocess.run([sys.executable, WORKER, "rs_traces", arith], capture_output=True, text=True, timeout=900,
                        env=dict(os.environ, SSP_ORTHO=ortho))
     assert r.returncode == 0 and "rs_traces OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

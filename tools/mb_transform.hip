@@ -1,0 +1,200 @@
+// The block self-orthonormalisation's transform (x_j <- sum_i t(i,j) x_i for 8 vectors, optionally with
+// the 36 pair dots of the outputs) under access variants (development tool, not part of the library):
+//   NL  loads   1 nontemporal (library) | 0 plain
+//   NS  stores  1 nontemporal (library) | 0 plain
+//   OOP 0 in place (library) | 1 into 8 other vectors
+//   U   windows of 64 lanes x 16 B per vector per wave visit
+//   H   1: one double per lane per position (8-byte accesses, half the registers per position)
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_transform.hip -o tools/mb_transform
+// Run:   tools/mb_transform [reps=10]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e = (x);                                                              \
+    if (e != hipSuccess) {                                                           \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+typedef double d2v __attribute__((ext_vector_type(2)));
+template <int NT>
+__device__ __forceinline__ double2 ld2(const double* p) {
+  if constexpr (NT) {
+    const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
+    return make_double2(v.x, v.y);
+  } else {
+    return *reinterpret_cast<const double2*>(p);
+  }
+}
+template <int NT>
+__device__ __forceinline__ void st2(double* p, double2 v) {
+  if constexpr (NT) {
+    d2v w = {v.x, v.y};
+    __builtin_nontemporal_store(w, reinterpret_cast<d2v*>(p));
+  } else {
+    *reinterpret_cast<double2*>(p) = v;
+  }
+}
+template <int NT>
+__device__ __forceinline__ double ld1(const double* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <int NT>
+__device__ __forceinline__ void st1(double* p, double v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+constexpr int M = 8, NP = 36;
+struct TArgs {
+  double* x[M];
+  double* y[M];
+  double t[M * M];
+  size_t n;
+  double* partial;
+};
+
+template <int GRAM, int NL, int NS, int OOP, int U, int H>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_t(const TArgs a) {
+  const int lane = threadIdx.x & 63;
+  const size_t gw = size_t(blockIdx.x) * 4 + (threadIdx.x >> 6), nw = size_t(gridDim.x) * 4;
+  double acc[GRAM ? NP : 1];
+#pragma unroll
+  for (int q = 0; q < (GRAM ? NP : 1); ++q) acc[q] = 0;
+  auto pairs = [&](const double (&y)[M]) {
+    if constexpr (GRAM) {
+      int q = 0;
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int j = i; j < M; ++j) {
+          acc[q] = fma(y[i], y[j], acc[q]);
+          ++q;
+        }
+    }
+  };
+  if constexpr (H) {  // one double per lane per position
+    const size_t win = 64 * U, nwin = a.n / win;
+    for (size_t c = gw; c < nwin; c += nw) {
+      const size_t p0 = c * win + lane;
+      double xv[U][M];
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u][i] = ld1<NL>(a.x[i] + p0 + 64 * u);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        double y[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          double v = 0;
+#pragma unroll
+          for (int i = 0; i < M; ++i) v = fma(a.t[i * M + j], xv[u][i], v);
+          y[j] = v;
+          st1<NS>((OOP ? a.y[j] : a.x[j]) + p0 + 64 * u, v);
+        }
+        pairs(y);
+      }
+    }
+  } else {
+    const size_t win = 64 * U, nwin = (a.n / 2) / win;
+    for (size_t c = gw; c < nwin; c += nw) {
+      const size_t p0 = c * win + lane;
+      double2 xv[U][M];
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u][i] = ld2<NL>(a.x[i] + 2 * (p0 + 64 * u));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        double ylo[M], yhi[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          double vl = 0, vh = 0;
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            vl = fma(a.t[i * M + j], xv[u][i].x, vl);
+            vh = fma(a.t[i * M + j], xv[u][i].y, vh);
+          }
+          ylo[j] = vl;
+          yhi[j] = vh;
+          st2<NS>((OOP ? a.y[j] : a.x[j]) + 2 * (p0 + 64 * u), make_double2(vl, vh));
+        }
+        pairs(ylo);
+        pairs(yhi);
+      }
+    }
+  }
+  if constexpr (GRAM) {  // per-thread partials (no fold: the cost of the pass itself)
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+      if (acc[q] == 12345.678) a.partial[q] = acc[q];  // keep the dots alive
+  }
+}
+
+template <int GRAM, int NL, int NS, int OOP, int U, int H>
+void run(const char* name, TArgs a, int grid, int reps, hipStream_t s) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> t;
+  for (int r = 0; r < reps + 2; ++r) {
+    CK(hipEventRecord(e0, s));
+    hipLaunchKernelGGL((k_t<GRAM, NL, NS, OOP, U, H>), dim3(grid), dim3(256), 0, s, a);
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (r >= 2) t.push_back(ms);
+  }
+  std::sort(t.begin(), t.end());
+  const float med = t[t.size() / 2];
+  printf("%-10zu %-28s grid %5d  %8.4f ms  %7.1f GB/s\n", a.n, name, grid, med, 16.0 * M * a.n / med / 1e6);
+}
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 10;
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  const size_t nmax = 100000000;
+  TArgs a{};
+  for (int i = 0; i < M; ++i) {
+    CK(hipMalloc(&a.x[i], nmax * sizeof(double)));
+    CK(hipMalloc(&a.y[i], nmax * sizeof(double)));
+    CK(hipMemset(a.x[i], 0, nmax * sizeof(double)));
+    CK(hipMemset(a.y[i], 0, nmax * sizeof(double)));
+  }
+  CK(hipMalloc(&a.partial, 4096));
+  for (int q = 0; q < M * M; ++q) a.t[q] = (q % 9 == 0) ? 1.0 : 1e-3;
+  for (size_t n : {size_t(100000000), size_t(12500000)}) {
+    a.n = n;
+    for (int per_cu : {8, 4}) {
+      const int g = cus * per_cu;
+      run<0, 1, 1, 0, 2, 0>("plain NL NS inplace U2", a, g, reps, s);
+      run<0, 0, 0, 0, 2, 0>("plain ld st inplace U2", a, g, reps, s);
+      run<0, 1, 0, 0, 2, 0>("plain NL st inplace U2", a, g, reps, s);
+      run<0, 1, 1, 1, 2, 0>("plain NL NS oop U2", a, g, reps, s);
+      run<0, 1, 1, 0, 1, 0>("plain NL NS inplace U1", a, g, reps, s);
+      run<0, 1, 1, 0, 2, 1>("plain NL NS inplace U2 half", a, g, reps, s);
+      run<0, 1, 1, 0, 4, 1>("plain NL NS inplace U4 half", a, g, reps, s);
+      run<1, 1, 1, 0, 1, 0>("gram NL NS inplace U1", a, g, reps, s);
+      run<1, 0, 0, 0, 1, 0>("gram ld st inplace U1", a, g, reps, s);
+      run<1, 1, 1, 1, 1, 0>("gram NL NS oop U1", a, g, reps, s);
+      run<1, 1, 1, 0, 1, 1>("gram NL NS inplace U1 half", a, g, reps, s);
+      run<1, 1, 1, 0, 2, 1>("gram NL NS inplace U2 half", a, g, reps, s);
+      run<1, 0, 0, 0, 2, 1>("gram ld st inplace U2 half", a, g, reps, s);
+    }
+  }
+  return 0;
+}
