@@ -17,6 +17,7 @@
 // through LDS, workgroups by a fixed-order second pass (ssp::launch_reduce_partials): bitwise
 // reproducible, and identical on every rank after the RCCL allreduce.
 #include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 #include <vector>
 
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner_row(const InnerArgs a) {
     for (int w = 1; w < kBlock / 64; ++w) v += red[w][threadIdx.x];
     ssp::store_partial(a.partial + size_t(blockIdx.x) * K + threadIdx.x, v);
   }
-  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+  if (a.tail.counter) ssp::fold_tail<K>(a.partial, a.tail);
 }
 
 template <int K, bool SC = false>
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner_row_win(const InnerArgs a
     for (int w = 1; w < kBlock / 64; ++w) v += red[w][threadIdx.x];
     ssp::store_partial(a.partial + size_t(blockIdx.x) * K + threadIdx.x, v);
   }
-  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+  if (a.tail.counter) ssp::fold_tail<K>(a.partial, a.tail);
 }
 
 struct OuterArgs {
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(kBlock) void k_axpy_inner(const AxpyInnerArgs a) {
     for (int w = 1; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
     ssp::store_partial(a.partial + size_t(blockIdx.x) * a.m + threadIdx.x, s);
   }
-  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+  if (a.tail.counter) ssp::fold_tail<(M < 8 ? M : 8)>(a.partial, a.tail);
 }
 
 // Per-block sums of acc[0..M) over the block's waves into partial[block][m].
@@ -583,7 +584,7 @@ __global__ __launch_bounds__(kBlock) void k_scal_inner(const ScalInnerArgs a) {
         for (int j = 0; j < a.m; ++j) acc[j] = fma(xs, a.y[j][e], acc[j]);
       });
   block_partials<M>(acc, a.m, a.partial);
-  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+  if (a.tail.counter) ssp::fold_tail<(M < 8 ? M : 8)>(a.partial, a.tail);
 }
 
 // y_j += c_j x; acc += y_0_new^2.
@@ -732,7 +733,7 @@ __global__ __launch_bounds__(kBlock) void k_axpy_gram(const AxpyGramArgs a) {
         }
       });
   block_partials<M>(acc, a.m, a.partial);
-  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+  if (a.tail.counter) ssp::fold_tail<(M < 8 ? M : 8)>(a.partial, a.tail);
 }
 
 // Block transform in place (the block self-orthonormalisation of the new R vectors,
@@ -744,7 +745,7 @@ __global__ __launch_bounds__(kBlock) void k_axpy_gram(const AxpyGramArgs a) {
 struct TransformArgs {
   double* x[ssp::kOuterDst];
   double s[ssp::kOuterDst];                     // deferred input scales
-  double t[ssp::kOuterDst * ssp::kOuterDst];    // t[i * m + j]
+  double t[ssp::kOuterDst * ssp::kOuterDst];    // transposed: t[j * m + i] = t(i, j)
   int m;
   size_t n;
   double* partial;     // [gridDim.x][M (M + 1) / 2]
@@ -757,6 +758,22 @@ __device__ __forceinline__ double tmul(double t, double x, double acc) {
 #pragma clang fp contract(off)
   if constexpr (FMA) return fma(t, x, acc);
   return acc + t * x;  // the product rounded before the add
+}
+
+// Coefficient column j (t(0..M-1, j), contiguous in the transposed layout), read from the kernel-argument
+// segment where it is used.  The 64 coefficients of an 8-vector transform are more than the SGPR file
+// holds beside the pointers; left to itself the compiler keeps them in VGPR lanes and re-reads every one
+// with two v_readlane per fma (2576 readlanes in the 8-vector window loop, against 256 fmas).  The empty
+// asm makes the segment pointer opaque at each column, so the column is fetched by s_load_dwordx16 right
+// before its fmas (kept in SGPRs, used as scalar operands) and dies after them: no readlanes, 385 instead
+// of 2957 instructions per window loop.  TransformArgs is the kernel's only argument (offset 0).
+typedef const __attribute__((address_space(4))) double* kernarg_dp;
+template <int M>
+__device__ __forceinline__ kernarg_dp transform_column(int j) {
+  kernarg_dp tp = (kernarg_dp)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                               offsetof(TransformArgs, t));
+  asm volatile("" : "+s"(tp));
+  return tp + j * M;
 }
 
 // M = m exactly (instantiated for m = 1..8): no per-vector branch in the streaming loop.
@@ -781,8 +798,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
         }
     }
   };
-  // Each output is stored as soon as it is formed (the GRAM instance keeps the window's outputs for
-  // the pair dots): far fewer live registers than forming all outputs first (tools/mb_transform.hip).
+  // Output j of every position of the window is formed and stored with column j's coefficients, then
+  // column j + 1 (the GRAM instance keeps the window's outputs for the pair dots).
   ssp::for_windows<U>(
       a.n,
       [&](size_t p0) {
@@ -791,24 +808,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
         for (int i = 0; i < M; ++i)
 #pragma unroll
           for (int u = 0; u < U; ++u) xv[u][i] = sc2<true>(ld2nt(a.x[i] + 2 * (p0 + 64 * u)), a.s[i]);
+        double ylo[M], yhi[M];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          double ylo[M], yhi[M];
+        for (int j = 0; j < M; ++j) {
+          const kernarg_dp tc = transform_column<M>(j);
 #pragma unroll
-          for (int j = 0; j < M; ++j) {
+          for (int u = 0; u < U; ++u) {
             double vl = 0, vh = 0;
 #pragma unroll
             for (int i = 0; i < M; ++i) {
-              vl = tmul<FMA>(a.t[i * M + j], xv[u][i].x, vl);
-              vh = tmul<FMA>(a.t[i * M + j], xv[u][i].y, vh);
+              vl = tmul<FMA>(tc[i], xv[u][i].x, vl);
+              vh = tmul<FMA>(tc[i], xv[u][i].y, vh);
             }
             st2nt(a.x[j] + 2 * (p0 + 64 * u), make_double2(vl, vh));
-            ylo[j] = vl;
+            ylo[j] = vl;  // (GRAM: U = 1)
             yhi[j] = vh;
           }
-          pairs(ylo);
-          pairs(yhi);
         }
+        pairs(ylo);
+        pairs(yhi);
       },
       [&](size_t p) {
         double2 xv[M];
@@ -817,11 +835,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
         double ylo[M], yhi[M];
 #pragma unroll
         for (int j = 0; j < M; ++j) {
+          const kernarg_dp tc = transform_column<M>(j);
           double vl = 0, vh = 0;
 #pragma unroll
           for (int i = 0; i < M; ++i) {
-            vl = tmul<FMA>(a.t[i * M + j], xv[i].x, vl);
-            vh = tmul<FMA>(a.t[i * M + j], xv[i].y, vh);
+            vl = tmul<FMA>(tc[i], xv[i].x, vl);
+            vh = tmul<FMA>(tc[i], xv[i].y, vh);
           }
           *reinterpret_cast<double2*>(a.x[j] + 2 * p) = make_double2(vl, vh);
           ylo[j] = vl;
@@ -836,9 +855,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
         for (int i = 0; i < M; ++i) x1[i] = a.x[i][e] * a.s[i];
 #pragma unroll
         for (int j = 0; j < M; ++j) {
+          const kernarg_dp tc = transform_column<M>(j);
           double v = 0;
 #pragma unroll
-          for (int i = 0; i < M; ++i) v = tmul<FMA>(a.t[i * M + j], x1[i], v);
+          for (int i = 0; i < M; ++i) v = tmul<FMA>(tc[i], x1[i], v);
           a.x[j][e] = v;
           y1[j] = v;
         }
@@ -846,16 +866,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
       });
   if constexpr (GRAM) {
     block_partials<NP>(acc, NP, a.partial);
-    if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+    // launched with at most 4 workgroups per CU (launch_transform): one trip per 8 outputs
+    if (a.tail.counter) ssp::fold_tail<(NP < 8 ? NP : 8), 4>(a.partial, a.tail);
   }
+}
+
+// The fused-Gram instance runs one resident round of workgroups (its occupancy per CU, at most 4):
+// each workgroup streams an equal share, and the last arriver folds the few partials in one load
+// trip per 8 outputs (fold_tail<8, 4>) -- with 8 workgroups per CU the fold of the 36 dots took
+// 20 dependent trips, 70 us of a 340 us launch at the C4 shard.
+template <int M>
+unsigned gram_grid(ssp_ctx* ctx, size_t n) {
+  static int per_cu = 0;  // resident workgroups per CU of k_transform<M, true, true>
+  if (per_cu == 0) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_transform<M, true, true>, kBlock, 0) != hipSuccess || occ < 1)
+      occ = 2;
+    per_cu = occ < 4 ? occ : 4;
+  }
+  return ssp::win_grid(ctx, n, 1, unsigned(per_cu));
 }
 
 template <int M>
 void launch_transform_m(ssp_ctx* ctx, unsigned grid, const TransformArgs& a, bool gram, bool exact) {
-  const dim3 g(grid), b(kBlock);
-  if (exact) hipLaunchKernelGGL((k_transform<M, false, false>), g, b, 0, ctx->stream, a);
-  else if (gram) hipLaunchKernelGGL((k_transform<M, true, true>), g, b, 0, ctx->stream, a);
-  else hipLaunchKernelGGL((k_transform<M, false, true>), g, b, 0, ctx->stream, a);
+  const dim3 b(kBlock);
+  if (exact) hipLaunchKernelGGL((k_transform<M, false, false>), dim3(grid), b, 0, ctx->stream, a);
+  else if (gram) hipLaunchKernelGGL((k_transform<M, true, true>), dim3(gram_grid<M>(ctx, a.n)), b, 0, ctx->stream, a);
+  else hipLaunchKernelGGL((k_transform<M, false, true>), dim3(grid), b, 0, ctx->stream, a);
 }
 
 void launch_transform(ssp_ctx* ctx, int m, unsigned grid, const TransformArgs& a, bool gram, bool exact) {
@@ -937,7 +974,7 @@ __global__ __launch_bounds__(kBlock) void k_axpy_pairs_norm(const AxpyPairsArgs 
         }
       });
   block_partials<M>(acc, a.m, a.partial);
-  if (a.tail.counter) ssp::fold_tail(a.partial, a.tail);
+  if (a.tail.counter) ssp::fold_tail<(M < 8 ? M : 8)>(a.partial, a.tail);
 }
 
 int check_ptrs(const double* const* v, int count, size_t n, const char* what) {
@@ -1578,7 +1615,7 @@ int ssp_transform_gram(ssp_ctx* ctx, const double* t, double* const* xx, const d
     a.s[i] = xs ? xs[i] : 1.0;
   }
   for (int i = 0; i < m; ++i)
-    for (int j = 0; j < m; ++j) a.t[i * m + j] = t[i * m + j];
+    for (int j = 0; j < m; ++j) a.t[j * m + i] = t[i * m + j];  // transposed: column j contiguous
   const int np = m * (m + 1) / 2;
   // the fused Gram only from the bandwidth kernel; short vectors take the reference's sequential dots
   const bool fused = gram && !exact && n > 0;

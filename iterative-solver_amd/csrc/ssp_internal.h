@@ -218,6 +218,30 @@ __device__ inline double block_sum256(double v) {
   return s;
 }
 
+// block_sum256 of K values at once (each value's tree exactly block_sum256's); results in thread 0.
+template <int K>
+__device__ inline void block_sum256_multi(double (&v)[K]) {
+  __shared__ double wsum[K][kBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_down(v[k], off, 64);
+    if (lane == 0) wsum[k][wave] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      double s = 0;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; ++w) s += wsum[k][w];
+      v[k] = s;
+    }
+  }
+  __syncthreads();
+}
+
 // Reduction tail fused into the kernel that writes the per-workgroup partials (results of at most
 // a few dozen doubles): the last workgroup to arrive folds partial[grid][nout] in exactly the order
 // of the separate k_reduce_partials pass (per output: thread t sums workgroups t, t + 256, ...,
@@ -255,6 +279,7 @@ __device__ inline void store_partial(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <int K = 1, int LK = 0>
 __device__ inline void fold_tail(const double* partial, const FoldTail& t) {
   __shared__ unsigned s_last;
   if (threadIdx.x < 64) {
@@ -291,26 +316,46 @@ __device__ inline void fold_tail(const double* partial, const FoldTail& t) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the loads are sc1
 #endif
   const int G = int(gridDim.x);
-  for (int o = 0; o < t.nout; ++o) {
-    // Thread t adds workgroups t, t + 256, ... in that order; the loads are issued 8 at a time so
-    // their (cross-XCD) latencies overlap.
-    double s = 0;
-    for (int b0 = threadIdx.x; b0 < G; b0 += 8 * kBlock) {
-      double v[8];
+  // K outputs at a time: their loads are issued together (K x L in flight per thread, L slots of
+  // each output) and their workgroup sums share one LDS round.  Per output the order is that of the
+  // separate pass whatever K is -- thread t adds workgroups t, t + 256, ... in that order, then
+  // block_sum256's tree -- so every K gives the same bits; a kernel with many outputs (the fused Gram
+  // of the block transform: 36) waits one cross-XCD load latency per K outputs instead of per output.
+  // L: slots per output and trip (LK when given; by default at most 16 loads in flight, so the fold
+  // adds few registers to a lean streaming kernel).  A launch of at most L * 256 workgroups folds each
+  // group of K outputs in one trip.
+  constexpr int L = LK > 0 ? LK : (K >= 2 ? (16 / K > 2 ? 16 / K : 2) : 8);
+  for (int o0 = 0; o0 < t.nout; o0 += K) {
+    double s[K];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int b = b0 + u * kBlock;
-        v[u] = b < G ? __hip_atomic_load(partial + size_t(b) * t.nout + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                     : 0.0;
-      }
+    for (int k = 0; k < K; ++k) s[k] = 0;
+    for (int b0 = threadIdx.x; b0 < G; b0 += L * kBlock) {
+      double v[K][L];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (b0 + u * kBlock < G) s += v[u];
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int u = 0; u < L; ++u) {
+          const int b = b0 + u * kBlock;
+          v[k][u] = b < G && o0 + k < t.nout
+                        ? __hip_atomic_load(partial + size_t(b) * t.nout + o0 + k, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)
+                        : 0.0;
+        }
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int u = 0; u < L; ++u)
+          if (b0 + u * kBlock < G) s[k] += v[k][u];
     }
-    s = block_sum256(s);
+    block_sum256_multi<K>(s);
     if (threadIdx.x == 0) {
-      if (t.host) __hip_atomic_store(t.host + o, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      else t.out[o] = s;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (o0 + k < t.nout) {
+          if (t.host) __hip_atomic_store(t.host + o0 + k, s[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          else t.out[o0 + k] = s[k];
+        }
+      }
     }
   }
   if (threadIdx.x == 0) {

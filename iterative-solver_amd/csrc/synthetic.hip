@@ -263,6 +263,41 @@ __device__ __forceinline__ double lowrank(unsigned mm, const double (&c)[R]) {
   return s;
 }
 
+// The low-rank sums of every sign pattern (R <= 8: 2^R patterns), built by each workgroup before it
+// streams: tab[v][m] = lowrank<R>(m, coeff of vector v0 + v), the same function of the same operands,
+// so a lookup is bit for bit the inline sum.  The inline form costs 2R VALU operations (mask-bit test,
+// conditional sign, add) per element and vector -- at rank 8 and 4 vectors ~500 VALU instructions per
+// wave visit of 8.4 KiB, a VALU issue ceiling near the HBM rate -- against one LDS read.  The P-space
+// update (ADD: no diagonal term, half the VALU work per byte) keeps the inline sums: building the table
+// in each of its up to 4096 workgroups cost more than it saved (C4 shard 2.27 -> 2.38 ms per solve).
+constexpr int kTabRank = 8;
+template <int R, int NV, bool ON = true>
+struct LowrankTab {
+  static constexpr bool kOn = ON && R <= kTabRank;
+  static constexpr int kSize = kOn ? (1 << R) : 1;
+  double* t;  // [NV][kSize] in LDS
+  __device__ __forceinline__ double operator()(int v, unsigned mm, const double (&c)[R]) const {
+    if constexpr (kOn) return t[v * kSize + (mm & unsigned(kSize - 1))];
+    return lowrank<R>(mm, c);
+  }
+};
+template <int R, int NV, bool ON>
+__device__ __forceinline__ LowrankTab<R, NV, ON> build_tab(const SynthArgs& a, int v0) {
+  using T = LowrankTab<R, NV, ON>;
+  __shared__ double tab[NV * T::kSize];
+  if constexpr (T::kOn) {
+    for (int i = int(threadIdx.x); i < NV * T::kSize; i += kBlock) {
+      const int v = i / T::kSize;
+      double c[R];
+#pragma unroll
+      for (int l = 0; l < R; ++l) c[l] = a.coeff[(v0 + v) * R + l];
+      tab[i] = lowrank<R>(unsigned(i % T::kSize), c);
+    }
+    __syncthreads();
+  }
+  return T{tab};
+}
+
 // y_v = d x_v + rho sum_l u_l coeff[v][l]   (ADD = false)
 // y_v += rho sum_l u_l coeff[v][l]          (ADD = true, the P-space low-rank term)
 // for the NV vectors v0 .. v0+NV-1, coefficients in registers, in the window shape of the streaming
@@ -274,6 +309,7 @@ template <int R, bool ADD, int NV, bool EX>
 __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a, int v0) {
   constexpr int U = kSynthU;
   const unsigned* mask2 = reinterpret_cast<const unsigned*>(a.mask);
+  const LowrankTab<R, NV, !ADD> tab = build_tab<R, NV, !ADD>(a, v0);
   double c[NV][R];
   const double* xp[NV];
   double* yp[NV];
@@ -281,7 +317,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a, int v
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
 #pragma unroll
-    for (int l = 0; l < R; ++l) c[v][l] = a.coeff[(v0 + v) * R + l];
+    for (int l = 0; l < R; ++l) c[v][l] = tab.kOn ? 0.0 : a.coeff[(v0 + v) * R + l];
     xp[v] = ADD ? a.y[v0 + v] : a.x[v0 + v];
     yp[v] = a.y[v0 + v];
     xs[v] = ADD ? 1.0 : a.xs[v0 + v];
@@ -292,7 +328,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a, int v
     const double d0 = synth_d(a.diag_kind, g), d1 = synth_d(a.diag_kind, g + 1);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const double s0 = lowrank<R>(mm, c[v]), s1 = lowrank<R>(mm >> 16, c[v]);
+      const double s0 = tab(v, mm, c[v]), s1 = tab(v, mm >> 16, c[v]);
       double2 out;
       if (ADD) {
         const double2 y = in[v];
@@ -331,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a, int v
         const double d = synth_d(a.diag_kind, a.offset + e);
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
-          const double s = lowrank<R>(mm, c[v]);
+          const double s = tab(v, mm, c[v]);
           if (EX)
             yp[v][e] = ADD ? add_mul(yp[v][e], a.rho, s) : mul_add_mul(d, xp[v][e] * xs[v], a.rho, s);
           else
@@ -349,6 +385,7 @@ template <int R, bool ADD, int NV, bool EX>
 __global__ __launch_bounds__(kBlock) void k_synth_apply_pipe(const SynthArgs a, int v0) {
   const size_t stride = size_t(gridDim.x) * kBlock, n2 = a.n >> 1;
   const unsigned* mask2 = reinterpret_cast<const unsigned*>(a.mask);
+  const LowrankTab<R, NV, !ADD> tab = build_tab<R, NV, !ADD>(a, v0);
   double c[NV][R];
   const double* xp[NV];
   double* yp[NV];
@@ -356,7 +393,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply_pipe(const SynthArgs a, 
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
 #pragma unroll
-    for (int l = 0; l < R; ++l) c[v][l] = a.coeff[(v0 + v) * R + l];
+    for (int l = 0; l < R; ++l) c[v][l] = tab.kOn ? 0.0 : a.coeff[(v0 + v) * R + l];
     xp[v] = ADD ? a.y[v0 + v] : a.x[v0 + v];
     yp[v] = a.y[v0 + v];
     xs[v] = ADD ? 1.0 : a.xs[v0 + v];
@@ -377,7 +414,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply_pipe(const SynthArgs a, 
       const double d0 = synth_d(a.diag_kind, g), d1 = synth_d(a.diag_kind, g + 1);
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
-        const double s0 = lowrank<R>(mm, c[v]), s1 = lowrank<R>(mm >> 16, c[v]);
+        const double s0 = tab(v, mm, c[v]), s1 = tab(v, mm >> 16, c[v]);
         double2 out;
         if (ADD) {
           const double2 y = in[v];
@@ -401,7 +438,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply_pipe(const SynthArgs a, 
     const double d = synth_d(a.diag_kind, a.offset + e);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const double s = lowrank<R>(mm, c[v]);
+      const double s = tab(v, mm, c[v]);
       if (EX)
         yp[v][e] = ADD ? add_mul(yp[v][e], a.rho, s) : mul_add_mul(d, xp[v][e] * xs[v], a.rho, s);
       else
