@@ -280,7 +280,7 @@ int p2p_allreduce_dev(ssp_ctx* ctx, double* buf, size_t n) {
     const unsigned c = unsigned(std::min(kP2PSlot, n - off));
     P2PArgs a = p2p_args(ctx, buf + off, c);
     a.dst = buf + off;
-    hipLaunchKernelGGL(k_p2p_allreduce, dim3(1), dim3(256), 0, ctx->stream, a);
+    SSP_LAUNCH(k_p2p_allreduce, dim3(1), dim3(256), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
   return SSP_OK;
@@ -300,7 +300,7 @@ int p2p_allreduce_fetch(ssp_ctx* ctx, const double* src, double* out, size_t n) 
   a.host_dst = ctx->result_host;
   a.host_flag = ctx->pub_flag;
   a.host_seq = ++ctx->pub_seq;
-  hipLaunchKernelGGL(k_p2p_allreduce, dim3(1), dim3(256), 0, ctx->stream, a);
+  SSP_LAUNCH(k_p2p_allreduce, dim3(1), dim3(256), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());
   bool seen = true;  // the kernel stores the sums into host memory itself: drained = visible
   SSP_TRY(wait_flag(ctx, a.host_seq, &seen));
@@ -385,7 +385,7 @@ int sspx_debug_stall(ssp_ctx* ctx, double ms) {
   if (!(ms >= 0) || ms > 60e3) return ssp::set_error(SSP_ERR_ARG, "sspx_debug_stall: 0 <= ms <= 60000");
   int khz = 0;
   SSP_TRY_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
-  hipLaunchKernelGGL(k_debug_stall, dim3(1), dim3(64), 0, ctx->stream,
+  SSP_LAUNCH(k_debug_stall, dim3(1), dim3(64), 0, ctx->stream,
                      static_cast<unsigned long long>(ms * double(khz)));
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;

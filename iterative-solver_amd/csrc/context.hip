@@ -229,7 +229,7 @@ int fetch_result(ssp_ctx* ctx, double* out, size_t n) {
                                ctx->stream));
     SSP_TRY_HIP(hipStreamWriteValue64(ctx->stream, ctx->pub_flag, seq, 0));
   } else {
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, ctx->stream, ctx->result_dev, n, ctx->result_host,
+    SSP_LAUNCH(k_publish, dim3(1), dim3(256), 0, ctx->stream, ctx->result_dev, n, ctx->result_host,
                        ctx->pub_flag, seq);
     SSP_TRY_HIP(hipGetLastError());
   }
@@ -310,21 +310,56 @@ int ledger_resolve(ssp_ctx* ctx) {
 }
 }  // namespace
 
+namespace {
+thread_local LedgerScope* t_scope = nullptr;  // innermost open dispatch-timed scope
+}
+
 LedgerScope::LedgerScope(ssp_ctx* ctx, const char* op, double bytes) : ctx_(ctx) {
   if (!ctx->ledger_on) return;
   slot_ = ledger_slot(ctx, op);
   ctx->ledger[slot_].calls += 1;
   ctx->ledger[slot_].bytes += bytes;
   start_ = take_event(ctx);
-  if (start_) (void)hipEventRecord(start_, ctx->stream);
+  if (!start_) return;
+  if (ctx->ledger_dispatch) {
+    stop_ = take_event(ctx);
+    if (!stop_) {
+      ctx->event_pool.push_back(start_);
+      start_ = nullptr;
+      return;
+    }
+    prev_ = t_scope;
+    t_scope = this;
+    return;
+  }
+  (void)hipEventRecord(start_, ctx->stream);
+}
+
+bool LedgerScope::dispatch_events(hipEvent_t* start, hipEvent_t* stop) {
+  LedgerScope* s = t_scope;
+  if (!s) return false;
+  *start = s->launched_ ? nullptr : s->start_;
+  *stop = s->stop_;
+  s->launched_ = true;
+  return true;
 }
 
 LedgerScope::~LedgerScope() {
   if (slot_ < 0 || !start_) return;
-  hipEvent_t end = take_event(ctx_);
-  if (!end) return;
-  (void)hipEventRecord(end, ctx_->stream);
-  ctx_->ledger[slot_].pending.emplace_back(start_, end);
+  if (stop_) {  // dispatch timing
+    t_scope = prev_;
+    if (!launched_) {  // no kernel in this op (e.g. its work went to a nested op)
+      ctx_->event_pool.push_back(start_);
+      ctx_->event_pool.push_back(stop_);
+      return;
+    }
+    ctx_->ledger[slot_].pending.emplace_back(start_, stop_);
+  } else {
+    hipEvent_t end = take_event(ctx_);
+    if (!end) return;
+    (void)hipEventRecord(end, ctx_->stream);
+    ctx_->ledger[slot_].pending.emplace_back(start_, end);
+  }
   if (ctx_->ledger[slot_].pending.size() > 4096) (void)ledger_resolve(ctx_);
 }
 
@@ -401,7 +436,11 @@ int ssp_ctx_create(int device, ssp_ctx** out) {
   if (const char* pc = std::getenv("SSP_PUBLISH")) ctx->publish_copy = std::string(pc) == "copy";
   if (const char* ex = std::getenv("SSP_EXACT_MAX")) ctx->exact_max = size_t(std::strtoull(ex, nullptr, 10));
   if (const char* ip = std::getenv("SSP_INNER_PER_CU")) ctx->inner_per_cu = std::max(1, std::atoi(ip));
-  if (const char* ss = std::getenv("SSP_SYNTH_SHAPE")) ctx->synth_stride = std::string(ss) == "stride";
+  if (const char* lt = std::getenv("SSP_LEDGER_TIMING")) ctx->ledger_dispatch = std::string(lt) == "dispatch";
+  if (const char* ss = std::getenv("SSP_SYNTH_SHAPE")) {
+    ctx->synth_stride = std::string(ss) == "stride";
+    ctx->synth_window = std::string(ss) == "window";
+  }
   if (const char* ct = std::getenv("SSP_COMM_TIMEOUT_S")) {
     const double v = std::atof(ct);
     if (v > 0) ctx->comm_timeout_s = v;

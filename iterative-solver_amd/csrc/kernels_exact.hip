@@ -228,7 +228,7 @@ int exact_inner(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, 
   a.out = ctx->result_dev;
   a.tail = tail;
   SSP_TRY(flush_uploads(ctx));
-  hipLaunchKernelGGL(k_exact_inner, dim3(unsigned(nout)), dim3(kBlock), 0, ctx->stream, a);
+  SSP_LAUNCH(k_exact_inner, dim3(unsigned(nout)), dim3(kBlock), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -253,7 +253,7 @@ int exact_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, con
     a.n = n;
     const size_t total = n * size_t(m);
     const unsigned grid = unsigned(std::min<size_t>((total + kBlock - 1) / kBlock, size_t(ctx->num_cus) * 4));
-    hipLaunchKernelGGL(k_exact_outer, dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_LAUNCH(k_exact_outer, dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
     return SSP_OK;
   }
@@ -276,7 +276,7 @@ int exact_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, con
   SSP_TRY(flush_uploads(ctx));
   const size_t total = n * size_t(m);
   const unsigned grid = unsigned(std::min<size_t>((total + kBlock - 1) / kBlock, size_t(ctx->num_cus) * 4));
-  hipLaunchKernelGGL(k_exact_outer, dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  SSP_LAUNCH(k_exact_outer, dim3(grid), dim3(kBlock), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }

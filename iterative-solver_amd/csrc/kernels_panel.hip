@@ -890,9 +890,9 @@ unsigned gram_grid(ssp_ctx* ctx, size_t n) {
 template <int M>
 void launch_transform_m(ssp_ctx* ctx, unsigned grid, const TransformArgs& a, bool gram, bool exact) {
   const dim3 b(kBlock);
-  if (exact) hipLaunchKernelGGL((k_transform<M, false, false>), dim3(grid), b, 0, ctx->stream, a);
-  else if (gram) hipLaunchKernelGGL((k_transform<M, true, true>), dim3(gram_grid<M>(ctx, a.n)), b, 0, ctx->stream, a);
-  else hipLaunchKernelGGL((k_transform<M, false, true>), dim3(grid), b, 0, ctx->stream, a);
+  if (exact) SSP_LAUNCH((k_transform<M, false, false>), dim3(grid), b, 0, ctx->stream, a);
+  else if (gram) SSP_LAUNCH((k_transform<M, true, true>), dim3(gram_grid<M>(ctx, a.n)), b, 0, ctx->stream, a);
+  else SSP_LAUNCH((k_transform<M, false, true>), dim3(grid), b, 0, ctx->stream, a);
 }
 
 void launch_transform(ssp_ctx* ctx, int m, unsigned grid, const TransformArgs& a, bool gram, bool exact) {
@@ -1004,7 +1004,7 @@ unsigned inner_grid(const ssp_ctx* ctx, size_t n) {
 
 template <int MG, int NG, bool SC>
 void launch_inner_t(ssp_ctx* ctx, unsigned grid, const InnerArgs& a) {
-  hipLaunchKernelGGL((k_gemm_inner<MG, NG, false, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  SSP_LAUNCH((k_gemm_inner<MG, NG, false, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
 }
 
 // Smallest instantiated NG >= need (need <= ng_max(MG)).
@@ -1029,10 +1029,10 @@ int launch_inner_mg(ssp_ctx* ctx, unsigned grid, const InnerArgs& a, int need) {
 template <bool SC>
 int launch_inner_sym_t(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
   switch ((a.m + 3) / 4) {
-    case 1: hipLaunchKernelGGL((k_gemm_inner<1, 1, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
-    case 2: hipLaunchKernelGGL((k_gemm_inner<2, 2, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
-    case 3: hipLaunchKernelGGL((k_gemm_inner<3, 3, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
-    default: hipLaunchKernelGGL((k_gemm_inner<4, 4, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    case 1: SSP_LAUNCH((k_gemm_inner<1, 1, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    case 2: SSP_LAUNCH((k_gemm_inner<2, 2, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    case 3: SSP_LAUNCH((k_gemm_inner<3, 3, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    default: SSP_LAUNCH((k_gemm_inner<4, 4, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
   }
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
@@ -1060,15 +1060,15 @@ int launch_inner(ssp_ctx* ctx, const InnerArgs& a, unsigned grid, bool sc) {
 template <bool DEV, bool SET, bool SC>
 void launch_outer_t(ssp_ctx* ctx, unsigned grid, const OuterArgs& a) {
   if (a.m <= 1)
-    hipLaunchKernelGGL((k_gemm_outer<1, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_LAUNCH((k_gemm_outer<1, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
   else if (a.m <= 2)
-    hipLaunchKernelGGL((k_gemm_outer<2, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_LAUNCH((k_gemm_outer<2, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
   else if (a.m <= 4)
-    hipLaunchKernelGGL((k_gemm_outer<4, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_LAUNCH((k_gemm_outer<4, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
   else if (a.m <= 8)
-    hipLaunchKernelGGL((k_gemm_outer<8, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_LAUNCH((k_gemm_outer<8, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
   else
-    hipLaunchKernelGGL((k_gemm_outer<16, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+    SSP_LAUNCH((k_gemm_outer<16, DEV, SET, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
 }
 
 template <bool SC>
@@ -1170,15 +1170,15 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
         a.tail = tail;
         const dim3 g(grid), b(kBlock);
         if (stride) {
-          if (C == 1 && sc) hipLaunchKernelGGL((k_gemm_inner_row<1, true>), g, b, 0, ctx->stream, a);
-          else if (C == 1) hipLaunchKernelGGL((k_gemm_inner_row<1>), g, b, 0, ctx->stream, a);
-          else if (sc) hipLaunchKernelGGL((k_gemm_inner_row<2, true>), g, b, 0, ctx->stream, a);
-          else hipLaunchKernelGGL((k_gemm_inner_row<2>), g, b, 0, ctx->stream, a);
+          if (C == 1 && sc) SSP_LAUNCH((k_gemm_inner_row<1, true>), g, b, 0, ctx->stream, a);
+          else if (C == 1) SSP_LAUNCH((k_gemm_inner_row<1>), g, b, 0, ctx->stream, a);
+          else if (sc) SSP_LAUNCH((k_gemm_inner_row<2, true>), g, b, 0, ctx->stream, a);
+          else SSP_LAUNCH((k_gemm_inner_row<2>), g, b, 0, ctx->stream, a);
         } else {
-          if (C == 1 && sc) hipLaunchKernelGGL((k_gemm_inner_row_win<1, true>), g, b, 0, ctx->stream, a);
-          else if (C == 1) hipLaunchKernelGGL((k_gemm_inner_row_win<1>), g, b, 0, ctx->stream, a);
-          else if (sc) hipLaunchKernelGGL((k_gemm_inner_row_win<2, true>), g, b, 0, ctx->stream, a);
-          else hipLaunchKernelGGL((k_gemm_inner_row_win<2>), g, b, 0, ctx->stream, a);
+          if (C == 1 && sc) SSP_LAUNCH((k_gemm_inner_row_win<1, true>), g, b, 0, ctx->stream, a);
+          else if (C == 1) SSP_LAUNCH((k_gemm_inner_row_win<1>), g, b, 0, ctx->stream, a);
+          else if (sc) SSP_LAUNCH((k_gemm_inner_row_win<2, true>), g, b, 0, ctx->stream, a);
+          else SSP_LAUNCH((k_gemm_inner_row_win<2>), g, b, 0, ctx->stream, a);
         }
         SSP_TRY_HIP(hipGetLastError());
       }
@@ -1359,13 +1359,13 @@ int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* y
     a.partial = ctx->partial;
     a.tail = tail;
     if (m <= 1)
-      hipLaunchKernelGGL((k_scal_inner<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_scal_inner<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (m <= 4)
-      hipLaunchKernelGGL((k_scal_inner<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_scal_inner<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (m <= 8)
-      hipLaunchKernelGGL((k_scal_inner<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_scal_inner<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else
-      hipLaunchKernelGGL((k_scal_inner<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_scal_inner<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
@@ -1405,13 +1405,13 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
     a.partial = ctx->partial;
     a.tail = tail;
     if (m <= 1)
-      hipLaunchKernelGGL((k_axpy_norm<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_norm<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (m <= 4)
-      hipLaunchKernelGGL((k_axpy_norm<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_norm<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (m <= 8)
-      hipLaunchKernelGGL((k_axpy_norm<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_norm<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else
-      hipLaunchKernelGGL((k_axpy_norm<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_norm<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
@@ -1460,13 +1460,13 @@ int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store
     a.partial = ctx->partial;
     a.tail = tail;
     if (m <= 1)
-      hipLaunchKernelGGL((k_axpy_gram<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_gram<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (m <= 4)
-      hipLaunchKernelGGL((k_axpy_gram<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_gram<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (m <= 8)
-      hipLaunchKernelGGL((k_axpy_gram<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_gram<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else
-      hipLaunchKernelGGL((k_axpy_gram<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_gram<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
@@ -1525,13 +1525,13 @@ int ssp_axpy_pairs_norm(ssp_ctx* ctx, const double* c, const double* const* xx, 
     a.partial = ctx->partial;
     a.tail = tail;
     if (m <= 1)
-      hipLaunchKernelGGL((k_axpy_pairs_norm<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_pairs_norm<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (m <= 4)
-      hipLaunchKernelGGL((k_axpy_pairs_norm<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_pairs_norm<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (m <= 8)
-      hipLaunchKernelGGL((k_axpy_pairs_norm<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_pairs_norm<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else
-      hipLaunchKernelGGL((k_axpy_pairs_norm<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_axpy_pairs_norm<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
   if (tail.counter) return ssp::fold_finish(ctx, tail, out);
@@ -1581,13 +1581,13 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
       a.partial = ctx->partial;
       a.tail = tail;
       if (a.m <= 1)
-        hipLaunchKernelGGL((k_axpy_inner<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+        SSP_LAUNCH((k_axpy_inner<1>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       else if (a.m <= 4)
-        hipLaunchKernelGGL((k_axpy_inner<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+        SSP_LAUNCH((k_axpy_inner<4>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       else if (a.m <= 8)
-        hipLaunchKernelGGL((k_axpy_inner<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+        SSP_LAUNCH((k_axpy_inner<8>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       else
-        hipLaunchKernelGGL((k_axpy_inner<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+        SSP_LAUNCH((k_axpy_inner<16>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
       if (!tail.counter)
         SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, a.m, ctx->result_dev, m, 0, j0));

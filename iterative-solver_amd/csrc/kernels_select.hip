@@ -256,13 +256,13 @@ int radix_candidates(ssp_ctx* ctx, int mode, const double* x, const double* y, s
     a.dmask = (1u << width) - 1u;
     SSP_TRY_HIP(hipMemsetAsync(hist, 0, sizeof(unsigned) * kBins, ctx->stream));
     if (mode == 1 && idx_phase)
-      hipLaunchKernelGGL((k_radix_hist<1, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_radix_hist<1, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (mode == 1)
-      hipLaunchKernelGGL((k_radix_hist<1, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_radix_hist<1, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else if (idx_phase)
-      hipLaunchKernelGGL((k_radix_hist<0, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_radix_hist<0, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     else
-      hipLaunchKernelGGL((k_radix_hist<0, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_radix_hist<0, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
     // hist is the context's result staging buffer: published to coherent host memory and polled
     // (ssp::fetch_result), not a D2H copy + stream synchronisation.
@@ -292,9 +292,9 @@ int radix_candidates(ssp_ctx* ctx, int mode, const double* x, const double* y, s
   a.counter = counter;
   SSP_TRY_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), ctx->stream));
   if (mode == 1)
-    hipLaunchKernelGGL(k_radix_compact<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, a, offset);
+    SSP_LAUNCH(k_radix_compact<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, a, offset);
   else
-    hipLaunchKernelGGL(k_radix_compact<0>, dim3(grid), dim3(kBlock), 0, ctx->stream, a, offset);
+    SSP_LAUNCH(k_radix_compact<0>, dim3(grid), dim3(kBlock), 0, ctx->stream, a, offset);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -368,7 +368,7 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
       a.max = max;
       a.ignore_sign = ignore_sign;
     }
-    hipLaunchKernelGGL(k_select_tile, dim3(unsigned(tiles)), dim3(kTileBlock), 0, ctx->stream, a);
+    SSP_LAUNCH(k_select_tile, dim3(unsigned(tiles)), dim3(kTileBlock), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
     count = tiles * size_t(keep);
     Cand* cur = buf0;
@@ -381,7 +381,7 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
       b.mode = 2;
       b.keep = keep;
       b.out = nxt;
-      hipLaunchKernelGGL(k_select_tile, dim3(unsigned(tiles)), dim3(kTileBlock), 0, ctx->stream, b);
+      SSP_LAUNCH(k_select_tile, dim3(unsigned(tiles)), dim3(kTileBlock), 0, ctx->stream, b);
       SSP_TRY_HIP(hipGetLastError());
       count = tiles * size_t(keep);
       std::swap(cur, nxt);
@@ -390,7 +390,7 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
     // returned values in one published block.
     const size_t real = std::min(n, nsel);
     SSP_TRY(ssp::ensure_result(ctx, 2 * real));
-    hipLaunchKernelGGL(k_select_values, dim3(unsigned((real + 255) / 256)), dim3(256), 0, ctx->stream, cur, int(real), x,
+    SSP_LAUNCH(k_select_values, dim3(unsigned((real + 255) / 256)), dim3(256), 0, ctx->stream, cur, int(real), x,
                        y, offset, mode, max, ignore_sign, ctx->result_dev);
     SSP_TRY_HIP(hipGetLastError());
     std::vector<double> pub(2 * real);

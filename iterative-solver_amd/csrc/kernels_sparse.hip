@@ -266,7 +266,7 @@ int launch_scatter_inline(ssp_ctx* ctx, double* x, const std::vector<unsigned lo
     a.li[e] = li[e];
     a.v[e] = lv[e];
   }
-  hipLaunchKernelGGL(k_scatter_inline, dim3(1), dim3(kInlineEntries), 0, ctx->stream, a);
+  SSP_LAUNCH(k_scatter_inline, dim3(1), dim3(kInlineEntries), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -300,7 +300,7 @@ int ssp_sparse_copy(ssp_ctx* ctx, double* x, size_t n, size_t offset, const size
   ssp::LedgerScope ls(ctx, "sparse_copy", 16.0 * li.size());
   const unsigned grid = unsigned(std::min<size_t>((li.size() + kBlock - 1) / kBlock, 1024));
   SSP_TRY(ssp::flush_uploads(ctx));
-  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), 1.0, 0);
+  SSP_LAUNCH(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), 1.0, 0);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -326,7 +326,7 @@ int ssp_sparse_axpy(ssp_ctx* ctx, double alpha, const size_t* idx, const double*
   // Distinct map keys never collide, so entries can be applied in parallel.
   const unsigned grid = unsigned(std::min<size_t>((li.size() + kBlock - 1) / kBlock, 1024));
   SSP_TRY(ssp::flush_uploads(ctx));
-  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), alpha, 1);
+  SSP_LAUNCH(k_scatter, dim3(grid), dim3(kBlock), 0, ctx->stream, x, dli, dv, li.size(), alpha, 1);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -394,7 +394,7 @@ int ssp_sparse_axpy_batch(ssp_ctx* ctx, int nvec, const size_t* ptr, const size_
           b.v[b.nnz++] = a.v[e];
         }
     }
-    hipLaunchKernelGGL(k_scatter_batch_inline, dim3(1), dim3(kBatchEntries), 0, ctx->stream, b);
+    SSP_LAUNCH(k_scatter_batch_inline, dim3(1), dim3(kBatchEntries), 0, ctx->stream, b);
     SSP_TRY_HIP(hipGetLastError());
   }
   return SSP_OK;
@@ -444,7 +444,7 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const do
         }
         a.out = ctx->result_dev + size_t(i0) * k;
         const int outs = a.m * a.k;
-        hipLaunchKernelGGL(k_sparse_inner_inline, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a,
+        SSP_LAUNCH(k_sparse_inner_inline, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a,
                            tail);
         SSP_TRY_HIP(hipGetLastError());
       }
@@ -471,7 +471,7 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const do
       a.out = ctx->result_dev + size_t(i0) * k;
       const int outs = a.m * a.k;
       SSP_TRY(ssp::flush_uploads(ctx));
-      hipLaunchKernelGGL(k_sparse_inner, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH(k_sparse_inner, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a);
       SSP_TRY_HIP(hipGetLastError());
     }
   }
@@ -518,7 +518,7 @@ int ssp_gemm_outer_sparse(ssp_ctx* ctx, const double* alphas, const size_t* ptr,
     a.li = dli;
     a.v = dv;
     SSP_TRY(ssp::flush_uploads(ctx));
-    hipLaunchKernelGGL(k_sparse_outer, dim3(1), dim3(64), 0, ctx->stream, a);
+    SSP_LAUNCH(k_sparse_outer, dim3(1), dim3(64), 0, ctx->stream, a);
     SSP_TRY_HIP(hipGetLastError());
   }
   return SSP_OK;
@@ -557,7 +557,7 @@ int solution_impl(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const 
     const size_t cnt = uidx.size() * size_t(m);
     SSP_TRY(ssp::ensure_partial(ctx, cnt));
     SSP_TRY(ssp::flush_uploads(ctx));
-    hipLaunchKernelGGL(k_gather_touched, dim3(unsigned((cnt + 255) / 256)), dim3(256), 0, ctx->stream,
+    SSP_LAUNCH(k_gather_touched, dim3(unsigned((cnt + 255) / 256)), dim3(256), 0, ctx->stream,
                        static_cast<const unsigned long long*>(p), uidx.size(), m, ydev, ctx->partial);
     SSP_TRY_HIP(hipGetLastError());
     saved = ctx->partial;  // nothing below resizes the partials workspace before the fix-up reads it
@@ -609,7 +609,7 @@ int solution_impl(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const 
                       8.0 * a.nu * m * (2.0 + k + (rmw ? 1.0 : 0.0)));
   const size_t threads = a.nu * size_t(m);
   SSP_TRY(ssp::flush_uploads(ctx));
-  hipLaunchKernelGGL(k_construct_fixup, dim3(unsigned((threads + 255) / 256)), dim3(256), 0, ctx->stream, a);
+  SSP_LAUNCH(k_construct_fixup, dim3(unsigned((threads + 255) / 256)), dim3(256), 0, ctx->stream, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }

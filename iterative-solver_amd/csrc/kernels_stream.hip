@@ -304,7 +304,7 @@ namespace ssp {
 int launch_reduce_partials(ssp_ctx* ctx, const double* partial, int nblocks, int rows, int cols, double* out, int ldo,
                            int row0, int col0) {
   if (rows * cols == 0) return SSP_OK;
-  hipLaunchKernelGGL(k_reduce_partials, dim3(rows * cols), dim3(kBlock), 0, ctx->stream, partial, nblocks, rows, cols,
+  SSP_LAUNCH(k_reduce_partials, dim3(rows * cols), dim3(kBlock), 0, ctx->stream, partial, nblocks, rows, cols,
                      out, ldo, row0, col0);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
@@ -318,7 +318,7 @@ int ssp_fill(ssp_ctx* ctx, double alpha, double* x, size_t n) {
   SSP_TRY(check_vec(x, n, "ssp_fill"));
   if (n == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "fill", 8.0 * n);
-  hipLaunchKernelGGL(k_fill, dim3(ssp::stream_grid(ctx, n / 2 + 1, 1, 64)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
+  SSP_LAUNCH(k_fill, dim3(ssp::stream_grid(ctx, n / 2 + 1, 1, 64)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -329,9 +329,9 @@ int ssp_scal(ssp_ctx* ctx, double alpha, double* x, size_t n) {
   if (n == 0) return SSP_OK;
   ssp::LedgerScope ls(ctx, "scal", 16.0 * n);
   if (n >= kWinMin)
-    hipLaunchKernelGGL(k_scal_win, dim3(ssp::win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
+    SSP_LAUNCH(k_scal_win, dim3(ssp::win_grid(ctx, n, kWinU, 16)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
   else
-    hipLaunchKernelGGL(k_scal, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
+    SSP_LAUNCH(k_scal, dim3(ssp::stream_grid(ctx, n / 2 + 1, 4, 64)), dim3(kBlock), 0, ctx->stream, x, n, alpha);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
 }
@@ -348,12 +348,12 @@ int copy_impl(ssp_ctx* ctx, double alpha, double* x, const double* y, size_t n, 
   ssp::LedgerScope ls(ctx, scaled ? "scal_copy" : "copy", 16.0 * n);
   if (n >= kWinMin) {
     const dim3 g(ssp::win_grid(ctx, n, kWinU, 16));
-    if (scaled) hipLaunchKernelGGL(k_copy_win<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
-    else hipLaunchKernelGGL(k_copy_win<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+    if (scaled) SSP_LAUNCH(k_copy_win<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+    else SSP_LAUNCH(k_copy_win<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
   } else {
     const dim3 g(ssp::stream_grid(ctx, n / 2 + 1, 4, 64));
-    if (scaled) hipLaunchKernelGGL(k_copy<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
-    else hipLaunchKernelGGL(k_copy<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+    if (scaled) SSP_LAUNCH(k_copy<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
+    else SSP_LAUNCH(k_copy<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha);
   }
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
@@ -370,12 +370,12 @@ int axpy_impl(ssp_ctx* ctx, double alpha, const double* x, double xs, double* y,
   if (ssp::exact_mode(ctx, n)) return ssp::exact_outer(ctx, &alpha, &x, &xs, 1, &y, &ys, 1, n, false);
   if (n >= kWinMin) {
     const dim3 g(ssp::win_grid(ctx, n, kWinU, 16));
-    if (sc) hipLaunchKernelGGL(k_axpy_win<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
-    else hipLaunchKernelGGL(k_axpy_win<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
+    if (sc) SSP_LAUNCH(k_axpy_win<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
+    else SSP_LAUNCH(k_axpy_win<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
   } else {
     const dim3 g(ssp::stream_grid(ctx, n / 2 + 1, 4, 64));
-    if (sc) hipLaunchKernelGGL(k_axpy<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
-    else hipLaunchKernelGGL(k_axpy<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
+    if (sc) SSP_LAUNCH(k_axpy<true>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
+    else SSP_LAUNCH(k_axpy<false>, g, dim3(kBlock), 0, ctx->stream, x, y, n, alpha, xs, ys);
   }
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
@@ -410,10 +410,10 @@ int dot_impl(ssp_ctx* ctx, const double* x, double xs, const double* y, double y
     ssp::LedgerScope ls(ctx, "dot", (same ? 8.0 : 16.0) * n);
     const dim3 g(grid);
     double* part = ctx->partial;
-    if (same && sc) hipLaunchKernelGGL((k_dot_partial<true, true>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
-    else if (same) hipLaunchKernelGGL((k_dot_partial<true, false>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
-    else if (sc) hipLaunchKernelGGL((k_dot_partial<false, true>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
-    else hipLaunchKernelGGL((k_dot_partial<false, false>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
+    if (same && sc) SSP_LAUNCH((k_dot_partial<true, true>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
+    else if (same) SSP_LAUNCH((k_dot_partial<true, false>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
+    else if (sc) SSP_LAUNCH((k_dot_partial<false, true>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
+    else SSP_LAUNCH((k_dot_partial<false, false>), g, dim3(kBlock), 0, ctx->stream, x, y, n, part, tail, xs, ys);
     SSP_TRY_HIP(hipGetLastError());
   }
   return ssp::fold_finish(ctx, tail, out);
@@ -460,7 +460,7 @@ int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, 
     }
     p.d = d;
     p.n = n;
-    hipLaunchKernelGGL(k_precondition, dim3(ssp::win_grid(ctx, n, 4, 8)), dim3(kBlock), 0, ctx->stream, p);
+    SSP_LAUNCH(k_precondition, dim3(ssp::win_grid(ctx, n, 4, 8)), dim3(kBlock), 0, ctx->stream, p);
     SSP_TRY_HIP(hipGetLastError());
   }
   return SSP_OK;

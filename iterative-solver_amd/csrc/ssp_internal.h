@@ -1,6 +1,7 @@
 // Internal declarations shared by the libsubspace_hip.so translation units.
 // Public surface: include/subspace_hip.h.  Design: DESIGN.md.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -35,6 +36,8 @@ struct ssp_ctx {
   int num_cus = 256;
   int inner_per_cu = 4;        // gemm_inner workgroups per CU (SSP_INNER_PER_CU: the A/B knob of tools/ab_inner.py)
   bool synth_stride = false;  // SSP_SYNTH_SHAPE=stride: the synthetic apply kernel grid-strided (A/B)
+  bool ledger_dispatch = false;  // SSP_LEDGER_TIMING=dispatch (LedgerScope)
+  bool synth_window = false;  // SSP_SYNTH_SHAPE=window: the synthetic apply kernel in the window shape (A/B)
   // Shape of the 1 x 1 / 1 x 2 gemm_inner row kernel: window (default) or, with SSP_ROW_SHAPE=stride
   // in the environment at context creation, the round-2 grid-stride shape (A/B: tools/row_shape_ab.py).
   bool row_stride = false;
@@ -164,18 +167,39 @@ __device__ __forceinline__ void st2nt(double* p, double2 v) {
 bool aligned16(const void* p);
 
 // Ledger scope: records a start event now and an end event at destruction (when enabled).
+// Two timings (SSP_LEDGER_TIMING, read at context creation):
+//   events   (default) an event recorded on the stream before the op's work and one after it: the op's
+//            time includes any wait of an idle stream for the host to submit the op's first kernel;
+//   dispatch the op's first kernel carries the start event and every kernel of the op the stop event
+//            (hipExtLaunchKernel, through SSP_LAUNCH): first kernel start to last kernel end, the
+//            interval a kernel trace shows for the op.
 class LedgerScope {
  public:
   LedgerScope(ssp_ctx* ctx, const char* op, double bytes);
   ~LedgerScope();
   LedgerScope(const LedgerScope&) = delete;
   LedgerScope& operator=(const LedgerScope&) = delete;
+  // dispatch timing: the events for the next kernel launched on this thread inside an open scope
+  static bool dispatch_events(hipEvent_t* start, hipEvent_t* stop);
 
  private:
   ssp_ctx* ctx_;
   int slot_ = -1;
   hipEvent_t start_ = nullptr;
+  hipEvent_t stop_ = nullptr;  // dispatch timing
+  bool launched_ = false;
+  LedgerScope* prev_ = nullptr;
 };
+
+// Kernel launch on the context's stream: hipLaunchKernelGGL, or with dispatch-timed ledger events.
+#define SSP_LAUNCH(K, G, B, SHM, ST, ...)                                                  \
+  do {                                                                                    \
+    hipEvent_t ssp_e0_ = nullptr, ssp_e1_ = nullptr;                                      \
+    if (::ssp::LedgerScope::dispatch_events(&ssp_e0_, &ssp_e1_))                          \
+      hipExtLaunchKernelGGL(K, G, B, SHM, ST, ssp_e0_, ssp_e1_, 0u, __VA_ARGS__);         \
+    else                                                                                  \
+      hipLaunchKernelGGL(K, G, B, SHM, ST, __VA_ARGS__);                                  \
+  } while (0)
 
 // Window shape for streaming kernels (tools/mb_glds.hip mode a, profiles/r1/mb_stream_shapes.txt):
 // a wave covers U x 64 consecutive double2 (U KiB) of each vector per visit.  Visits the whole

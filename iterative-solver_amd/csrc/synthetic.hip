@@ -459,10 +459,10 @@ void launch_coeff(unsigned grid, hipStream_t st, const SynthArgs& a) {
   constexpr int G = coeff_group<R>();
   for (int v0 = 0; v0 < a.nvec; v0 += G) {
     const int nv = std::min(G, a.nvec - v0);
-    if (nv == 4) hipLaunchKernelGGL((k_synth_coeff<R, (G >= 4 ? 4 : 1)>), dim3(grid), dim3(kBlock), 0, st, a, v0);
-    else if (nv == 3) hipLaunchKernelGGL((k_synth_coeff<R, (G >= 4 ? 3 : 1)>), dim3(grid), dim3(kBlock), 0, st, a, v0);
-    else if (nv == 2) hipLaunchKernelGGL((k_synth_coeff<R, 2>), dim3(grid), dim3(kBlock), 0, st, a, v0);
-    else hipLaunchKernelGGL((k_synth_coeff<R, 1>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    if (nv == 4) SSP_LAUNCH((k_synth_coeff<R, (G >= 4 ? 4 : 1)>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    else if (nv == 3) SSP_LAUNCH((k_synth_coeff<R, (G >= 4 ? 3 : 1)>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    else if (nv == 2) SSP_LAUNCH((k_synth_coeff<R, 2>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    else SSP_LAUNCH((k_synth_coeff<R, 1>), dim3(grid), dim3(kBlock), 0, st, a, v0);
   }
 }
 
@@ -484,7 +484,7 @@ void synth_coeff_exact(hipStream_t st, const SynthArgs& a, double* out) {
   switch (a.rank) {
 #define F(r)                                                                                          \
   case r:                                                                                             \
-    hipLaunchKernelGGL((k_synth_coeff_exact<r>), dim3(unsigned(a.nvec)), dim3(kBlock), 0, st, a, out); \
+    SSP_LAUNCH((k_synth_coeff_exact<r>), dim3(unsigned(a.nvec)), dim3(kBlock), 0, st, a, out); \
     break;
     SSP_RANK_CASES(F)
 #undef F
@@ -498,8 +498,8 @@ void launch_apply_ex(const ssp_ctx* ctx, hipStream_t st, const SynthArgs& a) {
   for (int v0 = 0; v0 < a.nvec; v0 += G) {
     const int nv = std::min(G, a.nvec - v0);
 #define SSP_APPLY(NV)                                                                                   \
-  if (WIN) hipLaunchKernelGGL((k_synth_apply<R, ADD, NV, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0); \
-  else hipLaunchKernelGGL((k_synth_apply_pipe<R, ADD, NV, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+  if (WIN) SSP_LAUNCH((k_synth_apply<R, ADD, NV, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0); \
+  else SSP_LAUNCH((k_synth_apply_pipe<R, ADD, NV, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
     if (nv == 4) { SSP_APPLY((G >= 4 ? 4 : 1)) }
     else if (nv == 3) { SSP_APPLY((G >= 4 ? 3 : 1)) }
     else if (nv == 2) { SSP_APPLY(2) }
@@ -513,9 +513,13 @@ void launch_apply_ex(const ssp_ctx* ctx, hipStream_t st, const SynthArgs& a) {
 // 2.26 against 2.34-2.59 ms) and the action from 2^24 elements (C3: 24.9 against 25.4-28.2 ms), while
 // at C4's shard the action's grid-strided pipelined form is ahead (3.33-3.40 against 3.61 ms: the
 // window kernel holds 256 registers per lane).  SSP_SYNTH_SHAPE=stride forces the strided form.
+// Round 5: with the action's low-rank sums tabulated (R <= kTabRank) the window kernel is no longer
+// register-bound, and it leads at the C4 shard too (3.19 against 3.31-3.41 ms per solve, alternating
+// processes, profiles/r5/ab_ledger_timing/): the window shape for every size there.
 template <int R, bool ADD>
 void launch_apply(const ssp_ctx* ctx, hipStream_t st, const SynthArgs& a) {
-  const bool win = !ctx->synth_stride && (ADD || a.n >= (size_t(1) << 24));
+  const bool win = ctx->synth_window ||
+                   (!ctx->synth_stride && (ADD || R <= kTabRank || a.n >= (size_t(1) << 24)));
   if (a.exact) win ? launch_apply_ex<R, ADD, true, true>(ctx, st, a) : launch_apply_ex<R, ADD, true, false>(ctx, st, a);
   else win ? launch_apply_ex<R, ADD, false, true>(ctx, st, a) : launch_apply_ex<R, ADD, false, false>(ctx, st, a);
 }
@@ -536,7 +540,7 @@ void synth_mask_kernel(unsigned grid, hipStream_t st, const SynthArgs& a, unsign
   switch (a.rank) {
 #define F(r)                                                                                \
   case r:                                                                                   \
-    hipLaunchKernelGGL((k_synth_mask<r>), dim3(grid), dim3(kBlock), 0, st, a, mask); \
+    SSP_LAUNCH((k_synth_mask<r>), dim3(grid), dim3(kBlock), 0, st, a, mask); \
     break;
     SSP_RANK_CASES(F)
 #undef F
@@ -723,7 +727,7 @@ int sspx_synth_diagonal(ssp_ctx* ctx, const sspx_synth* spec, double* d, size_t 
   SSP_CHECK_CTX(ctx);
   if (!spec) return ssp::set_error(SSP_ERR_ARG, "sspx_synth_diagonal: null spec");
   if (n == 0) return SSP_OK;
-  hipLaunchKernelGGL(k_synth_diag, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, d, n, offset,
+  SSP_LAUNCH(k_synth_diag, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, d, n, offset,
                      spec->rho, spec->rank, spec->diag_kind, spec->alpha);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
@@ -751,7 +755,7 @@ int sspx_fill_random(ssp_ctx* ctx, double* x, size_t n, size_t offset, unsigned 
                      unsigned long long vec) {
   SSP_CHECK_CTX(ctx);
   if (n == 0) return SSP_OK;
-  hipLaunchKernelGGL(k_fill_random, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, x, n, offset,
+  SSP_LAUNCH(k_fill_random, dim3(ssp::stream_grid(ctx, n, 1)), dim3(kBlock), 0, ctx->stream, x, n, offset,
                      stream_key(seed, vec));
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
@@ -773,7 +777,7 @@ int sspx_dense_action(ssp_ctx* ctx, const double* a, size_t n_global, const doub
     p.n = n;
     p.offset = offset;
     if (n > 0) {
-      hipLaunchKernelGGL(k_dense_action, dim3(unsigned((n + 127) / 128)), dim3(128), 0, ctx->stream, p);
+      SSP_LAUNCH(k_dense_action, dim3(unsigned((n + 127) / 128)), dim3(128), 0, ctx->stream, p);
       SSP_TRY_HIP(hipGetLastError());
     }
   }
