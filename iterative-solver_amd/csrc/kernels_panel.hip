@@ -866,8 +866,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
       });
   if constexpr (GRAM) {
     block_partials<NP>(acc, NP, a.partial);
-    // launched with at most 4 workgroups per CU (launch_transform): one trip per 8 outputs
-    if (a.tail.counter) ssp::fold_tail<(NP < 8 ? NP : 8), 4>(a.partial, a.tail);
+    // one load trip per 8 outputs (M >= 7: up to 2048 workgroups; else up to 1024, launch_transform)
+    if (a.tail.counter) ssp::fold_tail<(NP < 8 ? NP : 8), (M >= 7 ? 8 : 4)>(a.partial, a.tail);
   }
 }
 
@@ -883,6 +883,7 @@ unsigned gram_grid(ssp_ctx* ctx, size_t n) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_transform<M, true, true>, kBlock, 0) != hipSuccess || occ < 1)
       occ = 2;
     per_cu = occ < 4 ? occ : 4;
+    if (const char* e = std::getenv("SSP_GRAM_WG_PER_CU")) per_cu = std::max(1, std::min(8, std::atoi(e)));  // A/B
   }
   return ssp::win_grid(ctx, n, 1, unsigned(per_cu));
 }
