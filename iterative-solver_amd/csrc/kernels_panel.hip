@@ -1186,6 +1186,9 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
       // A symmetric overlap <xx_i, xx_j> of up to 16 vectors: one panel that loads each vector once.
       bool sym = m == k && m <= ssp::kInnerRows && !(R == 1 && C <= 2);
       for (int i = 0; sym && i < m; ++i) sym = xx[i] == yy[i] && rs[size_t(i)] == cs[size_t(i)];
+      // MFMA panels: with one rank the reduce passes publish to the host themselves (fold_begin's host
+      // tail; with a communicator it names result_dev and fold_finish exchanges as reduce_fetch did)
+      if (!(R == 1 && C <= 2)) SSP_TRY(ssp::fold_begin(ctx, int(total), &tail));
       if (sym) {
         InnerArgs a{};
         a.m = a.k = m;
@@ -1198,7 +1201,7 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
         SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * m * m));
         a.partial = ctx->partial;
         SSP_TRY(launch_inner_sym(ctx, a, grid, sc));
-        SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), m, m, ctx->result_dev, m, 0, 0));
+        SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), m, m, ctx->result_dev, m, 0, 0, &tail, true));
       }
       for (int r0 = 0; !sym && !(R == 1 && C <= 2) && r0 < R; r0 += ssp::kInnerRows) {
         const int mr = std::min(ssp::kInnerRows, R - r0);
@@ -1221,8 +1224,9 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
           SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * a.m * a.k));
           a.partial = ctx->partial;
           SSP_TRY(launch_inner(ctx, a, grid, sc_launch));
-          SSP_TRY(
-              ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), a.m, a.k, ctx->result_dev, C, r0, c0));
+          const bool last = r0 + ssp::kInnerRows >= R && c0 + cols_per_launch >= C;
+          SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), a.m, a.k, ctx->result_dev, C, r0, c0, &tail,
+                                              last));
         }
       }
     }

@@ -246,6 +246,42 @@ __global__ __launch_bounds__(kBlock) void k_reduce_partials(const double* __rest
   if (threadIdx.x == 0) out[size_t(row0 + r) * ldo + col0 + c] = s;
 }
 
+// The same pass publishing straight to the coherent host result buffer (one rank, no exchange), in
+// place of k_reduce_partials + the k_publish copy behind it: each workgroup stores its sum to host
+// memory (system scope) and, in the call's last pass (`flag` set), drains the store before its arrival
+// (two-level counter, as ssp::fold_tail's); the last arriver sets the flag.  The earlier passes of a
+// call completed before this one started (stream order), so their stores are in memory by then.  The
+// sums are k_reduce_partials' (same order, same tree).
+__global__ __launch_bounds__(kBlock) void k_reduce_publish(const double* __restrict__ partial, int nblocks, int rows,
+                                                           int cols, double* host, int ldo, int row0, int col0,
+                                                           unsigned* counter, unsigned long long* flag,
+                                                           unsigned long long seq) {
+  const int o = blockIdx.x;
+  const int r = o / cols, c = o % cols;
+  const size_t stride = size_t(rows) * cols;
+  double s = 0;
+  for (int b = threadIdx.x; b < nblocks; b += kBlock) s += partial[size_t(b) * stride + o];
+  s = block_sum(s);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(host + size_t(row0 + r) * ldo + col0 + c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (flag) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sum has reached host memory
+      const unsigned G = gridDim.x, sh = blockIdx.x & (ssp::kFoldShards - 1);
+      const unsigned nsh = G < ssp::kFoldShards ? G : ssp::kFoldShards;
+      const unsigned in_sh = (G - sh + ssp::kFoldShards - 1) / ssp::kFoldShards;
+      unsigned* cs = counter + ssp::kFoldLine * sh;
+      if (__hip_atomic_fetch_add(cs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_sh - 1) {
+        __hip_atomic_store(cs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned* top = counter + ssp::kFoldLine * ssp::kFoldShards;
+        if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1) {
+          __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
+  }
+}
+
 struct PrecArgs {
   double* a[ssp::kPrecVec];
   double shift[ssp::kPrecVec];
@@ -302,8 +338,14 @@ int check_vec(const void* p, size_t n, const char* what) {
 
 namespace ssp {
 int launch_reduce_partials(ssp_ctx* ctx, const double* partial, int nblocks, int rows, int cols, double* out, int ldo,
-                           int row0, int col0) {
+                           int row0, int col0, const FoldTail* pub, bool last) {
   if (rows * cols == 0) return SSP_OK;
+  if (pub && pub->host) {
+    SSP_LAUNCH(k_reduce_publish, dim3(rows * cols), dim3(kBlock), 0, ctx->stream, partial, nblocks, rows, cols,
+               pub->host, ldo, row0, col0, pub->counter, last ? pub->flag : nullptr, pub->seq);
+    SSP_TRY_HIP(hipGetLastError());
+    return SSP_OK;
+  }
   SSP_LAUNCH(k_reduce_partials, dim3(rows * cols), dim3(kBlock), 0, ctx->stream, partial, nblocks, rows, cols,
                      out, ldo, row0, col0);
   SSP_TRY_HIP(hipGetLastError());

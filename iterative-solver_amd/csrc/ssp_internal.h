@@ -434,8 +434,11 @@ int exact_outer(ssp_ctx* ctx, const double* alphas, const double* const* xx, con
                 double* const* yy, const double* ys, int m, size_t n, bool set);
 
 // kernels_stream.hip
+// pub (one rank: fold_begin's tail with a host buffer): the sums go straight to the coherent host result
+// buffer at the same offsets as in `out`, and the call's last pass (last = true) raises its flag;
+// fold_finish delivers them.  Else into `out` (device), for reduce_fetch.
 int launch_reduce_partials(ssp_ctx* ctx, const double* partial, int nblocks, int rows, int cols, double* out,
-                           int ldo, int row0, int col0);
+                           int ldo, int row0, int col0, const FoldTail* pub = nullptr, bool last = false);
 
 }  // namespace ssp
 

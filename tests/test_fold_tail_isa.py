@@ -177,3 +177,51 @@ def test_the_checker_follows_the_control_flow_not_the_layout():
     assert [v[:3] for v in check(GOOD.replace("offset:8 sc1", "offset:8"))] == ["(4)"]
     assert [v[:3] for v in check(GOOD.replace("  s_waitcnt vmcnt(0)\n", ""))] == ["(2)"]
     assert [v[:3] for v in check(GOOD.replace("s[0:1] sc1\n  s_cbranch_execz", "s[0:1]\n  s_cbranch_execz"))] == ["(1)"]
+
+
+def store_drain_violations(ins):
+    """(1)-(3) without (4), for a publishing pass whose last arriver reads nothing back: the nearest
+    store before the first counter add carries sc1 on some path and every path drains vmcnt(0)."""
+    adds = [i for i, s in enumerate(ins) if s.startswith("global_atomic_add")]
+    if not adds:
+        return ["(3) no counter add"]
+    first = adds[0]
+    starts, succ, pred, block_of = cfg(ins)
+    bounds = lambda b: (starts[b], starts[b + 1] if b + 1 < len(starts) else len(ins))
+    bad, nearest, seen, work = [], [], set(), [(block_of[first], first - 1, False)]
+    while work:
+        b, i, drained = work.pop()
+        lo, _ = bounds(b)
+        while i >= lo and not ins[i].startswith("global_store"):
+            drained |= bool(re.match(r"s_waitcnt vmcnt\(0\)", ins[i]))
+            i -= 1
+        if i >= lo:
+            nearest.append(ins[i])
+            if not drained:
+                bad.append("(2) no vmcnt(0) drain between " + ins[i] + " and the counter add")
+            continue
+        for p in pred[b]:
+            if (p, drained) not in seen:
+                seen.add((p, drained))
+                work.append((p, bounds(p)[1] - 1, drained))
+    if not any("sc1" in s for s in nearest):
+        bad.append("(1) published store without sc1: " + str(nearest))
+    return bad
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_reduce_pass_publishes_before_it_arrives():
+    """k_reduce_publish (the gemm_inner panels' reduce pass with one rank): each workgroup's sum is a
+    system-scope (sc0 sc1) store drained with vmcnt(0) before the arrival counter's atomic add, so the
+    last arriver's flag follows every sum into host memory."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "kernels_stream.s")
+        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
+                            "-I" + CSRC, "--cuda-device-only", "-S", os.path.join(CSRC, "kernels_stream.hip"), "-o", out],
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        found = [(name, store_drain_violations(ins)) for name, ins in kernels(open(out).read())
+                 if "k_reduce_publish" in name]
+    assert found, "k_reduce_publish not emitted"
+    for name, bad in found:
+        assert not bad, (name, bad)
