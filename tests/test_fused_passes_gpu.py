@@ -61,7 +61,9 @@ def test_fused_passes_take_the_call_by_call_steps():
 
 # ---- ssp_transform_gram: the block self-orthonormalisation's pass (hbm_handlers.h orthonormalise_block)
 @pytest.mark.parametrize("m,n,gram", [(8, 1_000_003, True), (3, 777_777, True), (5, 64, True), (7, 300_001, False),
-                                      (8, 2048, True)])
+                                      (8, 2048, True), (1, 400_001, True), (2, 131_071, True), (4, 200_003, False),
+                                      (4, 200_003, True), (6, 150_001, True), (6, 99_999, False), (8, 12_345, False),
+                                      (7, 65_537, True), (1, 1500, False), (2, 33, True)])
 def test_transform_gram_in_place(ctx, m, n, gram):
     import numpy as np
 
