@@ -29,9 +29,10 @@ std::shared_ptr<Device> borrow(ssp_ctx* ctx) {
   return std::make_shared<Device>(ctx, true);
 }
 
+// zero-initialised (deferred, hbm_vec.h: stored only if something reads it before overwriting it)
 Vec zero_vec(const std::shared_ptr<Device>& dev, size_t n) {
   Vec v(dev, n);
-  check(ssp_fill(dev->ctx(), 0.0, v.data_wo(), v.local_size()), "ssp_fill");
+  v.fill_deferred(0.0);
   return v;
 }
 

@@ -140,7 +140,8 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
     m_counter->scal++;
     x.scale_by(alpha);
   }
-  void fill(double alpha, Vec& x) override { check(ssp_fill(x.ctx(), alpha, x.data_wo(), x.local_size()), "ssp_fill"); }
+  // deferred to the next access that needs the block (hbm_vec.h): a write-only access drops it
+  void fill(double alpha, Vec& x) override { x.fill_deferred(alpha); }
   void axpy(double alpha, const Vec& x, Vec& y) override {
     m_counter->axpy++;
     if (x.size() < y.size()) error("ArrayHandlerHbm::axpy() incompatible x and y arrays, x.size() < y.size()");

@@ -425,6 +425,45 @@ void op_cases() {
     expect(xc.local_values() == std::vector<double>(n, 0.5) && xc.scale() == 1.0, "fill drops the scale");
     expect(hb.counter().scal == 10, "scal counted");
   });
+  run("deferred_fill_matches_eager", [] {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    const size_t n = 1001;
+    auto v = random_values(n, 31), w = random_values(n, 32);
+    // a pending fill reads as the fill value and is stored on the first read
+    auto x = make(v);
+    hb.fill(-2.5, x);
+    expect(x.fill_pending(), "fill pending");
+    expect(x.local_values() == std::vector<double>(n, -2.5), "materialised fill");
+    expect(!x.fill_pending(), "fill stored");
+    // a write-only destination drops it: no pass, and the kernel's values stand
+    auto y = make(v);
+    hb.fill(0.0, y);
+    auto z = make(w);
+    hb.copy(y, z);  // y = z
+    expect(y.local_values() == w, "copy over a pending fill");
+    // a fill then a read-modify-write (axpy) and a scal: the eager sequence's values
+    auto a = make(v), b = make(w);
+    hb.fill(0.5, a);
+    hb.axpy(2.0, b, a);
+    std::vector<double> want(n);
+    for (size_t i = 0; i < n; ++i) want[i] = 0.5 + 2.0 * w[i];
+    expect(a.local_values() == want, "axpy into a pending fill");
+    auto c = make(v);
+    hb.fill(3.0, c);
+    hb.scal(-0.25, c);
+    expect(c.local_values() == std::vector<double>(n, 3.0 * -0.25), "scal of a pending fill");
+    // copies share the pending fill; storing it for one leaves the other's value
+    auto d = make(v);
+    hb.fill(1.25, d);
+    auto e = hb.copy(d);
+    hb.axpy(1.0, b, e);
+    std::vector<double> we(n);
+    for (size_t i = 0; i < n; ++i) we[i] = 1.25 + w[i];
+    expect(e.local_values() == we, "copy of a pending fill, then axpy");
+    expect(d.local_values() == std::vector<double>(n, 1.25), "source keeps the fill");
+    expect(hb.dot(d, b) == hb.dot(make(std::vector<double>(n, 1.25)), b), "dot of a pending fill");
+  });
   run("error_types", [] {
     ArrayHandlerHbm handler;
     array::ArrayHandler<Vec, Vec>& hb = handler;
