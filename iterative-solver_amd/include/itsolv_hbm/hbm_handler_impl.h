@@ -225,6 +225,18 @@ class ArrayHandlerHbm : public array::ArrayHandler<Vec, Vec> {
                  const std::vector<std::reference_wrapper<const Vec>>& xx,
                  const std::vector<std::reference_wrapper<const Vec>>& yy,
                  std::vector<std::reference_wrapper<double>>& out) override {
+    // a batch of self-dots whose values the kernels that wrote the vectors have recorded
+    // (Vec::set_known_norm2: the block self-orthonormalisation's last Gram pass): no pass
+    bool known = !reg.empty();
+    std::vector<double> kv(reg.size());
+    for (size_t r = 0; known && r < reg.size(); ++r) {
+      const auto& [x, y, z] = reg[r];
+      known = &xx[x].get() == &yy[y].get() && xx[x].get().known_norm2(&kv[r]);
+    }
+    if (known) {
+      for (size_t r = 0; r < reg.size(); ++r) out[std::get<2>(reg[r])].get() = kv[r];
+      return;
+    }
     const auto m = gemm_inner(itsolv::CVecRef<Vec>(xx.begin(), xx.end()), itsolv::CVecRef<Vec>(yy.begin(), yy.end()));
     for (const auto& [x, y, z] : reg) out[z].get() = m(x, y);
   }

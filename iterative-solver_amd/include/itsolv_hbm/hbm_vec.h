@@ -101,6 +101,11 @@ class Device {
 // block is shared), while data_wo() drops it with the contents.  The runners' zero-initialised
 // vectors (the reference's test drivers' std::vector<double>(n)) that the action or the initial guess
 // then overwrites in full therefore cost no pass.
+//
+// A kernel that has just formed a vector's self-dot as a by-product (the last pass of the block
+// self-orthonormalisation forms the Gram matrix of the vectors it stores) records it
+// (set_known_norm2); the handlers' batched dots return it instead of reading the vector again, until
+// any access that may change the value (data_rw, data_wo, the deferred forms, a scal or a fill).
 class Vec {
   struct Block {
     std::shared_ptr<Device> dev;
@@ -142,6 +147,8 @@ class Vec {
     std::swap(m_scale, o.m_scale);
     std::swap(m_fill_pending, o.m_fill_pending);
     std::swap(m_fill_value, o.m_fill_value);
+    std::swap(m_norm2_known, o.m_norm2_known);
+    std::swap(m_norm2, o.m_norm2);
     std::swap(m_size, o.m_size);
     std::swap(m_local, o.m_local);
     std::swap(m_offset, o.m_offset);
@@ -161,12 +168,14 @@ class Vec {
   }
   //! Read-modify-write destination, scale applied first; the block is this vector's alone.
   double* data_rw() {
+    m_norm2_known = false;
     materialize();
     detach(true);
     return m_block ? m_block->p : nullptr;
   }
   //! Destination written in full without being read: contents, scale and pending fill are dropped.
   double* data_wo() {
+    m_norm2_known = false;
     m_scale = 1.0;
     m_fill_pending = false;
     detach(false);
@@ -174,6 +183,7 @@ class Vec {
   }
   //! The handlers' fill: x = alpha everywhere, deferred until an access needs the block (see above).
   void fill_deferred(double alpha) {
+    m_norm2_known = false;
     m_scale = 1.0;
     m_fill_pending = true;
     m_fill_value = alpha;
@@ -189,6 +199,7 @@ class Vec {
   //! the pending scale here) and stores the result in full; call scale_applied() once that kernel
   //! has been issued successfully (on an error the vector keeps its value: block and scale).
   double* data_rw_deferred(double* s) {
+    m_norm2_known = false;
     materialize_fill();
     detach(true);
     *s = m_scale;
@@ -199,6 +210,7 @@ class Vec {
   //! The handlers' scal: x *= a, deferred to the next kernel that reads x (see above).  A second
   //! scal before any kernel has applied the first stores the first (two roundings, as the reference).
   void scale_by(double a) {
+    m_norm2_known = false;
     materialize();
     m_scale = a;
   }
@@ -225,6 +237,15 @@ class Vec {
     m_fill_pending = false;
   }
   bool fill_pending() const { return m_fill_pending; }
+  //! The vector's self-dot as formed by the kernel that just wrote it (see above).
+  void set_known_norm2(double v) {
+    m_norm2 = v;
+    m_norm2_known = true;
+  }
+  bool known_norm2(double* v) const {
+    if (m_norm2_known) *v = m_norm2;
+    return m_norm2_known;
+  }
   //! Whether another Vec holds the same storage.
   bool shares_storage() const { return m_block && m_block.use_count() > 1; }
   ssp_ctx* ctx() const { return m_dev->ctx(); }
@@ -255,6 +276,8 @@ class Vec {
   mutable double m_scale = 1.0;
   mutable bool m_fill_pending = false;
   double m_fill_value = 0.0;
+  bool m_norm2_known = false;
+  double m_norm2 = 0.0;
 };
 
 }  // namespace molpro::linalg::hbm

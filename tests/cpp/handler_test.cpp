@@ -464,6 +464,49 @@ void op_cases() {
     expect(d.local_values() == std::vector<double>(n, 1.25), "source keeps the fill");
     expect(hb.dot(d, b) == hb.dot(make(std::vector<double>(n, 1.25)), b), "dot of a pending fill");
   });
+  run("known_self_dots", [] {
+    ArrayHandlerHbm handler;
+    array::ArrayHandler<Vec, Vec>& hb = handler;
+    const size_t n = 777;
+    auto x = make(random_values(n, 41)), y = make(random_values(n, 42));
+    const double dx = hb.dot(x, x), dy = hb.dot(y, y);
+    // recorded self-dots answer a batch of self-dots (the marker values prove no pass ran) ...
+    x.set_known_norm2(5.0);
+    y.set_known_norm2(7.0);
+    double a = 0, b = 0;
+    {
+      auto lazy = hb.lazy_handle();
+      lazy.dot(x, x, a);
+      lazy.dot(y, y, b);
+      lazy.eval();
+    }
+    expect(a == 5.0 && b == 7.0, "recorded self-dots returned");
+    // ... a batch with any other dot computes them all, and a write forgets the record
+    double c = 0, d = 0;
+    {
+      auto lazy = hb.lazy_handle();
+      lazy.dot(x, x, c);
+      lazy.dot(x, y, d);
+      lazy.eval();
+    }
+    expect(c == dx, "mixed batch computed");
+    hb.scal(1.0, y);
+    double e = 0;
+    {
+      auto lazy = hb.lazy_handle();
+      lazy.dot(y, y, e);
+      lazy.eval();
+    }
+    expect(e == dy, "record dropped by a scal");
+    x.data_rw();
+    double f = 0;
+    {
+      auto lazy = hb.lazy_handle();
+      lazy.dot(x, x, f);
+      lazy.eval();
+    }
+    expect(f == dx, "record dropped by a read-write access");
+  });
   run("error_types", [] {
     ArrayHandlerHbm handler;
     array::ArrayHandler<Vec, Vec>& hb = handler;

@@ -47,13 +47,13 @@ def emul_dir():
 
 def test_handlers_restated_base_emulated_device():
     out = build_and_run(emul_dir(), "ssp_emul")
-    assert "base: restated" in out and out.count("PASS ") == 20
+    assert "base: restated" in out and out.count("PASS ") == 21
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference tree not present")
 def test_handlers_on_the_reference_base_emulated_device():
     out = build_and_run(emul_dir(), "ssp_emul", ["-DWITH_REFERENCE_BASE", "-I" + REF_SRC])
-    assert "base: reference" in out and out.count("PASS ") == 19
+    assert "base: reference" in out and out.count("PASS ") == 20
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference tree not present")
@@ -78,4 +78,4 @@ def test_reference_handler_header_compiles_standalone():
 @pytest.mark.gpu
 def test_handlers_restated_base_on_mi355x():
     out = build_and_run(os.path.join(ROOT, "iterative-solver_amd", "lib"), "subspace_hip")
-    assert out.count("PASS ") == 20
+    assert out.count("PASS ") == 21
