@@ -186,6 +186,11 @@ int ssp_axpy_pairs_norm(ssp_ctx* ctx, const double* c, const double* const* xx, 
                         const double* ys, int m, size_t n, double* out);
 /* a[v][i] /= (d[i] - shift[v] + 1e-15) for v in [0,nvec)   reference itsolv/IterativeSolver.h:34-55 */
 int ssp_precondition(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n);
+/* The same with the self-dots of the results, norms2[v] = <a_v', a_v'> summed over ranks, formed in the
+ * same pass (short vectors: the reference's sequential dots, as ssp_gemm_inner).  0 <= nvec <= 8.
+ *                                                                          bytes 8N (1 + 2 nvec) */
+int ssp_precondition_norms(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n,
+                           double* norms2);
 
 /* ---- deferred scal (itsolv_hbm/hbm_vec.h, Vec::scale_by): an operand's value is s * (its stored
  *      contents); the kernel multiplies each element by s as it loads it -- the one rounding the

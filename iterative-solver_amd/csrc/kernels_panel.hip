@@ -909,6 +909,79 @@ void launch_transform(ssp_ctx* ctx, int m, unsigned grid, const TransformArgs& a
   }
 }
 
+// The Davidson preconditioner with the self-dots of its outputs (precondition_default, reference
+// IterativeSolver.h:52-53, followed by the normalisation of the new R vectors, propose_rspace.h:17-28):
+// a_v <- a_v / ((d - shift_v) + 1e-15), element for element k_precondition's operations, and
+// acc_v += a_v'^2 in the same pass.  M vectors per launch (compile-time bound, nvec <= M).
+struct PrecNormArgs {
+  double* a[ssp::kOuterDst];
+  double shift[ssp::kOuterDst];
+  const double* d;
+  int nvec;
+  size_t n;
+  double* partial;     // [gridDim.x][nvec]
+  ssp::FoldTail tail;  // fused fold when tail.counter is set
+};
+
+template <int M>
+__global__ __launch_bounds__(kBlock) void k_precondition_norms(const PrecNormArgs p) {
+  using ssp::ld2nt;
+  using ssp::st2nt;
+  constexpr int U = 4;
+  double acc[M];
+#pragma unroll
+  for (int v = 0; v < M; ++v) acc[v] = 0;
+  ssp::for_windows<U>(
+      p.n,
+      [&](size_t p0) {
+        double2 dv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) dv[u] = ld2nt(p.d + 2 * (p0 + 64 * u));
+#pragma unroll
+        for (int v = 0; v < M; ++v) {
+          if (v < p.nvec) {
+            double2 av[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) av[u] = ld2nt(p.a[v] + 2 * (p0 + 64 * u));
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              av[u].x = av[u].x / (dv[u].x - p.shift[v] + 1e-15);
+              av[u].y = av[u].y / (dv[u].y - p.shift[v] + 1e-15);
+              st2nt(p.a[v] + 2 * (p0 + 64 * u), av[u]);
+              acc[v] = fma(av[u].x, av[u].x, acc[v]);
+              acc[v] = fma(av[u].y, av[u].y, acc[v]);
+            }
+          }
+        }
+      },
+      [&](size_t i) {
+        const double2 dv = ld2(p.d + 2 * i);
+#pragma unroll
+        for (int v = 0; v < M; ++v) {
+          if (v < p.nvec) {
+            double2 av = ld2(p.a[v] + 2 * i);
+            av.x = av.x / (dv.x - p.shift[v] + 1e-15);
+            av.y = av.y / (dv.y - p.shift[v] + 1e-15);
+            *reinterpret_cast<double2*>(p.a[v] + 2 * i) = av;
+            acc[v] = fma(av.x, av.x, acc[v]);
+            acc[v] = fma(av.y, av.y, acc[v]);
+          }
+        }
+      },
+      [&](size_t j) {
+#pragma unroll
+        for (int v = 0; v < M; ++v) {
+          if (v < p.nvec) {
+            const double a = p.a[v][j] / (p.d[j] - p.shift[v] + 1e-15);
+            p.a[v][j] = a;
+            acc[v] = fma(a, a, acc[v]);
+          }
+        }
+      });
+  block_partials<M>(acc, p.nvec, p.partial);
+  if (p.tail.counter) ssp::fold_tail<(M < 8 ? M : 8)>(p.partial, p.tail);
+}
+
 // Residuals and their norms in one pass (construct_residual + update_errors, reference
 // LinearEigensystemDavidson.h:186-192 and IterativeSolverTemplate.h:95-102): y_j = y_j s^y_j +
 // c_j (x_j s^x_j) -- ssp_axpy_scaled's fma, element for element -- then acc_j += y_j^2.
@@ -1647,6 +1720,47 @@ int ssp_transform_gram(ssp_ctx* ctx, const double* t, double* const* xx, const d
   for (int i = 0, q = 0; i < m; ++i)
     for (int j = i; j < m; ++j, ++q) gram[size_t(i) * m + j] = gram[size_t(j) * m + i] = pr[size_t(q)];
   return SSP_OK;
+}
+
+int ssp_precondition_norms(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n,
+                           double* norms2) {
+  SSP_CHECK_CTX(ctx);
+  if (nvec < 0 || nvec > 8 || (nvec > 0 && (!a || !shift || !norms2)))
+    return ssp::set_error(SSP_ERR_ARG, "ssp_precondition_norms: bad vectors (0 <= nvec <= 8)");
+  if (nvec == 0) return SSP_OK;
+  // short vectors: the reference's arithmetic for the dots (sequential sums), as gemm_inner computes
+  // them; the bandwidth path's self-dots come from the pass itself
+  if (n == 0 || ssp::exact_mode(ctx, n)) {
+    SSP_TRY(ssp_precondition(ctx, a, nvec, d, shift, n));
+    std::vector<const double*> c(a, a + nvec);
+    std::vector<double> g(size_t(nvec) * nvec);
+    SSP_TRY(ssp_gemm_inner(ctx, c.data(), nvec, c.data(), nvec, n, g.data()));
+    for (int v = 0; v < nvec; ++v) norms2[v] = g[size_t(v) * nvec + v];
+    return SSP_OK;
+  }
+  SSP_TRY(check_ptrs(&d, 1, n, "ssp_precondition_norms"));
+  SSP_TRY(check_ptrs(const_cast<const double* const*>(a), nvec, n, "ssp_precondition_norms"));
+  PrecNormArgs p{};
+  p.nvec = nvec;
+  for (int v = 0; v < nvec; ++v) {
+    p.a[v] = a[v];
+    p.shift[v] = shift[v];
+  }
+  p.d = d;
+  p.n = n;
+  ssp::FoldTail tail{};
+  {
+    ssp::LedgerScope ls(ctx, "precondition", 8.0 * n * (1 + 2 * nvec));
+    const unsigned grid = ssp::win_grid(ctx, n, 4, 8);
+    SSP_TRY(ssp::fold_begin(ctx, nvec, &tail));
+    SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * nvec));
+    p.partial = ctx->partial;
+    p.tail = tail;
+    if (nvec <= 4) SSP_LAUNCH(k_precondition_norms<4>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+    else SSP_LAUNCH(k_precondition_norms<8>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+    SSP_TRY_HIP(hipGetLastError());
+  }
+  return ssp::fold_finish(ctx, tail, norms2);
 }
 
 }  // extern "C"

@@ -376,10 +376,21 @@ inline bool orthonormalise_two_pass(const itsolv::VecRef<Vec>& rr, double norm_t
 // Davidson preconditioner on HBM vectors: reference precondition_default (IterativeSolver.h:34-55)
 // as one fused kernel over all working-set vectors (d read once).  Found by argument-dependent
 // lookup from Problem<R>::precondition.
+// From the fused-pass size (fused_min_size) and up to 8 vectors the same pass forms the self-dots of
+// the results (ssp_precondition_norms), which the solver's normalisation of the new R vectors reads
+// next (propose_rspace.h:17-28, through Vec::known_norm2): no second pass over them.
 inline void precondition_default(const itsolv::VecRef<Vec>& action, const std::vector<double>& shift,
                                  const Vec& diagonals) {
   if (action.empty()) return;
   auto a = detail::rw_ptrs(action);
+  if (a.size() <= 8 && action[0].get().size() >= fused_min_size()) {
+    std::vector<double> n2(a.size());
+    check(ssp_precondition_norms(diagonals.ctx(), a.data(), int(a.size()), diagonals.data(), shift.data(),
+                                 diagonals.local_size(), n2.data()),
+          "ssp_precondition_norms");
+    for (size_t v = 0; v < a.size(); ++v) action[v].get().set_known_norm2(n2[v]);
+    return;
+  }
   check(ssp_precondition(diagonals.ctx(), a.data(), int(a.size()), diagonals.data(), shift.data(),
                          diagonals.local_size()),
         "ssp_precondition");

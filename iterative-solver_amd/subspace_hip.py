@@ -37,7 +37,7 @@ EXPORTS = [
     "ssp_ctx_set_exact_max",
     "ssp_ledger_enable", "ssp_ledger_reset", "ssp_ledger_count", "ssp_ledger_reserve",
     "ssp_ledger_entry", "ssp_fill", "ssp_scal", "ssp_copy", "ssp_axpy", "ssp_dot",
-    "ssp_gemm_inner", "ssp_gemm_outer", "ssp_gemm_outer_set", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_axpy_gram", "ssp_transform_gram", "ssp_axpy_pairs_norm", "ssp_precondition", "ssp_select", "ssp_select_max_dot",
+    "ssp_gemm_inner", "ssp_gemm_outer", "ssp_gemm_outer_set", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_axpy_gram", "ssp_transform_gram", "ssp_axpy_pairs_norm", "ssp_precondition", "ssp_precondition_norms", "ssp_select", "ssp_select_max_dot",
     "ssp_sparse_copy", "ssp_sparse_axpy", "ssp_sparse_axpy_batch", "ssp_sparse_dot", "ssp_gemm_inner_sparse", "ssp_gemm_outer_sparse",
     "ssp_construct_solution",
     "sspx_synthetic_action", "sspx_synthetic_add_lowrank", "sspx_synthetic_diagonal", "sspx_fill_random", "sspx_dense_action",
@@ -129,6 +129,7 @@ def _declare(lib):
         "ssp_transform_gram": (I, [P, PD, P, PD, I, Z, PD]),
         "ssp_axpy_pairs_norm": (I, [P, PD, P, PD, P, PD, I, Z, PD]),
         "ssp_precondition": (I, [P, P, I, P, PD, Z]),
+        "ssp_precondition_norms": (I, [P, P, I, P, PD, Z, PD]),
         "ssp_select": (I, [P, P, Z, Z, Z, I, I, PZ, PD, PZ]),
         "ssp_select_max_dot": (I, [P, P, P, Z, Z, Z, PZ, PD, PZ]),
         "ssp_sparse_copy": (I, [P, P, Z, Z, PZ, PD, Z]),
@@ -605,6 +606,13 @@ class Context:
     def precondition(self, aa: Sequence[DeviceVector], d: DeviceVector, shift: Sequence[float]):
         sh = np.ascontiguousarray(shift, dtype=np.float64)
         _check(self.lib.ssp_precondition(self.handle, _ptrs(aa), len(aa), d.ptr, _dptr(sh), d.n))
+
+    def precondition_norms(self, aa: Sequence[DeviceVector], d: DeviceVector, shift: Sequence[float]) -> np.ndarray:
+        """ssp_precondition plus the self-dots of the results, formed in the same pass."""
+        sh = np.ascontiguousarray(shift, dtype=np.float64)
+        out = np.zeros(max(1, len(aa)))
+        _check(self.lib.ssp_precondition_norms(self.handle, _ptrs(aa), len(aa), d.ptr, _dptr(sh), d.n, _dptr(out)))
+        return out[: len(aa)]
 
     def select(self, x: DeviceVector, nsel: int, max: bool = False, ignore_sign: bool = False, offset: int = 0):
         idx = np.zeros(max_(nsel), dtype=np.uint64)

@@ -424,6 +424,16 @@ int ssp_precondition(ssp_ctx*, double* const* a, int nvec, const double* d, cons
   return SSP_OK;
 }
 
+int ssp_precondition_norms(ssp_ctx* c, double* const* a, int nvec, const double* d, const double* shift, size_t n,
+                           double* norms2) {
+  if (nvec < 0 || nvec > 8 || (nvec > 0 && (!a || !shift || !norms2)))
+    return fail(SSP_ERR_ARG, "ssp_precondition_norms: bad vectors (0 <= nvec <= 8)");
+  if (nvec == 0) return SSP_OK;
+  ssp_precondition(c, a, nvec, d, shift, n);
+  for (int v = 0; v < nvec; ++v) norms2[v] = dot_n(a[v], a[v], n);
+  return reduce(c, norms2, size_t(nvec));
+}
+
 int ssp_select_merge(int nranks, const size_t* counts, size_t stride, const size_t* idx, const double* val,
                      size_t nsel, int max, size_t* io, double* vo, size_t* nout) {
   struct It {

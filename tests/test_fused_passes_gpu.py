@@ -109,3 +109,28 @@ def test_block_orthonormalisation_is_mgs_in_exact_arithmetic(ctx):
         for j in range(i + 1, m):
             mgs[j] -= (mgs[i] @ mgs[j]) * mgs[i]
     assert np.max(np.abs(Q - mgs)) < 1e-10
+
+
+# ---- ssp_precondition_norms: the preconditioner with the self-dots of its results
+@pytest.mark.parametrize("nvec,n", [(8, 1_000_003), (3, 262_145), (5, 2048), (1, 4097), (8, 777)])
+def test_precondition_norms(ctx, nvec, n):
+    import numpy as np
+
+    rng = np.random.default_rng(nvec * 7 + n % 101)
+    A = rng.uniform(-1, 1, (nvec, n))
+    dvals = 1.0 + np.arange(n, dtype=np.float64)
+    shift = rng.uniform(0.1, 0.9, nvec)
+    d = ctx.upload(dvals)
+    plain = [ctx.upload(v) for v in A]
+    fused = [ctx.upload(v) for v in A]
+    ctx.precondition(plain, d, shift)
+    norms = ctx.precondition_norms(fused, d, shift)
+    got = np.array([ctx.download(v) for v in fused])
+    want = np.array([ctx.download(v) for v in plain])
+    assert np.array_equal(got, want)  # the vectors: k_precondition's operations element for element
+    ref = np.einsum("ij,ij->i", want, want)
+    if n <= 2048:  # short vectors: the dots of ssp_gemm_inner (the reference's sequential sums)
+        g = ctx.gemm_inner(plain, plain)
+        assert np.array_equal(norms, np.diag(g))
+    else:
+        assert np.all(np.abs(norms - ref) <= 1e-13 * ref)
