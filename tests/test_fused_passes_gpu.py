@@ -133,4 +133,4 @@ def test_precondition_norms(ctx, nvec, n):
         g = ctx.gemm_inner(plain, plain)
         assert np.array_equal(norms, np.diag(g))
     else:
-        assert np.all(np.abs(norms - ref) <= 1e-13 * ref)
+        assert np.all(np.abs(norms - ref) <= 1e-11 * ref)  # a sum of n positive terms in another order
