@@ -140,10 +140,30 @@ void extract_solutions(Solver& solver, std::vector<R>& params, std::vector<R>& a
   }
 }
 
+// Batched form of residual_norm: out[i] = |H x_i - e_i x_i| / |x_i| for a batch of solutions at once.
+template <class R>
+using ResidualNormsBatch = std::function<void(const std::vector<const R*>&, const std::vector<double>&, std::vector<double>&)>;
+
+// extract_solutions with the whole batch handed over: each_batch(first root, count, params).
+template <class Solver, class R, class F>
+void extract_solution_batches(Solver& solver, std::vector<R>& params, std::vector<R>& actions, int nroots,
+                              F&& each_batch) {
+  const size_t batch = std::min(params.size(), actions.size());
+  if (batch == 0) return;
+  for (size_t r0 = 0; r0 < size_t(std::max(nroots, 0)); r0 += batch) {
+    const size_t nb = std::min(batch, size_t(nroots) - r0);
+    std::vector<int> roots(nb);
+    for (size_t i = 0; i < nb; ++i) roots[i] = int(r0 + i);
+    solver.solution(roots, params, actions);
+    each_batch(r0, nb, params);
+  }
+}
+
 template <class R, class Q, class P>
 void run_davidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R, P>& problem,
                   const std::function<R()>& make_vec, const std::function<double(const R&, double)>& residual_norm,
-                  const itsolv_options& o, itsolv_result& out, const std::function<void(size_t, const R&)>& emit) {
+                  const itsolv_options& o, itsolv_result& out, const std::function<void(size_t, const R&)>& emit,
+                  const ResidualNormsBatch<R>& residual_norms_batch = {}) {
   LinearEigensystemDavidson<R, Q, P> solver(handlers);
   LinearEigensystemDavidsonOptions opt;
   apply_options(o, opt);
@@ -176,7 +196,25 @@ void run_davidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Proble
     out.eigenvalues[i] = ev[i];
     out.errors[i] = i < int(solver.errors().size()) ? solver.errors()[i] : 0.0;
   }
-  // Solutions, residuals recomputed from the problem's action.
+  // Solutions, residuals recomputed from the problem's action (per root, or per batch of extracted
+  // roots when the caller has the batched form: one action over the batch, the residuals with their
+  // norms in one pass).
+  if (residual_norms_batch) {
+    extract_solution_batches(solver, params, actions, out.nroots, [&](size_t r0, size_t nb, std::vector<R>& xs) {
+      std::vector<const R*> px;
+      std::vector<double> e, rn(nb);
+      for (size_t i = 0; i < nb; ++i) {
+        px.push_back(&xs[i]);
+        e.push_back(ev[r0 + i]);
+      }
+      residual_norms_batch(px, e, rn);
+      for (size_t i = 0; i < nb; ++i) {
+        out.residual_norms[r0 + i] = rn[i];
+        if (emit) emit(r0 + i, xs[i]);
+      }
+    });
+    return;
+  }
   extract_solutions(solver, params, actions, out.nroots, [&](int r, const R& x) {
     out.residual_norms[r] = residual_norm(x, ev[size_t(r)]);
     if (emit) emit(size_t(r), x);
