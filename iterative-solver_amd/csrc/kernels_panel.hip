@@ -877,14 +877,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
 // 20 dependent trips, 70 us of a 340 us launch at the C4 shard.
 template <int M>
 unsigned gram_grid(ssp_ctx* ctx, size_t n) {
-  static int per_cu = 0;  // resident workgroups per CU of k_transform<M, true, true>
-  if (per_cu == 0) {
+  // resident workgroups per CU of k_transform<M, true, true> (thread-safe one-time initialisation)
+  static const int per_cu = [] {
+    if (const char* e = std::getenv("SSP_GRAM_WG_PER_CU")) return std::max(1, std::min(8, std::atoi(e)));  // A/B
     int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_transform<M, true, true>, kBlock, 0) != hipSuccess || occ < 1)
       occ = 2;
-    per_cu = occ < 4 ? occ : 4;
-    if (const char* e = std::getenv("SSP_GRAM_WG_PER_CU")) per_cu = std::max(1, std::min(8, std::atoi(e)));  // A/B
-  }
+    return occ < 4 ? occ : 4;
+  }();
   return ssp::win_grid(ctx, n, 1, unsigned(per_cu));
 }
 
