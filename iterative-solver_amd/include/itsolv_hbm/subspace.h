@@ -407,9 +407,25 @@ class XSpace {
       qx[EqnData::H].slice({0, d.oD}, {nn, d.oD + d.nD}) = util::overlap(lhs_h, da, h.rq());
       qq[EqnData::rhs] = util::overlap(params, rhs(), h.rq());
     }
-    qx[EqnData::S].slice({0, d.oP}, {nn, d.oP + d.nP}) = util::overlap(params, pp, h.rp());
+    bool p_rows_done = false;
+    if constexpr (array::batched_symmetric_overlap<R>::value) {
+      // device handlers: S(R, P) and H(P, R) as one sparse inner product over [params, actions] (one
+      // launch, one reduction; each element is the same sum over its P vector's entries either way)
+      if (m_hermitian && d.nP > 0 && nn > 0) {
+        CVecRef<R> both(params.begin(), params.end());
+        both.insert(both.end(), actions.begin(), actions.end());
+        const auto g = util::overlap(both, pp, h.rp());
+        for (size_t i = 0; i < nn; ++i)
+          for (size_t j = 0; j < d.nP; ++j) {
+            qx[EqnData::S](i, d.oP + j) = g(i, j);
+            xq[EqnData::H](d.oP + j, i) = g(nn + i, j);
+          }
+        p_rows_done = true;
+      }
+    }
+    if (!p_rows_done) qx[EqnData::S].slice({0, d.oP}, {nn, d.oP + d.nP}) = util::overlap(params, pp, h.rp());
     if (m_hermitian) {
-      xq[EqnData::H].slice({d.oP, 0}, {d.oP + d.nP, nn}) = util::overlap(pp, actions, h.rp());
+      if (!p_rows_done) xq[EqnData::H].slice({d.oP, 0}, {d.oP + d.nP, nn}) = util::overlap(pp, actions, h.rp());
       transpose_copy(xq[EqnData::H].slice({d.oQ, 0}, {d.oQ + d.nQ, nn}), qx[EqnData::H].slice({0, d.oQ}, {nn, d.oQ + d.nQ}));
       transpose_copy(xq[EqnData::H].slice({d.oD, 0}, {d.oD + d.nD, nn}), qx[EqnData::H].slice({0, d.oD}, {nn, d.oD + d.nD}));
       transpose_copy(qx[EqnData::H].slice({0, d.oP}, {nn, d.oP + d.nP}), xq[EqnData::H].slice({d.oP, 0}, {d.oP + d.nP, nn}));
