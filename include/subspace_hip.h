@@ -178,6 +178,11 @@ int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store
  *                                                                          bytes 16 N m */
 int ssp_transform_gram(ssp_ctx* ctx, const double* t, double* const* xx, const double* xs, int m, size_t n,
                        double* gram);
+/* The same transform with only the self-dots of the new vectors, norms2[j] = <x_j', x_j'> summed over
+ * ranks, formed in the same pass (the M accumulators of the plain kernel's window shape; short
+ * vectors: the reference's sequential dots).                               bytes 16 N m */
+int ssp_transform_norms(ssp_ctx* ctx, const double* t, double* const* xx, const double* xs, int m, size_t n,
+                        double* norms2);
 /* Residuals and their norms (construct_residual + update_errors, reference
  * LinearEigensystemDavidson.h:186-192, IterativeSolverTemplate.h:95-102) in one pass:
  *   yy[j] = ys[j] yy[j] + c[j] (xs[j] xx[j])  (= ssp_axpy_scaled per pair, yy bit-identical),

@@ -776,16 +776,19 @@ __device__ __forceinline__ kernarg_dp transform_column(int j) {
   return tp + j * M;
 }
 
-// M = m exactly (instantiated for m = 1..8): no per-vector branch in the streaming loop.
-template <int M, bool GRAM, bool FMA>
+// M = m exactly (instantiated for m = 1..8): no per-vector branch in the streaming loop.  DOTS: 0 none,
+// 1 the M self-dots <x_j', x_j'> (accumulated as each output is formed), 2 the M(M+1)/2 pair dots.
+template <int M, int DOTS, bool FMA>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_transform(const TransformArgs a) {
   using ssp::ld2nt;
   using ssp::st2nt;
+  constexpr bool GRAM = DOTS == 2, NORM = DOTS == 1;
   constexpr int NP = M * (M + 1) / 2;
+  constexpr int NA = GRAM ? NP : (NORM ? M : 1);
   constexpr int U = GRAM ? 1 : (M <= 4 ? 4 : 2);  // GRAM keeps every output of the window for the pair dots
-  double acc[GRAM ? NP : 1];
+  double acc[NA];
 #pragma unroll
-  for (int q = 0; q < (GRAM ? NP : 1); ++q) acc[q] = 0;
+  for (int q = 0; q < NA; ++q) acc[q] = 0;
   auto pairs = [&](const double (&y)[M]) {
     if constexpr (GRAM) {
       int q = 0;
@@ -823,6 +826,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
             st2nt(a.x[j] + 2 * (p0 + 64 * u), make_double2(vl, vh));
             ylo[j] = vl;  // (GRAM: U = 1)
             yhi[j] = vh;
+            if constexpr (NORM) {
+              acc[j] = fma(vl, vl, acc[j]);
+              acc[j] = fma(vh, vh, acc[j]);
+            }
           }
         }
         pairs(ylo);
@@ -845,6 +852,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
           *reinterpret_cast<double2*>(a.x[j] + 2 * p) = make_double2(vl, vh);
           ylo[j] = vl;
           yhi[j] = vh;
+          if constexpr (NORM) {
+            acc[j] = fma(vl, vl, acc[j]);
+            acc[j] = fma(vh, vh, acc[j]);
+          }
         }
         pairs(ylo);
         pairs(yhi);
@@ -861,6 +872,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
           for (int i = 0; i < M; ++i) v = tmul<FMA>(tc[i], x1[i], v);
           a.x[j][e] = v;
           y1[j] = v;
+          if constexpr (NORM) acc[j] = fma(v, v, acc[j]);
         }
         pairs(y1);
       });
@@ -868,6 +880,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     block_partials<NP>(acc, NP, a.partial);
     // one load trip per 8 outputs (M >= 7: up to 2048 workgroups; else up to 1024, launch_transform)
     if (a.tail.counter) ssp::fold_tail<(NP < 8 ? NP : 8), (M >= 7 ? 8 : 4)>(a.partial, a.tail);
+  } else if constexpr (NORM) {
+    block_partials<M>(acc, M, a.partial);
+    if (a.tail.counter) ssp::fold_tail<M, 4>(a.partial, a.tail);  // two trips at 2048 workgroups
   }
 }
 
@@ -877,11 +892,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
 // 20 dependent trips, 70 us of a 340 us launch at the C4 shard.
 template <int M>
 unsigned gram_grid(ssp_ctx* ctx, size_t n) {
-  // resident workgroups per CU of k_transform<M, true, true> (thread-safe one-time initialisation)
+  // resident workgroups per CU of k_transform<M, 2, true> (thread-safe one-time initialisation)
   static const int per_cu = [] {
     if (const char* e = std::getenv("SSP_GRAM_WG_PER_CU")) return std::max(1, std::min(8, std::atoi(e)));  // A/B
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_transform<M, true, true>, kBlock, 0) != hipSuccess || occ < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_transform<M, 2, true>, kBlock, 0) != hipSuccess || occ < 1)
       occ = 2;
     return occ < 4 ? occ : 4;
   }();
@@ -889,23 +904,24 @@ unsigned gram_grid(ssp_ctx* ctx, size_t n) {
 }
 
 template <int M>
-void launch_transform_m(ssp_ctx* ctx, unsigned grid, const TransformArgs& a, bool gram, bool exact) {
+void launch_transform_m(ssp_ctx* ctx, unsigned grid, const TransformArgs& a, int dots, bool exact) {
   const dim3 b(kBlock);
-  if (exact) SSP_LAUNCH((k_transform<M, false, false>), dim3(grid), b, 0, ctx->stream, a);
-  else if (gram) SSP_LAUNCH((k_transform<M, true, true>), dim3(gram_grid<M>(ctx, a.n)), b, 0, ctx->stream, a);
-  else SSP_LAUNCH((k_transform<M, false, true>), dim3(grid), b, 0, ctx->stream, a);
+  if (exact) SSP_LAUNCH((k_transform<M, 0, false>), dim3(grid), b, 0, ctx->stream, a);
+  else if (dots == 2) SSP_LAUNCH((k_transform<M, 2, true>), dim3(gram_grid<M>(ctx, a.n)), b, 0, ctx->stream, a);
+  else if (dots == 1) SSP_LAUNCH((k_transform<M, 1, true>), dim3(grid), b, 0, ctx->stream, a);
+  else SSP_LAUNCH((k_transform<M, 0, true>), dim3(grid), b, 0, ctx->stream, a);
 }
 
-void launch_transform(ssp_ctx* ctx, int m, unsigned grid, const TransformArgs& a, bool gram, bool exact) {
+void launch_transform(ssp_ctx* ctx, int m, unsigned grid, const TransformArgs& a, int dots, bool exact) {
   switch (m) {
-    case 1: return launch_transform_m<1>(ctx, grid, a, gram, exact);
-    case 2: return launch_transform_m<2>(ctx, grid, a, gram, exact);
-    case 3: return launch_transform_m<3>(ctx, grid, a, gram, exact);
-    case 4: return launch_transform_m<4>(ctx, grid, a, gram, exact);
-    case 5: return launch_transform_m<5>(ctx, grid, a, gram, exact);
-    case 6: return launch_transform_m<6>(ctx, grid, a, gram, exact);
-    case 7: return launch_transform_m<7>(ctx, grid, a, gram, exact);
-    default: return launch_transform_m<8>(ctx, grid, a, gram, exact);
+    case 1: return launch_transform_m<1>(ctx, grid, a, dots, exact);
+    case 2: return launch_transform_m<2>(ctx, grid, a, dots, exact);
+    case 3: return launch_transform_m<3>(ctx, grid, a, dots, exact);
+    case 4: return launch_transform_m<4>(ctx, grid, a, dots, exact);
+    case 5: return launch_transform_m<5>(ctx, grid, a, dots, exact);
+    case 6: return launch_transform_m<6>(ctx, grid, a, dots, exact);
+    case 7: return launch_transform_m<7>(ctx, grid, a, dots, exact);
+    default: return launch_transform_m<8>(ctx, grid, a, dots, exact);
   }
 }
 
@@ -1675,15 +1691,20 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
   return ssp::reduce_fetch(ctx, out, size_t(m));
 }
 
-int ssp_transform_gram(ssp_ctx* ctx, const double* t, double* const* xx, const double* xs, int m, size_t n,
-                       double* gram) {
+}  // extern "C"
+
+namespace {
+// ssp_transform_gram / ssp_transform_norms: dots 2 = the Gram matrix into out (m x m), 1 = the self-dots
+// into out (m), 0 = none.
+int transform_impl(ssp_ctx* ctx, const double* t, double* const* xx, const double* xs, int m, size_t n, int dots,
+                   double* out, const char* what) {
   SSP_CHECK_CTX(ctx);
-  if (m < 1 || m > 8) return ssp::set_error(SSP_ERR_ARG, "ssp_transform_gram: 1 <= m <= 8");
-  if (!t) return ssp::set_error(SSP_ERR_ARG, "ssp_transform_gram: null t");
-  SSP_TRY(check_ptrs(const_cast<const double* const*>(xx), m, n, "ssp_transform_gram"));
+  if (m < 1 || m > 8) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": 1 <= m <= 8");
+  if (!t) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null t");
+  SSP_TRY(check_ptrs(const_cast<const double* const*>(xx), m, n, what));
   for (int j = 0; j < m; ++j)
     for (int i = 0; i < j; ++i)
-      if (xx[i] == xx[j]) return ssp::set_error(SSP_ERR_ARG, "ssp_transform_gram: repeated vector");
+      if (xx[i] == xx[j]) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": repeated vector");
   const bool exact = ssp::exact_mode(ctx, n);
   TransformArgs a{};
   a.m = m;
@@ -1694,32 +1715,51 @@ int ssp_transform_gram(ssp_ctx* ctx, const double* t, double* const* xx, const d
   }
   for (int i = 0; i < m; ++i)
     for (int j = 0; j < m; ++j) a.t[j * m + i] = t[i * m + j];  // transposed: column j contiguous
-  const int np = m * (m + 1) / 2;
-  // the fused Gram only from the bandwidth kernel; short vectors take the reference's sequential dots
-  const bool fused = gram && !exact && n > 0;
+  const int nd = dots == 2 ? m * (m + 1) / 2 : (dots == 1 ? m : 0);
+  // the fused dots only from the bandwidth kernel; short vectors take the reference's sequential dots
+  const int fused = (dots > 0 && !exact && n > 0) ? dots : 0;
   ssp::FoldTail tail{};
   if (n > 0) {
-    ssp::LedgerScope ls(ctx, gram ? "transform_gram" : "transform", 16.0 * n * m);
-    const unsigned grid = ssp::win_grid(ctx, n, fused ? 1 : (m <= 4 ? 4 : 2), 8);
+    ssp::LedgerScope ls(ctx, dots ? "transform_gram" : "transform", 16.0 * n * m);
+    const unsigned grid = ssp::win_grid(ctx, n, fused == 2 ? 1 : (m <= 4 ? 4 : 2), 8);
     if (fused) {
-      SSP_TRY(ssp::fold_begin(ctx, np, &tail));
-      SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * np));
+      SSP_TRY(ssp::fold_begin(ctx, nd, &tail));
+      SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * nd));
       a.partial = ctx->partial;
       a.tail = tail;
     }
     launch_transform(ctx, m, grid, a, fused, exact);
     SSP_TRY_HIP(hipGetLastError());
   }
-  if (!gram) return SSP_OK;
-  if (!fused) {  // short (or empty) vectors: the Gram of the stored outputs as the reference's dots
+  if (!dots) return SSP_OK;
+  if (!fused) {  // short (or empty) vectors: the dots of the stored outputs as the reference's dots
     std::vector<const double*> c(xx, xx + m);
-    return ssp_gemm_inner(ctx, c.data(), m, c.data(), m, n, gram);
+    if (dots == 2) return ssp_gemm_inner(ctx, c.data(), m, c.data(), m, n, out);
+    std::vector<double> g(size_t(m) * m);
+    SSP_TRY(ssp_gemm_inner(ctx, c.data(), m, c.data(), m, n, g.data()));
+    for (int j = 0; j < m; ++j) out[j] = g[size_t(j) * m + j];
+    return SSP_OK;
   }
-  std::vector<double> pr(static_cast<size_t>(np));
+  if (dots == 1) return ssp::fold_finish(ctx, tail, out);
+  std::vector<double> pr(static_cast<size_t>(nd));
   SSP_TRY(ssp::fold_finish(ctx, tail, pr.data()));
   for (int i = 0, q = 0; i < m; ++i)
-    for (int j = i; j < m; ++j, ++q) gram[size_t(i) * m + j] = gram[size_t(j) * m + i] = pr[size_t(q)];
+    for (int j = i; j < m; ++j, ++q) out[size_t(i) * m + j] = out[size_t(j) * m + i] = pr[size_t(q)];
   return SSP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ssp_transform_gram(ssp_ctx* ctx, const double* t, double* const* xx, const double* xs, int m, size_t n,
+                       double* gram) {
+  return transform_impl(ctx, t, xx, xs, m, n, gram ? 2 : 0, gram, "ssp_transform_gram");
+}
+
+int ssp_transform_norms(ssp_ctx* ctx, const double* t, double* const* xx, const double* xs, int m, size_t n,
+                        double* norms2) {
+  if (!norms2) return ssp::set_error(SSP_ERR_ARG, "ssp_transform_norms: null norms2");
+  return transform_impl(ctx, t, xx, xs, m, n, 1, norms2, "ssp_transform_norms");
 }
 
 int ssp_precondition_norms(ssp_ctx* ctx, double* const* a, int nvec, const double* d, const double* shift, size_t n,

@@ -300,8 +300,8 @@ inline std::vector<double> upper_inverse(const std::vector<double>& u, size_t m)
 // diagonal is unique); the second round, on the Gram matrix of the stored first result, removes what
 // the first left of the rounding (CholeskyQR2: orthonormal to working precision while the vectors are
 // conditioned to well below 1e8).  Passes: the Gram matrix (gemm_inner), the transform with the new
-// Gram matrix in the same pass (ssp_transform_gram), the second transform with the Gram matrix of its
-// outputs, whose diagonal is the self-dots the solver's normalisation reads next -- 40 N m bytes and 3
+// Gram matrix in the same pass (ssp_transform_gram), the second transform with the self-dots of its
+// outputs (ssp_transform_norms), which the solver's normalisation reads next -- 40 N m bytes and 3
 // reductions for m vectors, against 8 N (m + 3m(m-1)/2 ...) and m reductions for the one-pass MGS and
 // the normalisation's 8 N m bytes and reduction (C3, m = 8: 320 N against 688 N bytes).  Declines (false) whenever a norm MGS
 // would compute is not resolved with a wide margin (mgs_cholesky) -- near-dependent vectors, a null
@@ -335,10 +335,11 @@ inline bool orthonormalise_block(const itsolv::VecRef<Vec>& rr, double norm_thre
     return false;
   }
   t = upper_inverse(u, m);
-  // the last pass forms the Gram matrix of what it stores too: the solver normalises the vectors next
-  // (propose_rspace.h:17-28 after :450-465), and their self-dots are its diagonal (Vec::known_norm2)
-  check(ssp_transform_gram(ctx, t.data(), yp.data(), nullptr, int(m), n, g.data()), "ssp_transform_gram");
-  for (size_t j = 0; j < m; ++j) rr[j].get().set_known_norm2(g[j * m + j]);
+  // the last pass forms the self-dots of what it stores too: the solver normalises the vectors next
+  // (propose_rspace.h:17-28 after :450-465) and reads them (Vec::known_norm2)
+  std::vector<double> n2(m);
+  check(ssp_transform_norms(ctx, t.data(), yp.data(), nullptr, int(m), n, n2.data()), "ssp_transform_norms");
+  for (size_t j = 0; j < m; ++j) rr[j].get().set_known_norm2(n2[j]);
   return true;
 }
 

@@ -37,7 +37,7 @@ EXPORTS = [
     "ssp_ctx_set_exact_max",
     "ssp_ledger_enable", "ssp_ledger_reset", "ssp_ledger_count", "ssp_ledger_reserve",
     "ssp_ledger_entry", "ssp_fill", "ssp_scal", "ssp_copy", "ssp_axpy", "ssp_dot",
-    "ssp_gemm_inner", "ssp_gemm_outer", "ssp_gemm_outer_set", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_axpy_gram", "ssp_transform_gram", "ssp_axpy_pairs_norm", "ssp_precondition", "ssp_precondition_norms", "ssp_select", "ssp_select_max_dot",
+    "ssp_gemm_inner", "ssp_gemm_outer", "ssp_gemm_outer_set", "ssp_axpy_inner", "ssp_scal_inner", "ssp_axpy_norm", "ssp_axpy_gram", "ssp_transform_gram", "ssp_transform_norms", "ssp_axpy_pairs_norm", "ssp_precondition", "ssp_precondition_norms", "ssp_select", "ssp_select_max_dot",
     "ssp_sparse_copy", "ssp_sparse_axpy", "ssp_sparse_axpy_batch", "ssp_sparse_dot", "ssp_gemm_inner_sparse", "ssp_gemm_outer_sparse",
     "ssp_construct_solution",
     "sspx_synthetic_action", "sspx_synthetic_add_lowrank", "sspx_synthetic_diagonal", "sspx_fill_random", "sspx_dense_action",
@@ -127,6 +127,7 @@ def _declare(lib):
         "ssp_axpy_norm": (I, [P, PD, P, P, I, Z, PD]),
         "ssp_axpy_gram": (I, [P, PD, P, D, I, P, I, Z, PD]),
         "ssp_transform_gram": (I, [P, PD, P, PD, I, Z, PD]),
+        "ssp_transform_norms": (I, [P, PD, P, PD, I, Z, PD]),
         "ssp_axpy_pairs_norm": (I, [P, PD, P, PD, P, PD, I, Z, PD]),
         "ssp_precondition": (I, [P, P, I, P, PD, Z]),
         "ssp_precondition_norms": (I, [P, P, I, P, PD, Z, PD]),
@@ -590,6 +591,16 @@ class Context:
         _check(self.lib.ssp_transform_gram(self.handle, _dptr(tt), _ptrs(xx), None if sx is None else _dptr(sx), m,
                                            xx[0].n if m else 0, None if g is None else _dptr(g)))
         return g
+
+    def transform_norms(self, t: np.ndarray, xx: Sequence[DeviceVector], xs: Sequence[float] = None) -> np.ndarray:
+        """The same transform; returns the self-dots of the new vectors, formed in the same pass."""
+        m = len(xx)
+        tt = np.ascontiguousarray(t, dtype=np.float64).reshape(m, m)
+        sx = None if xs is None else np.ascontiguousarray(xs, dtype=np.float64)
+        out = np.zeros(max(1, m))
+        _check(self.lib.ssp_transform_norms(self.handle, _dptr(tt), _ptrs(xx), None if sx is None else _dptr(sx), m,
+                                            xx[0].n if m else 0, _dptr(out)))
+        return out[:m]
 
     def axpy_pairs_norm(self, c: Sequence[float], xx: Sequence[DeviceVector], yy: Sequence[DeviceVector],
                         xs: Sequence[float] = None, ys: Sequence[float] = None) -> np.ndarray:

@@ -405,6 +405,14 @@ int ssp_transform_gram(ssp_ctx* c, const double* t, double* const* xx, const dou
     for (int j = i; j < m; ++j) gram[size_t(i) * m + j] = gram[size_t(j) * m + i] = dot_n(xx[i], xx[j], n);
   return reduce(c, gram, size_t(m) * m);
 }
+int ssp_transform_norms(ssp_ctx* c, const double* t, double* const* xx, const double* xs, int m, size_t n,
+                        double* norms2) {
+  if (!norms2) return fail(SSP_ERR_ARG, "ssp_transform_norms: null norms2");
+  const int rc = ssp_transform_gram(c, t, xx, xs, m, n, nullptr);
+  if (rc != SSP_OK) return rc;
+  for (int j = 0; j < m; ++j) norms2[j] = dot_n(xx[j], xx[j], n);
+  return reduce(c, norms2, size_t(m));
+}
 int ssp_axpy_pairs_norm(ssp_ctx* c, const double* cc, const double* const* xx, const double* xs, double* const* yy,
                         const double* ys, int m, size_t n, double* out) {
   if (m < 0 || (m > 0 && (!cc || !out))) return fail(SSP_ERR_ARG, "ssp_axpy_pairs_norm: bad arguments");

@@ -88,6 +88,28 @@ def test_transform_gram_in_place(ctx, m, n, gram):
         assert np.array_equal(g, g.T)
 
 
+# ---- ssp_transform_norms: the same pass forming only the self-dots (orthonormalise_block's last pass)
+@pytest.mark.parametrize("m,n", [(8, 1_000_003), (3, 777_777), (5, 64), (7, 300_001), (8, 2048), (1, 400_001),
+                                 (2, 131_071), (4, 200_003), (6, 150_001), (1, 1500)])
+def test_transform_norms_in_place(ctx, m, n):
+    import numpy as np
+
+    rng = np.random.default_rng(m * 31 + n % 991)
+    X = rng.uniform(-1, 1, (m, n))
+    t = np.triu(rng.uniform(-1, 1, (m, m))) + 2 * np.eye(m)
+    s = rng.uniform(0.5, 2.0, m)
+    a, b = [ctx.upload(v) for v in X], [ctx.upload(v) for v in X]
+    ctx.transform_gram(t, a, s, gram=False)
+    n2 = ctx.transform_norms(t, b, s)
+    got = np.array([ctx.download(v) for v in b])
+    assert np.array_equal(got, np.array([ctx.download(v) for v in a]))  # the same vectors, bit for bit
+    want = np.einsum("ij,ij->i", got, got)
+    if n <= 2048:  # short vectors: the reference's sequential dots
+        assert np.array_equal(n2, np.diag(ctx.gemm_inner(b, b)))
+    else:
+        assert np.all(np.abs(n2 - want) <= 1e-11 * want), np.max(np.abs(n2 - want) / want)
+
+
 def test_block_orthonormalisation_is_mgs_in_exact_arithmetic(ctx):
     # CholeskyQR2 of 8 well-conditioned vectors (what orthonormalise_block runs): orthonormal to
     # working precision, and the same vectors as the sequential MGS up to rounding
