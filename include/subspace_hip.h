@@ -218,6 +218,16 @@ int ssp_gemm_outer_set_scaled(ssp_ctx* ctx, const double* alphas, const double* 
 int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, size_t n,
                                  size_t offset, const size_t* ptr, const size_t* idx, const double* val, int k,
                                  double* out);
+/* The same m x k sparse inner products split in two: _begin queues them and returns at once, _end
+   delivers them to out (m*k doubles).  Other calls may come in between: the subspace update
+   (subspace.h new_qspace_data) queues S(R,P)/H(P,R) ahead of the dense overlap rows, so the wait for
+   those rows covers both and the sparse product needs no round trip of its own.  One product may be
+   pending per context: _begin discards an uncollected one, _end with nothing pending is SSP_ERR_ARG.  With a
+   communicator attached (a collective) or beyond the inline limits (m > 64, k > 32, > 64 local
+   entries) _begin computes the result at once. */
+int ssp_gemm_inner_sparse_begin(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, size_t n,
+                                size_t offset, const size_t* ptr, const size_t* idx, const double* val, int k);
+int ssp_gemm_inner_sparse_end(ssp_ctx* ctx, double* out);
 int ssp_construct_solution_scaled(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const size_t* idx,
                                   const double* val, int kp, const double* alphas, const double* const* xx,
                                   const double* xs, int k, double* const* yy, int m, size_t n, size_t offset);

@@ -201,12 +201,13 @@ __global__ __launch_bounds__(256) void k_publish(const double* src, size_t n, do
 // flag becoming visible (the writes of a finished kernel are visible all the same).  With a
 // communicator attached the wait is bounded (comm_poll: SSP_COMM_TIMEOUT_S, RCCL's asynchronous
 // error, the peer-memory transport's abort word), since the flag then depends on other ranks.
-int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen, const char* what) {
+int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen, const char* what, const unsigned long long* flag) {
+  if (!flag) flag = ctx->pub_flag;
   *seen = true;
   const bool ranks = comm_attached(ctx);
   const double t0 = ranks ? now_s() : 0.0;
   for (unsigned spin = 1;; ++spin) {
-    if (__atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq) return SSP_OK;
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return SSP_OK;
     if ((spin & 255) == 0) {
       const hipError_t e = hipStreamQuery(ctx->stream);
       if (e == hipErrorNotReady) {
@@ -214,11 +215,22 @@ int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen, const char* what
         continue;
       }
       if (e != hipSuccess) return hip_error(e, what);
-      *seen = __atomic_load_n(ctx->pub_flag, __ATOMIC_ACQUIRE) == seq;
+      *seen = __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq;
       return SSP_OK;
     }
     _mm_pause();
   }
+}
+
+int ensure_async(ssp_ctx* ctx) {
+  if (ctx->async_dev) return SSP_OK;
+  if (hipMalloc(reinterpret_cast<void**>(&ctx->async_dev), kAsyncResults * sizeof(double)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&ctx->async_host), kAsyncResults * sizeof(double),
+                    hipHostMallocCoherent) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&ctx->async_flag), 64, hipHostMallocCoherent) != hipSuccess)
+    return set_error(SSP_ERR_NOMEM, "allocation of the pending-result buffers failed");
+  __atomic_store_n(ctx->async_flag, ctx->async_seq, __ATOMIC_RELEASE);
+  return SSP_OK;
 }
 
 int fetch_result(ssp_ctx* ctx, double* out, size_t n) {
@@ -485,6 +497,9 @@ int ssp_ctx_destroy(ssp_ctx* ctx) {
   if (ctx->result_host) (void)hipHostFree(ctx->result_host);
   if (ctx->pub_flag) (void)hipHostFree(ctx->pub_flag);
   if (ctx->fold_counter) (void)hipFree(ctx->fold_counter);
+  if (ctx->async_dev) (void)hipFree(ctx->async_dev);
+  if (ctx->async_host) (void)hipHostFree(ctx->async_host);
+  if (ctx->async_flag) (void)hipHostFree(ctx->async_flag);
   if (ctx->synth_mask) (void)hipFree(ctx->synth_mask);
   if (ctx->ring_dev) (void)hipFree(ctx->ring_dev);
   if (ctx->ring_host) (void)hipHostFree(ctx->ring_host);

@@ -7,6 +7,7 @@
 // one lane in the reference's entry order, so the per-rank results are bitwise those of the
 // reference loop; cross-rank sums are RCCL allreduces.
 #include <algorithm>
+#include <cstring>
 #include <map>
 #include <vector>
 
@@ -187,13 +188,39 @@ struct ConstructFixArgs {
   const unsigned long long* ptr;   // kp+1 offsets into li/v
   const unsigned long long* li;
   const double* v;
+  int entries;                     // ptr[kp]
   const double* palpha;            // kp x m
   const double* alpha;             // k x m
   const double* const* x;          // k dense sources
   double* const* y;                // m destinations
 };
 
-__global__ void k_construct_fixup(const ConstructFixArgs a) {
+// The operand arrays the lanes of a fix-up read in sequence (P offsets, entries, coefficients, source
+// pointers) are staged in LDS first: one round of parallel loads instead of a chain of dependent
+// global loads per P entry (17.8 -> ~6 us a launch at the C4 shard).  Larger operands read global.
+constexpr int kFixEntries = 512, kFixP = 64, kFixPalpha = 1024, kFixSrc = 128;
+__global__ __launch_bounds__(256) void k_construct_fixup(const ConstructFixArgs a) {
+  __shared__ unsigned long long s_ptr[kFixP + 1];
+  __shared__ unsigned long long s_li[kFixEntries];
+  __shared__ double s_v[kFixEntries];
+  __shared__ double s_pal[kFixPalpha];
+  __shared__ const double* s_x[kFixSrc];
+  const bool staged = a.kp <= kFixP && a.entries <= kFixEntries && size_t(a.kp) * a.m <= kFixPalpha && a.k <= kFixSrc;
+  if (staged) {
+    for (int q = int(threadIdx.x); q <= a.kp; q += int(blockDim.x)) s_ptr[q] = a.ptr[q];
+    for (int q = int(threadIdx.x); q < a.entries; q += int(blockDim.x)) {
+      s_li[q] = a.li[q];
+      s_v[q] = a.v[q];
+    }
+    for (int q = int(threadIdx.x); q < a.kp * a.m; q += int(blockDim.x)) s_pal[q] = a.palpha[q];
+    for (int q = int(threadIdx.x); q < a.k; q += int(blockDim.x)) s_x[q] = a.x[q];
+    __syncthreads();
+  }
+  const unsigned long long* ptr = staged ? s_ptr : a.ptr;
+  const unsigned long long* li = staged ? s_li : a.li;
+  const double* pv = staged ? s_v : a.v;
+  const double* pal = staged ? s_pal : a.palpha;
+  const double* const* xsrc = staged ? s_x : a.x;
   const size_t t = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= a.nu * size_t(a.m)) return;
   const size_t u = t / a.m;
@@ -202,21 +229,24 @@ __global__ void k_construct_fixup(const ConstructFixArgs a) {
   double v = 0;
   if (a.rmw) v = a.saved[t] * a.ys[j];  // t = u * m + j
   for (int i = 0; i < a.kp; ++i) {
-    const double al = a.palpha[size_t(i) * a.m + j];
-    for (unsigned long long e = a.ptr[i]; e < a.ptr[i + 1]; ++e)
-      if (a.li[e] == g) v += al * a.v[e];
+    const double al = pal[size_t(i) * a.m + j];
+    for (unsigned long long e = ptr[i]; e < ptr[i + 1]; ++e)
+      if (li[e] == g) v += al * pv[e];
   }
-  // the dense sources in groups of 8: the group's loads are issued together, then the chain of adds
-  constexpr int G = 8;
+  // the dense sources in groups of 32: the group's loads are issued together (unconditionally: the
+  // index is clamped, so no branch splits them), then the chain of adds.  x * 1 is x exactly.
+  constexpr int G = 32;
   for (int s0 = 0; s0 < a.k; s0 += G) {
     double xv[G], al[G];
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-      const int s = s0 + u;
-      if (s < a.k) {
-        xv[u] = a.xs ? a.x[s][g] * a.xs[s] : a.x[s][g];
-        al[u] = a.alpha[size_t(s) * a.m + j];
-      }
+      const int s = min(s0 + u, a.k - 1);
+      xv[u] = xsrc[s][g];
+      al[u] = a.alpha[size_t(s) * a.m + j];
+    }
+    if (a.xs) {
+#pragma unroll
+      for (int u = 0; u < G; ++u) xv[u] *= a.xs[min(s0 + u, a.k - 1)];
     }
 #pragma unroll
     for (int u = 0; u < G; ++u)
@@ -273,6 +303,49 @@ int launch_scatter_inline(ssp_ctx* ctx, double* x, const std::vector<unsigned lo
 
 int check_entries(const size_t* idx, const double* val, size_t nnz, const char* what) {
   if (nnz && (!idx || !val)) return ssp::set_error(SSP_ERR_ARG, std::string(what) + ": null entries");
+  return SSP_OK;
+}
+
+// Local entries of k sparse vectors (CSR ptr/idx/val) inside this rank's shard [offset, offset+n):
+// lptr[j]..lptr[j+1] index li/lv for vector j.
+int sparse_local_entries(const size_t* ptr, const size_t* idx, const double* val, int k, size_t n, size_t offset,
+                         std::vector<unsigned long long>& lptr, std::vector<unsigned long long>& li,
+                         std::vector<double>& lv) {
+  lptr.assign(1, 0);
+  for (int j = 0; j < k; ++j) {
+    SSP_TRY(check_entries(idx + ptr[j], val + ptr[j], ptr[j + 1] - ptr[j], "ssp_gemm_inner_sparse"));
+    filter_local(idx + ptr[j], val + ptr[j], ptr[j + 1] - ptr[j], n, offset, li, lv);
+    lptr.push_back(li.size());
+  }
+  return SSP_OK;
+}
+
+// k <= 32 sparse vectors with at most kInlineEntries local entries in all: the entries travel in the
+// kernel arguments, one launch per 64 dense vectors, results to out_dev (and, with tail.host, published
+// by the last workgroup).
+int launch_sparse_inline(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, int k,
+                         const std::vector<unsigned long long>& lptr, const std::vector<unsigned long long>& li,
+                         const std::vector<double>& lv, double* out_dev, const ssp::FoldTail& tail) {
+  ssp::LedgerScope ls(ctx, "gemm_inner_sparse", 16.0 * li.size() * m);
+  for (int i0 = 0; i0 < m; i0 += 64) {
+    SparseInnerInline a{};
+    a.m = std::min(64, m - i0);
+    a.k = k;
+    for (int i = 0; i < a.m; ++i) {
+      a.x[i] = xx[i0 + i];
+      a.xs[i] = xs ? xs[i0 + i] : 1.0;
+      if (a.xs[i] != 1.0) a.sc = 1;
+    }
+    for (int j = 0; j <= k; ++j) a.ptr[j] = (unsigned short)lptr[size_t(j)];
+    for (size_t e = 0; e < li.size(); ++e) {
+      a.li[e] = li[e];
+      a.v[e] = lv[e];
+    }
+    a.out = out_dev + size_t(i0) * k;
+    const int outs = a.m * a.k;
+    SSP_LAUNCH(k_sparse_inner_inline, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a, tail);
+    SSP_TRY_HIP(hipGetLastError());
+  }
   return SSP_OK;
 }
 
@@ -412,13 +485,9 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const do
   if (m < 0 || k < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner_sparse: negative dimension");
   if (m == 0 || k == 0) return SSP_OK;
   if (!out || !ptr || (m > 0 && !xx)) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner_sparse: null argument");
-  std::vector<unsigned long long> lptr{0}, li;
+  std::vector<unsigned long long> lptr, li;
   std::vector<double> lv;
-  for (int j = 0; j < k; ++j) {
-    SSP_TRY(check_entries(idx + ptr[j], val + ptr[j], ptr[j + 1] - ptr[j], "ssp_gemm_inner_sparse"));
-    filter_local(idx + ptr[j], val + ptr[j], ptr[j + 1] - ptr[j], n, offset, li, lv);
-    lptr.push_back(li.size());
-  }
+  SSP_TRY(sparse_local_entries(ptr, idx, val, k, n, offset, lptr, li, lv));
   const size_t total = size_t(m) * k;
   SSP_TRY(ssp::ensure_result(ctx, total));
   if (k <= 32 && li.size() <= size_t(kInlineEntries)) {
@@ -426,29 +495,7 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const do
     const bool one = m <= 64;
     ssp::FoldTail tail{};
     if (one) SSP_TRY(ssp::fold_begin(ctx, int(total), &tail));
-    {
-      ssp::LedgerScope ls(ctx, "gemm_inner_sparse", 16.0 * li.size() * m);
-      for (int i0 = 0; i0 < m; i0 += 64) {
-        SparseInnerInline a{};
-        a.m = std::min(64, m - i0);
-        a.k = k;
-        for (int i = 0; i < a.m; ++i) {
-          a.x[i] = xx[i0 + i];
-          a.xs[i] = xs ? xs[i0 + i] : 1.0;
-          if (a.xs[i] != 1.0) a.sc = 1;
-        }
-        for (int j = 0; j <= k; ++j) a.ptr[j] = (unsigned short)lptr[size_t(j)];
-        for (size_t e = 0; e < li.size(); ++e) {
-          a.li[e] = li[e];
-          a.v[e] = lv[e];
-        }
-        a.out = ctx->result_dev + size_t(i0) * k;
-        const int outs = a.m * a.k;
-        SSP_LAUNCH(k_sparse_inner_inline, dim3((outs + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a,
-                           tail);
-        SSP_TRY_HIP(hipGetLastError());
-      }
-    }
+    SSP_TRY(launch_sparse_inline(ctx, xx, xs, m, k, lptr, li, lv, ctx->result_dev, tail));
     return one ? ssp::fold_finish(ctx, tail, out) : ssp::reduce_fetch(ctx, out, total);
   }
   unsigned long long *dptr, *dli;
@@ -476,6 +523,63 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* ctx, const double* const* xx, const do
     }
   }
   return ssp::reduce_fetch(ctx, out, total);
+}
+
+int ssp_gemm_inner_sparse_begin(ssp_ctx* ctx, const double* const* xx, const double* xs, int m, size_t n,
+                                size_t offset, const size_t* ptr, const size_t* idx, const double* val, int k) {
+  SSP_CHECK_CTX(ctx);
+  ctx->async_pending = false;  // an uncollected result is discarded (its launch precedes this one's)
+  if (m < 0 || k < 0) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner_sparse_begin: negative dimension");
+  const size_t total = size_t(m) * size_t(k);
+  if (total == 0) {
+    ctx->async_n = 0;
+    ctx->async_launched = false;
+    ctx->async_pending = true;
+    return SSP_OK;
+  }
+  if (!ptr || !xx) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner_sparse_begin: null argument");
+  std::vector<unsigned long long> lptr, li;
+  std::vector<double> lv;
+  SSP_TRY(sparse_local_entries(ptr, idx, val, k, n, offset, lptr, li, lv));
+  if (m <= 64 && k <= 32 && li.size() <= size_t(kInlineEntries) && !ssp::comm_attached(ctx)) {
+    // One inline launch publishing to the pending buffers.  Stream order finishes it before anything
+    // queued after it, so by the time a later reduction's flag is seen these results are in host
+    // memory too, and _end finds its flag already set.
+    SSP_TRY(ssp::ensure_async(ctx));
+    ssp::FoldTail tail{};
+    tail.counter = ctx->fold_counter;
+    tail.nout = int(total);
+    tail.flag = ctx->async_flag;
+    tail.host = ctx->async_host;
+    tail.seq = ++ctx->async_seq;
+    SSP_TRY(launch_sparse_inline(ctx, xx, xs, m, k, lptr, li, lv, ctx->async_dev, tail));
+    ctx->async_launched = true;
+  } else {  // with ranks (a collective) or beyond the inline limits: computed now, delivered by _end
+    ctx->async_sync.resize(total);
+    SSP_TRY(ssp_gemm_inner_sparse_scaled(ctx, xx, xs, m, n, offset, ptr, idx, val, k, ctx->async_sync.data()));
+    ctx->async_launched = false;
+  }
+  ctx->async_n = total;
+  ctx->async_pending = true;
+  return SSP_OK;
+}
+
+int ssp_gemm_inner_sparse_end(ssp_ctx* ctx, double* out) {
+  SSP_CHECK_CTX(ctx);
+  if (!ctx->async_pending) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner_sparse_end: nothing pending");
+  ctx->async_pending = false;
+  if (ctx->async_n == 0) return SSP_OK;
+  if (!out) return ssp::set_error(SSP_ERR_ARG, "ssp_gemm_inner_sparse_end: null argument");
+  if (!ctx->async_launched) {
+    std::memcpy(out, ctx->async_sync.data(), ctx->async_n * sizeof(double));
+    return SSP_OK;
+  }
+  bool seen = true;
+  SSP_TRY(ssp::wait_flag(ctx, ctx->async_seq, &seen, "ssp_gemm_inner_sparse_end", ctx->async_flag));
+  if (!seen)
+    SSP_TRY_HIP(hipMemcpy(ctx->async_host, ctx->async_dev, ctx->async_n * sizeof(double), hipMemcpyDeviceToHost));
+  std::memcpy(out, ctx->async_host, ctx->async_n * sizeof(double));
+  return SSP_OK;
 }
 
 int ssp_sparse_dot(ssp_ctx* ctx, const double* x, size_t n, size_t offset, const size_t* idx, const double* val,
@@ -574,6 +678,7 @@ int solution_impl(ssp_ctx* ctx, const double* palphas, const size_t* ptr, const 
   a.ptr = dptr;
   a.li = dli;
   a.v = dv;
+  a.entries = int(li.size());
   SSP_TRY(ssp::upload_small(ctx, uidx.data(), uidx.size() * sizeof(unsigned long long), &p));
   a.uidx = static_cast<const unsigned long long*>(p);
   SSP_TRY(ssp::upload_small(ctx, palphas, size_t(kp) * m * sizeof(double), &p));

@@ -67,6 +67,16 @@ struct ssp_ctx {
   unsigned long long pub_seq = 0;
   // Arrival counter of the fused reduction tails (FoldTail); zero between launches.
   unsigned* fold_counter = nullptr;
+  // One pending sparse inner product (ssp_gemm_inner_sparse_begin / _end): its own device staging,
+  // coherent host results and sequence flag, so reductions issued before _end cannot overwrite them.
+  double* async_dev = nullptr;
+  double* async_host = nullptr;
+  unsigned long long* async_flag = nullptr;
+  unsigned long long async_seq = 0;
+  bool async_pending = false;
+  bool async_launched = false;  // false: computed synchronously into async_sync
+  size_t async_n = 0;
+  std::vector<double> async_sync;
 
   // Upload ring: pinned host + device mirror for small per-call operand arrays (sparse index
   // lists).  Regions are reused only after a stream synchronisation at wrap-around.  The arrays one
@@ -147,7 +157,11 @@ int fetch_result(ssp_ctx* ctx, double* out, size_t n);
 // or the peer-memory transport's fused exchange-and-publish).
 int reduce_fetch(ssp_ctx* ctx, double* out, size_t n);
 // Waits (host poll) until the publish flag carries seq; bounded when a communicator is attached.
-int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen, const char* what = "reduction");
+int wait_flag(ssp_ctx* ctx, unsigned long long seq, bool* seen, const char* what = "reduction",
+              const unsigned long long* flag = nullptr);
+// Allocates the pending-sparse-inner buffers (kAsyncResults doubles) on first use.
+constexpr size_t kAsyncResults = 64 * 32;
+int ensure_async(ssp_ctx* ctx);
 // Grid size for streaming kernels: enough workgroups to fill 256 CUs, grid-stride beyond.
 // Workgroups for a grid-stride streaming launch: enough for work_items / (kBlock * per_thread),
 // at most blocks_per_cu per CU.

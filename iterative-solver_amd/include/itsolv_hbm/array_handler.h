@@ -386,6 +386,15 @@ bool fused_overlap_rows(H&, const RefL&, const std::vector<RefC>&, M&) {
   return false;
 }
 
+// Hook for an overlap whose result is needed only after more work has been queued (the subspace
+// update's S(R, P) / H(P, R) rows, queued ahead of the dense rows so that one wait covers both):
+// returns a function delivering gemm_inner(rows, cols), or an empty function when the handler has no
+// such form.  Found by argument-dependent lookup.
+template <class H, class RefL, class RefC>
+std::function<Matrix<double>()> queued_overlap(H&, const RefL&, const RefC&) {
+  return {};
+}
+
 // Hook for the residuals and their norms in one pass (construct_residual, reference
 // LinearEigensystemDavidson.h:186-192: r_i += c_i x_i, then update_errors' self-dots,
 // IterativeSolverTemplate.h:95-102): norms2[i] = <r_i, r_i> of the updated residuals; returns false

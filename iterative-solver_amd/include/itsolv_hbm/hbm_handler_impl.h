@@ -367,6 +367,31 @@ class ArrayHandlerHbmSparse : public array::ArrayHandler<Vec, SparseP> {
     }
     return itsolv::subspace::Matrix<double>(std::move(buf), {xx.size(), yy.size()});
   }
+  // gemm_inner in two halves (ssp_gemm_inner_sparse_begin / _end; the array::queued_overlap hook):
+  // the products are queued now, the returned function delivers them.  The same kernel and operands
+  // as gemm_inner above, so the same numbers.
+  std::function<itsolv::subspace::Matrix<double>()> gemm_inner_queued(const itsolv::CVecRef<Vec>& xx,
+                                                                       const itsolv::CVecRef<SparseP>& yy) {
+    m_counter->gemm_inner++;
+    const size_t m = xx.size(), k = yy.size();
+    if (m == 0 || k == 0)
+      return [m, k] { return itsolv::subspace::Matrix<double>(std::vector<double>(m * k, 0.0), {m, k}); };
+    std::vector<size_t> ptr, idx;
+    std::vector<double> val;
+    detail::pack(yy, ptr, idx, val);
+    std::vector<double> xs;
+    auto xp = detail::deferred_ptrs(xx, xs);
+    const auto& x0 = xx.front().get();
+    ssp_ctx* ctx = x0.ctx();
+    check(ssp_gemm_inner_sparse_begin(ctx, xp.data(), xs.data(), int(m), x0.local_size(), x0.offset(), ptr.data(),
+                                      idx.data(), val.data(), int(k)),
+          "ssp_gemm_inner_sparse_begin");
+    return [ctx, m, k] {
+      std::vector<double> buf(m * k, 0.0);
+      check(ssp_gemm_inner_sparse_end(ctx, buf.data()), "ssp_gemm_inner_sparse_end");
+      return itsolv::subspace::Matrix<double>(std::move(buf), {m, k});
+    };
+  }
   // |x_i v_i| over the entries of y, reduced over ranks, then the reference's top-n rule of
   // select_max_dot_iter_sparse (util/select_max_dot.h:59-85): the first n entries of y are pushed
   // onto its heap without pops, out-of-range ones skipped, and every later in-range entry is pushed

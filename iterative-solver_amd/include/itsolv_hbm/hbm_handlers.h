@@ -158,6 +158,16 @@ inline bool fused_overlap_rows(array::ArrayHandler<Vec, Vec>& h, const itsolv::C
   return true;
 }
 
+// The sparse rows of the subspace update queued ahead of the dense ones (array::queued_overlap hook,
+// ssp_gemm_inner_sparse_begin): the dense rows' reduction then covers them, and the sparse product
+// costs no host round trip of its own.  From fused_min_size(), as the fused passes.
+inline std::function<itsolv::subspace::Matrix<double>()> queued_overlap(
+    array::ArrayHandler<Vec, SparseP>& h, const itsolv::CVecRef<Vec>& rows, const itsolv::CVecRef<SparseP>& cols) {
+  auto* sp = dynamic_cast<ArrayHandlerHbmSparse*>(&h);
+  if (!sp || rows.empty() || rows.front().get().size() < fused_min_size()) return {};
+  return sp->gemm_inner_queued(rows, cols);
+}
+
 // construct_residual's axpys and update_errors' self-dots as one pass (array::fused_residual_norms
 // hook, ssp_axpy_pairs_norm): the residuals element for element the handler's axpy, the norms the
 // same dots up to summation order; from fused_min_size() (as the other fused solver passes).

@@ -350,6 +350,19 @@ class XSpace {
     const auto qp = cparamsq(), qa = cactionsq(), dp = cparamsd(), da = cactionsd();
     const auto& lhs_h = m_action_dot_action ? actions : params;
     bool fused = false;
+    // S(R, P) and H(P, R) as one sparse inner product over [params, actions] (one launch, one
+    // reduction; each element is the same sum over its P vector's entries either way), queued ahead of
+    // the dense rows where the handler can (array::queued_overlap): the wait for those covers it
+    std::function<Matrix<double>()> p_rows;
+    CVecRef<R> both;
+    if constexpr (array::batched_symmetric_overlap<R>::value) {
+      if (m_hermitian && d.nP > 0 && nn > 0) {
+        both.assign(params.begin(), params.end());
+        both.insert(both.end(), actions.begin(), actions.end());
+        using array::queued_overlap;
+        p_rows = queued_overlap(h.rp(), both, pp);
+      }
+    }
     if constexpr (std::is_same_v<R, Q>) {
       // every block whose rows are the new parameters, as one batched overlap where the handler has
       // it: columns [params, actions, Q params, Q actions, D params, D actions, rhs]
@@ -409,12 +422,8 @@ class XSpace {
     }
     bool p_rows_done = false;
     if constexpr (array::batched_symmetric_overlap<R>::value) {
-      // device handlers: S(R, P) and H(P, R) as one sparse inner product over [params, actions] (one
-      // launch, one reduction; each element is the same sum over its P vector's entries either way)
-      if (m_hermitian && d.nP > 0 && nn > 0) {
-        CVecRef<R> both(params.begin(), params.end());
-        both.insert(both.end(), actions.begin(), actions.end());
-        const auto g = util::overlap(both, pp, h.rp());
+      if (!both.empty()) {
+        const auto g = p_rows ? p_rows() : util::overlap(both, pp, h.rp());
         for (size_t i = 0; i < nn; ++i)
           for (size_t j = 0; j < d.nP; ++j) {
             qx[EqnData::S](i, d.oP + j) = g(i, j);

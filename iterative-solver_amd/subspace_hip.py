@@ -46,6 +46,8 @@ EXPORTS = [
     "ssp_scal_copy", "ssp_axpy_scaled", "ssp_dot_scaled", "ssp_gemm_inner_scaled", "ssp_gemm_outer_scaled",
     "ssp_gemm_outer_set_scaled", "ssp_gemm_inner_sparse_scaled", "ssp_construct_solution_scaled", "ssp_block_update",
     "sspx_synth_action_scaled",
+    # a sparse inner product queued ahead of other work
+    "ssp_gemm_inner_sparse_begin", "ssp_gemm_inner_sparse_end",
 ]
 
 
@@ -155,6 +157,8 @@ def _declare(lib):
         "ssp_gemm_outer_scaled": (I, [P, PD, P, PD, I, P, PD, I, Z]),
         "ssp_gemm_outer_set_scaled": (I, [P, PD, P, PD, I, P, I, Z]),
         "ssp_gemm_inner_sparse_scaled": (I, [P, P, PD, I, Z, Z, PZ, PZ, PD, I, PD]),
+        "ssp_gemm_inner_sparse_begin": (I, [P, P, PD, I, Z, Z, PZ, PZ, PD, I]),
+        "ssp_gemm_inner_sparse_end": (I, [P, PD]),
         "ssp_construct_solution_scaled": (I, [P, PD, PZ, PZ, PD, I, PD, P, PD, I, P, I, Z, Z]),
         "ssp_block_update": (I, [P, PD, PZ, PZ, PD, I, PD, P, PD, I, P, PD, I, Z, Z]),
         "sspx_synth_action_scaled": (I, [P, P, P, PD, P, I, Z, Z]),
@@ -754,6 +758,21 @@ class Context:
         n = xx[0].n if m else 0
         _check(self.lib.ssp_gemm_inner_sparse_scaled(self.handle, _ptrs(xx), _dptr(a), m, n, offset, _zptr(ptr),
                                                      _zptr(idx), _dptr(val), k, _dptr(out)))
+        return out
+
+    def gemm_inner_sparse_begin(self, xx, ps, xs=None, offset: int = 0) -> tuple:
+        """Queues gemm_inner_sparse(xx, ps); gemm_inner_sparse_end() delivers it."""
+        ptr, idx, val = self._pack_sparse(ps)
+        m, k = len(xx), len(ps)
+        a = self._scales(xs, m)
+        n = xx[0].n if m else 0
+        _check(self.lib.ssp_gemm_inner_sparse_begin(self.handle, _ptrs(xx), _dptr(a), m, n, offset, _zptr(ptr),
+                                                    _zptr(idx), _dptr(val), k))
+        return (m, k)
+
+    def gemm_inner_sparse_end(self, shape: tuple) -> np.ndarray:
+        out = np.zeros(shape)
+        _check(self.lib.ssp_gemm_inner_sparse_end(self.handle, _dptr(out)))
         return out
 
     def construct_solution_scaled(self, palphas, ps, alphas, xx, xs, yy, offset: int = 0):

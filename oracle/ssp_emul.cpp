@@ -38,6 +38,9 @@ struct ssp_ctx {
   };
   bool ledger_on = false;
   std::vector<Entry> ledger;
+  // ssp_gemm_inner_sparse_begin / _end: computed at _begin, delivered at _end
+  bool sparse_pending = false;
+  std::vector<double> sparse_result;
 };
 
 namespace {
@@ -735,6 +738,26 @@ int ssp_gemm_inner_sparse_scaled(ssp_ctx* c, const double* const* xx, const doub
                                  const size_t* ptr, const size_t* idx, const double* val, int k, double* out) {
   Scaled sx(xx, xs, m, n);
   return ssp_gemm_inner_sparse(c, sx.p.data(), m, n, off, ptr, idx, val, k, out);
+}
+int ssp_gemm_inner_sparse_begin(ssp_ctx* c, const double* const* xx, const double* xs, int m, size_t n, size_t off,
+                                const size_t* ptr, const size_t* idx, const double* val, int k) {
+  c->sparse_pending = false;  // an uncollected result is discarded
+  if (m < 0 || k < 0) return fail(SSP_ERR_ARG, "ssp_gemm_inner_sparse_begin: negative dimension");
+  c->sparse_result.assign(size_t(m) * size_t(k), 0.0);
+  if (m > 0 && k > 0)
+    if (int st = ssp_gemm_inner_sparse_scaled(c, xx, xs, m, n, off, ptr, idx, val, k, c->sparse_result.data()))
+      return st;
+  c->sparse_pending = true;
+  return SSP_OK;
+}
+int ssp_gemm_inner_sparse_end(ssp_ctx* c, double* out) {
+  if (!c->sparse_pending) return fail(SSP_ERR_ARG, "ssp_gemm_inner_sparse_end: nothing pending");
+  c->sparse_pending = false;
+  if (!c->sparse_result.empty()) {
+    if (!out) return fail(SSP_ERR_ARG, "ssp_gemm_inner_sparse_end: null argument");
+    std::copy(c->sparse_result.begin(), c->sparse_result.end(), out);
+  }
+  return SSP_OK;
 }
 int ssp_construct_solution_scaled(ssp_ctx* c, const double* palphas, const size_t* ptr, const size_t* idx,
                                   const double* val, int kp, const double* alphas, const double* const* xx,

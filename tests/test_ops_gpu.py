@@ -481,6 +481,36 @@ def test_sparse_gemm_inner_shapes(ctx, m, k, per):
         assert np.array_equal(ctx.gemm_inner_sparse(dx, ps), ref)
 
 
+@pytest.mark.parametrize("m,k,per", [(16, 8, 1), (64, 32, 2), (65, 3, 4), (5, 33, 1), (6, 4, 40), (0, 3, 1)])
+def test_sparse_gemm_inner_queued(ctx, m, k, per):
+    # ssp_gemm_inner_sparse_begin / _end around other reductions (the subspace update queues S(R,P) /
+    # H(P,R) ahead of the dense rows): the same numbers as the one-call form, bit for bit, whether
+    # the inline launch publishes to the pending buffers or the fallback computes at _begin.
+    n = 300_007
+    r = rng(m * 31 + k * 7 + per)
+    xs = [r.uniform(-1, 1, n) for _ in range(m)]
+    ps = [{int(i): float(v) for i, v in zip(r.choice(n, per, replace=False), r.uniform(-1, 1, per))} for _ in range(k)]
+    dx = [ctx.upload(v) for v in xs]
+    ref = np.array([[oracle.sparse_dot(x, sorted(p), [p[i] for i in sorted(p)]) for p in ps] for x in xs]).reshape(m, k)
+    dense = [ctx.upload(r.uniform(-1, 1, n)) for _ in range(3)]
+    g_ref = ctx.gemm_inner(dense, dense)
+    for _ in range(2):
+        shape = ctx.gemm_inner_sparse_begin(dx, ps)
+        g = ctx.gemm_inner(dense, dense)  # its own reduction, published while the sparse one is pending
+        d = ctx.dot(dense[0], dense[1])
+        got = ctx.gemm_inner_sparse_end(shape)
+        assert np.array_equal(got, ref)
+        assert np.array_equal(g, g_ref) and d == ctx.dot(dense[0], dense[1])
+    # an uncollected result is discarded by the next _begin; _end with nothing pending is an error
+    ctx.gemm_inner_sparse_begin(dx, ps)
+    shape = ctx.gemm_inner_sparse_begin(dx, ps)
+    assert np.array_equal(ctx.gemm_inner_sparse_end(shape), ref)
+    import subspace_hip as sh
+
+    with pytest.raises(sh.SspError):
+        ctx.gemm_inner_sparse_end(shape)
+
+
 @pytest.mark.parametrize("rank", [1, 4])
 def test_synthetic_action(ctx, rank):
     n, rho, seed = 10_007, 0.1, 99
