@@ -904,24 +904,36 @@ unsigned gram_grid(ssp_ctx* ctx, size_t n) {
 }
 
 template <int M>
-void launch_transform_m(ssp_ctx* ctx, unsigned grid, const TransformArgs& a, int dots, bool exact) {
+void launch_transform_m(ssp_ctx* ctx, unsigned grid, const TransformArgs& a, int dots, bool exact, bool pass) {
   const dim3 b(kBlock);
   if (exact) SSP_LAUNCH((k_transform<M, 0, false>), dim3(grid), b, 0, ctx->stream, a);
-  else if (dots == 2) SSP_LAUNCH((k_transform<M, 2, true>), dim3(gram_grid<M>(ctx, a.n)), b, 0, ctx->stream, a);
+  else if (dots == 2)
+    SSP_LAUNCH((k_transform<M, 2, true>), dim3(pass ? grid : gram_grid<M>(ctx, a.n)), b, 0, ctx->stream, a);
   else if (dots == 1) SSP_LAUNCH((k_transform<M, 1, true>), dim3(grid), b, 0, ctx->stream, a);
   else SSP_LAUNCH((k_transform<M, 0, true>), dim3(grid), b, 0, ctx->stream, a);
 }
 
-void launch_transform(ssp_ctx* ctx, int m, unsigned grid, const TransformArgs& a, int dots, bool exact) {
+// The pair dots of the fused-Gram transform: by a reduce pass after the kernel (full streaming grid,
+// one workgroup per dot) unless SSP_GRAM_FOLD=kernel (the last arriver folds them, one resident round
+// of workgroups: gram_grid).  A/B switch, read once.
+bool gram_reduce_pass() {
+  static const bool v = [] {
+    const char* e = std::getenv("SSP_GRAM_FOLD");
+    return !(e && std::string(e) == "kernel");
+  }();
+  return v;
+}
+
+void launch_transform(ssp_ctx* ctx, int m, unsigned grid, const TransformArgs& a, int dots, bool exact, bool pass) {
   switch (m) {
-    case 1: return launch_transform_m<1>(ctx, grid, a, dots, exact);
-    case 2: return launch_transform_m<2>(ctx, grid, a, dots, exact);
-    case 3: return launch_transform_m<3>(ctx, grid, a, dots, exact);
-    case 4: return launch_transform_m<4>(ctx, grid, a, dots, exact);
-    case 5: return launch_transform_m<5>(ctx, grid, a, dots, exact);
-    case 6: return launch_transform_m<6>(ctx, grid, a, dots, exact);
-    case 7: return launch_transform_m<7>(ctx, grid, a, dots, exact);
-    default: return launch_transform_m<8>(ctx, grid, a, dots, exact);
+    case 1: return launch_transform_m<1>(ctx, grid, a, dots, exact, pass);
+    case 2: return launch_transform_m<2>(ctx, grid, a, dots, exact, pass);
+    case 3: return launch_transform_m<3>(ctx, grid, a, dots, exact, pass);
+    case 4: return launch_transform_m<4>(ctx, grid, a, dots, exact, pass);
+    case 5: return launch_transform_m<5>(ctx, grid, a, dots, exact, pass);
+    case 6: return launch_transform_m<6>(ctx, grid, a, dots, exact, pass);
+    case 7: return launch_transform_m<7>(ctx, grid, a, dots, exact, pass);
+    default: return launch_transform_m<8>(ctx, grid, a, dots, exact, pass);
   }
 }
 
@@ -1722,14 +1734,17 @@ int transform_impl(ssp_ctx* ctx, const double* t, double* const* xx, const doubl
   if (n > 0) {
     ssp::LedgerScope ls(ctx, dots ? "transform_gram" : "transform", 16.0 * n * m);
     const unsigned grid = ssp::win_grid(ctx, n, fused == 2 ? 1 : (m <= 4 ? 4 : 2), 8);
+    const bool pass = fused == 2 && gram_reduce_pass();
     if (fused) {
       SSP_TRY(ssp::fold_begin(ctx, nd, &tail));
       SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * nd));
       a.partial = ctx->partial;
-      a.tail = tail;
+      if (!pass) a.tail = tail;  // else the kernel leaves its partials to the reduce pass below
     }
-    launch_transform(ctx, m, grid, a, fused, exact);
+    launch_transform(ctx, m, grid, a, fused, exact, pass);
     SSP_TRY_HIP(hipGetLastError());
+    if (pass)  // one workgroup per pair dot, publishing to the host (as the gemm_inner panels)
+      SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, nd, ctx->result_dev, nd, 0, 0, &tail, true));
   }
   if (!dots) return SSP_OK;
   if (!fused) {  // short (or empty) vectors: the dots of the stored outputs as the reference's dots
