@@ -570,6 +570,18 @@ void op_cases() {
     expect(throws<std::logic_error>([&] { hb.copy(q); }), "copy-construct from sparse");
     Mat m = hb.gemm_inner(CVecRef<Vec>{std::cref(x)}, CVecRef<SparseP>{std::cref(p), std::cref(q)});
     expect(m(0, 0) == -9.0 && m(0, 1) == 3.0, "sparse gemm_inner");
+    // the same overlap queued (ssp_gemm_inner_sparse_begin / _end) around another reduction
+    {
+      const CVecRef<Vec> rows{std::cref(x), std::cref(y)};
+      const CVecRef<SparseP> cols{std::cref(p), std::cref(q)};
+      auto pending = handler.gemm_inner_queued(rows, cols);
+      const Mat direct = hb.gemm_inner(rows, cols);
+      const Mat queued = pending();
+      bool same = queued.rows() == 2 && queued.cols() == 2;
+      for (size_t i = 0; same && i < 2; ++i)
+        for (size_t j = 0; j < 2; ++j) same = same && queued(i, j) == direct(i, j);
+      expect(same && queued(0, 0) == -9.0 && queued(1, 1) == 5.0, "queued sparse gemm_inner");
+    }
     // testArrayHandlerIterableSparse.cpp:22-29 analogue: largest |x_i p_i|
     auto sel = hb.select_max_dot(2, x, p);
     expect(sel == std::map<size_t, double>({{1, 4.0}, {4, 3.0}}), "sparse select_max_dot");
