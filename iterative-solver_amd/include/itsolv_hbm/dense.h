@@ -510,6 +510,46 @@ inline void eigenproblem(std::vector<double>& eigenvectors, std::vector<double>&
     }
     for (size_t i = 0; i < rank; ++i) Hbar[i + rank * j] = svmh[i] * acc[i] * svmh[j];
   }
+  if (hermitian) {
+    // The Hermitian case in real arrays: the complex form below carries zero imaginary parts through
+    // the back-transform, the sort and the sign fix, and its real parts are these numbers exactly
+    // (the same operations in the same order), so the results are bit for bit the same.
+    std::vector<double> ev, vec;
+    dense::sym_eigen(rank, Hbar, ev, vec);
+    std::vector<double> X(n * rank, 0.0), Xr(n);
+    for (size_t k = 0; k < rank; ++k) {
+      std::fill(Xr.begin(), Xr.end(), 0.0);
+      for (size_t l = 0; l < rank; ++l) {
+        const double ylk = vec[l + rank * k], sl = svmh[l];
+        const double* vl = &V[n * l];
+        for (size_t i = 0; i < n; ++i) Xr[i] += vl[i] * sl * ylk;
+      }
+      std::copy(Xr.begin(), Xr.end(), X.begin() + long(n * k));
+    }
+    // selection sort ascending (first minimum wins), sign fixed on the largest of the first `rank`
+    // components
+    std::vector<char> used(rank, 0);
+    eigenvectors.resize(n * rank);
+    eigenvalues.resize(rank);
+    for (size_t k = 0; k < rank; ++k) {
+      size_t ll = 0;
+      while (used[ll]) ++ll;
+      for (size_t l = 0; l < rank; ++l)
+        if (!used[l] && ev[l] < ev[ll]) ll = l;
+      used[ll] = 1;
+      eigenvalues[k] = ev[ll];
+      double* col = &eigenvectors[n * k];
+      std::copy(X.begin() + long(n * ll), X.begin() + long(n * (ll + 1)), col);
+      size_t mc = 0;
+      for (size_t l = 0; l < rank && l < n; ++l)
+        if (std::abs(col[l]) > std::abs(col[mc])) mc = l;
+      if (col[mc] < 0)
+        for (size_t i = 0; i < n; ++i) col[i] = -col[i];
+    }
+    (void)verbosity;
+    (void)condone_complex;
+    return;
+  }
   std::vector<cd> evals_c(rank), y(rank * rank);
   if (hermitian) {
     std::vector<double> ev, vec;
