@@ -200,8 +200,26 @@ def gpu_c2_solve(ctx, world, n=None):
     t0 = time.perf_counter()
     r = ih.davidson_synthetic(ctx, n, rho, rank, seed, n_local=0, solutions=False, **kw)
     ctx.synchronize()
-    return {"wall_s": round(time.perf_counter() - t0, 4), "iterations": r["iterations"],
-            "r_creations": r["r_creations"], "eigenvalues": [round(float(e), 12) for e in r["eigenvalues"][:4]]}
+    wall = time.perf_counter() - t0
+    # the same solve once more under the HIP-event ledger: kernel time, rate and idle, as the other
+    # in-solver blocks report them
+    ctx.ledger_reset()
+    ctx.ledger_enable(True)
+    ih.davidson_synthetic(ctx, n, rho, rank, seed, n_local=0, solutions=False, **kw)
+    ctx.synchronize()
+    ctx.ledger_enable(False)
+    led = ctx.ledger()
+    ms = sum(v["ms"] for v in led.values())
+    nb = sum(v["bytes"] for v in led.values())
+    top = sorted(led.items(), key=lambda kv: -kv[1]["ms"])[:4]
+    return {"wall_s": round(wall, 4), "iterations": r["iterations"],
+            "r_creations": r["r_creations"], "eigenvalues": [round(float(e), 12) for e in r["eigenvalues"][:4]],
+            "kernel_ms_rank0": round(ms, 3), "algorithmic_GB_rank0": round(nb / 1e9, 2),
+            "kernel_GBs_rank0": round(nb / (ms / 1e3) / 1e9, 1) if ms else None,
+            "idle_frac_of_wall": round((wall - ms / 1e3) / wall, 4),
+            "top_ops": {op: {"calls": v["calls"], "ms": round(v["ms"], 2),
+                             "GBs": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] else None}
+                        for op, v in top}}
 
 
 def pin_this_thread():
@@ -414,8 +432,9 @@ def in_solver(ctx, n_global, world, barrier, repeat=3, kind="davidson"):
 
 def setup_context(args, world, rank, local_rank):
     """This rank's context on its device, with the rank transport attached at N > 1.  Every wait on
-    the other ranks -- RCCL's join included (non-blocking init, polled; csrc/context.hip) -- is bounded
-    by SSP_COMM_TIMEOUT_S (120 s here unless set), so a rank that never arrives ends the run with an
+    the other ranks -- RCCL's join included (a helper thread under the deadline; csrc/context.hip) -- is
+    bounded by SSP_COMM_TIMEOUT_S (120 s here unless set).  A failed RCCL join on any rank makes every
+    rank fall back to the host hub in the same process; any other setup failure ends the run with an
     error record (main) instead of a hang."""
     ctx = sh.Context(local_rank % max(1, sh.device_count()))
     if world > 1:
@@ -439,14 +458,68 @@ def setup_context(args, world, rank, local_rank):
         if uid_path:  # attach returned on rank 0: every rank has read the id
             os.remove(uid_path)
     if world > 1 and transport == "rccl":
-        uid, uid_path = rendezvous_uid(rank, world, timeout=float(os.environ.get("SSP_COMM_TIMEOUT_S", "120")))
+        err, uid_path = None, None
         try:
+            uid, uid_path = rendezvous_uid(rank, world, timeout=float(os.environ.get("SSP_COMM_TIMEOUT_S", "120")))
+            if os.environ.get("SSP_BENCH_FAIL_RCCL_RANK") == str(rank):  # rehearsal of a failed join
+                raise sh.SspError(5, "injected RCCL attach failure (SSP_BENCH_FAIL_RCCL_RANK)")
             ctx.attach_comm(world, rank, uid)  # collective: returns once every rank has joined, or fails
-        finally:
-            if uid_path:
-                os.remove(uid_path)
+        except (sh.SspError, TimeoutError) as e:
+            err = e
+        # Every rank agrees on the outcome through the launcher's file rendezvous (no collective of the
+        # transport that may have failed).  If any rank's RCCL join failed, every rank attaches the host
+        # hub in this same process (no re-exec, no restart): the run still yields a measured number, and
+        # the JSON line names the transport that produced it.
+        failed = agree_failures(rank, world, err)
+        if uid_path:  # rank 0, once every rank has reported (so has read the id, or given up on it)
+            os.remove(uid_path)
+        if failed:
+            log(f"rank {rank}: RCCL join failed on rank(s) {failed} ({err if err else 'this rank joined'}); "
+                "every rank falls back to the host hub")
+            port = int(os.environ.get("MASTER_PORT", "29500")) + 1
+            ctx.attach_host_comm(sh.HubComm(rank, world, os.environ.get("MASTER_ADDR", "127.0.0.1"), port))
+            transport = "host"
+            args.comm_fallback = {"from": "rccl", "failed_ranks": failed,
+                                  "reason": str(err) if err else f"RCCL join failed on rank(s) {failed}"}
     args.comm_used = transport
     return ctx
+
+
+def agree_failures(rank, world, err, timeout=None):
+    """The ranks whose attach failed, agreed by every rank: each writes its outcome to a file keyed by
+    the launcher (as rendezvous_uid) and reads every rank's.  Bounded by SSP_COMM_TIMEOUT_S; a rank
+    that never reports counts as failed."""
+    timeout = float(os.environ.get("SSP_COMM_TIMEOUT_S", "120")) if timeout is None else timeout
+    tag = "{}_{}_{}".format(os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"),
+                            os.getppid())
+    base = os.path.join(tempfile.gettempdir(), f"ssp_bench_attach_{tag}")
+    with open(f"{base}.{rank}.tmp", "w") as f:
+        f.write("fail" if err else "ok")
+    os.replace(f"{base}.{rank}.tmp", f"{base}.{rank}")
+    t0, failed = time.time(), []
+    for r in range(world):
+        path = f"{base}.{r}"
+        while not os.path.exists(path) and time.time() - t0 < timeout:
+            time.sleep(0.05)
+        try:
+            with open(path) as f:
+                ok = f.read() == "ok"
+        except OSError:
+            ok = False
+        if not ok:
+            failed.append(r)
+    return failed
+
+
+def remove_attach_files(world):
+    """Rank 0, after the last barrier (every rank has read them): agree_failures' files."""
+    tag = "{}_{}_{}".format(os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"),
+                            os.getppid())
+    for r in range(world):
+        try:
+            os.remove(os.path.join(tempfile.gettempdir(), f"ssp_bench_attach_{tag}.{r}"))
+        except OSError:
+            pass
 
 
 def main():
@@ -621,9 +694,27 @@ def main():
         t_s = time.perf_counter() - t_s
         if world > 1:
             t_s = max(struct.unpack("<d", b)[0] for b in ctx.allgather_bytes(struct.pack("<d", t_s)))
+        # its roofline as the headline's: the dominant op's average launch over a few ledgered steps
+        # (HIP events on the context stream, after the timed region)
+        ctx.ledger_reset()
+        ctx.ledger_enable(True)
+        for _ in range(5):
+            wls.step()
+        ctx.synchronize()
+        ctx.ledger_enable(False)
+        led_s = ctx.ledger()
         wls.free()
+        dom_s = max(led_s, key=lambda op: led_s[op]["ms"])
+        es = led_s[dom_s]
+        ach_s = (es["bytes"] / es["calls"]) / (es["ms"] / es["calls"] / 1e3) / 1e9
         small = {"n_global": ns_global, "steps": s_steps, "ms_per_step": round(1e3 * t_s / s_steps, 4),
-                 "GBs": round(step_bytes(ns_global, m, k) * s_steps / t_s / 1e9, 2)}
+                 "GBs": round(step_bytes(ns_global, m, k) * s_steps / t_s / 1e9, 2),
+                 "frac_of_hbm_peak": round(step_bytes(ns_global, m, k) * s_steps / t_s / 1e9 / HBM_PEAK_GBS, 4),
+                 "roofline": {"bound": "hbm", "kernel": dom_s, "achieved": round(ach_s, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": float(f"{ach_s / HBM_PEAK_GBS:.4g}"),
+                              "avg_launch_us": round(1e3 * es["ms"] / es["calls"], 2),
+                              "bytes_per_launch": es["bytes"] / es["calls"],
+                              "ledger": "HIP events over 5 steps after the timed region"}}
     solve = solve_diis = gpu_c2 = shard = None
     if not args.no_in_solver:
         solve = in_solver(ctx, n_global, world, barrier)
@@ -674,8 +765,11 @@ def main():
                 "parallelism": f"index-range shards x{world} ("
                                + {"rccl": "RCCL", "p2p": "peer-memory", "host": "host-hub"}[getattr(args, "comm_used", args.comm)]
                                + " allreduce for reductions)",
+
                 "bytes_per_step": step_bytes(n_global, m, k),
             },
+            "comm": getattr(args, "comm_used", args.comm) if world > 1 else None,
+            "comm_fallback": getattr(args, "comm_fallback", None),
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,
@@ -725,7 +819,15 @@ def main():
         result["sustained"] = sustained
         print(json.dumps(result), flush=True)
     barrier()
+    if rank == 0 and world > 1:
+        remove_attach_files(world)
     ctx.close()
+    if getattr(args, "comm_fallback", None):
+        # an abandoned RCCL join leaves its helper thread inside RCCL's bootstrap: end the process
+        # without the interpreter's teardown (the JSON line is out)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

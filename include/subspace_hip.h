@@ -37,7 +37,10 @@ typedef enum {
   SSP_ERR_HIP = 4,       /* HIP runtime failure                                      */
   SSP_ERR_COMM = 5,      /* RCCL failure                                             */
   SSP_ERR_NOMEM = 6,     /* device or pinned allocation failed                      */
-  SSP_ERR_UNSUPPORTED = 7 /* operation not defined for these operands -> logic_error */
+  SSP_ERR_UNSUPPORTED = 7, /* operation not defined for these operands -> logic_error */
+  SSP_ERR_COMM_ABANDONED = 8 /* an RCCL join of this process was abandoned at its deadline: no further
+                                RCCL attach in this process (end it); the host-callback and peer-memory
+                                transports stay available */
 } ssp_status;
 
 typedef struct ssp_ctx ssp_ctx;
@@ -65,8 +68,11 @@ int ssp_download(ssp_ctx* ctx, double* dst_host, const double* src_dev, size_t n
  * by rank 0 with ssp_comm_unique_id and distributed by the caller (e.g. torch.distributed). */
 #define SSP_UNIQUE_ID_BYTES 128
 int ssp_comm_unique_id(char* id_out);
-/* Collective: returns once every rank has joined, or SSP_ERR_COMM when the communicator has not formed
- * within the communication deadline (ssp_ctx_set_comm_timeout; a rank is missing). */
+/* Collective: returns once every rank has joined, SSP_ERR_COMM when RCCL reports the join failed, or
+ * SSP_ERR_COMM_ABANDONED when the communicator has not formed within the communication deadline
+ * (ssp_ctx_set_comm_timeout; a rank is missing).  An abandoned join leaves its helper thread inside
+ * RCCL's bootstrap, so every later ssp_ctx_attach_comm of the process returns SSP_ERR_COMM_ABANDONED at
+ * once: do not retry -- end the process, or attach the host-callback / peer-memory transport. */
 int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id);
 int ssp_ctx_rank(ssp_ctx* ctx);
 int ssp_ctx_nranks(ssp_ctx* ctx);

@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -347,9 +348,11 @@ LedgerScope::LedgerScope(ssp_ctx* ctx, const char* op, double bytes) : ctx_(ctx)
   (void)hipEventRecord(start_, ctx->stream);
 }
 
-bool LedgerScope::dispatch_events(hipEvent_t* start, hipEvent_t* stop) {
+bool LedgerScope::dispatch_events(hipStream_t stream, hipEvent_t* start, hipEvent_t* stop) {
   LedgerScope* s = t_scope;
-  if (!s) return false;
+  // only a launch on the open scope's own context stream carries its events (a kernel of another
+  // context launched from this thread inside the scope keeps a plain launch)
+  if (!s || stream != s->ctx_->stream) return false;
   *start = s->launched_ ? nullptr : s->start_;
   *stop = s->stop_;
   s->launched_ = true;
@@ -606,9 +609,20 @@ int ssp_comm_unique_id(char* id_out) {
   return SSP_OK;
 }
 
+namespace {
+// Set when a join is abandoned at its deadline: its helper thread stays blocked in RCCL's bootstrap
+// (holding its socket and a device context), and a second bootstrap beside it in the same process is
+// not something RCCL supports -- so no RCCL attach is attempted again in this process.
+std::atomic<bool> g_rccl_join_abandoned{false};
+}  // namespace
+
 int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id) {
   SSP_CHECK_CTX(ctx);
   if (nranks < 1 || rank < 0 || rank >= nranks || !id) return ssp::set_error(SSP_ERR_ARG, "ssp_ctx_attach_comm: bad rank");
+  if (g_rccl_join_abandoned.load())
+    return ssp::set_error(SSP_ERR_COMM_ABANDONED,
+                          "ssp_ctx_attach_comm: an earlier RCCL join of this process was abandoned; end the process "
+                          "(or attach the host-callback / peer-memory transport) -- do not retry RCCL");
   if (ctx->comm) {
     ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
@@ -631,8 +645,8 @@ int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id) {
   // its non-blocking form (ncclConfig_t blocking = 0) does too (measured on the MI355X boxes:
   // tools/rccl_alone_probe.py, profiles/r5/rccl_alone_probe.txt), so the deadline cannot be polled from
   // inside RCCL.  The abandoned helper keeps the join's state alive on the heap; if the missing ranks
-  // ever arrive it aborts the late communicator itself.  A process whose join failed should end
-  // (bench.py: an error record, then os._exit).
+  // ever arrive it aborts the late communicator itself.  The process is then marked: every later RCCL
+  // attach returns SSP_ERR_COMM_ABANDONED (bench.py falls back to the host hub on every rank).
   struct Join {
     std::mutex m;
     std::condition_variable cv;
@@ -671,12 +685,15 @@ int ssp_ctx_attach_comm(ssp_ctx* ctx, int nranks, int rank, const char* id) {
   const auto limit = std::chrono::duration<double>(ctx->comm_timeout_s);
   if (!job->cv.wait_for(lk, limit, [&] { return job->done; })) {
     job->abandoned = true;
+    g_rccl_join_abandoned.store(true);
     say("deadline: join abandoned");
     char t[64];
     std::snprintf(t, sizeof(t), "%g", ctx->comm_timeout_s);
-    return ssp::set_error(SSP_ERR_COMM, std::string("ncclCommInitRank: rank ") + std::to_string(rank) + " of " +
-                                            std::to_string(nranks) + ": the communicator did not form within " + t +
-                                            " s (SSP_COMM_TIMEOUT_S): another rank is missing");
+    return ssp::set_error(SSP_ERR_COMM_ABANDONED,
+                          std::string("ncclCommInitRank: rank ") + std::to_string(rank) + " of " + std::to_string(nranks) +
+                              ": the communicator did not form within " + t +
+                              " s (SSP_COMM_TIMEOUT_S): another rank is missing; the join is abandoned (no further "
+                              "RCCL attach in this process)");
   }
   say("joined");
   if (job->r != ncclSuccess) {

@@ -53,7 +53,17 @@ struct InnerArgs {
 // SYM: xx == yy (a symmetric overlap, MG == NG): each vector is loaded once and used as both
 // operands of the MFMA.  SC: operands with deferred scales (each loaded element times its vector's
 // scale before the MFMA).
-template <int MG, int NG, bool SYM = false, bool SC = false>
+// PIPE: the loads of the wave's next chunk are issued before the MFMAs of the current one (two
+// register stages), so a wave keeps a chunk of every vector in flight while its matrix cores work.
+// The chunks are accumulated in the same order (ch, ch + nw, ch + 2 nw, ...), so the results are
+// bit-identical to the one-stage loop.  Operand lanes of absent vectors (4 g + r >= m) read their
+// group's first vector -- the same addresses as that lane-group's valid lanes in the same load
+// instruction, so no extra traffic -- and only feed accumulator rows / columns that are never
+// stored (C[i][j] of the 4x4x4 MFMA depends on row i of A and column j of B alone).  Whole absent
+// groups (4 g >= m: the instantiated NG above the panel's) skip their loads by a wave-uniform branch
+// (re-reading one fixed line instead made every wave of the chip hit one L2 channel: 8 x 40 ran 6 %
+// slower).  No load carries an exec-mask guard.
+template <int MG, int NG, bool SYM = false, bool SC = false, bool PIPE = false>
 __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
   static_assert(!SYM || MG == NG, "symmetric panel needs square groups");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -61,15 +71,18 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
   const double* xp[MG];
   const double* yp[NG];
   double xsc[MG], ysc[NG];
+  bool xok[MG], yok[NG];  // this lane's vector exists (remainder loop)
 #pragma unroll
   for (int g = 0; g < MG; ++g) {
-    xp[g] = (4 * g + r < a.m) ? a.x[4 * g + r] : nullptr;
-    xsc[g] = (SC && 4 * g + r < a.m) ? a.xs[4 * g + r] : 1.0;
+    xok[g] = 4 * g + r < a.m;
+    xp[g] = xok[g] ? a.x[4 * g + r] : a.x[4 * g < a.m ? 4 * g : 0];
+    xsc[g] = (SC && xok[g]) ? a.xs[4 * g + r] : 1.0;
   }
 #pragma unroll
   for (int h = 0; h < NG; ++h) {
-    yp[h] = (4 * h + r < a.k) ? a.y[4 * h + r] : nullptr;
-    ysc[h] = (SC && 4 * h + r < a.k) ? a.ys[4 * h + r] : 1.0;
+    yok[h] = 4 * h + r < a.k;
+    yp[h] = yok[h] ? a.y[4 * h + r] : a.y[4 * h < a.k ? 4 * h : 0];
+    ysc[h] = (SC && yok[h]) ? a.ys[4 * h + r] : 1.0;
   }
   double acc[MG][NG];
 #pragma unroll
@@ -77,19 +90,20 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
 #pragma unroll
     for (int h = 0; h < NG; ++h) acc[g][h] = 0;
 
-  const size_t gw = size_t(blockIdx.x) * (kBlock / 64) + wave;
+  // wave-uniform loop control in scalar registers
+  const size_t gw = size_t(__builtin_amdgcn_readfirstlane(int(blockIdx.x * (kBlock / 64) + wave)));
   const size_t nw = size_t(gridDim.x) * (kBlock / 64);
   const size_t nchunks = a.n / 32;
   const double2 z2 = make_double2(0, 0);
-  for (size_t ch = gw; ch < nchunks; ch += nw) {
+  const auto load = [&](size_t ch, double2(&xv)[MG], double2(&yv)[NG]) {
     const size_t e = ch * 32 + 2 * p;
-    double2 xv[MG], yv[NG];
 #pragma unroll
-    for (int g = 0; g < MG; ++g) xv[g] = xp[g] ? ssp::ld2nt(xp[g] + e) : z2;
+    for (int g = 0; g < MG; ++g) xv[g] = 4 * g < a.m ? ssp::ld2nt(xp[g] + e) : z2;
 #pragma unroll
-    for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : (yp[h] ? ssp::ld2nt(yp[h] + e) : z2);
-    // scales after every load of the chunk is in flight (a multiply inside the guarded load would
-    // make each load wait for the previous one)
+    for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : (4 * h < a.k ? ssp::ld2nt(yp[h] + e) : z2);
+  };
+  const auto mac = [&](double2(&xv)[MG], double2(&yv)[NG]) {
+    // scales after every load of the chunk is in flight
     if constexpr (SC) {
 #pragma unroll
       for (int g = 0; g < MG; ++g) xv[g] = sc2<SC>(xv[g], xsc[g]);
@@ -103,6 +117,33 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
         acc[g][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(xv[g].x, yv[h].x, acc[g][h], 0, 0, 0);
         acc[g][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(xv[g].y, yv[h].y, acc[g][h], 0, 0, 0);
       }
+  };
+  if constexpr (PIPE) {
+    double2 xa[MG], ya[NG], xb[MG], yb[NG];
+    size_t ch = gw;
+    if (ch < nchunks) load(ch, xa, ya);
+    for (;;) {
+      if (ch + nw >= nchunks) {
+        if (ch < nchunks) mac(xa, ya);
+        break;
+      }
+      load(ch + nw, xb, yb);
+      mac(xa, ya);
+      ch += nw;
+      if (ch + nw >= nchunks) {
+        mac(xb, yb);
+        break;
+      }
+      load(ch + nw, xa, ya);
+      mac(xb, yb);
+      ch += nw;
+    }
+  } else {
+    for (size_t ch = gw; ch < nchunks; ch += nw) {
+      double2 xv[MG], yv[NG];
+      load(ch, xv, yv);
+      mac(xv, yv);
+    }
   }
   // Remainder [32 * nchunks, n): 32-element chunks spread over the waves, guarded element loads.
   for (size_t s = nchunks * 32 + gw * 32; s < a.n; s += nw * 32) {
@@ -110,13 +151,13 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
     double x0[MG], x1[MG];
 #pragma unroll
     for (int g = 0; g < MG; ++g) {
-      x0[g] = (xp[g] && i0 < a.n) ? sc1<SC>(xp[g][i0], xsc[g]) : 0.0;
-      x1[g] = (xp[g] && i1 < a.n) ? sc1<SC>(xp[g][i1], xsc[g]) : 0.0;
+      x0[g] = (xok[g] && i0 < a.n) ? sc1<SC>(xp[g][i0], xsc[g]) : 0.0;
+      x1[g] = (xok[g] && i1 < a.n) ? sc1<SC>(xp[g][i1], xsc[g]) : 0.0;
     }
 #pragma unroll
     for (int h = 0; h < NG; ++h) {
-      const double y0 = SYM ? x0[h] : ((yp[h] && i0 < a.n) ? sc1<SC>(yp[h][i0], ysc[h]) : 0.0);
-      const double y1 = SYM ? x1[h] : ((yp[h] && i1 < a.n) ? sc1<SC>(yp[h][i1], ysc[h]) : 0.0);
+      const double y0 = SYM ? x0[h] : ((yok[h] && i0 < a.n) ? sc1<SC>(yp[h][i0], ysc[h]) : 0.0);
+      const double y1 = SYM ? x1[h] : ((yok[h] && i1 < a.n) ? sc1<SC>(yp[h][i1], ysc[h]) : 0.0);
 #pragma unroll
       for (int g = 0; g < MG; ++g) {
         acc[g][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(x0[g], y0, acc[g][h], 0, 0, 0);
@@ -1104,8 +1145,29 @@ unsigned inner_grid(const ssp_ctx* ctx, size_t n) {
   return unsigned(std::max<size_t>(1, std::min(blocks, cap)));
 }
 
+// Two-stage loads (k_gemm_inner PIPE) for the small panels (at most 8 accumulator tiles, and the
+// symmetric ones), whose second register stage still leaves >= 2 waves per SIMD.  SSP_INNER_PIPE:
+// 0 off, 1 (default) small panels, 2 also up to 16 tiles (A/B knob, read once).
+int inner_pipe_level() {
+  static const int v = [] {
+    const char* e = std::getenv("SSP_INNER_PIPE");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+template <int MG, int NG, bool SYM, bool SC>
+constexpr int inner_pipe_min_level() {
+  return (SYM || MG * NG <= 8) ? 1 : (MG * NG <= 16 ? 2 : 99);
+}
+
 template <int MG, int NG, bool SC>
 void launch_inner_t(ssp_ctx* ctx, unsigned grid, const InnerArgs& a) {
+  if constexpr (inner_pipe_min_level<MG, NG, false, SC>() < 99) {
+    if (inner_pipe_level() >= inner_pipe_min_level<MG, NG, false, SC>()) {
+      SSP_LAUNCH((k_gemm_inner<MG, NG, false, SC, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      return;
+    }
+  }
   SSP_LAUNCH((k_gemm_inner<MG, NG, false, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
 }
 
@@ -1128,13 +1190,21 @@ int launch_inner_mg(ssp_ctx* ctx, unsigned grid, const InnerArgs& a, int need) {
   return SSP_OK;
 }
 
+template <int G, bool SC>
+void launch_inner_sym_g(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
+  if (inner_pipe_level() >= 1)
+    SSP_LAUNCH((k_gemm_inner<G, G, true, SC, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  else
+    SSP_LAUNCH((k_gemm_inner<G, G, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+}
+
 template <bool SC>
 int launch_inner_sym_t(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
   switch ((a.m + 3) / 4) {
-    case 1: SSP_LAUNCH((k_gemm_inner<1, 1, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
-    case 2: SSP_LAUNCH((k_gemm_inner<2, 2, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
-    case 3: SSP_LAUNCH((k_gemm_inner<3, 3, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
-    default: SSP_LAUNCH((k_gemm_inner<4, 4, true, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a); break;
+    case 1: launch_inner_sym_g<1, SC>(ctx, a, grid); break;
+    case 2: launch_inner_sym_g<2, SC>(ctx, a, grid); break;
+    case 3: launch_inner_sym_g<3, SC>(ctx, a, grid); break;
+    default: launch_inner_sym_g<4, SC>(ctx, a, grid); break;
   }
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;
@@ -1747,13 +1817,23 @@ int transform_impl(ssp_ctx* ctx, const double* t, double* const* xx, const doubl
       SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, nd, ctx->result_dev, nd, 0, 0, &tail, true));
   }
   if (!dots) return SSP_OK;
-  if (!fused) {  // short (or empty) vectors: the dots of the stored outputs as the reference's dots
-    std::vector<const double*> c(xx, xx + m);
-    if (dots == 2) return ssp_gemm_inner(ctx, c.data(), m, c.data(), m, n, out);
-    std::vector<double> g(size_t(m) * m);
-    SSP_TRY(ssp_gemm_inner(ctx, c.data(), m, c.data(), m, n, g.data()));
-    for (int j = 0; j < m; ++j) out[j] = g[size_t(j) * m + j];
-    return SSP_OK;
+  if (!fused) {
+    // Short (or empty) vectors: the dots of the stored outputs as the reference's sequential dots
+    // (each the number ssp_gemm_inner's short path gives), reduced in the fused kernel's layout -- the
+    // nd pair dots (a <= b) or the m self-dots -- so that a rank whose shard takes this branch posts
+    // the same collective as a rank on the bandwidth kernel (shards of spread_remainder differ by one
+    // element and may straddle exact_max; a rank may hold none).
+    std::vector<const double*> ra, rb;
+    for (int i = 0; i < m; ++i)
+      for (int j = i; j < (dots == 2 ? m : i + 1); ++j) {
+        ra.push_back(xx[i]);
+        rb.push_back(xx[j]);
+      }
+    SSP_TRY(ssp::fold_begin(ctx, nd, &tail));
+    {
+      ssp::LedgerScope ls(ctx, "gemm_inner", 8.0 * n * m);
+      SSP_TRY(ssp::exact_inner(ctx, ra.data(), nullptr, nd, rb.data(), nullptr, nd, n, true, tail));
+    }
   }
   if (dots == 1) return ssp::fold_finish(ctx, tail, out);
   std::vector<double> pr(static_cast<size_t>(nd));
@@ -1783,15 +1863,19 @@ int ssp_precondition_norms(ssp_ctx* ctx, double* const* a, int nvec, const doubl
   if (nvec < 0 || nvec > 8 || (nvec > 0 && (!a || !shift || !norms2)))
     return ssp::set_error(SSP_ERR_ARG, "ssp_precondition_norms: bad vectors (0 <= nvec <= 8)");
   if (nvec == 0) return SSP_OK;
-  // short vectors: the reference's arithmetic for the dots (sequential sums), as gemm_inner computes
-  // them; the bandwidth path's self-dots come from the pass itself
+  // short (or empty) vectors: the reference's arithmetic for the dots (sequential sums, the numbers
+  // gemm_inner's short path gives), reduced as the bandwidth pass's nvec self-dots are (one collective
+  // of nvec values whichever branch a rank's shard takes)
   if (n == 0 || ssp::exact_mode(ctx, n)) {
     SSP_TRY(ssp_precondition(ctx, a, nvec, d, shift, n));
     std::vector<const double*> c(a, a + nvec);
-    std::vector<double> g(size_t(nvec) * nvec);
-    SSP_TRY(ssp_gemm_inner(ctx, c.data(), nvec, c.data(), nvec, n, g.data()));
-    for (int v = 0; v < nvec; ++v) norms2[v] = g[size_t(v) * nvec + v];
-    return SSP_OK;
+    ssp::FoldTail tail{};
+    SSP_TRY(ssp::fold_begin(ctx, nvec, &tail));
+    {
+      ssp::LedgerScope ls(ctx, "gemm_inner", 8.0 * n * nvec);
+      SSP_TRY(ssp::exact_inner(ctx, c.data(), nullptr, nvec, c.data(), nullptr, nvec, n, true, tail));
+    }
+    return ssp::fold_finish(ctx, tail, norms2);
   }
   SSP_TRY(check_ptrs(&d, 1, n, "ssp_precondition_norms"));
   SSP_TRY(check_ptrs(const_cast<const double* const*>(a), nvec, n, "ssp_precondition_norms"));

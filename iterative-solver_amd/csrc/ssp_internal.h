@@ -193,8 +193,9 @@ class LedgerScope {
   ~LedgerScope();
   LedgerScope(const LedgerScope&) = delete;
   LedgerScope& operator=(const LedgerScope&) = delete;
-  // dispatch timing: the events for the next kernel launched on this thread inside an open scope
-  static bool dispatch_events(hipEvent_t* start, hipEvent_t* stop);
+  // dispatch timing: the events for the next kernel launched on this thread inside an open scope, when
+  // it is launched on that scope's context stream
+  static bool dispatch_events(hipStream_t stream, hipEvent_t* start, hipEvent_t* stop);
 
  private:
   ssp_ctx* ctx_;
@@ -209,7 +210,7 @@ class LedgerScope {
 #define SSP_LAUNCH(K, G, B, SHM, ST, ...)                                                  \
   do {                                                                                    \
     hipEvent_t ssp_e0_ = nullptr, ssp_e1_ = nullptr;                                      \
-    if (::ssp::LedgerScope::dispatch_events(&ssp_e0_, &ssp_e1_))                          \
+    if (::ssp::LedgerScope::dispatch_events(ST, &ssp_e0_, &ssp_e1_))                      \
       hipExtLaunchKernelGGL(K, G, B, SHM, ST, ssp_e0_, ssp_e1_, 0u, __VA_ARGS__);         \
     else                                                                                  \
       hipLaunchKernelGGL(K, G, B, SHM, ST, __VA_ARGS__);                                  \

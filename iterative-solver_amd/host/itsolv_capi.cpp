@@ -227,38 +227,40 @@ double residual_norm(const P& problem, const std::shared_ptr<Device>& dev, const
 
 // residual_norm for a batch of solutions (run_davidson's batched form): one action over the batch,
 // r_i = H x_i - e_i x_i with |r_i|^2 in one pass (ssp_axpy_pairs_norm: element for element
-// ssp_axpy's), |x_i|^2 from one symmetric overlap.  From the fused-pass size up (shorter vectors keep
+// ssp_axpy's), |x_i|^2 from one symmetric overlap.  Batches of more than 16 roots (one fused launch's
+// destinations) run as consecutive chunks of 16.  From the fused-pass size up (shorter vectors keep
 // the per-root form and its sequential dots).
 template <class P>
 pr::ResidualNormsBatch<Vec> residual_norms_batch(const P& problem, const std::shared_ptr<Device>& dev, size_t n) {
   if (n < molpro::linalg::hbm::fused_min_size()) return {};
   return [&problem, dev, n](const std::vector<const Vec*>& xs, const std::vector<double>& e, std::vector<double>& out) {
-    const size_t m = xs.size();
-    if (m == 0) return;
-    if (m > 16) throw std::invalid_argument("residual_norms_batch: more than 16 roots in a batch");
-    std::vector<Vec> ax;
-    ax.reserve(m);
-    for (size_t i = 0; i < m; ++i) ax.emplace_back(dev, n);
-    CVecRef<Vec> cx;
-    VecRef<Vec> wa;
-    for (size_t i = 0; i < m; ++i) {
-      cx.emplace_back(std::cref(*xs[i]));
-      wa.emplace_back(std::ref(ax[i]));
+    constexpr size_t kChunk = 16;
+    for (size_t i0 = 0; i0 < xs.size(); i0 += kChunk) {
+      const size_t m = std::min(kChunk, xs.size() - i0);
+      std::vector<Vec> ax;
+      ax.reserve(m);
+      for (size_t i = 0; i < m; ++i) ax.emplace_back(dev, n);
+      CVecRef<Vec> cx;
+      VecRef<Vec> wa;
+      for (size_t i = 0; i < m; ++i) {
+        cx.emplace_back(std::cref(*xs[i0 + i]));
+        wa.emplace_back(std::ref(ax[i]));
+      }
+      problem.action(cx, wa);
+      std::vector<const double*> xp;
+      std::vector<double*> ap;
+      std::vector<double> c(m), rr(m), g(m * m);
+      for (size_t i = 0; i < m; ++i) {
+        xp.push_back(xs[i0 + i]->data());
+        ap.push_back(ax[i].data_rw());
+        c[i] = -e[i0 + i];
+      }
+      const size_t local = xs[i0]->local_size();
+      check(ssp_axpy_pairs_norm(dev->ctx(), c.data(), xp.data(), nullptr, ap.data(), nullptr, int(m), local, rr.data()),
+            "ssp_axpy_pairs_norm");
+      check(ssp_gemm_inner(dev->ctx(), xp.data(), int(m), xp.data(), int(m), local, g.data()), "ssp_gemm_inner");
+      for (size_t i = 0; i < m; ++i) out[i0 + i] = std::sqrt(std::abs(rr[i]) / std::abs(g[i * m + i]));
     }
-    problem.action(cx, wa);
-    std::vector<const double*> xp;
-    std::vector<double*> ap;
-    std::vector<double> c(m), rr(m), g(m * m);
-    for (size_t i = 0; i < m; ++i) {
-      xp.push_back(xs[i]->data());
-      ap.push_back(ax[i].data_rw());
-      c[i] = -e[i];
-    }
-    const size_t local = xs[0]->local_size();
-    check(ssp_axpy_pairs_norm(dev->ctx(), c.data(), xp.data(), nullptr, ap.data(), nullptr, int(m), local, rr.data()),
-          "ssp_axpy_pairs_norm");
-    check(ssp_gemm_inner(dev->ctx(), xp.data(), int(m), xp.data(), int(m), local, g.data()), "ssp_gemm_inner");
-    for (size_t i = 0; i < m; ++i) out[i] = std::sqrt(std::abs(rr[i]) / std::abs(g[i * m + i]));
   };
 }
 

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -265,17 +266,10 @@ int device_for(int64_t fcomm) {
   return nd > 0 ? nr % nd : 0;
 }
 
-std::shared_ptr<void> attach(ssp_ctx* ctx, int64_t fcomm, const char* transport) {
-  Bridge* b = bridge();
-  if (!b || !b->active()) throw std::runtime_error("MPI bridge: no initialised MPI library in this process");
-  if (!b->valid(fcomm)) throw std::runtime_error("MPI bridge: " + std::to_string(fcomm) + " is not a communicator");
-  std::string t = transport && *transport ? transport : "";
-  if (t.empty()) {
-    const char* e = std::getenv("ITSOLV_HBM_COMM");
-    t = e && *e ? e : "mpi";
-  }
-  const int size = b->size(fcomm), rank = b->rank(fcomm);
-  if (size < 1 || rank < 0) throw std::runtime_error("MPI bridge: MPI_Comm_size / MPI_Comm_rank failed");
+namespace {
+// One transport, attached collectively: every rank of fcomm takes the same outcome (an exception on
+// every rank, with the first failing rank's reason, or success on every rank).
+std::shared_ptr<void> attach_one(ssp_ctx* ctx, Bridge* b, int64_t fcomm, const std::string& t, int size, int rank) {
   if (t == "mpi") {
     auto link = std::make_shared<HostLink>(HostLink{b, fcomm});
     need(ssp_ctx_attach_host_comm(ctx, size, rank, link_allreduce, link_allgather, link.get()),
@@ -304,11 +298,49 @@ std::shared_ptr<void> attach(ssp_ctx* ctx, int64_t fcomm, const char* transport)
   if (b->allreduce_sum(fcomm, &failed, 1) != 0) throw std::runtime_error("MPI bridge: MPI_Allreduce failed");
   if (failed > 0) throw std::runtime_error("MPI bridge: rank 0 could not create the " + t + " communicator id");
   if (b->bcast(fcomm, id, sizeof(id), 0) != 0) throw std::runtime_error("MPI bridge: MPI_Bcast failed");
-  if (t == "p2p")
-    need(ssp_ctx_attach_p2p(ctx, size, rank, id), "ssp_ctx_attach_p2p");
-  else
-    need(ssp_ctx_attach_comm(ctx, size, rank, id), "ssp_ctx_attach_comm");
+  const int st = t == "p2p" ? ssp_ctx_attach_p2p(ctx, size, rank, id) : ssp_ctx_attach_comm(ctx, size, rank, id);
+  const std::string why = st == SSP_OK ? std::string() : std::string(ssp_last_error());
+  // the attach returns on every rank (joined, refused, or at the deadline): agree on its outcome
+  double nfail = st == SSP_OK ? 0.0 : 1.0;
+  if (b->allreduce_sum(fcomm, &nfail, 1) != 0) throw std::runtime_error("MPI bridge: MPI_Allreduce failed");
+  if (nfail > 0)
+    throw std::runtime_error("MPI bridge: " + std::string(t == "p2p" ? "ssp_ctx_attach_p2p" : "ssp_ctx_attach_comm") +
+                             ": failed on " + std::to_string(int(nfail)) + " rank(s)" + (why.empty() ? "" : ": " + why));
   return nullptr;
+}
+}  // namespace
+
+std::shared_ptr<void> attach(ssp_ctx* ctx, int64_t fcomm, const char* transport) {
+  Bridge* b = bridge();
+  if (!b || !b->active()) throw std::runtime_error("MPI bridge: no initialised MPI library in this process");
+  if (!b->valid(fcomm)) throw std::runtime_error("MPI bridge: " + std::to_string(fcomm) + " is not a communicator");
+  std::string t = transport && *transport ? transport : "";
+  if (t.empty()) {
+    const char* e = std::getenv("ITSOLV_HBM_COMM");
+    t = e && *e ? e : "mpi";
+  }
+  const int size = b->size(fcomm), rank = b->rank(fcomm);
+  if (size < 1 || rank < 0) throw std::runtime_error("MPI bridge: MPI_Comm_size / MPI_Comm_rank failed");
+  // A comma-separated preference list ("rccl,mpi"): the first transport every rank could attach.  A
+  // failed RCCL join leaves this process unable to try RCCL again (SSP_ERR_COMM_ABANDONED), but the
+  // MPI and peer-memory transports attach in the same process.
+  std::vector<std::string> prefs;
+  for (size_t p0 = 0; p0 <= t.size();) {
+    const size_t p1 = std::min(t.find(',', p0), t.size());
+    if (p1 > p0) prefs.push_back(t.substr(p0, p1 - p0));
+    p0 = p1 + 1;
+  }
+  if (prefs.empty()) prefs.push_back("mpi");
+  for (size_t i = 0;; ++i) {
+    try {
+      return attach_one(ctx, b, fcomm, prefs[i], size, rank);
+    } catch (const std::exception& e) {
+      if (i + 1 == prefs.size()) throw;
+      if (rank == 0)
+        std::fprintf(stderr, "[itsolv_hbm] transport %s unavailable (%s); trying %s\n", prefs[i].c_str(), e.what(),
+                     prefs[i + 1].c_str());
+    }
+  }
 }
 
 }  // namespace molpro::linalg::hbm::mpi

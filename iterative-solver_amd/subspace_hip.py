@@ -25,6 +25,7 @@ STATUS = {
     5: "SSP_ERR_COMM",
     6: "SSP_ERR_NOMEM",
     7: "SSP_ERR_UNSUPPORTED",
+    8: "SSP_ERR_COMM_ABANDONED",
 }
 
 # Every symbol include/subspace_hip.h declares (checked by tests/test_boundary.py).

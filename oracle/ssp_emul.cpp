@@ -208,8 +208,19 @@ int ssp_comm_unique_id(char* id) {
   std::memset(id, 0, SSP_UNIQUE_ID_BYTES);
   return SSP_OK;
 }
-int ssp_ctx_attach_comm(ssp_ctx*, int nranks, int, const char*) {
-  return nranks == 1 ? SSP_OK : fail(SSP_ERR_UNSUPPORTED, "emul: no RCCL; use ssp_ctx_attach_host_comm");
+int ssp_ctx_attach_comm(ssp_ctx* c, int nranks, int rank, const char*) {
+  if (nranks == 1) return SSP_OK;
+  // SSP_EMUL_RCCL_JOIN=1 (the fallback rehearsal of tests/test_bench.py): the join "succeeds" with no
+  // exchange behind it -- a caller must replace it (bench.py does, when another rank's join failed)
+  const char* j = std::getenv("SSP_EMUL_RCCL_JOIN");
+  if (j && *j == '1') {
+    c->nranks = nranks;
+    c->rank = rank;
+    c->allreduce = nullptr;
+    c->allgather = nullptr;
+    return SSP_OK;
+  }
+  return fail(SSP_ERR_UNSUPPORTED, "emul: no RCCL; use ssp_ctx_attach_host_comm");
 }
 int ssp_ctx_attach_host_comm(ssp_ctx* c, int nranks, int rank, ssp_host_allreduce_fn ar, ssp_host_allgather_fn ag,
                              void* user) {
@@ -404,9 +415,15 @@ int ssp_transform_gram(ssp_ctx* c, const double* t, double* const* xx, const dou
     }
   }
   if (!gram) return SSP_OK;
+  // one collective of the m (m + 1) / 2 pair dots (a <= b), the layout the device path reduces
+  std::vector<double> pr;
   for (int i = 0; i < m; ++i)
-    for (int j = i; j < m; ++j) gram[size_t(i) * m + j] = gram[size_t(j) * m + i] = dot_n(xx[i], xx[j], n);
-  return reduce(c, gram, size_t(m) * m);
+    for (int j = i; j < m; ++j) pr.push_back(dot_n(xx[i], xx[j], n));
+  const int rc = reduce(c, pr.data(), pr.size());
+  if (rc != SSP_OK) return rc;
+  for (int i = 0, q = 0; i < m; ++i)
+    for (int j = i; j < m; ++j, ++q) gram[size_t(i) * m + j] = gram[size_t(j) * m + i] = pr[size_t(q)];
+  return SSP_OK;
 }
 int ssp_transform_norms(ssp_ctx* c, const double* t, double* const* xx, const double* xs, int m, size_t n,
                         double* norms2) {

@@ -143,6 +143,33 @@ def case_gpu_ops(comm):
         ctx.synthetic_action([xs[0]], [y], 0.1, 3, 11, offset=off)
         ref = oracle.synthetic_action(X[0], 0.1, 3, 11)[off:off + ln]
         assert np.allclose(ctx.download(y), ref, rtol=1e-12, atol=1e-9)
+    # The fused passes' reductions (transform with its pair dots / self-dots, precondition with its
+    # self-dots) on shards either side of exact_max (4097: 2049 / 2048 on 2 ranks) and with a rank
+    # holding no element (n = 1): whichever branch a rank's shard takes, every rank posts a collective
+    # of the same length (a mismatch hangs RCCL or fails the p2p exchange).
+    for n in (1, 4097, 100_003):
+        off, ln = sh.shard_range(n, world, rank)
+        rng = np.random.default_rng(n + 7)
+        m = 3
+        X = rng.uniform(-1, 1, (m, n))
+        dvals = 2.0 + np.arange(n, dtype=np.float64)
+        shift = np.array([0.25, 0.5, 0.75])
+        T = np.eye(m) + 0.1 * rng.uniform(-1, 1, (m, m))
+        up = lambda v: ctx.upload(np.ascontiguousarray(v[off:off + ln]))  # noqa: E731
+        xs = [up(v) for v in X]
+        G = ctx.transform_gram(T, xs)  # x_j <- sum_i t(i, j) x_i, then the Gram matrix
+        Y = T.T @ X
+        assert np.all(np.abs(G - Y @ Y.T) <= 1e-12 * (np.abs(Y) @ np.abs(Y).T) + 1e-300), (n, G)
+        nr = ctx.transform_norms(T, xs)
+        Y = T.T @ Y
+        ref = np.einsum("ij,ij->i", Y, Y)
+        assert np.all(np.abs(nr - ref) <= 1e-12 * ref), (n, nr, ref)
+        pv = [up(v) for v in X]
+        pn = ctx.precondition_norms(pv, up(dvals), shift)
+        P = X / ((dvals[None, :] - shift[:, None]) + 1e-15)
+        ref = np.einsum("ij,ij->i", P, P)
+        assert np.all(np.abs(pn - ref) <= 1e-12 * ref), (n, pn, ref)
+        assert len(set(ctx.allgather_bytes(np.concatenate([G.ravel(), nr, pn]).tobytes()))) == 1
     ctx.close()
 
 

@@ -128,6 +128,24 @@ def test_bench_two_ranks_host_hub():
 
 
 @pytest.mark.gpu
+def test_bench_two_ranks_rccl_refused_falls_back_to_the_host_hub():
+    # the driver's launch with the default --comm rccl, two ranks on the box's one device: RCCL's join
+    # fails (a duplicate device), every rank agrees through the file rendezvous and attaches the host
+    # hub in the same process, and rank 0's line names the transport that produced the value
+    env = dict(os.environ, SSP_COMM_TIMEOUT_S="60")
+    for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--n-global", "4000001", "--no-in-solver"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = parse(r.stdout)
+    assert d["n_gpus"] == 2 and d["comm"] == "host" and d["comm_fallback"]["from"] == "rccl"
+    assert "host-hub" in d["config"]["parallelism"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("comm", ["p2p", "auto"])
 def test_bench_two_ranks_peer_memory(comm):
     # the driver's launch with the peer-memory transport (two ranks on the one device): the attach
@@ -188,3 +206,26 @@ def test_rccl_id_rendezvous_eight_ranks():
     for r, (p, out) in enumerate(zip(procs, outs)):
         assert p.returncode == 0, out[-2000:]
         assert f"uid {r} {want}" in out, out[-2000:]
+
+
+def test_bench_eight_ranks_rccl_join_failure_falls_back_to_the_host_hub():
+    """The driver's 8-GPU launch with the default --comm rccl when one rank's RCCL join fails: every
+    rank learns it through the launcher's file rendezvous and attaches the host hub in the same
+    process, and rank 0 prints one JSON line naming the transport that produced the value.  Over the
+    host emulation, whose RCCL join "succeeds" on the other ranks (SSP_EMUL_RCCL_JOIN=1); rank 3's
+    attach is made to fail (SSP_BENCH_FAIL_RCCL_RANK=3)."""
+    env = dict(os.environ, SSP_EMUL_RCCL_JOIN="1", SSP_BENCH_FAIL_RCCL_RANK="3", SSP_COMM_TIMEOUT_S="60")
+    for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    n = 8 * 12_500 + 5
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "bench_emul.py"), "bench",
+           "--gpus", "8", "--steps", "2", "--warmup", "1", "--ledger-steps", "1", "--n-global", str(n),
+           "--no-in-solver"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = parse(r.stdout)
+    assert d["n_gpus"] == 8 and d["comm"] == "host" and "host-hub" in d["config"]["parallelism"]
+    assert d["comm_fallback"]["from"] == "rccl" and d["comm_fallback"]["failed_ranks"] == [3]
+    assert r.stderr.count("every rank falls back to the host hub") == 8

@@ -156,3 +156,35 @@ def test_precondition_norms(ctx, nvec, n):
         assert np.array_equal(norms, np.diag(g))
     else:
         assert np.all(np.abs(norms - ref) <= 1e-11 * ref)  # a sum of n positive terms in another order
+
+
+# ---- the runner's batched residual norms with more roots than one fused launch holds (16): the batch
+# runs as chunks of 16 (itsolv_capi.cpp residual_norms_batch), and takes the per-root form's values
+CHILD_ROOTS = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+import itsolv_hbm as ih
+import subspace_hip as sh
+with sh.Context(0) as ctx:
+    d = ih.davidson_synthetic(ctx, int(sys.argv[2]), 0.1, 8, 1, solutions=False, nroots=20, max_size_qspace=60,
+                              convergence_threshold=1e-8)
+print(json.dumps({k: (v.tolist() if hasattr(v, "tolist") else v) for k, v in d.items()
+                  if k in ("iterations", "converged", "eigenvalues", "residual_norms")}))
+"""
+
+
+def test_batched_residual_norms_beyond_16_roots():
+    n = 200_003
+    out = []
+    for min_size in (0, 10**15):  # batched (chunks of 16 + 4) / per root
+        env = dict(os.environ, SSP_FUSED_MIN_SIZE=str(min_size))
+        p = subprocess.run([sys.executable, "-c", CHILD_ROOTS, PKG, str(n)], capture_output=True, text=True,
+                           timeout=300, env=env)
+        assert p.returncode == 0, p.stderr[-3000:]
+        out.append(json.loads(p.stdout.strip().splitlines()[-1]))
+    a, b = out
+    assert a["converged"] and b["converged"] and a["iterations"] == b["iterations"], (a["iterations"], b["iterations"])
+    ra, rb = a["residual_norms"][:20], b["residual_norms"][:20]
+    assert all(0 < x <= 1e-6 for x in ra), ra
+    # residuals of converged roots cancel to ~1e-9 of |H x|: the two summation orders agree to that
+    assert all(abs(x - y) <= 1e-3 * y + 1e-13 for x, y in zip(ra, rb)), (ra, rb)

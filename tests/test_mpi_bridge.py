@@ -70,6 +70,14 @@ def test_unusable_transport_fails_every_rank():
     r = mpirun(2, "transport_error", "emul", "unknown transport", env_extra={"ITSOLV_HBM_COMM": "tcp"})
 
 
+def test_transport_preference_list_falls_back_on_every_rank():
+    # "p2p,mpi": the peer-memory attach fails (the emulation shares no device memory), every rank learns
+    # it from the agreed outcome and attaches the MPI transport in the same process; the C-API loops then
+    # take the CPU path's steps with MPICH's sums, bit for bit, as under "mpi"
+    r = mpirun(2, "capi", "emul", env_extra={"ITSOLV_HBM_COMM": "p2p,mpi"})
+    assert "transport p2p unavailable" in r.stderr and "trying mpi" in r.stderr, r.stderr[-2000:]
+
+
 def test_mpich_records_pin_the_association_model():
     # the committed records are reproduced by the restated CPU path under the association model
     # (make_mpi_traces.py re-checks this when it writes them; here without MPI)

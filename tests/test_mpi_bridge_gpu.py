@@ -39,3 +39,10 @@ def test_synthetic_solves_match_mpich_records_on_hbm(transport, nproc):
 def test_rccl_with_two_ranks_on_one_device_is_refused():
     r = mpirun(2, "transport_error", "gpu", "a device per rank", env_extra={"ITSOLV_HBM_COMM": "rccl"})
     assert r.stdout.count("transport_error:") == 2
+
+
+def test_rccl_preference_list_falls_back_to_mpi_on_hbm():
+    # "rccl,mpi" with two ranks on one device: RCCL is refused on every rank (agreed), every rank attaches
+    # the MPI transport in the same process, and the loops take the CPU path's steps bit for bit
+    r = mpirun(2, "capi", "gpu", env_extra={"ITSOLV_HBM_COMM": "rccl,mpi", "SSP_COMM_TIMEOUT_S": "60"}, timeout=900)
+    assert "transport rccl unavailable" in r.stderr and "trying mpi" in r.stderr, r.stderr[-2000:]
