@@ -332,6 +332,7 @@ LedgerScope::LedgerScope(ssp_ctx* ctx, const char* op, double bytes) : ctx_(ctx)
   slot_ = ledger_slot(ctx, op);
   ctx->ledger[slot_].calls += 1;
   ctx->ledger[slot_].bytes += bytes;
+  last_bytes_ = bytes;
   start_ = take_event(ctx);
   if (!start_) return;
   if (ctx->ledger_dispatch) {
@@ -357,6 +358,19 @@ bool LedgerScope::dispatch_events(hipStream_t stream, hipEvent_t* start, hipEven
   *stop = s->stop_;
   s->launched_ = true;
   return true;
+}
+
+void LedgerScope::detail(const std::string& tag) {
+  if (slot_ < 0 || !ctx_->ledger_detail) return;
+  const std::string name = ctx_->ledger[slot_].name + " [" + tag + "]";
+  auto& from = ctx_->ledger[slot_];
+  from.calls -= 1;
+  const double b = last_bytes_;
+  from.bytes -= b;
+  const int to = ledger_slot(ctx_, name.c_str());
+  ctx_->ledger[to].calls += 1;
+  ctx_->ledger[to].bytes += b;
+  slot_ = to;
 }
 
 LedgerScope::~LedgerScope() {
@@ -452,6 +466,7 @@ int ssp_ctx_create(int device, ssp_ctx** out) {
   if (const char* ex = std::getenv("SSP_EXACT_MAX")) ctx->exact_max = size_t(std::strtoull(ex, nullptr, 10));
   if (const char* ip = std::getenv("SSP_INNER_PER_CU")) ctx->inner_per_cu = std::max(1, std::atoi(ip));
   if (const char* lt = std::getenv("SSP_LEDGER_TIMING")) ctx->ledger_dispatch = std::string(lt) == "dispatch";
+  ctx->ledger_detail = std::getenv("SSP_LEDGER_DETAIL") != nullptr;
   if (const char* ss = std::getenv("SSP_SYNTH_SHAPE")) {
     ctx->synth_stride = std::string(ss) == "stride";
     ctx->synth_window = std::string(ss) == "window";

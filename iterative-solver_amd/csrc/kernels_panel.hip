@@ -17,6 +17,7 @@
 // through LDS, workgroups by a fixed-order second pass (ssp::launch_reduce_partials): bitwise
 // reproducible, and identical on every rank after the RCCL allreduce.
 #include <algorithm>
+#include <cstdio>
 #include <cstddef>
 #include <cstdlib>
 #include <vector>
@@ -1264,6 +1265,14 @@ int launch_outer(ssp_ctx* ctx, const OuterArgs& a) {
   return SSP_OK;
 }
 
+// SSP_LEDGER_DETAIL tags: the kernel instance and the panel's shape
+int ng_inst(int need) { return need <= 4 ? need : need <= 6 ? 6 : need <= 8 ? 8 : need <= 12 ? 12 : 16; }
+std::string shape_tag(const char* kind, int a, int b, int c, int d, bool sc) {
+  char t[96];
+  std::snprintf(t, sizeof(t), "%s<%d,%d> %dx%d%s", kind, a, b, c, d, sc ? " sc" : "");
+  return t;
+}
+
 bool any_scaled(const double* s, int n) {
   for (int i = 0; s && i < n; ++i)
     if (s[i] != 1.0) return true;
@@ -1371,6 +1380,7 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
         const unsigned grid = inner_grid(ctx, n);
         SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * m * m));
         a.partial = ctx->partial;
+        ls.detail(shape_tag("sym", (m + 3) / 4, (m + 3) / 4, m, m, sc));
         SSP_TRY(launch_inner_sym(ctx, a, grid, sc));
         SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), m, m, ctx->result_dev, m, 0, 0, &tail, true));
       }
@@ -1394,6 +1404,8 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
           const unsigned grid = inner_grid(ctx, n);
           SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * a.m * a.k));
           a.partial = ctx->partial;
+          if (r0 == 0 && c0 == 0)
+            ls.detail(shape_tag("mfma", (a.m + 3) / 4, ng_inst((a.k + 3) / 4), a.m, a.k, sc_launch));
           SSP_TRY(launch_inner(ctx, a, grid, sc_launch));
           const bool last = r0 + ssp::kInnerRows >= R && c0 + cols_per_launch >= C;
           SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), a.m, a.k, ctx->result_dev, C, r0, c0, &tail,
@@ -1475,6 +1487,10 @@ int gemm_outer_impl(ssp_ctx* ctx, const double* alphas, const double* const* xx,
         a.alpha_dev = static_cast<const double*>(p);
       }
       SSP_TRY(ssp::flush_uploads(ctx));
+      if (j0 == 0 && i0 == 0) {
+        const int mi = a.m <= 1 ? 1 : a.m <= 2 ? 2 : a.m <= 4 ? 4 : a.m <= 8 ? 8 : 16;
+        ls.detail(shape_tag(dev ? "dev" : "arg", mi, a.set, a.k, mm, a.scale_dev != nullptr));
+      }
       SSP_TRY(launch_outer(ctx, a));
     }
   }
@@ -1811,6 +1827,7 @@ int transform_impl(ssp_ctx* ctx, const double* t, double* const* xx, const doubl
       a.partial = ctx->partial;
       if (!pass) a.tail = tail;  // else the kernel leaves its partials to the reduce pass below
     }
+    ls.detail(shape_tag("transform", m, fused, m, m, xs != nullptr));
     launch_transform(ctx, m, grid, a, fused, exact, pass);
     SSP_TRY_HIP(hipGetLastError());
     if (pass)  // one workgroup per pair dot, publishing to the host (as the gemm_inner panels)

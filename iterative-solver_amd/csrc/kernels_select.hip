@@ -15,6 +15,9 @@
 //     one compaction pass then collects them.
 //  2. Each workgroup sorts a tile of up to 2048 candidates in LDS with a bitonic network
 //     (descending) and keeps its best n; levels repeat until one tile remains.
+//  1'. For n <= 16 (the solvers' selections: nroots, max_p) one pass instead: each thread keeps its
+//     best K in registers, each wave merges its lanes' lists by shuffles and writes its K best
+//     (k_select_local) -- no host round trip per digit.
 // Ranks then all-gather their local best n and every rank merges the same candidate set with the
 // same order on the host (deterministic, identical on all ranks).
 #include <algorithm>
@@ -230,6 +233,62 @@ __global__ __launch_bounds__(kBlock) void k_radix_compact(const RadixArgs a, siz
   });
 }
 
+// Single pass for a small n (nsel <= K <= 16; the solvers select nroots and max_p elements): every
+// thread keeps its K best composites in registers, sorted, while it streams its elements (radix_stream's
+// order); the wave then merges its 64 lists through lane shuffles -- the K best of two sorted lists are
+// the elementwise better of one and the other reversed (a bitonic sequence), sorted by a bitonic
+// clean-up -- and writes its K best.  One read of the shard and no host round trip before the tile
+// levels, where the radix path needs a histogram pass, a host decision per digit and a compaction pass.
+constexpr size_t kLocalMaxK = 16;
+
+template <int K>
+__device__ __forceinline__ void cand_cswap(Cand& a, Cand& b) {  // a <- better, b <- worse
+  const bool sw = better(b, a);
+  const Cand x = a, y = b;
+  a = sw ? y : x;
+  b = sw ? x : y;
+}
+
+template <int K>
+__device__ __forceinline__ void cand_insert(Cand (&L)[K], Cand c) {
+  if (!better(c, L[K - 1])) return;
+  L[K - 1] = c;
+#pragma unroll
+  for (int j = K - 1; j > 0; --j) cand_cswap<K>(L[j - 1], L[j]);
+}
+
+template <int MODE, int K>
+__global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size_t offset, Cand* out) {
+  Cand L[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) L[j] = Cand{0ull, 0ull};  // sorts after every real candidate
+  radix_stream<MODE>(a, [&](unsigned long long key, unsigned long long i, bool ok) {
+    if (ok) cand_insert<K>(L, Cand{key, offset + i});
+  });
+  // wave merge: after the round with lane distance d, every lane holds the K best of its 2d-lane group
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    Cand P[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      P[j].key = __shfl_xor(L[j].key, d, 64);
+      P[j].idx = __shfl_xor(L[j].idx, d, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) L[j] = better(L[j], P[K - 1 - j]) ? L[j] : P[K - 1 - j];
+#pragma unroll
+    for (int h = K / 2; h > 0; h >>= 1)
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if ((j & h) == 0) cand_cswap<K>(L[j], L[j + h]);
+  }
+  if (__lane_id() == 0) {
+    Cand* o = out + (size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6)) * K;
+#pragma unroll
+    for (int j = 0; j < K; ++j) o[j] = L[j];
+  }
+}
+
 // Fixes digits of the composite threshold until at most kRadixCap elements lie at or above it,
 // then compacts them into `cand`; returns their number in *count.
 int radix_candidates(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t n, size_t offset,
@@ -353,7 +412,27 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
     SelectArgs a{};
     a.keep = keep;
     a.out = buf0;
-    if (radix) {
+    if (radix && nsel <= kLocalMaxK) {
+      // one pass: each wave's K best (K = 8 or 16 >= nsel) into `cand`, grid * 4 * K <= kRadixCap
+      RadixArgs r{};
+      r.x = x;
+      r.y = y;
+      r.n = n;
+      r.neg = !max;
+      r.abs = ignore_sign;
+      const unsigned lgrid = std::min<unsigned>(grid, unsigned(kRadixCap / (4 * kLocalMaxK)));
+      const int K = nsel <= 8 ? 8 : 16;
+      if (mode == 1 && K == 8) SSP_LAUNCH((k_select_local<1, 8>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand);
+      else if (mode == 1) SSP_LAUNCH((k_select_local<1, 16>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand);
+      else if (K == 8) SSP_LAUNCH((k_select_local<0, 8>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand);
+      else SSP_LAUNCH((k_select_local<0, 16>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand);
+      SSP_TRY_HIP(hipGetLastError());
+      count = size_t(lgrid) * (kBlock / 64) * size_t(K);
+      tiles = (count + kTile - 1) / kTile;
+      a.in = cand;
+      a.count = count;
+      a.mode = 2;
+    } else if (radix) {
       SSP_TRY(radix_candidates(ctx, mode, x, y, n, offset, nsel, max, ignore_sign, cand, hist, counter, grid, &count));
       tiles = (count + kTile - 1) / kTile;
       a.in = cand;

@@ -37,6 +37,7 @@ struct ssp_ctx {
   int inner_per_cu = 4;        // gemm_inner workgroups per CU (SSP_INNER_PER_CU: the A/B knob of tools/ab_inner.py)
   bool synth_stride = false;  // SSP_SYNTH_SHAPE=stride: the synthetic apply kernel grid-strided (A/B)
   bool ledger_dispatch = false;  // SSP_LEDGER_TIMING=dispatch (LedgerScope)
+  bool ledger_detail = false;    // SSP_LEDGER_DETAIL: per-instance ledger rows (LedgerScope::detail)
   bool synth_window = false;  // SSP_SYNTH_SHAPE=window: the synthetic apply kernel in the window shape (A/B)
   // Shape of the 1 x 1 / 1 x 2 gemm_inner row kernel: window (default) or, with SSP_ROW_SHAPE=stride
   // in the environment at context creation, the round-2 grid-stride shape (A/B: tools/row_shape_ab.py).
@@ -193,6 +194,9 @@ class LedgerScope {
   ~LedgerScope();
   LedgerScope(const LedgerScope&) = delete;
   LedgerScope& operator=(const LedgerScope&) = delete;
+  // SSP_LEDGER_DETAIL (read at context creation): the op's call and bytes move to the entry
+  // "<op> [tag]" -- per-instance ledger rows (kernel shape) for the development tools
+  void detail(const std::string& tag);
   // dispatch timing: the events for the next kernel launched on this thread inside an open scope, when
   // it is launched on that scope's context stream
   static bool dispatch_events(hipStream_t stream, hipEvent_t* start, hipEvent_t* stop);
@@ -203,6 +207,7 @@ class LedgerScope {
   hipEvent_t start_ = nullptr;
   hipEvent_t stop_ = nullptr;  // dispatch timing
   bool launched_ = false;
+  double last_bytes_ = 0;
   LedgerScope* prev_ = nullptr;
 };
 

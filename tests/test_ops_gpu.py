@@ -341,9 +341,10 @@ def test_select_bit_exact(ctx, n, nsel, mode):
     assert np.array_equal(val, rval)
 
 
-# Shards above kRadixMin (2^17) take the radix-threshold path (kernels_select.hip): distributions
-# that end the digit search early (spread values), late (narrow ranges, heavy ties -> index digits)
-# and in the index phase (constant vectors), with signed zeros and a shard offset.
+# Shards above kRadixMin (2^17) take the one-pass register path for n <= 16 (k_select_local: K = 8
+# for n <= 8, else 16) and the radix-threshold path above (kernels_select.hip): distributions that end
+# the digit search early (spread values), late (narrow ranges, heavy ties -> index digits) and in the
+# index phase (constant vectors), with signed zeros and a shard offset.
 def _radix_inputs(n, r):
     return {
         "uniform": r.uniform(-1, 1, n),
@@ -356,7 +357,7 @@ def _radix_inputs(n, r):
 
 
 @pytest.mark.parametrize("kind", ["uniform", "narrow", "ties", "constant", "zeros", "diag"])
-@pytest.mark.parametrize("nsel", [1, 16, 1024])
+@pytest.mark.parametrize("nsel", [1, 8, 9, 16, 17, 1024])
 @pytest.mark.parametrize("mode", [(False, False), (True, False), (False, True), (True, True)])
 def test_select_radix_path_bit_exact(ctx, kind, nsel, mode):
     n = 300_007
@@ -368,22 +369,24 @@ def test_select_radix_path_bit_exact(ctx, kind, nsel, mode):
     assert np.array_equal(val, rval) and np.array_equal(np.signbit(val), np.signbit(rval))
 
 
-def test_select_radix_path_offset_and_large(ctx):
+@pytest.mark.parametrize("nsel", [16, 100])
+def test_select_radix_path_offset_and_large(ctx, nsel):
     n, off = 5_000_011, 123_456_789
     x = rng(5).uniform(-1, 1, n)
-    idx, val = ctx.select(ctx.upload(x), 100, offset=off)
-    ridx, rval = oracle.select(x, 100)
+    idx, val = ctx.select(ctx.upload(x), nsel, offset=off)
+    ridx, rval = oracle.select(x, nsel)
     assert idx.tolist() == (ridx + off).tolist() and np.array_equal(val, rval)
 
 
 @pytest.mark.parametrize("kind", ["uniform", "ties", "constant"])
-def test_select_max_dot_radix_path(ctx, kind):
+@pytest.mark.parametrize("nsel", [5, 16, 37])
+def test_select_max_dot_radix_path(ctx, kind, nsel):
     n = 400_003
     r = rng(9)
     x = _radix_inputs(n, r)[kind]
     y = np.round(r.uniform(-3, 3, n))
-    idx, val = ctx.select_max_dot(ctx.upload(x), ctx.upload(y), 37)
-    ridx, rval = oracle.select_max_dot(x, y, 37)
+    idx, val = ctx.select_max_dot(ctx.upload(x), ctx.upload(y), nsel)
+    ridx, rval = oracle.select_max_dot(x, y, nsel)
     assert idx.tolist() == ridx.tolist() and np.array_equal(val, rval)
 
 
