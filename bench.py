@@ -384,6 +384,8 @@ def in_solver(ctx, n_global, world, barrier, repeat=3, kind="davidson"):
         ctx.synchronize()
         walls.append(allmax(time.perf_counter() - t0))
         ctx.ledger_enable(False)
+        if rep == repeat - 2:
+            ha = r["host_algebra"]  # the warm solve's host subspace algebra
     led = ctx.ledger()
     ms = sum(v["ms"] for v in led.values())
     nb = sum(v["bytes"] for v in led.values())
@@ -416,6 +418,10 @@ def in_solver(ctx, n_global, world, barrier, repeat=3, kind="davidson"):
         "wall_s_cold": round(walls[0], 4),
         "wall_s_ledger_on": round(walls[-1], 4),
         "idle_frac_of_wall": round((walls[-2] - ms / 1e3) / walls[-2], 4),
+        # of that idle: the host's subspace algebra (eigenproblem / svd_system / solve_DIIS, dense.h)
+        "host_algebra_ms_rank0": round(1e3 * ha["seconds"], 3),
+        "host_algebra_calls": ha["calls"],
+        "host_algebra_max_dim": ha["max_dim"],
         "kernel_ms_rank0": round(ms, 3),
         "algorithmic_GB_rank0": round(nb / 1e9, 2),
         "kernel_GBs_rank0": round(nb / (ms / 1e3) / 1e9, 1) if ms else None,

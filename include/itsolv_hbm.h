@@ -71,6 +71,12 @@ typedef struct {
   int redundant_params;
   int null_params;
   int trace_screened[ITSOLV_TRACE_ITER];
+  /* host time of the subspace algebra (extension, instrumentation): wall seconds, calls and the
+   * largest dimension of the eigenproblem / svd_system / solve_DIIS / solve_LinearEquations calls
+   * of the solve (itsolv_hbm/dense.h AlgebraClock) */
+  double host_algebra_seconds;
+  int host_algebra_calls;
+  int host_algebra_max_dim;
 } itsolv_result;
 
 const char* itsolv_last_error(void);

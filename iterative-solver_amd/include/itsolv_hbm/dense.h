@@ -16,6 +16,7 @@
 // a Hessenberg-QR eigensolver; those paths are only exercised by the non-hermitian tests.
 #pragma once
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <complex>
 #include <limits>
@@ -35,6 +36,40 @@ struct SVD {
 };
 
 namespace dense {
+
+// Host time of the subspace algebra (instrumentation only): the outermost eigenproblem /
+// svd_system / solve_DIIS / solve_LinearEquations call of this thread adds its wall time, its
+// count and its dimension; run_davidson / run_diis reset it per solve and report it in
+// itsolv_result.host_algebra_*.  Two clock reads per call.
+struct AlgebraClock {
+  static inline thread_local double seconds = 0;
+  static inline thread_local int calls = 0;
+  static inline thread_local int depth = 0;
+  static inline thread_local size_t max_dim = 0;
+  static void reset() { seconds = 0, calls = 0, depth = 0, max_dim = 0; }
+};
+class AlgebraScope {
+ public:
+  explicit AlgebraScope(size_t dim) : m_outer(AlgebraClock::depth++ == 0) {
+    if (m_outer) {
+      m_t0 = std::chrono::steady_clock::now();
+      AlgebraClock::max_dim = std::max(AlgebraClock::max_dim, dim);
+    }
+  }
+  ~AlgebraScope() {
+    --AlgebraClock::depth;
+    if (m_outer) {
+      AlgebraClock::seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - m_t0).count();
+      ++AlgebraClock::calls;
+    }
+  }
+  AlgebraScope(const AlgebraScope&) = delete;
+  AlgebraScope& operator=(const AlgebraScope&) = delete;
+
+ private:
+  bool m_outer;
+  std::chrono::steady_clock::time_point m_t0;
+};
 
 // Symmetric eigen-decomposition of the n x n matrix a (either storage order: only the symmetric
 // part is used).  On return evals is ascending and column i of evecs (evecs[j + n*i]) is the
@@ -428,6 +463,7 @@ size_t get_rank(const std::list<SVD<value_type>>& svds, value_type threshold) {
 // m is row-major nrows x ncols.
 inline std::list<SVD<double>> svd_system(size_t nrows, size_t ncols, const std::vector<double>& m, double threshold,
                                          bool hermitian = false, bool reduce_to_rank = false) {
+  dense::AlgebraScope clock_(std::max(nrows, ncols));
   std::list<SVD<double>> svds;
   if (m.empty()) return svds;
   if (hermitian) {
@@ -464,6 +500,7 @@ inline std::list<SVD<double>> svd_system(size_t nrows, size_t ncols, const std::
 inline void eigenproblem(std::vector<double>& eigenvectors, std::vector<double>& eigenvalues,
                          const std::vector<double>& matrix, const std::vector<double>& metric, size_t dimension,
                          bool hermitian, double svdThreshold, int verbosity, bool condone_complex) {
+  dense::AlgebraScope clock_(dimension);
   using cd = std::complex<double>;
   const size_t n = dimension;
   std::vector<double> H(n * n);  // column-major copy of the row-major input
@@ -704,6 +741,7 @@ inline void householder_qr_solve(size_t n, std::vector<double> A, std::vector<do
 // DIIS extrapolation coefficients (reference :619-669).  matrix: column-major dimension^2.
 inline void solve_DIIS(std::vector<double>& solution, const std::vector<double>& matrix, const size_t dimension,
                        double svdThreshold, int verbosity = 0) {
+  dense::AlgebraScope clock_(dimension);
   const size_t na = dimension + 1;
   std::vector<double> B(na * na, 0.0), rhs(na, 0.0);
   for (size_t i = 0; i < dimension; ++i)
@@ -739,6 +777,7 @@ inline void solve_LinearEquations(std::vector<double>& solution, std::vector<dou
                                   const std::vector<double>& matrix, const std::vector<double>& metric,
                                   const std::vector<double>& rhs, const size_t dimension, size_t nroot,
                                   double augmented_hessian, double svdThreshold, int verbosity) {
+  dense::AlgebraScope clock_(dimension);
   const size_t nX = dimension;
   solution.assign(nX * nroot, 0.0);
   if (augmented_hessian > 0) {

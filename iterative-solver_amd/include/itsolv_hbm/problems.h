@@ -181,9 +181,13 @@ void run_davidson(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Proble
   }
   out.n_eig_trace = 0;
   solver.iteration_hook = [&] { record_trace(solver, solver.eigenvalues(), out); };
+  dense::AlgebraClock::reset();
   const auto t0 = std::chrono::steady_clock::now();
   out.converged = solver.solve(params, actions, problem, o.generate_initial_guess != 0);
   out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  out.host_algebra_seconds = dense::AlgebraClock::seconds;
+  out.host_algebra_calls = dense::AlgebraClock::calls;
+  out.host_algebra_max_dim = int(dense::AlgebraClock::max_dim);
   const auto& st = solver.statistics();
   out.iterations = st.iterations;
   out.r_creations = st.r_creations;
@@ -248,9 +252,13 @@ void run_linear_equations(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, cons
   }
   out.n_eig_trace = 0;
   solver.iteration_hook = [&] { record_trace(solver, std::vector<double>{}, out); };
+  dense::AlgebraClock::reset();
   const auto t0 = std::chrono::steady_clock::now();
   out.converged = solver.solve(params, actions, problem, o.generate_initial_guess != 0);
   out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  out.host_algebra_seconds = dense::AlgebraClock::seconds;
+  out.host_algebra_calls = dense::AlgebraClock::calls;
+  out.host_algebra_max_dim = int(dense::AlgebraClock::max_dim);
   const auto& st = solver.statistics();
   out.iterations = st.iterations;
   out.r_creations = st.r_creations;
@@ -294,9 +302,13 @@ void run_optimize(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Proble
   init(x);
   out.n_eig_trace = 0;
   solver->iteration_hook = [&] { record_trace(*solver, std::vector<double>{solver->value()}, out); };
+  dense::AlgebraClock::reset();
   const auto t0 = std::chrono::steady_clock::now();
   out.converged = solver->solve(x, g, problem);
   out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  out.host_algebra_seconds = dense::AlgebraClock::seconds;
+  out.host_algebra_calls = dense::AlgebraClock::calls;
+  out.host_algebra_max_dim = int(dense::AlgebraClock::max_dim);
   const auto& st = solver->statistics();
   out.iterations = st.iterations;
   out.r_creations = st.r_creations;
@@ -328,9 +340,13 @@ void run_diis(std::shared_ptr<ArrayHandlers<R, Q, P>> handlers, const Problem<R,
   init(x);
   out.n_eig_trace = 0;
   solver.iteration_hook = [&] { record_trace(solver, std::vector<double>{}, out); };
+  dense::AlgebraClock::reset();
   const auto t0 = std::chrono::steady_clock::now();
   out.converged = solver.solve(x, g, problem);
   out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  out.host_algebra_seconds = dense::AlgebraClock::seconds;
+  out.host_algebra_calls = dense::AlgebraClock::calls;
+  out.host_algebra_max_dim = int(dense::AlgebraClock::max_dim);
   const auto& st = solver.statistics();
   out.iterations = st.iterations;
   out.r_creations = st.r_creations;

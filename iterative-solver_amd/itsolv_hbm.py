@@ -78,6 +78,9 @@ class Result(C.Structure):
         ("redundant_params", C.c_int),
         ("null_params", C.c_int),
         ("trace_screened", C.c_int * TRACE_ITER),
+        ("host_algebra_seconds", C.c_double),
+        ("host_algebra_calls", C.c_int),
+        ("host_algebra_max_dim", C.c_int),
     ]
 
     def as_dict(self):
@@ -93,6 +96,8 @@ class Result(C.Structure):
             "errors": np.array(self.errors[:k]),
             "residual_norms": np.array(self.residual_norms[:k]),
             "seconds": self.seconds,
+            "host_algebra": {"seconds": self.host_algebra_seconds, "calls": self.host_algebra_calls,
+                             "max_dim": self.host_algebra_max_dim},
             "eig_trace": np.array(self.eig_trace[: self.n_eig_trace]),
             "trace": self.trace(),
         }

@@ -50,7 +50,7 @@ def run(ctx, name, repeat=2):
         cold = run_once(ctx, name)["wall_s"]
     out = run_once(ctx, name)
     out["wall_s_cold"] = cold
-    print(json.dumps({k: out[k] for k in ("config", "iterations", "wall_s", "wall_s_cold", "kernel_ms", "kernel_GBs", "reductions_per_iteration", "host_overhead_ms",
+    print(json.dumps({k: out[k] for k in ("config", "iterations", "wall_s", "wall_s_cold", "kernel_ms", "kernel_GBs", "reductions_per_iteration", "host_overhead_ms", "host_algebra",
                                             "wall_GBs")}), flush=True)
     return out
 
@@ -82,7 +82,9 @@ def run_once(ctx, name):
            "reductions_per_iteration": round(sum(v["calls"] for op, v in led.items() if op.split("(")[0] in REDUCING)
                                              / max(1, r["iterations"]), 1),
            "launches_per_iteration": round(sum(v["calls"] for v in led.values()) / max(1, r["iterations"]), 1),
-           "host_overhead_ms": round(1e3 * wall - ms, 2)}
+           "host_overhead_ms": round(1e3 * wall - ms, 2),
+           "host_algebra": {"ms": round(1e3 * r["host_algebra"]["seconds"], 3), "calls": r["host_algebra"]["calls"],
+                            "max_dim": r["host_algebra"]["max_dim"]}}
     if solver == "davidson":
         out["eigenvalues"] = [float(e) for e in r["eigenvalues"]]
     return out
