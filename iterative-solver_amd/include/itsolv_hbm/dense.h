@@ -71,6 +71,37 @@ class AlgebraScope {
   std::chrono::steady_clock::time_point m_t0;
 };
 
+// True when every eigenvalue that sym_eigen would compute for the symmetric n x n matrix a (row-major,
+// either triangle) is certainly above `thresh`: the Cholesky factorisation of a - tau I runs to the
+// end with positive pivots, tau = thresh + margin.  A factorisation that succeeds in floating point
+// proves lambda_min(a) > tau - (n + 1) eps max_i a_ii (its backward error), and sym_eigen's
+// eigenvalues lie within a small multiple of n eps ||a||_F of the exact ones (backward-stable
+// Householder + QL); margin = 1e3 n eps ||a||_F covers both with room to spare.  A false return
+// only means "not proven" (near-null directions, NaN, n = 0): the caller then decomposes.  O(n^3 / 6),
+// against O(9 n^3) for the decomposition it lets the redundancy screen skip.
+inline bool eigenvalues_exceed(size_t n, const std::vector<double>& a, double thresh) {
+  if (n == 0 || a.size() < n * n) return false;
+  AlgebraScope clock_(n);
+  double fro = 0;
+  for (size_t i = 0; i < n * n; ++i) fro += a[i] * a[i];
+  fro = std::sqrt(fro);
+  if (!(fro < std::numeric_limits<double>::infinity())) return false;
+  const double tau = std::max(thresh, 0.0) + 1e3 * double(n) * std::numeric_limits<double>::epsilon() * fro;
+  std::vector<double> L(n * n, 0.0);  // lower triangle, row-major
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j <= i; ++j) {
+      double s = 0.5 * (a[i * n + j] + a[j * n + i]) - (i == j ? tau : 0.0);
+      for (size_t k = 0; k < j; ++k) s -= L[i * n + k] * L[j * n + k];
+      if (i == j) {
+        if (!(s > 0)) return false;
+        L[i * n + i] = std::sqrt(s);
+      } else {
+        L[i * n + j] = s / L[j * n + j];
+      }
+    }
+  return true;
+}
+
 // Symmetric eigen-decomposition of the n x n matrix a (either storage order: only the symmetric
 // part is used).  On return evals is ascending and column i of evecs (evecs[j + n*i]) is the
 // unit eigenvector of evals[i].

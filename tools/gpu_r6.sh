@@ -1,0 +1,67 @@
+#!/bin/bash
+# Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
+# host algebra clock), and a kernel trace of the C4-shard solve.
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,seltests,gputests
+# Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
+# the session.
+set -u -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${SESSION:-r6}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+(while sleep 50; do echo "[heartbeat $(date +%T)]"; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+step() {
+  local name=$1 t=$2
+  shift 2
+  echo "== $name (limit ${t}s): $*"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  tail -3 "$OUT/$name.log"
+  echo "== $name rc=$rc"
+  return $rc
+}
+for s in ${1//,/ }; do
+  case $s in
+    bench)
+      step bench 600 python -u bench.py || exit $?
+      grep '^{' "$OUT/bench.log" > "$OUT/bench.json" || true
+      ;;
+    c4ledger)
+      SSP_LEDGER_DETAIL=1 step c4ledger 300 python -u tools/solver_ledger.py --configs C4-shard,C3,C5 \
+        --out "$OUT/c4_ledger.json" || exit $?
+      ;;
+    c4pipe2)
+      SSP_INNER_PIPE=2 SSP_LEDGER_DETAIL=1 step c4pipe2 300 python -u tools/solver_ledger.py --configs C4-shard \
+        --out "$OUT/c4_ledger_pipe2.json" || exit $?
+      ;;
+    seltests)
+      step seltests 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu -k "select" \
+        tests/test_ops_gpu.py tests/test_fullsize_gpu.py tests/test_distributed_gpu.py tests/test_rccl_gpu.py || exit $?
+      ;;
+    gputests)
+      step gputests 1500 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests || exit $?
+      ;;
+    c4trace)
+      rm -rf "$OUT/c4trace"
+      step c4trace 300 rocprofv3 --kernel-trace -d "$OUT/c4trace" -o run --output-format csv -- \
+        python3 tools/trace_c4.py || exit $?
+      ;;
+    c4hiptrace)
+      rm -rf "$OUT/c4hiptrace"
+      step c4hiptrace 300 rocprofv3 --kernel-trace --hip-runtime-trace -d "$OUT/c4hiptrace" -o run --output-format csv -- \
+        python3 tools/trace_c4.py || exit $?
+      ;;
+    c4prof)
+      rm -rf "$OUT/c4prof"
+      step c4prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/c4prof" -o run --output-format csv -- \
+        python3 tools/solver_ledger.py --configs C4-shard --out "$OUT/c4prof_ledger.json" || exit $?
+      ;;
+    *)
+      echo "unknown step $s"
+      exit 2
+      ;;
+  esac
+done
+echo "session done"
