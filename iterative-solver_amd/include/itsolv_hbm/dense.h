@@ -102,6 +102,48 @@ inline bool eigenvalues_exceed(size_t n, const std::vector<double>& a, double th
   return true;
 }
 
+// C = A B (column-major; A M x K, lda; B K x N, ldb; C M x N, ldc), each element the sum over
+// l = 0..K-1 in order of the rounded products A[i,l] B[l,j] -- the numbers of the plain triple loop
+// (with -ffp-contract=off, as every host build here is) -- in 8 x 4 register tiles: the same
+// operations per element, several elements per instruction.
+inline void ordered_gemm(size_t M, size_t N, size_t K, const double* A, size_t lda, const double* B, size_t ldb,
+                         double* C, size_t ldc) {
+  typedef double v4d __attribute__((vector_size(32), aligned(8), may_alias));
+  size_t j = 0;
+  for (; j + 4 <= N; j += 4) {
+    size_t i = 0;
+    for (; i + 8 <= M; i += 8) {
+      v4d c[4][2] = {};
+      const double* b = B + ldb * j;
+      for (size_t l = 0; l < K; ++l) {
+        const double* a = A + lda * l + i;
+        const v4d a0 = *reinterpret_cast<const v4d*>(a), a1 = *reinterpret_cast<const v4d*>(a + 4);
+        for (int q = 0; q < 4; ++q) {
+          const double bq = b[l + ldb * size_t(q)];
+          c[q][0] = c[q][0] + a0 * bq;
+          c[q][1] = c[q][1] + a1 * bq;
+        }
+      }
+      for (int q = 0; q < 4; ++q) {
+        *reinterpret_cast<v4d*>(C + i + ldc * (j + size_t(q))) = c[q][0];
+        *reinterpret_cast<v4d*>(C + i + 4 + ldc * (j + size_t(q))) = c[q][1];
+      }
+    }
+    for (; i < M; ++i)
+      for (size_t q = 0; q < 4; ++q) {
+        double s = 0;
+        for (size_t l = 0; l < K; ++l) s += A[i + lda * l] * B[l + ldb * (j + q)];
+        C[i + ldc * (j + q)] = s;
+      }
+  }
+  for (; j < N; ++j)
+    for (size_t i = 0; i < M; ++i) {
+      double s = 0;
+      for (size_t l = 0; l < K; ++l) s += A[i + lda * l] * B[l + ldb * j];
+      C[i + ldc * j] = s;
+    }
+}
+
 // Symmetric eigen-decomposition of the n x n matrix a (either storage order: only the symmetric
 // part is used).  On return evals is ascending and column i of evecs (evecs[j + n*i]) is the
 // unit eigenvector of evals[i].
@@ -527,10 +569,13 @@ inline std::list<SVD<double>> svd_system(size_t nrows, size_t ncols, const std::
 
 // Generalised eigenproblem H c = e S c of the subspace (reference :318-543).  matrix (H) is
 // row-major, metric (S) is read column-major as the reference's Eigen::Map does (S is symmetric in
-// the hermitian case).  eigenvectors: column-major dimension x nsol (column k = root k).
+// the hermitian case).  eigenvectors: column-major dimension x nsol (column k = root k).  nvec
+// (hermitian case): only the eigenvectors of the nvec lowest roots are formed (the Davidson solver
+// keeps nroots of them; eigenvalues are returned for every root).
 inline void eigenproblem(std::vector<double>& eigenvectors, std::vector<double>& eigenvalues,
                          const std::vector<double>& matrix, const std::vector<double>& metric, size_t dimension,
-                         bool hermitian, double svdThreshold, int verbosity, bool condone_complex) {
+                         bool hermitian, double svdThreshold, int verbosity, bool condone_complex,
+                         size_t nvec = std::numeric_limits<size_t>::max()) {
   dense::AlgebraScope clock_(dimension);
   using cd = std::complex<double>;
   const size_t n = dimension;
@@ -553,61 +598,51 @@ inline void eigenproblem(std::vector<double>& eigenvectors, std::vector<double>&
   }
   std::vector<double> svmh(rank);
   for (size_t k = 0; k < rank; ++k) svmh[k] = sing[k] > 1e-14 ? 1 / std::sqrt(sing[k]) : 0;
-  // Hbar = diag(svmh) U_r^T H V_r diag(svmh)  (rank x rank, column-major).  HV[i,j] accumulates
-  // H[i,l] V[l,j] over l = 0..n-1 in order for every i at once (unit stride in i).
-  std::vector<double> HV(n * rank, 0.0);
-  for (size_t j = 0; j < rank; ++j) {
-    double* hv = &HV[n * j];
-    for (size_t l = 0; l < n; ++l) {
-      const double vlj = V[l + n * j];
-      const double* hl = &H[n * l];
-      for (size_t i = 0; i < n; ++i) hv[i] += hl[i] * vlj;
-    }
-  }
-  // Hbar[i,j] = svmh[i] (sum_l U[l,i] HV[l,j], l in order) svmh[j]: U_r transposed once so that the
-  // sums of one column j advance together over l (unit stride in i).
-  std::vector<double> Hbar(rank * rank, 0.0), Ut(n * rank), acc(rank);
+  // Hbar = diag(svmh) U_r^T H V_r diag(svmh)  (rank x rank, column-major): HV[i,j] = sum_l H[i,l]
+  // V[l,j] and then Hbar[i,j] = svmh[i] (sum_l U[l,i] HV[l,j]) svmh[j], every sum over l = 0..n-1 in
+  // order (ordered_gemm).
+  std::vector<double> HV(n * rank);
+  dense::ordered_gemm(n, rank, n, H.data(), n, V.data(), n, HV.data(), n);
+  std::vector<double> Hbar(rank * rank), Ut(n * rank);
   for (size_t i = 0; i < rank; ++i)
     for (size_t l = 0; l < n; ++l) Ut[l * rank + i] = U[l + n * i];
-  for (size_t j = 0; j < rank; ++j) {
-    std::fill(acc.begin(), acc.end(), 0.0);
-    for (size_t l = 0; l < n; ++l) {
-      const double hv = HV[l + n * j];
-      const double* ul = &Ut[l * rank];
-      for (size_t i = 0; i < rank; ++i) acc[i] += ul[i] * hv;
-    }
-    for (size_t i = 0; i < rank; ++i) Hbar[i + rank * j] = svmh[i] * acc[i] * svmh[j];
-  }
+  dense::ordered_gemm(rank, rank, n, Ut.data(), rank, HV.data(), n, Hbar.data(), rank);
+  for (size_t j = 0; j < rank; ++j)
+    for (size_t i = 0; i < rank; ++i) Hbar[i + rank * j] = svmh[i] * Hbar[i + rank * j] * svmh[j];
   if (hermitian) {
     // The Hermitian case in real arrays: the complex form below carries zero imaginary parts through
     // the back-transform, the sort and the sign fix, and its real parts are these numbers exactly
     // (the same operations in the same order), so the results are bit for bit the same.
     std::vector<double> ev, vec;
     dense::sym_eigen(rank, Hbar, ev, vec);
-    std::vector<double> X(n * rank, 0.0), Xr(n);
-    for (size_t k = 0; k < rank; ++k) {
-      std::fill(Xr.begin(), Xr.end(), 0.0);
-      for (size_t l = 0; l < rank; ++l) {
-        const double ylk = vec[l + rank * k], sl = svmh[l];
-        const double* vl = &V[n * l];
-        for (size_t i = 0; i < n; ++i) Xr[i] += vl[i] * sl * ylk;
+    // Selection sort ascending (first minimum wins) of all `rank` eigenvalues; the back-transformed
+    // vectors X[:, k] = sum_l (V[:, l] svmh[l]) vec[l, k] (l in order) only for the first `nvec` of
+    // that order -- each column is formed on its own, so the kept ones are the same numbers.
+    std::vector<size_t> order;
+    {
+      std::vector<char> used(rank, 0);
+      for (size_t k = 0; k < rank; ++k) {
+        size_t ll = 0;
+        while (used[ll]) ++ll;
+        for (size_t l = 0; l < rank; ++l)
+          if (!used[l] && ev[l] < ev[ll]) ll = l;
+        used[ll] = 1;
+        order.push_back(ll);
       }
-      std::copy(Xr.begin(), Xr.end(), X.begin() + long(n * k));
     }
-    // selection sort ascending (first minimum wins), sign fixed on the largest of the first `rank`
-    // components
-    std::vector<char> used(rank, 0);
-    eigenvectors.resize(n * rank);
+    const size_t nkeep = std::min(nvec, rank);
+    std::vector<double> Vs(n * rank), Y(rank * nkeep);
+    for (size_t l = 0; l < rank; ++l)
+      for (size_t i = 0; i < n; ++i) Vs[i + n * l] = V[i + n * l] * svmh[l];
+    for (size_t k = 0; k < nkeep; ++k)
+      std::copy(vec.begin() + long(rank * order[k]), vec.begin() + long(rank * (order[k] + 1)), Y.begin() + long(rank * k));
+    eigenvectors.resize(n * nkeep);
     eigenvalues.resize(rank);
-    for (size_t k = 0; k < rank; ++k) {
-      size_t ll = 0;
-      while (used[ll]) ++ll;
-      for (size_t l = 0; l < rank; ++l)
-        if (!used[l] && ev[l] < ev[ll]) ll = l;
-      used[ll] = 1;
-      eigenvalues[k] = ev[ll];
+    dense::ordered_gemm(n, nkeep, rank, Vs.data(), n, Y.data(), rank, eigenvectors.data(), n);
+    for (size_t k = 0; k < rank; ++k) eigenvalues[k] = ev[order[k]];
+    // sign fixed on the largest of the first `rank` components
+    for (size_t k = 0; k < nkeep; ++k) {
       double* col = &eigenvectors[n * k];
-      std::copy(X.begin() + long(n * ll), X.begin() + long(n * (ll + 1)), col);
       size_t mc = 0;
       for (size_t l = 0; l < rank && l < n; ++l)
         if (std::abs(col[l]) > std::abs(col[mc])) mc = l;

@@ -196,7 +196,7 @@ class SubspaceSolverLinEig : public SubspaceSolver {
     const auto& s = data.at(EqnData::S);
     const size_t dim = h.rows();
     std::vector<double> evec;
-    eigenproblem(evec, m_eigenvalues, h.data(), s.data(), dim, m_hermitian, m_svd_solver_threshold, 0, true);
+    eigenproblem(evec, m_eigenvalues, h.data(), s.data(), dim, m_hermitian, m_svd_solver_threshold, 0, true, nroots_max);
     const size_t nsol = dim ? evec.size() / dim : 0;
     const size_t nroots = std::min(nroots_max, nsol);
     m_eigenvalues.resize(nroots);

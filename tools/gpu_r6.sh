@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
 # host algebra clock), and a kernel trace of the C4-shard solve.
-#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,seltests,gputests
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,gputests
 # Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
 # the session.
 set -u -o pipefail
@@ -52,6 +52,12 @@ for s in ${1//,/ }; do
       rm -rf "$OUT/c4hiptrace"
       step c4hiptrace 300 rocprofv3 --kernel-trace --hip-runtime-trace -d "$OUT/c4hiptrace" -o run --output-format csv -- \
         python3 tools/trace_c4.py || exit $?
+      ;;
+    gapprobe)
+      step gapprobe 300 python -u tools/gap_probe.py --out "$OUT/gap_probe.json" || exit $?
+      ;;
+    sizeprobe)
+      step sizeprobe 400 python -u tools/size_probe.py --out "$OUT/size_probe.json" || exit $?
       ;;
     c4prof)
       rm -rf "$OUT/c4prof"
