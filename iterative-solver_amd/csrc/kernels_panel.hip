@@ -64,9 +64,15 @@ struct InnerArgs {
 // groups (4 g >= m: the instantiated NG above the panel's) skip their loads by a wave-uniform branch
 // (re-reading one fixed line instead made every wave of the chip hit one L2 channel: 8 x 40 ran 6 %
 // slower).  No load carries an exec-mask guard.
-template <int MG, int NG, bool SYM = false, bool SC = false, bool PIPE = false>
+// PRE: the panel's first 4 MG columns are its rows (y[j] == x[j], ys[j] == xs[j] for j < m, columns
+// m .. 4 MG - 1 padding whose results are dropped): those column groups take the row groups'
+// registers instead of loading the same vectors again -- the batched overlap rows of the subspace
+// update ([params, actions, Q, ...] against params) read each vector once.
+template <int MG, int NG, bool SYM = false, bool SC = false, bool PIPE = false, bool PRE = false>
 __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
   static_assert(!SYM || MG == NG, "symmetric panel needs square groups");
+  static_assert(!PRE || (!SYM && NG >= MG), "column prefix needs at least the row groups");
+  constexpr auto own = [](int h) { return SYM || (PRE && h < MG); };  // column group h = row group h
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 3, p = lane >> 2;
   const double* xp[MG];
@@ -101,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
 #pragma unroll
     for (int g = 0; g < MG; ++g) xv[g] = 4 * g < a.m ? ssp::ld2nt(xp[g] + e) : z2;
 #pragma unroll
-    for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : (4 * h < a.k ? ssp::ld2nt(yp[h] + e) : z2);
+    for (int h = 0; h < NG; ++h) yv[h] = own(h) ? xv[h] : (4 * h < a.k ? ssp::ld2nt(yp[h] + e) : z2);
   };
   const auto mac = [&](double2(&xv)[MG], double2(&yv)[NG]) {
     // scales after every load of the chunk is in flight
@@ -109,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
 #pragma unroll
       for (int g = 0; g < MG; ++g) xv[g] = sc2<SC>(xv[g], xsc[g]);
 #pragma unroll
-      for (int h = 0; h < NG; ++h) yv[h] = SYM ? xv[h] : sc2<SC>(yv[h], ysc[h]);
+      for (int h = 0; h < NG; ++h) yv[h] = own(h) ? xv[h] : sc2<SC>(yv[h], ysc[h]);
     }
 #pragma unroll
     for (int g = 0; g < MG; ++g)
@@ -157,8 +163,8 @@ __global__ __launch_bounds__(kBlock) void k_gemm_inner(const InnerArgs a) {
     }
 #pragma unroll
     for (int h = 0; h < NG; ++h) {
-      const double y0 = SYM ? x0[h] : ((yok[h] && i0 < a.n) ? sc1<SC>(yp[h][i0], ysc[h]) : 0.0);
-      const double y1 = SYM ? x1[h] : ((yok[h] && i1 < a.n) ? sc1<SC>(yp[h][i1], ysc[h]) : 0.0);
+      const double y0 = own(h) ? x0[h] : ((yok[h] && i0 < a.n) ? sc1<SC>(yp[h][i0], ysc[h]) : 0.0);
+      const double y1 = own(h) ? x1[h] : ((yok[h] && i1 < a.n) ? sc1<SC>(yp[h][i1], ysc[h]) : 0.0);
 #pragma unroll
       for (int g = 0; g < MG; ++g) {
         acc[g][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(x0[g], y0, acc[g][h], 0, 0, 0);
@@ -1161,30 +1167,40 @@ constexpr int inner_pipe_min_level() {
   return (SYM || MG * NG <= 8) ? 1 : (MG * NG <= 16 ? 2 : 99);
 }
 
-template <int MG, int NG, bool SC>
-void launch_inner_t(ssp_ctx* ctx, unsigned grid, const InnerArgs& a) {
+template <int MG, int NG, bool SC, bool PRE>
+void launch_inner_tp(ssp_ctx* ctx, unsigned grid, const InnerArgs& a) {
   if constexpr (inner_pipe_min_level<MG, NG, false, SC>() < 99) {
     if (inner_pipe_level() >= inner_pipe_min_level<MG, NG, false, SC>()) {
-      SSP_LAUNCH((k_gemm_inner<MG, NG, false, SC, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+      SSP_LAUNCH((k_gemm_inner<MG, NG, false, SC, true, PRE>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
       return;
     }
   }
-  SSP_LAUNCH((k_gemm_inner<MG, NG, false, SC>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+  SSP_LAUNCH((k_gemm_inner<MG, NG, false, SC, false, PRE>), dim3(grid), dim3(kBlock), 0, ctx->stream, a);
+}
+
+// pre: the column-prefix form (k_gemm_inner PRE), instantiated for MG <= 2 (up to 8 rows, the
+// solvers' working sets)
+template <int MG, int NG, bool SC>
+void launch_inner_t(ssp_ctx* ctx, unsigned grid, const InnerArgs& a, bool pre) {
+  if constexpr (MG <= 2 && NG >= MG) {
+    if (pre) return launch_inner_tp<MG, NG, SC, true>(ctx, grid, a);
+  }
+  launch_inner_tp<MG, NG, SC, false>(ctx, grid, a);
 }
 
 // Smallest instantiated NG >= need (need <= ng_max(MG)).
 template <int MG, bool SC>
-int launch_inner_mg(ssp_ctx* ctx, unsigned grid, const InnerArgs& a, int need) {
-  if (need <= 1) launch_inner_t<MG, 1, SC>(ctx, grid, a);
-  else if (need <= 2) launch_inner_t<MG, 2, SC>(ctx, grid, a);
-  else if (need <= 3) launch_inner_t<MG, 3, SC>(ctx, grid, a);
-  else if (need <= 4) launch_inner_t<MG, 4, SC>(ctx, grid, a);
-  else if (need <= 6) launch_inner_t<MG, 6, SC>(ctx, grid, a);
+int launch_inner_mg(ssp_ctx* ctx, unsigned grid, const InnerArgs& a, int need, bool pre) {
+  if (need <= 1) launch_inner_t<MG, 1, SC>(ctx, grid, a, pre);
+  else if (need <= 2) launch_inner_t<MG, 2, SC>(ctx, grid, a, pre);
+  else if (need <= 3) launch_inner_t<MG, 3, SC>(ctx, grid, a, pre);
+  else if (need <= 4) launch_inner_t<MG, 4, SC>(ctx, grid, a, pre);
+  else if (need <= 6) launch_inner_t<MG, 6, SC>(ctx, grid, a, pre);
   else if constexpr (ng_max(MG) >= 8) {
-    if (need <= 8) launch_inner_t<MG, 8, SC>(ctx, grid, a);
+    if (need <= 8) launch_inner_t<MG, 8, SC>(ctx, grid, a, pre);
     else if constexpr (ng_max(MG) >= 12) {
-      if (need <= 12) launch_inner_t<MG, 12, SC>(ctx, grid, a);
-      else if constexpr (ng_max(MG) >= 16) launch_inner_t<MG, 16, SC>(ctx, grid, a);
+      if (need <= 12) launch_inner_t<MG, 12, SC>(ctx, grid, a, pre);
+      else if constexpr (ng_max(MG) >= 16) launch_inner_t<MG, 16, SC>(ctx, grid, a, pre);
     }
   }
   SSP_TRY_HIP(hipGetLastError());
@@ -1216,18 +1232,18 @@ int launch_inner_sym(ssp_ctx* ctx, const InnerArgs& a, unsigned grid, bool sc) {
 }
 
 template <bool SC>
-int launch_inner_sc(ssp_ctx* ctx, const InnerArgs& a, unsigned grid) {
+int launch_inner_sc(ssp_ctx* ctx, const InnerArgs& a, unsigned grid, bool pre) {
   const int mg = (a.m + 3) / 4, need = (a.k + 3) / 4;
   switch (mg) {
-    case 1: return launch_inner_mg<1, SC>(ctx, grid, a, need);
-    case 2: return launch_inner_mg<2, SC>(ctx, grid, a, need);
-    case 3: return launch_inner_mg<3, SC>(ctx, grid, a, need);
-    default: return launch_inner_mg<4, SC>(ctx, grid, a, need);
+    case 1: return launch_inner_mg<1, SC>(ctx, grid, a, need, pre);
+    case 2: return launch_inner_mg<2, SC>(ctx, grid, a, need, pre);
+    case 3: return launch_inner_mg<3, SC>(ctx, grid, a, need, false);
+    default: return launch_inner_mg<4, SC>(ctx, grid, a, need, false);
   }
 }
 
-int launch_inner(ssp_ctx* ctx, const InnerArgs& a, unsigned grid, bool sc) {
-  return sc ? launch_inner_sc<true>(ctx, a, grid) : launch_inner_sc<false>(ctx, a, grid);
+int launch_inner(ssp_ctx* ctx, const InnerArgs& a, unsigned grid, bool sc, bool pre = false) {
+  return sc ? launch_inner_sc<true>(ctx, a, grid, pre) : launch_inner_sc<false>(ctx, a, grid, pre);
 }
 
 template <bool DEV, bool SET, bool SC>
@@ -1306,7 +1322,27 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
   for (int i = 0; i < m; ++i) (swap ? cs : rs)[size_t(i)] = xs ? xs[i] : 1.0;
   for (int j = 0; j < k; ++j) (swap ? rs : cs)[size_t(j)] = ys ? ys[j] : 1.0;
   const bool sc = any_scaled(rs.data(), R) || any_scaled(cs.data(), C);
-  const size_t total = size_t(R) * C;
+  // Column prefix (k_gemm_inner PRE): when the first R columns are the rows themselves (the batched
+  // overlap rows [params, actions, Q, ...] against params), the panel takes them from the row
+  // registers.  The columns are laid out with 4 ceil(R / 4) - R padding columns after that prefix
+  // (computed, never read back), in every branch below, so that every rank reduces the same count
+  // whichever branch its shard length takes.
+  int pad = -1;
+  if (R <= 8 && C > R && !(R == 1 && C <= 2)) {
+    bool pre = true;
+    for (int i = 0; pre && i < R; ++i) pre = cols[i] == rows[i] && cs[size_t(i)] == rs[size_t(i)];
+    if (pre) pad = 4 * ((R + 3) / 4) - R;
+  }
+  std::vector<const double*> cols_pad;
+  if (pad >= 0) {
+    cols_pad.assign(cols, cols + R);
+    cols_pad.insert(cols_pad.end(), size_t(pad), rows[0]);
+    cols_pad.insert(cols_pad.end(), cols + R, cols + C);
+    cs.insert(cs.begin() + R, size_t(pad), 1.0);
+    cols = cols_pad.data();
+  }
+  const int C2 = pad >= 0 ? C + pad : C;  // columns as launched and reduced
+  const size_t total = size_t(R) * C2;
   ssp::FoldTail tail{};
   if (ssp::exact_mode(ctx, n)) {
     // The reference's sequential dots (each the same number whichever operand is the row), in the
@@ -1319,7 +1355,7 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
     std::sort(distinct.begin(), distinct.end());
     const double nvec = double(std::unique(distinct.begin(), distinct.end()) - distinct.begin());
     ssp::LedgerScope ls(ctx, "gemm_inner", 8.0 * n * nvec);
-    SSP_TRY(ssp::exact_inner(ctx, rows, rs.data(), R, cols, cs.data(), C, n, false, tail));
+    SSP_TRY(ssp::exact_inner(ctx, rows, rs.data(), R, cols, cs.data(), C2, n, false, tail));
   } else {
     SSP_TRY(ssp::ensure_result(ctx, total));
     if (n == 0) {
@@ -1387,10 +1423,10 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
       for (int r0 = 0; !sym && !(R == 1 && C <= 2) && r0 < R; r0 += ssp::kInnerRows) {
         const int mr = std::min(ssp::kInnerRows, R - r0);
         const int cols_per_launch = 4 * ng_max((mr + 3) / 4);
-        for (int c0 = 0; c0 < C; c0 += cols_per_launch) {
+        for (int c0 = 0; c0 < C2; c0 += cols_per_launch) {
           InnerArgs a{};
           a.m = mr;
-          a.k = std::min(cols_per_launch, C - c0);
+          a.k = std::min(cols_per_launch, C2 - c0);
           a.n = n;
           for (int i = 0; i < a.m; ++i) {
             a.x[i] = rows[r0 + i];
@@ -1404,22 +1440,31 @@ int ssp_gemm_inner_scaled(ssp_ctx* ctx, const double* const* xx, const double* x
           const unsigned grid = inner_grid(ctx, n);
           SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * a.m * a.k));
           a.partial = ctx->partial;
+          const bool pre = pad >= 0 && c0 == 0;
           if (r0 == 0 && c0 == 0)
-            ls.detail(shape_tag("mfma", (a.m + 3) / 4, ng_inst((a.k + 3) / 4), a.m, a.k, sc_launch));
-          SSP_TRY(launch_inner(ctx, a, grid, sc_launch));
-          const bool last = r0 + ssp::kInnerRows >= R && c0 + cols_per_launch >= C;
-          SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), a.m, a.k, ctx->result_dev, C, r0, c0, &tail,
+            ls.detail(shape_tag(pre ? "mfma-pre" : "mfma", (a.m + 3) / 4, ng_inst((a.k + 3) / 4), a.m, a.k, sc_launch));
+          SSP_TRY(launch_inner(ctx, a, grid, sc_launch, pre));
+          const bool last = r0 + ssp::kInnerRows >= R && c0 + cols_per_launch >= C2;
+          SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), a.m, a.k, ctx->result_dev, C2, r0, c0, &tail,
                                               last));
         }
       }
     }
   }
-  std::vector<double> t(swap ? total : 0);
-  double* dst = swap ? t.data() : out;
+  std::vector<double> t(swap || pad >= 0 ? total : 0);
+  double* dst = swap || pad >= 0 ? t.data() : out;
   if (tail.counter) {
     SSP_TRY(ssp::fold_finish(ctx, tail, dst));
   } else {
     SSP_TRY(ssp::reduce_fetch(ctx, dst, total));
+  }
+  if (pad >= 0) {  // drop the padding columns: R x C2 -> R x C (row-major)
+    for (int i = 0; i < R; ++i)
+      for (int j = 0; j < C; ++j) t[size_t(i) * C + j] = t[size_t(i) * C2 + (j < R ? j : j + pad)];
+    if (!swap) {
+      std::copy(t.begin(), t.begin() + long(size_t(R) * C), out);
+      return SSP_OK;
+    }
   }
   if (!swap) return SSP_OK;
   for (int i = 0; i < m; ++i)

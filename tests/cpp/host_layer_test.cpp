@@ -14,6 +14,8 @@
 //                                                (test/itsolv/subspace/CMakeLists.txt:1) and targets
 //                                                functions its QSpace.h no longer has
 //   dspace_resetter_do_reset                     DSpaceResetter.h:80-83
+//   ordered_gemm_*, eigenproblem_kept_vectors,   the host algebra's fast paths against their plain
+//   screen_cholesky_proof                        forms (dense.h; no reference test)
 //   "svd" mode prints the restated eigensolver_lapacke_dsyev / svd_system on the matrix of
 //   test_svd_system.cpp:17-35 for the Python side to check against LAPACK (numpy), as :64-90 does
 //   against Eigen.
@@ -23,6 +25,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <list>
 #include <numeric>
@@ -352,6 +355,79 @@ void qspace_cases() {
   });
 }
 
+// The host algebra's fast paths against their plain forms (dense.h): the register-tiled products are
+// the triple loop's numbers, the eigenproblem's kept eigenvectors do not depend on how many are
+// kept, and the redundancy screen's Cholesky proof never skips a decomposition that would have
+// reported an eigenvalue at or below the threshold.
+void dense_cases() {
+  std::mt19937_64 g(11);
+  std::uniform_real_distribution<double> u(-1, 1);
+  run("ordered_gemm_is_the_triple_loop", [&] {
+    for (size_t M : {1, 5, 8, 13, 64})
+      for (size_t N : {1, 3, 4, 9})
+        for (size_t K : {1, 7, 40}) {
+          std::vector<double> A(M * K), B(K * N), C(M * N), R(M * N, 0.0);
+          for (auto& x : A) x = u(g);
+          for (auto& x : B) x = u(g);
+          it::dense::ordered_gemm(M, N, K, A.data(), M, B.data(), K, C.data(), M);
+          for (size_t j = 0; j < N; ++j)
+            for (size_t l = 0; l < K; ++l)
+              for (size_t i = 0; i < M; ++i) R[i + M * j] += A[i + M * l] * B[l + K * j];
+          expect(std::memcmp(C.data(), R.data(), sizeof(double) * M * N) == 0, "bitwise");
+        }
+  });
+  run("eigenproblem_kept_vectors", [&] {
+    for (size_t n : {1, 6, 24, 40}) {
+      std::vector<double> H(n * n), S(n * n, 0.0);
+      for (size_t i = 0; i < n; ++i)
+        for (size_t j = 0; j <= i; ++j) {
+          H[i * n + j] = H[j * n + i] = u(g) + (i == j ? double(i) : 0.0);
+          S[i * n + j] = S[j * n + i] = (i == j ? 1.0 : 1e-3 * u(g));
+        }
+      std::vector<double> v_all, e_all, v_few, e_few;
+      it::eigenproblem(v_all, e_all, H, S, n, true, 1e-14, 0, true);
+      const size_t keep = std::min<size_t>(3, n);
+      it::eigenproblem(v_few, e_few, H, S, n, true, 1e-14, 0, true, keep);
+      expect(e_all == e_few && e_all.size() == n, "eigenvalues of every root");
+      expect(v_few.size() == n * keep && v_all.size() == n * n, "vector counts");
+      expect(std::memcmp(v_all.data(), v_few.data(), sizeof(double) * n * keep) == 0, "kept vectors bitwise");
+    }
+  });
+  run("screen_cholesky_proof", [&] {
+    int proven = 0, skipped_wrongly = 0;
+    for (int trial = 0; trial < 400; ++trial) {
+      const size_t n = 2 + size_t(trial % 30), r = 1 + size_t(trial % 7);
+      // Gram matrices of n vectors in d dimensions, some near-dependent, and scaled
+      const size_t d = (trial % 4 == 0 && n > r) ? n - r : n;  // rank-deficient every fourth trial
+      std::vector<double> X(n * d);
+      for (auto& x : X) x = u(g);
+      if (trial % 5 == 1)
+        for (size_t j = 0; j < d; ++j) X[(n - 1) * d + j] = X[j] + 1e-9 * u(g);
+      const double scale = std::pow(10.0, double(trial % 9) - 4.0);
+      std::vector<double> A(n * n);
+      for (size_t i = 0; i < n; ++i)
+        for (size_t j = 0; j < n; ++j) {
+          double s = 0;
+          for (size_t k = 0; k < d; ++k) s += X[i * d + k] * X[j * d + k];
+          A[i * n + j] = scale * s;
+        }
+      for (double thresh : {1e-12, 1e-8 * scale}) {
+        const bool ok = it::dense::eigenvalues_exceed(n, A, thresh);
+        const bool none = it::svd_system(n, n, A, thresh, true).empty();
+        proven += ok;
+        skipped_wrongly += ok && !none;
+      }
+    }
+    expect(skipped_wrongly == 0, "a proof skipped a decomposition with an eigenvalue <= threshold");
+    expect(proven > 200, "the proof holds on the well-conditioned cases");
+    std::vector<double> nan(9, 0.0);
+    nan[0] = nan[4] = nan[8] = 1.0;
+    nan[4] = std::nan("");
+    expect(!it::dense::eigenvalues_exceed(3, nan, 1e-12), "NaN: not proven");
+    expect(!it::dense::eigenvalues_exceed(0, {}, 1e-12), "empty: not proven");
+  });
+}
+
 // test_svd_system.cpp:17-35: the symmetric test matrix from the C library's rand() (unseeded).
 void svd_dump() {
   const size_t dim = 5;
@@ -416,6 +492,7 @@ int main(int argc, char** argv) {
   itsolv_util_cases();
   solver_factory_cases();
   qspace_cases();
+  dense_cases();
   std::printf("%s %d failure(s)\n", g_fail ? "FAILED" : "OK", g_fail);
   return g_fail ? 1 : 0;
 }

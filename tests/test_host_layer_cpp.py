@@ -65,9 +65,10 @@ def test_matrix_reference_header_same_cases():
 def test_host_layer_components(host_exe):
     out = run_cases(host_exe)
     for name in ("overlap_reverse_params", "parameter_batches", "resize_qspace", "max_overlap_with_R_qparams_0",
-                 "StringFacet_parse_keyval_string", "solver_factory_string_constructor", "qspace_prepend_and_blocks"):
+                 "StringFacet_parse_keyval_string", "solver_factory_string_constructor", "qspace_prepend_and_blocks",
+                 "ordered_gemm_is_the_triple_loop", "eigenproblem_kept_vectors", "screen_cholesky_proof"):
         assert "PASS " + name in out
-    assert out.count("PASS ") == 27
+    assert out.count("PASS ") == 30
 
 
 def test_svd_system_against_lapack(host_exe):

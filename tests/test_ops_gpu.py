@@ -124,6 +124,42 @@ def test_gemm_inner_symmetric_panel(ctx, m, n):
             assert abs(s[i, j] - math.fsum(xs[i] * xs[j])) <= red_tol(xs[i] * xs[j])
 
 
+@pytest.mark.parametrize("m,extra", [(1, 2), (3, 5), (5, 7), (8, 40), (8, 60), (6, 61), (2, 1)])
+@pytest.mark.parametrize("n", [1, 33, 1003, 100_003])
+@pytest.mark.parametrize("scaled", [False, True])
+def test_gemm_inner_column_prefix(ctx, m, extra, n, scaled):
+    # gemm_inner(xx, [xx, yy]) -- the subspace update's batched overlap rows -- takes its first column
+    # groups from the row registers (k_gemm_inner PRE, padded to whole groups); every element is the
+    # same sum as with distinct copies of xx in those columns, so the results are bit-identical, also
+    # when the padded columns need a second launch (8 + 60 > 64) and with the operands swapped.
+    r = rng(m * 100 + extra + n)
+    xs = [r.uniform(-1, 1, n) for _ in range(m)]
+    ys = [r.uniform(-1, 1, n) for _ in range(extra)]
+    dx = [ctx.upload(v) for v in xs]
+    dc = [ctx.upload(v) for v in xs]
+    dy = [ctx.upload(v) for v in ys]
+    if scaled:
+        sx = list(r.uniform(0.5, 2, m))
+        sy = list(r.uniform(0.5, 2, extra))
+        got = ctx.gemm_inner_scaled(dx, sx, dx + dy, sx + sy)
+        ref = ctx.gemm_inner_scaled(dx, sx, dc + dy, sx + sy)
+        got_t = ctx.gemm_inner_scaled(dx + dy, sx + sy, dx, sx)
+    else:
+        got = ctx.gemm_inner(dx, dx + dy)
+        ref = ctx.gemm_inner(dx, dc + dy)
+        got_t = ctx.gemm_inner(dx + dy, dx)
+    assert got.shape == (m, m + extra)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(got_t, ref.T)
+    cols = xs + ys
+    for i in range(m):
+        for j in range(m + extra):
+            t = xs[i] * cols[j] * ((sx[i] * (sx + sy)[j]) if scaled else 1.0)
+            assert abs(got[i, j] - math.fsum(t)) <= red_tol(t)
+    for v in dx + dc + dy:
+        v.free()
+
+
 def test_gemm_inner_asymmetric_layout(ctx):
     # Exact integer data: catches row/col swaps in the MFMA accumulator mapping.
     n = 4096 + 24
