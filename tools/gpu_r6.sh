@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
 # host algebra clock), and a kernel trace of the C4-shard solve.
-#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,innertests,gputests
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,gputests
 # Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
 # the session.
 set -u -o pipefail
@@ -43,6 +43,11 @@ for s in ${1//,/ }; do
     innertests)
       step innertests 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu -k "gemm_inner or traces or solver or sharded or fused" \
         tests/test_ops_gpu.py tests/test_traces_gpu.py tests/test_solver_gpu.py tests/test_distributed_gpu.py tests/test_fused_passes_gpu.py tests/test_exact_gpu.py || exit $?
+      ;;
+    selprobe)
+      rm -rf "$OUT/selprof"
+      step selprobe 300 rocprofv3 --kernel-trace --stats -d "$OUT/selprof" -o run --output-format csv -- \
+        python3 tools/select_probe.py 12.5e6 --nsel 8,16 || exit $?
       ;;
     gputests)
       step gputests 1500 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests || exit $?
