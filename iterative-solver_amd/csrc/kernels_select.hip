@@ -235,10 +235,12 @@ __global__ __launch_bounds__(kBlock) void k_radix_compact(const RadixArgs a, siz
 
 // Single pass for a small n (nsel <= K <= 16; the solvers select nroots and max_p elements): every
 // thread keeps its K best composites in registers, sorted, while it streams its elements (radix_stream's
-// order); the wave then merges its 64 lists through lane shuffles -- the K best of two sorted lists are
-// the elementwise better of one and the other reversed (a bitonic sequence), sorted by a bitonic
-// clean-up -- and writes its K best.  One read of the shard and no host round trip before the tile
-// levels, where the radix path needs a histogram pass, a host decision per digit and a compaction pass.
+// order).  The lists then meet in three merges, each "the K best of two sorted lists are the elementwise
+// better of one and the other reversed (a bitonic sequence), sorted by a bitonic clean-up": the wave's
+// 64 lists through lane shuffles, the workgroup's 4 wave lists through LDS, and -- in the last
+// workgroup to arrive -- every workgroup's list.  One read of the shard, one launch, no host round
+// trip; the radix path needs a histogram pass and a host decision per digit, a compaction pass and the
+// tile levels (k_select_tile) after it.
 constexpr size_t kLocalMaxK = 16;
 
 // Field-wise selects: a select between two whole Cand values becomes a select between their
@@ -263,43 +265,103 @@ __device__ __forceinline__ void cand_insert(Cand (&L)[K], Cand c) {
   for (int j = K - 1; j > 0; --j) cand_cswap<K>(L[j - 1], L[j]);
 }
 
+// L <- the K best of the sorted lists L and P (both best first), sorted.  Counted loops with
+// compile-time trip counts only: a shift-stepped loop was left rolled, and its uniform index sent L to
+// scratch memory (2.3 ms per call at 12.5e6 elements).
+template <int K>
+__device__ __forceinline__ void cand_merge(Cand (&L)[K], const Cand (&P)[K]) {
+  constexpr int kLogK = K == 8 ? 3 : 4;
+  static_assert(K == 8 || K == 16, "cand_merge: K is 8 or 16");
+#pragma unroll
+  for (int j = 0; j < K; ++j) L[j] = cand_pick(better(L[j], P[K - 1 - j]), L[j], P[K - 1 - j]);
+#pragma unroll
+  for (int sh = 0; sh < kLogK; ++sh) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int h = (K / 2) >> sh;
+      if ((j & h) == 0) cand_cswap<K>(L[j], L[j + h]);
+    }
+  }
+}
+
+// Butterfly over lane distances 1, 2, .., 2^(R-1): afterwards every lane holds the merge of its
+// 2^R-lane group's lists.
+template <int K, int R>
+__device__ __forceinline__ void wave_merge(Cand (&L)[K]) {
+#pragma unroll
+  for (int sd = 0; sd < R; ++sd) {
+    Cand P[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      P[j].key = __shfl_xor(L[j].key, 1 << sd, 64);
+      P[j].idx = __shfl_xor(L[j].idx, 1 << sd, 64);
+    }
+    cand_merge<K>(L, P);
+  }
+}
+
+// The workgroup's 4 wave lists (every lane of a wave holds its wave's) merged into wave 0's lanes.
+template <int K>
+__device__ __forceinline__ void block_merge(Cand (&L)[K], Cand (&s_lists)[kBlock / 64][K]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < K; ++j) s_lists[wave][j] = L[j];
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) L[j] = lane < kBlock / 64 ? s_lists[lane][j] : Cand{0ull, 0ull};
+    wave_merge<K, 2>(L);
+  }
+}
+
 template <int MODE, int K>
-__global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size_t offset, Cand* out) {
+__global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size_t offset, Cand* wg_lists, Cand* out,
+                                                         unsigned* counter) {
+  __shared__ Cand s_lists[kBlock / 64][K];
+  __shared__ unsigned s_last;
   Cand L[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) L[j] = Cand{0ull, 0ull};  // sorts after every real candidate
   radix_stream<MODE>(a, [&](unsigned long long key, unsigned long long i, bool ok) {
     if (ok) cand_insert<K>(L, Cand{key, offset + i});
   });
-  // wave merge: after the round with lane distance d, every lane holds the K best of its 2d-lane group.
-  // Counted loops with compile-time trip counts only (a shift-stepped loop was left rolled, and its
-  // uniform index sent L to scratch memory: 2.3 ms per call at 12.5e6 elements).
-  constexpr int kLogK = K == 8 ? 3 : 4;
-  static_assert(K == 8 || K == 16, "k_select_local: K is 8 or 16");
-#pragma unroll
-  for (int sd = 0; sd < 6; ++sd) {
-    const int d = 1 << sd;
-    Cand P[K];
+  wave_merge<K, 6>(L);
+  block_merge<K>(L, s_lists);
+  // This workgroup's list, written through to the device scope (agent-scope atomic stores), then the
+  // arrival; the last arriver reads every list with agent-scope loads (the fold_tail pattern).
+  if (threadIdx.x == 0) {
+    Cand* o = wg_lists + size_t(blockIdx.x) * K;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      P[j].key = __shfl_xor(L[j].key, d, 64);
-      P[j].idx = __shfl_xor(L[j].idx, d, 64);
+      __hip_atomic_store(&o[j].key, L[j].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&o[j].idx, L[j].idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#pragma unroll
-    for (int j = 0; j < K; ++j) L[j] = cand_pick(better(L[j], P[K - 1 - j]), L[j], P[K - 1 - j]);
-#pragma unroll
-    for (int sh = 0; sh < kLogK; ++sh) {
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const int h = (K / 2) >> sh;
-        if ((j & h) == 0) cand_cswap<K>(L[j], L[j + h]);
-      }
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
-  if (__lane_id() == 0) {
-    Cand* o = out + (size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6)) * K;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the loads are agent-scope
 #pragma unroll
-    for (int j = 0; j < K; ++j) o[j] = L[j];
+  for (int j = 0; j < K; ++j) L[j] = Cand{0ull, 0ull};
+  for (unsigned g = threadIdx.x; g < gridDim.x; g += kBlock) {
+    Cand P[K];
+    const Cand* w = wg_lists + size_t(g) * K;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      P[j].key = __hip_atomic_load(&w[j].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      P[j].idx = __hip_atomic_load(&w[j].idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    cand_merge<K>(L, P);
+  }
+  wave_merge<K, 6>(L);
+  __syncthreads();  // s_lists is reused
+  block_merge<K>(L, s_lists);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) out[j] = L[j];
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
   }
 }
 
@@ -426,26 +488,26 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
     SelectArgs a{};
     a.keep = keep;
     a.out = buf0;
+    bool local = false;  // k_select_local has left the K best in buf0
     if (radix && nsel <= kLocalMaxK) {
-      // one pass: each wave's K best (K = 8 or 16 >= nsel) into `cand`, grid * 4 * K <= kRadixCap
+      // one pass, one launch: the K best (K = 8 or 16 >= nsel) of the shard into buf0, then the values
+      // (k_select_local); two workgroups per CU (the K = 16 lists allow two waves per SIMD)
       RadixArgs r{};
       r.x = x;
       r.y = y;
       r.n = n;
       r.neg = !max;
       r.abs = ignore_sign;
-      const unsigned lgrid = std::min<unsigned>(grid, unsigned(kRadixCap / (4 * kLocalMaxK)));
+      const unsigned lgrid = std::min<unsigned>(grid, unsigned(ctx->num_cus) * 2);
       const int K = nsel <= 8 ? 8 : 16;
-      if (mode == 1 && K == 8) SSP_LAUNCH((k_select_local<1, 8>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand);
-      else if (mode == 1) SSP_LAUNCH((k_select_local<1, 16>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand);
-      else if (K == 8) SSP_LAUNCH((k_select_local<0, 8>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand);
-      else SSP_LAUNCH((k_select_local<0, 16>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand);
+      SSP_TRY_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned), ctx->stream));
+      auto* cnt = reinterpret_cast<unsigned*>(counter);
+      if (mode == 1 && K == 8) SSP_LAUNCH((k_select_local<1, 8>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, buf0, cnt);
+      else if (mode == 1) SSP_LAUNCH((k_select_local<1, 16>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, buf0, cnt);
+      else if (K == 8) SSP_LAUNCH((k_select_local<0, 8>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, buf0, cnt);
+      else SSP_LAUNCH((k_select_local<0, 16>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, buf0, cnt);
       SSP_TRY_HIP(hipGetLastError());
-      count = size_t(lgrid) * (kBlock / 64) * size_t(K);
-      tiles = (count + kTile - 1) / kTile;
-      a.in = cand;
-      a.count = count;
-      a.mode = 2;
+      local = true;
     } else if (radix) {
       SSP_TRY(radix_candidates(ctx, mode, x, y, n, offset, nsel, max, ignore_sign, cand, hist, counter, grid, &count));
       tiles = (count + kTile - 1) / kTile;
@@ -461,12 +523,14 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
       a.max = max;
       a.ignore_sign = ignore_sign;
     }
-    SSP_LAUNCH(k_select_tile, dim3(unsigned(tiles)), dim3(kTileBlock), 0, ctx->stream, a);
-    SSP_TRY_HIP(hipGetLastError());
-    count = tiles * size_t(keep);
+    if (!local) {
+      SSP_LAUNCH(k_select_tile, dim3(unsigned(tiles)), dim3(kTileBlock), 0, ctx->stream, a);
+      SSP_TRY_HIP(hipGetLastError());
+      count = tiles * size_t(keep);
+    }
     Cand* cur = buf0;
     Cand* nxt = buf1;
-    while (tiles > 1) {
+    while (!local && tiles > 1) {
       tiles = (count + kTile - 1) / kTile;
       SelectArgs b{};
       b.in = cur;
