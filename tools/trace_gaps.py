@@ -1,3 +1,10 @@
+#!/usr/bin/env python3
+"""Idle gaps of one solve in a rocprofv3 kernel trace (tools/trace_c4.py under --kernel-trace): the
+last solve's wall, busy and idle time, a histogram of the gaps between consecutive kernels, and the
+gaps summed by (previous kernel, next kernel) pair.
+
+usage: python tools/trace_gaps.py RUN_kernel_trace.csv [nocut]   (nocut: the last segment is one solve)
+"""
 import csv, collections, re, sys
 import numpy as np
 rows=list(csv.DictReader(open(sys.argv[1])))
