@@ -1269,13 +1269,8 @@ void launch_outer_sc(ssp_ctx* ctx, unsigned grid, const OuterArgs& a) {
 }
 
 int launch_outer(ssp_ctx* ctx, const OuterArgs& a) {
-  // SSP_OUTER_WG_PER_CU: workgroups per CU of the launch (default 8; A/B knob, tools/outer_grid_ab.py)
-  static const unsigned per_cu = [] {
-    const char* e = std::getenv("SSP_OUTER_WG_PER_CU");
-    const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? unsigned(v) : 8u;
-  }();
-  const unsigned grid = ssp::stream_grid(ctx, a.n / 2 + 1, kOuterWin, per_cu);
+  // workgroups per CU of the launch: ctx->outer_per_cu (SSP_OUTER_WG_PER_CU at context creation)
+  const unsigned grid = ssp::stream_grid(ctx, a.n / 2 + 1, kOuterWin, unsigned(ctx->outer_per_cu));
   a.scale_dev ? launch_outer_sc<true>(ctx, grid, a) : launch_outer_sc<false>(ctx, grid, a);
   SSP_TRY_HIP(hipGetLastError());
   return SSP_OK;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
 # host algebra clock), and a kernel trace of the C4-shard solve.
-#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,gputests
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,gputests
 # Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
 # the session.
 set -u -o pipefail
@@ -48,6 +48,21 @@ for s in ${1//,/ }; do
       rm -rf "$OUT/selprof"
       step selprobe 300 rocprofv3 --kernel-trace --stats -d "$OUT/selprof" -o run --output-format csv -- \
         python3 tools/select_probe.py 12.5e6 --nsel 8,16 || exit $?
+      ;;
+    csab)
+      for v in 0 1 0 1; do
+        SSP_INNER_CS=$v SSP_LEDGER_DETAIL=1 step "csab_$v" 300 python -u tools/solver_ledger.py --configs C4-shard \
+          --out "$OUT/c4_ledger_cs$v.json" || exit $?
+      done
+      ;;
+    outercu)
+      for v in 8 2 4 8 2 4; do
+        SSP_OUTER_WG_PER_CU=$v step "outercu_$v" 300 python -u tools/size_probe.py --ops gemm_outer_set,gemm_outer,axpy_pairs_norm \
+          --ns 6250000,12500000,25000000,100000000 --out "$OUT/outercu_$v.json" || exit $?
+      done
+      ;;
+    outerab)
+      step outerab 400 python -u tools/outer_cu_ab.py --out "$OUT/outer_cu_ab.json" || exit $?
       ;;
     gputests)
       step gputests 1500 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests || exit $?

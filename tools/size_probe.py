@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "size_probe.json"))
     ap.add_argument("--ops", default="gemm_inner,gemm_outer_set,gemm_outer,transform_gram,axpy_pairs_norm")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--ns", default=",".join(str(n) for n in NS), help="comma-separated lengths")
     a = ap.parse_args()
     ops = a.ops.split(",")
     m, k = 8, 48
@@ -34,7 +35,7 @@ def main():
     alphas = rng.uniform(-1, 1, (k, m)) / k
     t8 = np.eye(m) + rng.uniform(-1e-3, 1e-3, (m, m))
     res = []
-    for n in NS:
+    for n in (int(float(v)) for v in a.ns.split(",")):
         xs = [ctx.alloc(n) for _ in range(m)]
         ys = [ctx.alloc(n) for _ in range(k)]
         for i, v in enumerate(xs + ys):
