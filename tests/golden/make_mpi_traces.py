@@ -35,6 +35,11 @@ def main():
         if r.returncode != 0:
             raise SystemExit(r.stdout[-3000:] + r.stderr[-3000:])
     rec = json.load(open(OUT))
+    sys.path.insert(0, HERE)
+    from make_traces import ORACLE_REVISION
+
+    rec["_parity"] = "bit_exact"
+    rec["_oracle_revision"] = ORACLE_REVISION
     rec["_generator"] = ("tests/golden/make_mpi_traces.py: CPU path (product host code over oracle/ssp_emul.cpp, "
                          "sequential rank-local dots) under mpiexec -n P of /opt/conda MPICH 3.3.2, rank partials "
                          "summed by MPI_Allreduce(MPI_SUM)")

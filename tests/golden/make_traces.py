@@ -112,6 +112,28 @@ VARIANTS = {"reordered": 1,          # 8 interleaved partial sums (a vectorising
             "mpi2": 102, "mpi3": 103, "mpi4": 104, "mpi8": 108, "mpi16": 116}
 DEFAULT_VARIANTS = ("reordered", "reordered_blocked")
 
+# What each record pins, and the oracle revision that produced it (stamped into every record).
+#   bit_exact  -- the GPU (short-vector arithmetic, exact_max raised where needed) and the CPU path must
+#                 give these bits: C1 here, every record of mpi_traces.json / mpich_traces.json.  They
+#                 change whenever the shared host algebra changes (iterative-solver_amd/include/itsolv_hbm/
+#                 dense.h); all are regenerated here in seconds.
+#   tolerance  -- N >= 2^21: held to the trace bar (tests/trace_check.py: same steps, eigenvalues to 1e-10,
+#                 errors within the reference's own deviation under reordered sums), which absorbs valid
+#                 re-roundings, including a revision of the host algebra; the N = 1e8 ones need a host with
+#                 more memory than this container, so they keep the revision that produced them.
+BIT_EXACT = ("C1_rank1", "C1_rank8")
+# (A faster sym_eigen -- dlartg-form rotation radii, 4-sum tridiagonal dots: 20-30 % less host time --
+# was tried in round 6 and not adopted: it moved the reference's own linear-equations criterion
+# (test_LinearEquationsF.f90:80, residual <= 1e-4 on its ill-conditioned i+j+1 matrix, a value set by
+# rounding) from 8.7e-5 to 1.04e-4 in one of the CPU path's summation-order variants.)
+ORACLE_REVISION = "r5: dense.h sym_eigen with std::hypot rotation radii and sequential tridiagonal dots"
+
+
+def stamp(name, rec, revision=ORACLE_REVISION):
+    rec["parity"] = "bit_exact" if name in BIT_EXACT else "tolerance"
+    rec["oracle_revision"] = revision
+    return rec
+
 
 def variant_record(c, r, v):
     """Deviation of variant run v from the reference run r (dict of trace arrays)."""
@@ -177,7 +199,7 @@ def run(name, variants=DEFAULT_VARIANTS, base=None):
     }
     for key in variants:
         out[key] = variant_record(c, r, runs[key])
-    return name, out
+    return name, stamp(name, out)
 
 
 def _run_args(args):
@@ -223,7 +245,7 @@ def merge_parts(parts):
     for p in parts:
         if p["part"] != "base":
             out[p["part"]] = variant_record(c, base, p)
-    return base["case"], out
+    return base["case"], stamp(base["case"], out)
 
 
 # Short-vector cases for rank-order sums (tests/golden/mpi_traces.json): the whole solve record -- every
@@ -254,7 +276,8 @@ def mpi_golden(out_path):
     import oracle
 
     out = {"_generator": "tests/golden/make_traces.py --mpi-golden: oracle (reference CPU path restated, "
-                         "-ffp-contract=off), dots in the rank order of P MPI ranks"}
+                         "-ffp-contract=off), dots in the rank order of P MPI ranks",
+           "_parity": "bit_exact", "_oracle_revision": ORACLE_REVISION}
     for name, c in MPI_CASES.items():
         fn = oracle.davidson_synthetic if c["kind"] == "davidson" else oracle.diis_synthetic
         rec = {"case": c, "options": mpi_options(c)}

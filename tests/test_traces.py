@@ -106,3 +106,28 @@ def test_openmp_oracle_is_bit_identical_to_the_sequential_cpu_path():
         assert r.returncode == 0, r.stderr[-3000:]
         runs.append(r.stdout)
     assert runs[0] == runs[1]
+
+
+def test_fixture_parity_classes_and_revisions():
+    # Every committed trace says what it pins and which oracle revision wrote it (make_traces.py
+    # BIT_EXACT / ORACLE_REVISION): the bit-exact fixtures (C1, and every record of mpi_traces.json and
+    # mpich_traces.json) carry the current revision of the shared host algebra; the tolerance traces
+    # (N >= 2^21) may carry an older one, which their bar absorbs.
+    import sys
+
+    golden = os.path.join(os.path.dirname(__file__), "golden")
+    sys.path.insert(0, golden)
+    from make_traces import BIT_EXACT, ORACLE_REVISION
+
+    for name, rec in T.items():
+        if name.startswith("_"):
+            continue
+        assert rec["parity"] == ("bit_exact" if name in BIT_EXACT else "tolerance"), name
+        assert rec["oracle_revision"].split(":")[0] in ("r5",), name
+        if rec["parity"] == "bit_exact":
+            assert rec["oracle_revision"] == ORACLE_REVISION, name
+        else:
+            assert rec["case"]["n"] >= 1 << 21, name
+    for f in ("mpi_traces.json", "mpich_traces.json"):
+        d = json.load(open(os.path.join(golden, f)))
+        assert d["_parity"] == "bit_exact" and d["_oracle_revision"] == ORACLE_REVISION, f
