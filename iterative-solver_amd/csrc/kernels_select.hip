@@ -235,12 +235,11 @@ __global__ __launch_bounds__(kBlock) void k_radix_compact(const RadixArgs a, siz
 
 // Single pass for a small n (nsel <= K <= 16; the solvers select nroots and max_p elements): every
 // thread keeps its K best composites in registers, sorted, while it streams its elements (radix_stream's
-// order).  The lists then meet in three merges, each "the K best of two sorted lists are the elementwise
-// better of one and the other reversed (a bitonic sequence), sorted by a bitonic clean-up": the wave's
-// 64 lists through lane shuffles, the workgroup's 4 wave lists through LDS, and -- in the last
-// workgroup to arrive -- every workgroup's list.  One read of the shard, one launch, no host round
-// trip; the radix path needs a histogram pass and a host decision per digit, a compaction pass and the
-// tile levels (k_select_tile) after it.
+// order).  The workgroup's 256 lists then meet in a 4-way merge tree in LDS (4 levels of K-step merges),
+// and the last workgroup to arrive merges every workgroup's list the same way.  One read of the shard,
+// one launch, no host round trip; the radix path needs a histogram pass and a host decision per digit,
+// a compaction pass and the tile levels (k_select_tile) after it.  (Round 6 first merged the lists by
+// lane-shuffle butterflies of bitonic merges: 0.08 / 0.15 ms per call for K = 8 / 16, mostly merging.)
 constexpr size_t kLocalMaxK = 16;
 
 // Field-wise selects: a select between two whole Cand values becomes a select between their
@@ -284,41 +283,52 @@ __device__ __forceinline__ void cand_merge(Cand (&L)[K], const Cand (&P)[K]) {
   }
 }
 
-// Butterfly over lane distances 1, 2, .., 2^(R-1): afterwards every lane holds the merge of its
-// 2^R-lane group's lists.
-template <int K, int R>
-__device__ __forceinline__ void wave_merge(Cand (&L)[K]) {
+// The K best of four sorted lists (best first) in LDS, into registers: K steps, each taking the better
+// head of four (a tournament of three comparisons).  At step s the four read positions sum to s, so
+// none passes K - 1.
+template <int K>
+__device__ __forceinline__ void merge4_lds(const Cand* l0, const Cand* l1, const Cand* l2, const Cand* l3,
+                                           Cand (&out)[K]) {
+  int i0 = 0, i1 = 0, i2 = 0, i3 = 0;
 #pragma unroll
-  for (int sd = 0; sd < R; ++sd) {
-    Cand P[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      P[j].key = __shfl_xor(L[j].key, 1 << sd, 64);
-      P[j].idx = __shfl_xor(L[j].idx, 1 << sd, 64);
-    }
-    cand_merge<K>(L, P);
+  for (int s = 0; s < K; ++s) {
+    const Cand h0 = l0[i0], h1 = l1[i1], h2 = l2[i2], h3 = l3[i3];
+    const bool a01 = !better(h1, h0), a23 = !better(h3, h2);  // ties: the earlier list
+    const Cand w01 = cand_pick(a01, h0, h1), w23 = cand_pick(a23, h2, h3);
+    const bool lo = !better(w23, w01);
+    out[s] = cand_pick(lo, w01, w23);
+    i0 += lo && a01;
+    i1 += lo && !a01;
+    i2 += !lo && a23;
+    i3 += !lo && !a23;
   }
 }
 
-// The workgroup's 4 wave lists (every lane of a wave holds its wave's) merged into wave 0's lanes.
+// Every thread's list (registers, sorted) merged into s_lists[0] by a 4-way tree in LDS
+// (256 -> 64 -> 16 -> 4 -> 1 lists).
 template <int K>
-__device__ __forceinline__ void block_merge(Cand (&L)[K], Cand (&s_lists)[kBlock / 64][K]) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0)
+__device__ __forceinline__ void block_tree(const Cand (&L)[K], Cand (&s_lists)[kBlock][K]) {
+  const int t = threadIdx.x;
 #pragma unroll
-    for (int j = 0; j < K; ++j) s_lists[wave][j] = L[j];
+  for (int j = 0; j < K; ++j) s_lists[t][j] = L[j];
   __syncthreads();
-  if (wave == 0) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) L[j] = lane < kBlock / 64 ? s_lists[lane][j] : Cand{0ull, 0ull};
-    wave_merge<K, 2>(L);
+  for (int q = kBlock / 4; q >= 1; q /= 4) {
+    Cand o[K];
+    if (t < q) merge4_lds<K>(s_lists[4 * t], s_lists[4 * t + 1], s_lists[4 * t + 2], s_lists[4 * t + 3], o);
+    __syncthreads();
+    if (t < q)
+#pragma unroll
+      for (int j = 0; j < K; ++j) s_lists[t][j] = o[j];
+    __syncthreads();
   }
 }
 
 template <int MODE, int K>
 __global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size_t offset, Cand* wg_lists, Cand* out,
                                                          unsigned* counter) {
-  __shared__ Cand s_lists[kBlock / 64][K];
+  static_assert(kBlock == 256, "block_tree: 4^4 lists");
+  __shared__ Cand s_lists[kBlock][K];
   __shared__ unsigned s_last;
   Cand L[K];
 #pragma unroll
@@ -326,43 +336,46 @@ __global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size
   radix_stream<MODE>(a, [&](unsigned long long key, unsigned long long i, bool ok) {
     if (ok) cand_insert<K>(L, Cand{key, offset + i});
   });
-  wave_merge<K, 6>(L);
-  block_merge<K>(L, s_lists);
+  block_tree<K>(L, s_lists);
   // This workgroup's list, written through to the device scope (agent-scope atomic stores), then the
   // arrival; the last arriver reads every list with agent-scope loads (the fold_tail pattern).
-  if (threadIdx.x == 0) {
-    Cand* o = wg_lists + size_t(blockIdx.x) * K;
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      __hip_atomic_store(&o[j].key, L[j].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&o[j].idx, L[j].idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  if (threadIdx.x < K) {
+    Cand* o = wg_lists + size_t(blockIdx.x) * K + threadIdx.x;
+    __hip_atomic_store(&o->key, s_lists[0][threadIdx.x].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&o->idx, s_lists[0][threadIdx.x].idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x < 64) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's list stores have completed
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (!s_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the loads are agent-scope
+  // The workgroups' lists, kBlock at a time through the same tree; the running result rides along as
+  // thread 0's input of the next chunk.
+  Cand acc[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) L[j] = Cand{0ull, 0ull};
-  for (unsigned g = threadIdx.x; g < gridDim.x; g += kBlock) {
+  for (int j = 0; j < K; ++j) acc[j] = Cand{0ull, 0ull};
+  for (unsigned base = 0; base < gridDim.x; base += kBlock) {
+    const unsigned g = base + threadIdx.x;
     Cand P[K];
-    const Cand* w = wg_lists + size_t(g) * K;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      P[j].key = __hip_atomic_load(&w[j].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      P[j].idx = __hip_atomic_load(&w[j].idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      P[j] = Cand{0ull, 0ull};
+      if (g < gridDim.x) {
+        P[j].key = __hip_atomic_load(&wg_lists[size_t(g) * K + j].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        P[j].idx = __hip_atomic_load(&wg_lists[size_t(g) * K + j].idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
-    cand_merge<K>(L, P);
-  }
-  wave_merge<K, 6>(L);
-  __syncthreads();  // s_lists is reused
-  block_merge<K>(L, s_lists);
-  if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && base > 0) cand_merge<K>(P, acc);
+    __syncthreads();  // s_lists is reused
+    block_tree<K>(P, s_lists);
 #pragma unroll
-    for (int j = 0; j < K; ++j) out[j] = L[j];
-    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+    for (int j = 0; j < K; ++j) acc[j] = s_lists[0][j];
   }
+  if (threadIdx.x < K) out[threadIdx.x] = s_lists[0][threadIdx.x];  // = acc (LDS: no register indexing)
+  if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Fixes digits of the composite threshold until at most kRadixCap elements lie at or above it,

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
 # host algebra clock), and a kernel trace of the C4-shard solve.
-#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,gputests
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,gputests
 # Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
 # the session.
 set -u -o pipefail
@@ -63,6 +63,27 @@ for s in ${1//,/ }; do
       ;;
     outerab)
       step outerab 400 python -u tools/outer_cu_ab.py --out "$OUT/outer_cu_ab.json" || exit $?
+      ;;
+    selsizes)
+      for n in 1.5e5 1.25e6 1.25e7 1e8; do
+        step "selsize_$n" 200 python -u tools/select_probe.py $n --nsel 8,16 || exit $?
+      done
+      ;;
+    kernargab)
+      for round in 1 2; do
+        step "ka_default_$round" 120 python -u tools/trace_c4.py --repeat 6 --tag default || exit $?
+        HIP_FORCE_DEV_KERNARG=1 step "ka_dev_$round" 120 python -u tools/trace_c4.py --repeat 6 --tag dev_kernarg || exit $?
+        HIP_FORCE_DEV_KERNARG=0 step "ka_host_$round" 120 python -u tools/trace_c4.py --repeat 6 --tag host_kernarg || exit $?
+        HSA_KERNARG_POOL_SIZE=33554432 step "ka_pool_$round" 120 python -u tools/trace_c4.py --repeat 6 --tag pool32m || exit $?
+      done
+      ;;
+    kernargab2)
+      for round in 1 2 3; do
+        step "kb_default_$round" 120 python -u tools/trace_c4.py --repeat 6 --tag default || exit $?
+        HIP_FORCE_DEV_KERNARG=1 step "kb_dev_$round" 120 python -u tools/trace_c4.py --repeat 6 --tag dev_kernarg || exit $?
+        HSA_KERNARG_POOL_SIZE=33554432 step "kb_pool_$round" 120 python -u tools/trace_c4.py --repeat 6 --tag pool32m || exit $?
+        HIP_FORCE_DEV_KERNARG=1 HSA_KERNARG_POOL_SIZE=33554432 step "kb_both_$round" 120 python -u tools/trace_c4.py --repeat 6 --tag both || exit $?
+      done
       ;;
     gputests)
       step gputests 1500 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests || exit $?

@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=12_500_000)
     ap.add_argument("--repeat", type=int, default=3)
+    ap.add_argument("--tag", default="")
     a = ap.parse_args()
     ctx = sh.Context(0)
     for rep in range(a.repeat):
@@ -31,7 +32,7 @@ def main():
         r = ih.davidson_synthetic(ctx, a.n, n_local=0, solutions=False, **C3)
         ctx.synchronize()
         wall = time.perf_counter() - t0
-        print(json.dumps({"rep": rep, "wall_ms": round(1e3 * wall, 3), "iterations": r["iterations"],
+        print(json.dumps({"tag": a.tag, "rep": rep, "wall_ms": round(1e3 * wall, 3), "iterations": r["iterations"],
                           "host_algebra_ms": round(1e3 * r["host_algebra"]["seconds"], 3),
                           "host_algebra_calls": r["host_algebra"]["calls"]}), flush=True)
         time.sleep(0.01)  # a marker gap between solves in the trace
