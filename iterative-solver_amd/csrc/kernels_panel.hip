@@ -1580,7 +1580,7 @@ int ssp_scal_inner(ssp_ctx* ctx, double alpha, double* x, const double* const* y
   } else {
     SSP_TRY(ssp::fold_begin(ctx, m, &tail));
     ssp::LedgerScope ls(ctx, "scal_inner", 8.0 * n * (2.0 + m));
-    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, 8);
+    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, unsigned(ctx->fused_per_cu));
     ScalInnerArgs a{};
     a.x = x;
     a.alpha = alpha;
@@ -1624,7 +1624,7 @@ int ssp_axpy_norm(ssp_ctx* ctx, const double* c, const double* x, double* const*
   } else {
     SSP_TRY(ssp::fold_begin(ctx, 1, &tail));
     ssp::LedgerScope ls(ctx, "axpy_norm", 8.0 * n * (1.0 + 2.0 * m));
-    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, 8);
+    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, unsigned(ctx->fused_per_cu));
     AxpyInnerArgs a{};
     a.x = x;
     a.m = m;
@@ -1677,7 +1677,7 @@ int ssp_axpy_gram(ssp_ctx* ctx, const double* c, double* x, double xs, int store
     SSP_TRY(ssp::fold_begin(ctx, m, &tail));
     const bool st = store_x && xs != 1.0;
     ssp::LedgerScope ls(ctx, "axpy_gram", 8.0 * n * ((st ? 2.0 : 1.0) + 2.0 * m));
-    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, 8);
+    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, unsigned(ctx->fused_per_cu));
     AxpyGramArgs a{};
     a.x = x;
     a.xs = xs;
@@ -1742,7 +1742,7 @@ int ssp_axpy_pairs_norm(ssp_ctx* ctx, const double* c, const double* const* xx, 
   } else {
     SSP_TRY(ssp::fold_begin(ctx, m, &tail));
     ssp::LedgerScope ls(ctx, "axpy_pairs_norm", 24.0 * n * m);
-    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, 8);
+    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, unsigned(ctx->fused_per_cu));
     AxpyPairsArgs a{};
     a.m = m;
     a.n = n;
@@ -1798,7 +1798,7 @@ int ssp_axpy_inner(ssp_ctx* ctx, const double* c, const double* x, double* const
   } else {
     if (m <= ssp::kOuterDst) SSP_TRY(ssp::fold_begin(ctx, m, &tail));  // one launch: fused fold
     ssp::LedgerScope ls(ctx, "axpy_inner", 8.0 * n * (2.0 + 2.0 * m));
-    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, 8);
+    const unsigned grid = ssp::win_grid(ctx, n, kFusedU, unsigned(ctx->fused_per_cu));
     for (int j0 = 0; j0 < m; j0 += ssp::kOuterDst) {
       AxpyInnerArgs a{};
       a.m = std::min(ssp::kOuterDst, m - j0);
@@ -1859,7 +1859,7 @@ int transform_impl(ssp_ctx* ctx, const double* t, double* const* xx, const doubl
   ssp::FoldTail tail{};
   if (n > 0) {
     ssp::LedgerScope ls(ctx, dots ? "transform_gram" : "transform", 16.0 * n * m);
-    const unsigned grid = ssp::win_grid(ctx, n, fused == 2 ? 1 : (m <= 4 ? 4 : 2), 8);
+    const unsigned grid = ssp::win_grid(ctx, n, fused == 2 ? 1 : (m <= 4 ? 4 : 2), unsigned(ctx->fused_per_cu));
     const bool pass = fused == 2 && gram_reduce_pass();
     if (fused) {
       SSP_TRY(ssp::fold_begin(ctx, nd, &tail));
@@ -1947,7 +1947,7 @@ int ssp_precondition_norms(ssp_ctx* ctx, double* const* a, int nvec, const doubl
   ssp::FoldTail tail{};
   {
     ssp::LedgerScope ls(ctx, "precondition", 8.0 * n * (1 + 2 * nvec));
-    const unsigned grid = ssp::win_grid(ctx, n, 4, 8);
+    const unsigned grid = ssp::win_grid(ctx, n, 4, unsigned(ctx->fused_per_cu));
     SSP_TRY(ssp::fold_begin(ctx, nvec, &tail));
     SSP_TRY(ssp::ensure_partial(ctx, size_t(grid) * nvec));
     p.partial = ctx->partial;

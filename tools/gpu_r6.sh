@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
 # host algebra clock), and a kernel trace of the C4-shard solve.
-#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,gputests
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
 # Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
 # the session.
 set -u -o pipefail
@@ -84,6 +84,9 @@ for s in ${1//,/ }; do
         HSA_KERNARG_POOL_SIZE=33554432 step "kb_pool_$round" 120 python -u tools/trace_c4.py --repeat 6 --tag pool32m || exit $?
         HIP_FORCE_DEV_KERNARG=1 HSA_KERNARG_POOL_SIZE=33554432 step "kb_both_$round" 120 python -u tools/trace_c4.py --repeat 6 --tag both || exit $?
       done
+      ;;
+    fusedab)
+      step fusedab 400 python -u tools/fused_cu_ab.py --out "$OUT/fused_cu_ab.json" || exit $?
       ;;
     gputests)
       step gputests 1500 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests || exit $?
