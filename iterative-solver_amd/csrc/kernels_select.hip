@@ -256,12 +256,21 @@ __device__ __forceinline__ void cand_cswap(Cand& a, Cand& b) {  // a <- better, 
   b = cand_pick(sw, x, y);
 }
 
+// c into the sorted list L (best first) when it beats the last entry.  The K comparisons with c are
+// independent of one another (c's position is where they turn true), and every entry is then
+// chosen from the old list -- its own value, c, or its predecessor -- so nothing waits on a chain of
+// compare-and-swaps (a 15-deep chain of dependent 64-bit compares per insertion before).
 template <int K>
 __device__ __forceinline__ void cand_insert(Cand (&L)[K], Cand c) {
   if (!better(c, L[K - 1])) return;
-  L[K - 1] = c;
+  bool b[K];
 #pragma unroll
-  for (int j = K - 1; j > 0; --j) cand_cswap<K>(L[j - 1], L[j]);
+  for (int j = 0; j < K; ++j) b[j] = better(c, L[j]);
+  Cand N[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) N[j] = cand_pick(!b[j], L[j], j > 0 && b[j > 0 ? j - 1 : 0] ? L[j > 0 ? j - 1 : 0] : c);
+#pragma unroll
+  for (int j = 0; j < K; ++j) L[j] = N[j];
 }
 
 // L <- the K best of the sorted lists L and P (both best first), sorted.  Counted loops with
