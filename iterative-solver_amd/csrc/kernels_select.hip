@@ -16,8 +16,9 @@
 //  2. Each workgroup sorts a tile of up to 2048 candidates in LDS with a bitonic network
 //     (descending) and keeps its best n; levels repeat until one tile remains.
 //  1'. For n <= 16 (the solvers' selections: nroots, max_p) one pass instead: each thread keeps its
-//     best K in registers, each wave merges its lanes' lists by shuffles and writes its K best
-//     (k_select_local) -- no host round trip per digit.
+//     best K in registers, 4-way merge trees in LDS reduce a workgroup's lists to one, and the last
+//     workgroup to arrive merges those and publishes the selected (index, value) pairs to the host
+//     (k_select_local) -- one launch and no host round trip per digit.
 // Ranks then all-gather their local best n and every rank merges the same candidate set with the
 // same order on the host (deterministic, identical on all ranks).
 #include <algorithm>
@@ -273,21 +274,122 @@ __device__ __forceinline__ void cand_insert(Cand (&L)[K], Cand c) {
   for (int j = 0; j < K; ++j) L[j] = N[j];
 }
 
-// L <- the K best of the sorted lists L and P (both best first), sorted.  Counted loops with
-// compile-time trip counts only: a shift-stepped loop was left rolled, and its uniform index sent L to
-// scratch memory (2.3 ms per call at 12.5e6 elements).
-template <int K>
-__device__ __forceinline__ void cand_merge(Cand (&L)[K], const Cand (&P)[K]) {
+// L <- the K best of the sorted list L and the H-entry sorted list c (both best first; c stands for
+// the K-list c followed by padding), sorted: the better of L[K-1-i] and c[i] (a bitonic sequence
+// holding the K best), then a bitonic clean.  Counted loops with compile-time trip counts only: a
+// shift-stepped loop was left rolled, and its uniform index sent L to scratch memory (2.3 ms per call
+// at 12.5e6 elements).
+template <int K, int H>
+__device__ __forceinline__ void cand_merge_into(Cand (&L)[K], const Cand (&c)[H]) {
   constexpr int kLogK = K == 8 ? 3 : 4;
-  static_assert(K == 8 || K == 16, "cand_merge: K is 8 or 16");
+  static_assert((K == 8 || K == 16) && H <= K, "cand_merge_into: K is 8 or 16, H <= K");
 #pragma unroll
-  for (int j = 0; j < K; ++j) L[j] = cand_pick(better(L[j], P[K - 1 - j]), L[j], P[K - 1 - j]);
+  for (int i = 0; i < H; ++i) L[K - 1 - i] = cand_pick(better(L[K - 1 - i], c[i]), L[K - 1 - i], c[i]);
 #pragma unroll
   for (int sh = 0; sh < kLogK; ++sh) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const int h = (K / 2) >> sh;
       if ((j & h) == 0) cand_cswap<K>(L[j], L[j + h]);
+    }
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void cand_merge(Cand (&L)[K], const Cand (&P)[K]) {
+  cand_merge_into<K, K>(L, P);
+}
+
+// Sorts 8 candidates, best first (the 19-comparator network).
+__device__ __forceinline__ void sort8(Cand (&c)[8]) {
+  constexpr int kNet[19][2] = {{0, 2}, {1, 3}, {4, 6}, {5, 7}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {0, 1}, {2, 3},
+                               {4, 5}, {6, 7}, {2, 4}, {3, 5}, {1, 4}, {3, 6}, {1, 2}, {3, 4}, {5, 6}};
+#pragma unroll
+  for (int s = 0; s < 19; ++s) cand_cswap<8>(c[kNet[s][0]], c[kNet[s][1]]);
+}
+
+// The largest head h (a lane's best key) that at least K heads of the wave reach (0 if none): K
+// entries of the wave have a key >= it, so a key below it cannot be among the K best.  seg: the
+// wave's 64 LDS slots; every lane of the wave takes part.
+template <int K>
+__device__ __forceinline__ unsigned long long wave_threshold(unsigned long long h, unsigned long long* seg) {
+  __builtin_amdgcn_wave_barrier();
+  seg[__lane_id()] = h;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  int cnt = 0;
+#pragma unroll 16
+  for (int j = 0; j < 64; ++j) cnt += seg[j] >= h;
+  unsigned long long prop = cnt >= K ? h : 0ull;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const unsigned long long o = __shfl_xor(prop, off, 64);
+    prop = o > prop ? o : prop;
+  }
+  return prop;
+}
+
+// k_select_local's pass over the shard (radix_stream's order and slots): each lane's 8 elements of an
+// iteration that beat both its list's last entry and the wave threshold T are sorted by a network and
+// merged into the list at once (one merge instead of up to 8 insertions, each a K-wide compare and
+// select); T is refreshed after the first merge and after every later one that follows an element
+// T turned away (a refresh when T filters nothing -- ascending data -- is wasted).  The guarded tail
+// inserts one element at a time.
+template <int MODE, int K>
+__device__ __forceinline__ void select_stream(const RadixArgs& a, size_t offset, Cand (&L)[K], unsigned long long* seg) {
+  static_assert(kRadixU == 4, "select_stream: 8 elements per lane and iteration");
+  const size_t stride = size_t(gridDim.x) * kBlock, npair = a.n / 2, n2 = (a.n + 1) / 2;
+  size_t p0 = size_t(blockIdx.x) * kBlock;
+  unsigned long long T = 0;
+  bool stale = true;  // wave-uniform: refresh T at the next merge (T has turned an element away since)
+  for (; p0 + (kRadixU - 1) * stride + kBlock <= npair; p0 += kRadixU * stride) {
+    double2 xv[kRadixU], yv[kRadixU];
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) {
+      const size_t i = 2 * (p0 + threadIdx.x + u * stride);
+      xv[u] = ssp::ld2nt(a.x + i);
+      if (MODE == 1) yv[u] = ssp::ld2nt(a.y + i);
+    }
+    Cand c[2 * kRadixU];
+    bool any = false, rej = false;
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const unsigned long long key =
+            elem_key<MODE>(a, e ? xv[u].y : xv[u].x, MODE == 1 ? (e ? yv[u].y : yv[u].x) : 0.0);
+        const Cand ce{key, offset + 2 * (p0 + threadIdx.x + u * stride) + e};
+        const bool b = better(ce, L[K - 1]), keep = b && key >= T;
+        c[2 * u + e] = cand_pick(keep, ce, Cand{0ull, 0ull});
+        any |= keep;
+        rej |= b && !keep;
+      }
+    }
+    stale |= __ballot(rej) != 0;
+    if (__ballot(any) == 0) continue;
+    if (any) {
+      sort8(c);
+      cand_merge_into<K, 2 * kRadixU>(L, c);
+    }
+    if (stale) {  // skipped while T turns nothing away (e.g. every element better than the last)
+      const unsigned long long t = wave_threshold<K>(L[0].key, seg);
+      T = t > T ? t : T;
+      stale = false;
+    }
+  }
+  for (; p0 < n2; p0 += kRadixU * stride) {
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) {
+      const size_t i = 2 * (p0 + threadIdx.x + u * stride);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const bool ok = i + e < a.n;
+        const double xe = ok ? a.x[i + e] : 0.0;
+        const double ye = (MODE == 1 && ok) ? a.y[i + e] : 0.0;
+        const unsigned long long key = elem_key<MODE>(a, xe, ye);
+        if (ok && key >= T) cand_insert<K>(L, Cand{key, offset + i + e});
+      }
     }
   }
 }
@@ -333,19 +435,106 @@ __device__ __forceinline__ void block_tree(const Cand (&L)[K], Cand (&s_lists)[k
   }
 }
 
+// The block_tree result by a threshold and ranks, for lists whose best entries are few.  T is the
+// largest head (L[0].key) that at least K heads of its wave reach: K entries of the workgroup have a
+// key >= T, so an entry whose key is below T is beaten by K others and cannot be among the K best.
+// The entries at or above T (M of them, at least K) are collected in LDS, and each one's rank --
+// the entries better than it, plus equal composites at lower slots (only the empty-slot padding
+// repeats) -- places it; ranks 0..K-1 are the result.  No chain of dependent merge steps: a count
+// over 64 heads and one over M candidates.  When more than kBlock entries pass (spread-out data,
+// short shards with padded lists), the tree merges instead; the result is the same either way.
+template <int K>
+__device__ __forceinline__ void block_rank(const Cand (&L)[K], Cand (&s_lists)[kBlock][K], bool rank) {
+  __shared__ unsigned long long s_heads[kBlock];
+  __shared__ Cand s_c[kBlock];
+  __shared__ unsigned long long s_t;
+  __shared__ unsigned s_m;
+  if (!rank) return block_tree<K>(L, s_lists);
+  const int t = threadIdx.x;
+  const unsigned long long h = L[0].key;
+  if (t == 0) {
+    s_t = 0ull;
+    s_m = 0u;
+  }
+  s_heads[t] = h;
+  __syncthreads();
+  const unsigned long long* wh = s_heads + (t & ~63);
+  int cnt = 0;
+#pragma unroll 16
+  for (int j = 0; j < 64; ++j) cnt += wh[j] >= h;
+  unsigned long long prop = cnt >= K ? h : 0ull;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const unsigned long long o = __shfl_xor(prop, off, 64);
+    prop = o > prop ? o : prop;
+  }
+  if ((t & 63) == 0) atomicMax(&s_t, prop);
+  __syncthreads();
+  const unsigned long long T = s_t;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) c += L[j].key >= T;
+  unsigned pos = 0;
+  if (c) pos = atomicAdd(&s_m, unsigned(c));
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    if (j < c && pos + j < unsigned(kBlock)) s_c[pos + j] = L[j];
+  __syncthreads();
+  const unsigned M = s_m;
+  if (M > unsigned(kBlock)) return block_tree<K>(L, s_lists);  // uniform: M is read after the barrier
+  if (unsigned(t) < M) {
+    const Cand me = s_c[t];
+    int r = 0;
+    for (unsigned j = 0; j < M; ++j) {
+      const Cand o = s_c[j];
+      r += better(o, me) || (o.key == me.key && o.idx == me.idx && j < unsigned(t));
+    }
+    if (r < K) s_lists[0][r] = me;
+  }
+  __syncthreads();
+}
+
+// Where the last workgroup of k_select_local leaves the result: the K best composites in `out`
+// (device), or -- host != nullptr -- the first `real` of them as (global index bits, returned value)
+// pairs written through to coherent host memory, then `seq` in `flag` (k_publish's protocol, without
+// the k_select_values and k_publish launches).
+struct LocalOut {
+  Cand* out;
+  bool rank;  // block_rank's threshold-and-rank merge (else the LDS tree alone)
+  double* host;
+  unsigned long long* flag;
+  unsigned long long seq;
+  int real;
+};
+
+// The value the reference returns for a selected element (select.h:52: max ? v' : -v', so the sign
+// of a zero is the element's, not the key's); k_select_values computes the same.
+template <int MODE>
+__device__ __forceinline__ double returned_value(const RadixArgs& a, size_t li) {
+  const double xv = a.x[li];
+  if (MODE == 1) return fabs(xv * a.y[li]);
+  const double v = a.neg ? (a.abs ? -fabs(xv) : -xv) : (a.abs ? fabs(xv) : xv);
+  return a.neg ? -v : v;
+}
+
 template <int MODE, int K>
-__global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size_t offset, Cand* wg_lists, Cand* out,
-                                                         unsigned* counter) {
+__global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size_t offset, Cand* wg_lists,
+                                                         const LocalOut lo, unsigned* counter) {
   static_assert(kBlock == 256, "block_tree: 4^4 lists");
   __shared__ Cand s_lists[kBlock][K];
   __shared__ unsigned s_last;
   Cand L[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) L[j] = Cand{0ull, 0ull};  // sorts after every real candidate
-  radix_stream<MODE>(a, [&](unsigned long long key, unsigned long long i, bool ok) {
-    if (ok) cand_insert<K>(L, Cand{key, offset + i});
-  });
-  block_tree<K>(L, s_lists);
+  if (lo.rank) {
+    __shared__ unsigned long long s_wave[kBlock];
+    select_stream<MODE, K>(a, offset, L, s_wave + (threadIdx.x & ~63u));
+  } else {
+    radix_stream<MODE>(a, [&](unsigned long long key, unsigned long long i, bool ok) {
+      if (ok) cand_insert<K>(L, Cand{key, offset + i});
+    });
+  }
+  block_rank<K>(L, s_lists, lo.rank);
   // This workgroup's list, written through to the device scope (agent-scope atomic stores), then the
   // arrival; the last arriver reads every list with agent-scope loads (the fold_tail pattern).
   if (threadIdx.x < K) {
@@ -379,12 +568,27 @@ __global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size
     }
     if (threadIdx.x == 0 && base > 0) cand_merge<K>(P, acc);
     __syncthreads();  // s_lists is reused
-    block_tree<K>(P, s_lists);
+    block_rank<K>(P, s_lists, lo.rank);
 #pragma unroll
     for (int j = 0; j < K; ++j) acc[j] = s_lists[0][j];
   }
-  if (threadIdx.x < K) out[threadIdx.x] = s_lists[0][threadIdx.x];  // = acc (LDS: no register indexing)
-  if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // s_lists[0] = acc (read from LDS: no register indexing)
+  if (!lo.host) {
+    if (threadIdx.x < K) lo.out[threadIdx.x] = s_lists[0][threadIdx.x];
+  } else if (threadIdx.x < unsigned(lo.real)) {
+    const unsigned long long gi = s_lists[0][threadIdx.x].idx;
+    __hip_atomic_store(lo.host + 2 * threadIdx.x, __longlong_as_double((long long)gi), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(lo.host + 2 * threadIdx.x + 1, returned_value<MODE>(a, size_t(gi - offset)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x < 64) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's result stores have completed (real <= 16)
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lo.host) __hip_atomic_store(lo.flag, lo.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // Fixes digits of the composite threshold until at most kRadixCap elements lie at or above it,
@@ -510,7 +714,8 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
     SelectArgs a{};
     a.keep = keep;
     a.out = buf0;
-    bool local = false;  // k_select_local has left the K best in buf0
+    bool local = false;      // k_select_local has left the K best in buf0
+    bool published = false;  // ... or published the (index, value) pairs to the host itself
     if (radix && nsel <= kLocalMaxK) {
       // one pass, one launch: the K best (K = 8 or 16 >= nsel) of the shard into buf0, then the values
       // (k_select_local); two workgroups per CU (the K = 16 lists allow two waves per SIMD)
@@ -522,14 +727,35 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
       r.abs = ignore_sign;
       const unsigned lgrid = std::min<unsigned>(grid, unsigned(ctx->num_cus) * 2);
       const int K = nsel <= 8 ? 8 : 16;
-      SSP_TRY_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned), ctx->stream));
-      auto* cnt = reinterpret_cast<unsigned*>(counter);
-      if (mode == 1 && K == 8) SSP_LAUNCH((k_select_local<1, 8>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, buf0, cnt);
-      else if (mode == 1) SSP_LAUNCH((k_select_local<1, 16>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, buf0, cnt);
-      else if (K == 8) SSP_LAUNCH((k_select_local<0, 8>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, buf0, cnt);
-      else SSP_LAUNCH((k_select_local<0, 16>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, buf0, cnt);
+      // The arrival counter is the reduction tails' top counter (zero between launches: every last
+      // arriver resets it; one stream).  Unless results go by copy (SSP_PUBLISH=copy), the kernel
+      // publishes the (index, value) pairs itself.
+      unsigned* cnt = ctx->fold_counter + ssp::kFoldLine * ssp::kFoldShards;
+      const size_t real = std::min(n, nsel);
+      SSP_TRY(ssp::ensure_result(ctx, 2 * real));
+      LocalOut lo{buf0, ctx->select_rank, nullptr, nullptr, 0, int(real)};
+      if (!ctx->publish_copy) {
+        lo.host = ctx->result_host;
+        lo.flag = ctx->pub_flag;
+        lo.seq = ++ctx->pub_seq;
+      }
+      if (mode == 1 && K == 8) SSP_LAUNCH((k_select_local<1, 8>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, lo, cnt);
+      else if (mode == 1) SSP_LAUNCH((k_select_local<1, 16>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, lo, cnt);
+      else if (K == 8) SSP_LAUNCH((k_select_local<0, 8>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, lo, cnt);
+      else SSP_LAUNCH((k_select_local<0, 16>), dim3(lgrid), dim3(kBlock), 0, ctx->stream, r, offset, cand, lo, cnt);
       SSP_TRY_HIP(hipGetLastError());
       local = true;
+      if (lo.host) {
+        bool seen = true;
+        SSP_TRY(ssp::wait_flag(ctx, lo.seq, &seen, "select"));
+        for (size_t e = 0; e < real; ++e) {
+          unsigned long long gi;
+          std::memcpy(&gi, &ctx->result_host[2 * e], sizeof(gi));
+          sel_idx.push_back(size_t(gi));
+          sel_val.push_back(ctx->result_host[2 * e + 1]);
+        }
+        published = true;
+      }
     } else if (radix) {
       SSP_TRY(radix_candidates(ctx, mode, x, y, n, offset, nsel, max, ignore_sign, cand, hist, counter, grid, &count));
       tiles = (count + kTile - 1) / kTile;
@@ -567,18 +793,20 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
     }
     // The best `real` candidates of this rank (padding sorts after them when n < nsel): indices and
     // returned values in one published block.
-    const size_t real = std::min(n, nsel);
-    SSP_TRY(ssp::ensure_result(ctx, 2 * real));
-    SSP_LAUNCH(k_select_values, dim3(unsigned((real + 255) / 256)), dim3(256), 0, ctx->stream, cur, int(real), x,
-                       y, offset, mode, max, ignore_sign, ctx->result_dev);
-    SSP_TRY_HIP(hipGetLastError());
-    std::vector<double> pub(2 * real);
-    SSP_TRY(ssp::fetch_result(ctx, pub.data(), 2 * real));
-    for (size_t e = 0; e < real; ++e) {
-      unsigned long long gi;
-      std::memcpy(&gi, &pub[2 * e], sizeof(gi));
-      sel_idx.push_back(size_t(gi));
-      sel_val.push_back(pub[2 * e + 1]);
+    if (!published) {
+      const size_t real = std::min(n, nsel);
+      SSP_TRY(ssp::ensure_result(ctx, 2 * real));
+      SSP_LAUNCH(k_select_values, dim3(unsigned((real + 255) / 256)), dim3(256), 0, ctx->stream, cur, int(real), x,
+                 y, offset, mode, max, ignore_sign, ctx->result_dev);
+      SSP_TRY_HIP(hipGetLastError());
+      std::vector<double> pub(2 * real);
+      SSP_TRY(ssp::fetch_result(ctx, pub.data(), 2 * real));
+      for (size_t e = 0; e < real; ++e) {
+        unsigned long long gi;
+        std::memcpy(&gi, &pub[2 * e], sizeof(gi));
+        sel_idx.push_back(size_t(gi));
+        sel_val.push_back(pub[2 * e + 1]);
+      }
     }
   }
   // This rank's best n as (global index, returned value), then the fixed-size exchange: nsel

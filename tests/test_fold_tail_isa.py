@@ -225,3 +225,25 @@ def test_reduce_pass_publishes_before_it_arrives():
     assert found, "k_reduce_publish not emitted"
     for name, bad in found:
         assert not bad, (name, bad)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_select_lists_reach_the_last_workgroup_write_through():
+    """k_select_local: each workgroup's list is stored write-through (sc1) and drained before the
+    arrival add, and the last arriver reads the lists with sc1 loads.  Its only other loads after the
+    add are of the input shard (the selected elements' returned values: x, and y for select_max_dot),
+    which no workgroup of the launch writes."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "kernels_select.s")
+        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
+                            "-I" + CSRC, "--cuda-device-only", "-S", os.path.join(CSRC, "kernels_select.hip"), "-o", out],
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        found = [(name, fold_tail_violations(ins)) for name, ins in kernels(open(out).read())
+                 if "k_select_local" in name]
+    assert len(found) == 4, [n for n, _ in found]
+    for name, bad in found:
+        assert bad is not None, name
+        inputs = 2 if "k_select_localILi1E" in name else 1
+        assert all(b.startswith("(4) tail load without sc1") for b in bad), (name, bad)
+        assert len(bad) <= inputs, (name, bad)

@@ -426,6 +426,37 @@ def test_select_max_dot_radix_path(ctx, kind, nsel):
     assert idx.tolist() == ridx.tolist() and np.array_equal(val, rval)
 
 
+@pytest.mark.parametrize("publish,merge", [("kernel", "rank"), ("copy", "tree"), ("kernel", "tree")])
+def test_select_local_path_both_publications(monkeypatch, publish, merge):
+    # k_select_local's last workgroup publishes the (index, value) pairs to host memory itself; with
+    # SSP_PUBLISH=copy (read at context creation) the pairs go through k_select_values and a copy.
+    # SSP_SELECT_MERGE=tree: per-element insertion and the LDS tree instead of the batched merges,
+    # the wave threshold and the ranks.  All give the oracle's bits, twice in a row (the arrival
+    # counter is back at zero after a call).
+    import subspace_hip as sh
+
+    monkeypatch.setenv("SSP_PUBLISH", publish)
+    monkeypatch.setenv("SSP_SELECT_MERGE", merge)
+    n = 1_000_003
+    r = rng(17)
+    with sh.Context(0) as c:
+        x = np.round(r.uniform(-5, 5, n))
+        y = r.uniform(-1, 1, n)
+        dx, dy = c.upload(x), c.upload(y)
+        for nsel in (1, 8, 13, 16):
+            for mx, ab in ((False, False), (True, True)):
+                for _ in range(2):
+                    idx, val = c.select(dx, nsel, max=mx, ignore_sign=ab)
+                    ridx, rval = oracle.select(x, nsel, max=mx, ignore_sign=ab)
+                    assert idx.tolist() == ridx.tolist()
+                    assert np.array_equal(val, rval) and np.array_equal(np.signbit(val), np.signbit(rval))
+            idx, val = c.select_max_dot(dx, dy, nsel)
+            ridx, rval = oracle.select_max_dot(x, y, nsel)
+            assert idx.tolist() == ridx.tolist() and np.array_equal(val, rval)
+            # a reduction between selections shares the arrival counter
+            assert abs(c.dot(dx, dy) - oracle.dot(x, y)) <= red_tol(x * y)
+
+
 def test_select_diagonal_guess(ctx):
     # initial guess / P-space selection on diagonals (reference IterativeSolverTemplate.h:340, :354)
     d = oracle.synthetic_diagonal(200_000, 0.1, 1)[::-1].copy()

@@ -64,6 +64,9 @@ for s in ${1//,/ }; do
     outerab)
       step outerab 400 python -u tools/outer_cu_ab.py --out "$OUT/outer_cu_ab.json" || exit $?
       ;;
+    selab)
+      step selab 300 python -u tools/select_ab.py --out "$OUT/select_ab.json" || exit $?
+      ;;
     selsizes)
       for n in 1.5e5 1.25e6 1.25e7 1e8; do
         step "selsize_$n" 200 python -u tools/select_probe.py $n --nsel 8,16 || exit $?
