@@ -23,6 +23,7 @@
 // same order on the host (deterministic, identical on all ranks).
 #include <algorithm>
 #include <cstring>
+#include <optional>
 #include <vector>
 
 #include "ssp_internal.h"
@@ -435,30 +436,57 @@ __device__ __forceinline__ void block_tree(const Cand (&L)[K], Cand (&s_lists)[k
   }
 }
 
+// LDS of the threshold-and-rank merges (block_rank, and the last workgroup's final merge).
+struct RankLds {
+  unsigned long long heads[2 * kBlock];
+  Cand c[kBlock];  // the collected candidates
+  unsigned long long t;
+  unsigned m;      // their number
+};
+
+// Places the M collected candidates (R.c[0, M), M <= kBlock) by rank: each one's rank is the number
+// of candidates better than it, plus equal composites at lower slots (only the empty-slot padding
+// repeats), and ranks 0..K-1 go to s_lists[0].  8 candidates per step, their LDS reads issued
+// together (one read at a time left every step waiting on LDS latency); R.c has kBlock slots and
+// M <= kBlock, so j0 + 7 < kBlock, and slots at or past M are read and not counted.
+template <int K>
+__device__ __forceinline__ void rank_place(const RankLds& R, unsigned M, Cand (&s_lists)[kBlock][K]) {
+  const unsigned t = threadIdx.x;
+  if (t >= M) return;
+  const Cand me = R.c[t];
+  int r = 0;
+  for (unsigned j0 = 0; j0 < M; j0 += 8) {
+    Cand o[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) o[u] = R.c[j0 + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const unsigned j = j0 + u;
+      r += j < M && (better(o[u], me) || (o[u].key == me.key && o[u].idx == me.idx && j < t));
+    }
+  }
+  if (r < K) s_lists[0][r] = me;
+}
+
 // The block_tree result by a threshold and ranks, for lists whose best entries are few.  T is the
 // largest head (L[0].key) that at least K heads of its wave reach: K entries of the workgroup have a
 // key >= T, so an entry whose key is below T is beaten by K others and cannot be among the K best.
-// The entries at or above T (M of them, at least K) are collected in LDS, and each one's rank --
-// the entries better than it, plus equal composites at lower slots (only the empty-slot padding
-// repeats) -- places it; ranks 0..K-1 are the result.  No chain of dependent merge steps: a count
-// over 64 heads and one over M candidates.  When more than kBlock entries pass (spread-out data,
-// short shards with padded lists), the tree merges instead; the result is the same either way.
+// The entries at or above T (M of them, at least K) are collected in LDS and placed by rank
+// (rank_place).  No chain of dependent merge steps: a count over 64 heads and one over M
+// candidates.  When more than kBlock entries pass (spread-out data, short shards with padded lists),
+// the tree merges instead; the result is the same either way.
 template <int K>
-__device__ __forceinline__ void block_rank(const Cand (&L)[K], Cand (&s_lists)[kBlock][K], bool rank) {
-  __shared__ unsigned long long s_heads[kBlock];
-  __shared__ Cand s_c[kBlock];
-  __shared__ unsigned long long s_t;
-  __shared__ unsigned s_m;
+__device__ __forceinline__ void block_rank(const Cand (&L)[K], Cand (&s_lists)[kBlock][K], RankLds& R, bool rank) {
   if (!rank) return block_tree<K>(L, s_lists);
   const int t = threadIdx.x;
   const unsigned long long h = L[0].key;
   if (t == 0) {
-    s_t = 0ull;
-    s_m = 0u;
+    R.t = 0ull;
+    R.m = 0u;
   }
-  s_heads[t] = h;
+  R.heads[t] = h;
   __syncthreads();
-  const unsigned long long* wh = s_heads + (t & ~63);
+  const unsigned long long* wh = R.heads + (t & ~63);
   int cnt = 0;
 #pragma unroll 16
   for (int j = 0; j < 64; ++j) cnt += wh[j] >= h;
@@ -468,29 +496,21 @@ __device__ __forceinline__ void block_rank(const Cand (&L)[K], Cand (&s_lists)[k
     const unsigned long long o = __shfl_xor(prop, off, 64);
     prop = o > prop ? o : prop;
   }
-  if ((t & 63) == 0) atomicMax(&s_t, prop);
+  if ((t & 63) == 0) atomicMax(&R.t, prop);
   __syncthreads();
-  const unsigned long long T = s_t;
+  const unsigned long long T = R.t;
   int c = 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) c += L[j].key >= T;
   unsigned pos = 0;
-  if (c) pos = atomicAdd(&s_m, unsigned(c));
+  if (c) pos = atomicAdd(&R.m, unsigned(c));
 #pragma unroll
   for (int j = 0; j < K; ++j)
-    if (j < c && pos + j < unsigned(kBlock)) s_c[pos + j] = L[j];
+    if (j < c && pos + j < unsigned(kBlock)) R.c[pos + j] = L[j];
   __syncthreads();
-  const unsigned M = s_m;
+  const unsigned M = R.m;
   if (M > unsigned(kBlock)) return block_tree<K>(L, s_lists);  // uniform: M is read after the barrier
-  if (unsigned(t) < M) {
-    const Cand me = s_c[t];
-    int r = 0;
-    for (unsigned j = 0; j < M; ++j) {
-      const Cand o = s_c[j];
-      r += better(o, me) || (o.key == me.key && o.idx == me.idx && j < unsigned(t));
-    }
-    if (r < K) s_lists[0][r] = me;
-  }
+  rank_place<K>(R, M, s_lists);
   __syncthreads();
 }
 
@@ -501,6 +521,9 @@ __device__ __forceinline__ void block_rank(const Cand (&L)[K], Cand (&s_lists)[k
 struct LocalOut {
   Cand* out;
   bool rank;  // block_rank's threshold-and-rank merge (else the LDS tree alone)
+  // rank: the largest K-th best key over the workgroups (agent-scope atomic max; zero between
+  // launches, reset by the last workgroup), the final merge's threshold
+  unsigned long long* thresh;
   double* host;
   unsigned long long* flag;
   unsigned long long seq;
@@ -517,12 +540,21 @@ __device__ __forceinline__ double returned_value(const RadixArgs& a, size_t li) 
   return a.neg ? -v : v;
 }
 
+#ifdef SSP_SELECT_CLOCKS
+// Development probe (a build with -DSSP_SELECT_CLOCKS, never the shipped library): per-workgroup
+// phase times of k_select_local (100 MHz wall clock), summarised by the last workgroup with printf.
+__device__ unsigned long long g_sel_clk[4096][3];
+#endif
+
 template <int MODE, int K>
 __global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size_t offset, Cand* wg_lists,
                                                          const LocalOut lo, unsigned* counter) {
   static_assert(kBlock == 256, "block_tree: 4^4 lists");
   __shared__ Cand s_lists[kBlock][K];
   __shared__ unsigned s_last;
+#ifdef SSP_SELECT_CLOCKS
+  const unsigned long long c0 = wall_clock64();
+#endif
   Cand L[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) L[j] = Cand{0ull, 0ull};  // sorts after every real candidate
@@ -534,7 +566,20 @@ __global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size
       if (ok) cand_insert<K>(L, Cand{key, offset + i});
     });
   }
-  block_rank<K>(L, s_lists, lo.rank);
+#ifdef SSP_SELECT_CLOCKS
+  __syncthreads();
+  const unsigned long long c1 = wall_clock64();
+#endif
+  __shared__ RankLds s_rank;
+  block_rank<K>(L, s_lists, s_rank, lo.rank);
+#ifdef SSP_SELECT_CLOCKS
+  if (threadIdx.x == 0) {
+    const unsigned long long c2 = wall_clock64();
+    __hip_atomic_store(&g_sel_clk[blockIdx.x & 4095][0], c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&g_sel_clk[blockIdx.x & 4095][1], c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&g_sel_clk[blockIdx.x & 4095][2], c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#endif
   // This workgroup's list, written through to the device scope (agent-scope atomic stores), then the
   // arrival; the last arriver reads every list with agent-scope loads (the fold_tail pattern).
   if (threadIdx.x < K) {
@@ -542,20 +587,97 @@ __global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size
     __hip_atomic_store(&o->key, s_lists[0][threadIdx.x].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&o->idx, s_lists[0][threadIdx.x].idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // This list's K-th best key: K entries of the launch reach it, so it is a threshold for all of them.
+  if (lo.thresh && threadIdx.x == 0)
+    (void)__hip_atomic_fetch_max(lo.thresh, s_lists[0][K - 1].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x < 64) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's list stores have completed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's list stores (and the max) have completed
     if (threadIdx.x == 0)
       s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (!s_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the loads are agent-scope
-  // The workgroups' lists, kBlock at a time through the same tree; the running result rides along as
+#ifdef SSP_SELECT_CLOCKS
+  unsigned long long cc[3] = {(unsigned long long)wall_clock64(), 0, 0};
+  int nchunk = 0;
+#endif
+  // The final merge by a threshold: only list entries at or above it are collected (a prefix of each
+  // sorted list; most lists have none, and only their head is read), then placed by rank.  (Every
+  // list in full through block_rank, two chunks of 256 lists at the C4 shard, took 15 / 38 us of the
+  // 42 / 67 us K = 8 / 16 kernel.)  The threshold is the larger of two that K entries reach: the
+  // launch's largest K-th best key (tight when the best elements sit together, e.g. a sorted
+  // diagonal) and, per wave, the K-th best of its 2 x 64 workgroup heads (tight when they are spread
+  // out).  More than kBlock entries at the threshold (ties): the chunked merge below.
+  bool done = false;
+  if (lo.thresh && gridDim.x <= 2 * kBlock) {
+    const unsigned t = threadIdx.x;
+    if (t == 0) {
+      s_rank.t = __hip_atomic_load(lo.thresh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_rank.m = 0u;
+    }
+    unsigned long long hd[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const unsigned g = t + q * kBlock;
+      hd[q] = g < gridDim.x
+                  ? __hip_atomic_load(&wg_lists[size_t(g) * K].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                  : 0ull;
+      s_rank.heads[(t & ~63u) * 2 + q * 64 + (t & 63u)] = hd[q];
+    }
+    __syncthreads();
+    const unsigned long long* wh = s_rank.heads + (t & ~63u) * 2;
+    int cnt[2] = {0, 0};
+#pragma unroll 16
+    for (int j = 0; j < 128; ++j) {
+      const unsigned long long v = wh[j];
+      cnt[0] += v >= hd[0];
+      cnt[1] += v >= hd[1];
+    }
+    unsigned long long prop = cnt[0] >= K ? hd[0] : 0ull;
+    prop = cnt[1] >= K && hd[1] > prop ? hd[1] : prop;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const unsigned long long o = __shfl_xor(prop, off, 64);
+      prop = o > prop ? o : prop;
+    }
+    if ((t & 63u) == 0) atomicMax(&s_rank.t, prop);
+    __syncthreads();
+    const unsigned long long T = s_rank.t;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const unsigned g = t + q * kBlock;
+      const Cand* wl = wg_lists + size_t(g) * K;
+      if (g < gridDim.x && hd[q] >= T) {
+        Cand P[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          P[j].key = __hip_atomic_load(&wl[j].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          P[j].idx = __hip_atomic_load(&wl[j].idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) c += P[j].key >= T;
+        const unsigned pos = atomicAdd(&s_rank.m, unsigned(c));
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          if (j < c && pos + j < unsigned(kBlock)) s_rank.c[pos + j] = P[j];
+      }
+    }
+    __syncthreads();
+    const unsigned M = s_rank.m;
+    if (M <= unsigned(kBlock)) {  // uniform: read after the barrier
+      rank_place<K>(s_rank, M, s_lists);
+      __syncthreads();
+      done = true;
+    }
+  }
+  // The workgroups' lists, kBlock at a time through block_rank; the running result rides along as
   // thread 0's input of the next chunk.
   Cand acc[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) acc[j] = Cand{0ull, 0ull};
-  for (unsigned base = 0; base < gridDim.x; base += kBlock) {
+  for (unsigned base = 0; !done && base < gridDim.x; base += kBlock) {
     const unsigned g = base + threadIdx.x;
     Cand P[K];
 #pragma unroll
@@ -568,10 +690,37 @@ __global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size
     }
     if (threadIdx.x == 0 && base > 0) cand_merge<K>(P, acc);
     __syncthreads();  // s_lists is reused
-    block_rank<K>(P, s_lists, lo.rank);
+    block_rank<K>(P, s_lists, s_rank, lo.rank);
+#ifdef SSP_SELECT_CLOCKS
+    if (nchunk < 2) cc[1 + nchunk++] = wall_clock64();
+#endif
 #pragma unroll
     for (int j = 0; j < K; ++j) acc[j] = s_lists[0][j];
   }
+#ifdef SSP_SELECT_CLOCKS
+  if (threadIdx.x == 0) {
+    const unsigned long long c3 = wall_clock64();
+    unsigned long long t0min = ~0ull, t0max = 0, t1max = 0, t2max = 0;
+    double ss = 0, sm = 0;
+    for (unsigned g = 0; g < gridDim.x && g < 4096; ++g) {
+      const unsigned long long u0 = __hip_atomic_load(&g_sel_clk[g][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long u1 = __hip_atomic_load(&g_sel_clk[g][1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long u2 = __hip_atomic_load(&g_sel_clk[g][2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t0min = u0 < t0min ? u0 : t0min;
+      t0max = u0 > t0max ? u0 : t0max;
+      t1max = u1 > t1max ? u1 : t1max;
+      t2max = u2 > t2max ? u2 : t2max;
+      ss += double(u1 - u0);
+      sm += double(u2 - u1);
+    }
+    const double G = double(gridDim.x);
+    printf("SELCLK K=%d G=%u n=%lu start_spread=%.2f stream_end=%.2f wg_merge_end=%.2f last_wg_done=%.2f "
+           "mean_stream=%.2f mean_wg_merge=%.2f last: arrived=%.2f chunk0=%.2f chunk1=%.2f us\n", K, gridDim.x,
+           (unsigned long)a.n, 0.01 * double(t0max - t0min), 0.01 * double(t1max - t0min), 0.01 * double(t2max - t0min),
+           0.01 * double(c3 - t0min), 0.01 * ss / G, 0.01 * sm / G, 0.01 * double(cc[0] - t0min),
+           0.01 * double(cc[1] - t0min), 0.01 * double(cc[2] - t0min));
+  }
+#endif
   // s_lists[0] = acc (read from LDS: no register indexing)
   if (!lo.host) {
     if (threadIdx.x < K) lo.out[threadIdx.x] = s_lists[0][threadIdx.x];
@@ -586,6 +735,7 @@ __global__ __launch_bounds__(kBlock) void k_select_local(const RadixArgs a, size
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's result stores have completed (real <= 16)
     if (threadIdx.x == 0) {
       __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lo.thresh) __hip_atomic_store(lo.thresh, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (lo.host) __hip_atomic_store(lo.flag, lo.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
@@ -693,7 +843,11 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
   std::vector<size_t> sel_idx;  // this rank's best (global index, returned value)
   std::vector<double> sel_val;
   if (keep > 0 && n > 0) {
-    ssp::LedgerScope ls(ctx, mode == 1 ? "select_max_dot" : "select", (mode == 1 ? 16.0 : 8.0) * n);
+    // the op's ledger scope; the one-pass form closes it at its launch, so that the host's wait for the
+    // published pairs is not counted as device time (the radix form's host decisions between its
+    // passes are part of the op and stay inside)
+    std::optional<ssp::LedgerScope> ls;
+    ls.emplace(ctx, mode == 1 ? "select_max_dot" : "select", (mode == 1 ? 16.0 : 8.0) * n);
     // Level 0 reads the shard (short shards) or the radix candidates; later levels read the
     // previous level's survivors.
     const bool radix = n > kRadixMin;
@@ -733,7 +887,9 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
       unsigned* cnt = ctx->fold_counter + ssp::kFoldLine * ssp::kFoldShards;
       const size_t real = std::min(n, nsel);
       SSP_TRY(ssp::ensure_result(ctx, 2 * real));
-      LocalOut lo{buf0, ctx->select_rank, nullptr, nullptr, 0, int(real)};
+      // the launch threshold: a 64-bit slot on the top counter's line (unused by the reduction tails)
+      auto* thresh = reinterpret_cast<unsigned long long*>(cnt + 16);
+      LocalOut lo{buf0, ctx->select_rank, ctx->select_rank ? thresh : nullptr, nullptr, nullptr, 0, int(real)};
       if (!ctx->publish_copy) {
         lo.host = ctx->result_host;
         lo.flag = ctx->pub_flag;
@@ -746,6 +902,7 @@ int select_impl(ssp_ctx* ctx, int mode, const double* x, const double* y, size_t
       SSP_TRY_HIP(hipGetLastError());
       local = true;
       if (lo.host) {
+        ls.reset();
         bool seen = true;
         SSP_TRY(ssp::wait_flag(ctx, lo.seq, &seen, "select"));
         for (size_t e = 0; e < real; ++e) {

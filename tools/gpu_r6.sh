@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
 # host algebra clock), and a kernel trace of the C4-shard solve.
-#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,shapetab,selkern,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
 # Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
 # the session.
 set -u -o pipefail
@@ -93,6 +93,17 @@ for s in ${1//,/ }; do
       ;;
     gputests)
       step gputests 1500 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests || exit $?
+      ;;
+    shapetab)
+      rm -rf "$OUT/shapetab"
+      SSP_LEDGER_DETAIL=1 SSP_LEDGER_TIMING=dispatch step shapetab 300 rocprofv3 --kernel-trace -d "$OUT/shapetab" -o run \
+        --output-format csv -- python3 tools/solver_ledger.py --configs C4-shard --out "$OUT/shapetab_ledger.json" || exit $?
+      python3 tools/shape_table.py "$OUT/shapetab_ledger.json" "$OUT/shapetab/run_kernel_trace.csv" > "$OUT/shape_table.md" || exit $?
+      ;;
+    selkern)
+      rm -rf "$OUT/selkern"
+      step selkern 300 rocprofv3 --kernel-trace --stats -d "$OUT/selkern" -o run --output-format csv -- \
+        python3 tools/select_probe.py 1.25e7 --nsel 8,16 || exit $?
       ;;
     c4trace)
       rm -rf "$OUT/c4trace"
