@@ -359,11 +359,12 @@ def cpu_trace(kind, n_global):
 REDUCING_OPS = ("dot", "gemm_inner", "axpy_inner", "scal_inner", "axpy_norm", "axpy_gram", "axpy_pairs_norm", "select", "gemm_inner_sparse")
 
 
-def in_solver(ctx, n_global, world, barrier, repeat=3, kind="davidson"):
+def in_solver(ctx, n_global, world, barrier, repeat=5, kind="davidson"):
     """Whole solves: Davidson with C3's options (sharded over the ranks = C4 at N > 1) or, kind =
-    "diis", NonLinearEquationsDIIS with C5's.  The first (cold) and second (warm) solves run without
-    the ledger -- their wall times carry no HIP-event records -- and the last one with it, for the
-    kernel time and bytes.  Returns the warm wall time, the cold one, and the ledgered solve's numbers."""
+    "diis", NonLinearEquationsDIIS with C5's.  The first (cold) solve and the warm ones after it run
+    without the ledger -- their wall times carry no HIP-event records -- and the last one with it, for
+    the kernel time and bytes.  Returns the median warm wall time (repeat - 2 warm solves: one solve's
+    wall moves by a few percent with the host's jitter), the cold one, and the ledgered solve's numbers."""
     import itsolv_hbm as ih
 
     def allmax(x):
@@ -371,7 +372,7 @@ def in_solver(ctx, n_global, world, barrier, repeat=3, kind="davidson"):
             return x
         return max(struct.unpack("<d", b)[0] for b in ctx.allgather_bytes(struct.pack("<d", x)))
 
-    walls = []
+    walls, has = [], []
     for rep in range(repeat):
         ctx.ledger_reset()
         ctx.ledger_enable(rep == repeat - 1)  # the last solve: the ledger
@@ -384,8 +385,10 @@ def in_solver(ctx, n_global, world, barrier, repeat=3, kind="davidson"):
         ctx.synchronize()
         walls.append(allmax(time.perf_counter() - t0))
         ctx.ledger_enable(False)
-        if rep == repeat - 2:
-            ha = r["host_algebra"]  # the warm solve's host subspace algebra
+        if 0 < rep < repeat - 1:
+            has.append(r["host_algebra"])  # the warm solves' host subspace algebra
+    warm = float(np.median(walls[1:-1]))
+    ha = sorted(has, key=lambda h: h["seconds"])[len(has) // 2]
     led = ctx.ledger()
     ms = sum(v["ms"] for v in led.values())
     nb = sum(v["bytes"] for v in led.values())
@@ -414,10 +417,11 @@ def in_solver(ctx, n_global, world, barrier, repeat=3, kind="davidson"):
         "converged": bool(r["converged"]),
         "iterations": r["iterations"],
         "r_creations": r["r_creations"],
-        "wall_s": round(walls[-2], 4),
+        "wall_s": round(warm, 4),
+        "wall_s_warm_all": [round(w, 4) for w in walls[1:-1]],
         "wall_s_cold": round(walls[0], 4),
         "wall_s_ledger_on": round(walls[-1], 4),
-        "idle_frac_of_wall": round((walls[-2] - ms / 1e3) / walls[-2], 4),
+        "idle_frac_of_wall": round((warm - ms / 1e3) / warm, 4),
         # of that idle: the host's subspace algebra (eigenproblem / svd_system / solve_DIIS, dense.h)
         "host_algebra_ms_rank0": round(1e3 * ha["seconds"], 3),
         "host_algebra_calls": ha["calls"],
@@ -425,7 +429,7 @@ def in_solver(ctx, n_global, world, barrier, repeat=3, kind="davidson"):
         "kernel_ms_rank0": round(ms, 3),
         "algorithmic_GB_rank0": round(nb / 1e9, 2),
         "kernel_GBs_rank0": round(nb / (ms / 1e3) / 1e9, 1) if ms else None,
-        "wall_GBs_all_ranks": round(world * nb / walls[-2] / 1e9, 1),
+        "wall_GBs_all_ranks": round(world * nb / warm / 1e9, 1),
         "reductions_per_iteration": round(red / it, 1),
         "top_ops": {op: {"calls": v["calls"], "ms": round(v["ms"], 2),
                          "GBs": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] else None}

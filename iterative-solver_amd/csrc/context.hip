@@ -467,6 +467,7 @@ int ssp_ctx_create(int device, ssp_ctx** out) {
   if (const char* ip = std::getenv("SSP_INNER_PER_CU")) ctx->inner_per_cu = std::max(1, std::atoi(ip));
   if (const char* op = std::getenv("SSP_OUTER_WG_PER_CU")) ctx->outer_per_cu = std::max(1, std::atoi(op));
   if (const char* fp = std::getenv("SSP_FUSED_PER_CU")) ctx->fused_per_cu = std::max(1, std::atoi(fp));
+  if (const char* tw = std::getenv("SSP_TRANSFORM_WIDE")) ctx->transform_wide = std::atoi(tw) != 0;
   if (const char* sm = std::getenv("SSP_SELECT_MERGE")) ctx->select_rank = std::string(sm) != "tree";
   if (const char* lt = std::getenv("SSP_LEDGER_TIMING")) ctx->ledger_dispatch = std::string(lt) == "dispatch";
   ctx->ledger_detail = std::getenv("SSP_LEDGER_DETAIL") != nullptr;

@@ -826,14 +826,19 @@ __device__ __forceinline__ kernarg_dp transform_column(int j) {
 
 // M = m exactly (instantiated for m = 1..8): no per-vector branch in the streaming loop.  DOTS: 0 none,
 // 1 the M self-dots <x_j', x_j'> (accumulated as each output is formed), 2 the M(M+1)/2 pair dots.
-template <int M, int DOTS, bool FMA>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_transform(const TransformArgs a) {
+// WIDE: twice the window for M > 4 -- more bytes in flight per lane at two waves per SIMD instead of
+// three.  Used for the self-dot instance (DOTS = 1; SSP_TRANSFORM_WIDE=0 turns it off, per context):
+// on the same vectors 4989 -> 5276 GB/s at 1.25e7 elements and 5285 -> 5626 at 1e8, while the Gram
+// instance lost (5147 -> 5028, 5511 -> 5074; profiles/r6/ab_transform_wide/).
+template <int M, int DOTS, bool FMA, bool WIDE = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 3))) void k_transform(const TransformArgs a) {
   using ssp::ld2nt;
   using ssp::st2nt;
   constexpr bool GRAM = DOTS == 2, NORM = DOTS == 1;
   constexpr int NP = M * (M + 1) / 2;
   constexpr int NA = GRAM ? NP : (NORM ? M : 1);
-  constexpr int U = GRAM ? 1 : (M <= 4 ? 4 : 2);  // GRAM keeps every output of the window for the pair dots
+  // GRAM keeps every output of the window for the pair dots
+  constexpr int U = GRAM ? (WIDE ? 2 : 1) : (M <= 4 ? 4 : (WIDE ? 4 : 2));
   double acc[NA];
 #pragma unroll
   for (int q = 0; q < NA; ++q) acc[q] = 0;
@@ -859,7 +864,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
         for (int i = 0; i < M; ++i)
 #pragma unroll
           for (int u = 0; u < U; ++u) xv[u][i] = sc2<true>(ld2nt(a.x[i] + 2 * (p0 + 64 * u)), a.s[i]);
-        double ylo[M], yhi[M];
+        double ylo[U][M], yhi[U][M];
 #pragma unroll
         for (int j = 0; j < M; ++j) {
           const kernarg_dp tc = transform_column<M>(j);
@@ -872,16 +877,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
               vh = tmul<FMA>(tc[i], xv[u][i].y, vh);
             }
             st2nt(a.x[j] + 2 * (p0 + 64 * u), make_double2(vl, vh));
-            ylo[j] = vl;  // (GRAM: U = 1)
-            yhi[j] = vh;
+            ylo[u][j] = vl;
+            yhi[u][j] = vh;
             if constexpr (NORM) {
               acc[j] = fma(vl, vl, acc[j]);
               acc[j] = fma(vh, vh, acc[j]);
             }
           }
         }
-        pairs(ylo);
-        pairs(yhi);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          pairs(ylo[u]);
+          pairs(yhi[u]);
+        }
       },
       [&](size_t p) {
         double2 xv[M];
@@ -954,6 +962,12 @@ unsigned gram_grid(ssp_ctx* ctx, size_t n) {
 template <int M>
 void launch_transform_m(ssp_ctx* ctx, unsigned grid, const TransformArgs& a, int dots, bool exact, bool pass) {
   const dim3 b(kBlock);
+  if constexpr (M > 4) {
+    if (ctx->transform_wide && !exact && dots == 1) {
+      SSP_LAUNCH((k_transform<M, 1, true, true>), dim3(grid), b, 0, ctx->stream, a);
+      return;
+    }
+  }
   if (exact) SSP_LAUNCH((k_transform<M, 0, false>), dim3(grid), b, 0, ctx->stream, a);
   else if (dots == 2)
     SSP_LAUNCH((k_transform<M, 2, true>), dim3(pass ? grid : gram_grid<M>(ctx, a.n)), b, 0, ctx->stream, a);
@@ -1859,7 +1873,9 @@ int transform_impl(ssp_ctx* ctx, const double* t, double* const* xx, const doubl
   ssp::FoldTail tail{};
   if (n > 0) {
     ssp::LedgerScope ls(ctx, dots ? "transform_gram" : "transform", 16.0 * n * m);
-    const unsigned grid = ssp::win_grid(ctx, n, fused == 2 ? 1 : (m <= 4 ? 4 : 2), unsigned(ctx->fused_per_cu));
+    const bool wide = ctx->transform_wide && m > 4 && fused == 1;  // k_transform's WIDE instance
+    const unsigned grid = ssp::win_grid(ctx, n, fused == 2 ? 1 : (m <= 4 ? 4 : (wide ? 4 : 2)),
+                                        unsigned(ctx->fused_per_cu));
     const bool pass = fused == 2 && gram_reduce_pass();
     if (fused) {
       SSP_TRY(ssp::fold_begin(ctx, nd, &tail));

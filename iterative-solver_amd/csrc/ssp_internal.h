@@ -38,6 +38,7 @@ struct ssp_ctx {
   int outer_per_cu = 8;        // gemm_outer workgroups per CU (SSP_OUTER_WG_PER_CU: the A/B knob of tools/outer_cu_ab.py)
   int fused_per_cu = 8;        // workgroups per CU of the fused window passes (SSP_FUSED_PER_CU: tools/fused_cu_ab.py)
   bool select_rank = true;     // k_select_local's threshold-and-rank merge (SSP_SELECT_MERGE=tree: the LDS tree only)
+  bool transform_wide = true;   // k_transform's doubled window for the self-dot instance, m > 4 (SSP_TRANSFORM_WIDE=0: off)
   bool synth_stride = false;  // SSP_SYNTH_SHAPE=stride: the synthetic apply kernel grid-strided (A/B)
   bool ledger_dispatch = false;  // SSP_LEDGER_TIMING=dispatch (LedgerScope)
   bool ledger_detail = false;    // SSP_LEDGER_DETAIL: per-instance ledger rows (LedgerScope::detail)

@@ -100,6 +100,9 @@ for s in ${1//,/ }; do
         --output-format csv -- python3 tools/solver_ledger.py --configs C4-shard --out "$OUT/shapetab_ledger.json" || exit $?
       python3 tools/shape_table.py "$OUT/shapetab_ledger.json" "$OUT/shapetab/run_kernel_trace.csv" > "$OUT/shape_table.md" || exit $?
       ;;
+    transab)
+      step transab 300 python -u tools/transform_ab.py --out "$OUT/transform_ab.json" || exit $?
+      ;;
     selkern)
       rm -rf "$OUT/selkern"
       step selkern 300 rocprofv3 --kernel-trace --stats -d "$OUT/selkern" -o run --output-format csv -- \
