@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
 # host algebra clock), and a kernel trace of the C4-shard solve.
-#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,shapetab,selkern,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,benchprof,shapetab,selkern,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
 # Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
 # the session.
 set -u -o pipefail
@@ -99,6 +99,12 @@ for s in ${1//,/ }; do
       SSP_LEDGER_DETAIL=1 SSP_LEDGER_TIMING=dispatch step shapetab 300 rocprofv3 --kernel-trace -d "$OUT/shapetab" -o run \
         --output-format csv -- python3 tools/solver_ledger.py --configs C4-shard --out "$OUT/shapetab_ledger.json" || exit $?
       python3 tools/shape_table.py "$OUT/shapetab_ledger.json" "$OUT/shapetab/run_kernel_trace.csv" > "$OUT/shape_table.md" || exit $?
+      ;;
+    benchprof)
+      rm -rf "$OUT/benchprof"
+      step benchprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/benchprof" -o run --output-format csv -- \
+        python3 -u bench.py --steps 10 --warmup 3 || exit $?
+      grep '^{' "$OUT/benchprof.log" > "$OUT/bench_under_rocprof.json" || true
       ;;
     transab)
       step transab 300 python -u tools/transform_ab.py --out "$OUT/transform_ab.json" || exit $?
