@@ -556,7 +556,7 @@ def main():
                     help="rank transport at N > 1: RCCL; the peer-memory communicator (p2p: IPC-shared device "
                          "inboxes, rank-order sums); auto = p2p when its attach self-test passes on every rank, "
                          "else RCCL; or the host socket hub (tests: several ranks on ONE device)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r4", "pmc_traffic_n1e8.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r6", "pmc_traffic_n1e8_r6.json"),
                     help="rocprofv3 --pmc summary of this workload (roofline.traffic)")
     ap.add_argument("--mfma-json", default=os.path.join(ROOT, "profiles", "r3", "mfma_util_n1e8.json"),
                     help="rocprofv3 --pmc MfmaUtil summary of this workload (mfma.mfma_util_pct)")

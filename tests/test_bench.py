@@ -54,6 +54,15 @@ def test_pmc_traffic_lookup_r2_names_the_rmw_instance():
     assert src.endswith("k_gemm_outer<8, false, true>") and abs(t - 8 * 10**8 * (48 + 8)) / t < 0.02
 
 
+def test_pmc_traffic_lookup_r6_default():
+    # the file bench.py reports as roofline.traffic by default (round-6 final tree): the RMW gemm_outer
+    # moves its algorithmic bytes, read 48 + 8 vectors, write 8
+    path = os.path.join(ROOT, "profiles", "r6", "pmc_traffic_n1e8_r6.json")
+    t, src = bench.pmc_traffic(path, "gemm_outer", 10**8, 8, 48, 1)
+    assert src == "profiles/r6/pmc_traffic_n1e8_r6.json:k_gemm_outer<8, false, false, false>"
+    assert abs(t - 8 * 10**8 * (48 + 16)) / t < 1e-4
+
+
 def test_mfma_util_lookup():
     path = os.path.join(ROOT, "profiles", "r1", "mfma_util_n1e8.json")
     util, src = bench.mfma_util(path)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
 # host algebra clock), and a kernel trace of the C4-shard solve.
-#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,benchprof,shapetab,selkern,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,benchprof,pmcbench,pmcc4,shapetab,selkern,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
 # Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
 # the session.
 set -u -o pipefail
@@ -105,6 +105,20 @@ for s in ${1//,/ }; do
       step benchprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/benchprof" -o run --output-format csv -- \
         python3 -u bench.py --steps 10 --warmup 3 || exit $?
       grep '^{' "$OUT/benchprof.log" > "$OUT/bench_under_rocprof.json" || true
+      ;;
+    pmcbench)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        rm -rf "$OUT/pmcb_$c"
+        step "pmcb_$c" 600 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmcb_$c" -o run --output-format csv -- \
+          python3 bench.py --steps 2 --warmup 1 --ledger-steps 1 --no-cpu-baseline --no-in-solver --no-small || exit $?
+      done
+      ;;
+    pmcc4)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        rm -rf "$OUT/pmcc4_$c"
+        step "pmcc4_$c" 300 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmcc4_$c" -o run --output-format csv -- \
+          python3 tools/solver_ledger.py --configs C4-shard --out "$OUT/pmcc4_ledger_$c.json" || exit $?
+      done
       ;;
     transab)
       step transab 300 python -u tools/transform_ab.py --out "$OUT/transform_ab.json" || exit $?
