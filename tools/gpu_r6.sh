@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
 # host algebra clock), and a kernel trace of the C4-shard solve.
-#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,benchprof,pmcbench,pmcc4,shapetab,selkern,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,benchprof,shapes,smoke,pmcbench,pmcc4,shapetab,selkern,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
 # Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
 # the session.
 set -u -o pipefail
@@ -119,6 +119,14 @@ for s in ${1//,/ }; do
         step "pmcc4_$c" 300 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmcc4_$c" -o run --output-format csv -- \
           python3 tools/solver_ledger.py --configs C4-shard --out "$OUT/pmcc4_ledger_$c.json" || exit $?
       done
+      ;;
+    shapes)
+      for n in 1e8 1e7; do
+        step "shapes_$n" 300 python -u tools/shapes_bench.py --n $n --reps 10 --out "$OUT/shapes_n$n.json" || exit $?
+      done
+      ;;
+    smoke)
+      step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $?
       ;;
     transab)
       step transab 300 python -u tools/transform_ab.py --out "$OUT/transform_ab.json" || exit $?

@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Per-shape microbenchmark of the handler ops at fixed N (SURVEY.md §8d "Concrete synthetic
 inputs", shapes: gemm_inner 8x48, 8x1, 1x6; gemm_outer 48->8, 1->8, 6->1; axpy; dot ...).
-Times come from the library's HIP-event ledger (events on the context stream around each op);
-bytes are the algorithmic bytes of DESIGN.md §4.
+Times come from the library's HIP-event ledger (events on the context stream around each op), one
+ledger window per call: two warm-up calls, then the median (and mean) over --reps calls, as §8d
+prescribes (median of 10 after 2 warm-ups); bytes are the algorithmic bytes of DESIGN.md §4.
 
-usage: python tools/shapes_bench.py [--n 1e8] [--reps 5] [--out gpurun_out/shapes.json]
+usage: python tools/shapes_bench.py [--n 1e8] [--reps 10] [--out gpurun_out/shapes.json]
 """
 import argparse
 import json
@@ -24,7 +25,7 @@ PEAK = 8000.0
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=float, default=1e8)
-    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "shapes.json"))
     a = ap.parse_args()
     n = int(a.n)
@@ -60,17 +61,22 @@ def main():
     ]
     res = []
     for name, op, fn in cases:
-        fn()
-        ctx.synchronize()
-        ctx.ledger_reset()
-        ctx.ledger_enable(True)
-        for _ in range(a.reps):
+        for _ in range(2):
             fn()
-        ctx.ledger_enable(False)
-        e = ctx.ledger()[op]
-        us = 1e3 * e["ms"] / e["calls"]
-        gbs = e["bytes"] / (e["ms"] / 1e3) / 1e9
-        res.append({"case": name, "avg_us": round(us, 2), "bytes_per_call": e["bytes"] / e["calls"],
+        ctx.synchronize()
+        per_call, nbytes = [], 0.0
+        for _ in range(a.reps):
+            ctx.ledger_reset()
+            ctx.ledger_enable(True)
+            fn()
+            ctx.ledger_enable(False)
+            e = ctx.ledger()[op]
+            per_call.append(e["ms"] / e["calls"])
+            nbytes = e["bytes"] / e["calls"]
+        med = float(np.median(per_call))
+        us, mean_us = 1e3 * med, 1e3 * float(np.mean(per_call))
+        gbs = nbytes / (med / 1e3) / 1e9
+        res.append({"case": name, "median_us": round(us, 2), "mean_us": round(mean_us, 2), "bytes_per_call": nbytes,
                     "GBs": round(gbs, 1), "frac_of_8TBs": round(gbs / PEAK, 4)})
         print(f"{name:22s} {us:10.1f} us {gbs:8.1f} GB/s", flush=True)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
