@@ -475,6 +475,7 @@ int ssp_ctx_create(int device, ssp_ctx** out) {
     ctx->synth_stride = std::string(ss) == "stride";
     ctx->synth_window = std::string(ss) == "window";
   }
+  if (const char* sm = std::getenv("SSP_SYNTH_MERGE")) ctx->synth_merge = std::atoi(sm) != 0;
   if (const char* ct = std::getenv("SSP_COMM_TIMEOUT_S")) {
     const double v = std::atof(ct);
     if (v > 0) ctx->comm_timeout_s = v;

@@ -43,6 +43,7 @@ struct ssp_ctx {
   bool ledger_dispatch = false;  // SSP_LEDGER_TIMING=dispatch (LedgerScope)
   bool ledger_detail = false;    // SSP_LEDGER_DETAIL: per-instance ledger rows (LedgerScope::detail)
   bool synth_window = false;  // SSP_SYNTH_SHAPE=window: the synthetic apply kernel in the window shape (A/B)
+  bool synth_merge = true;    // one launch for all full vector groups of a synthetic action (SSP_SYNTH_MERGE=0: one per group)
   // Shape of the 1 x 1 / 1 x 2 gemm_inner row kernel: window (default) or, with SSP_ROW_SHAPE=stride
   // in the environment at context creation, the round-2 grid-stride shape (A/B: tools/row_shape_ab.py).
   bool row_stride = false;
@@ -232,15 +233,19 @@ class LedgerScope {
 // the lane's first position of a window (its others are p0 + 64 u), f(p) one position, fo(e) the
 // odd element.
 template <int U, typename FW, typename F, typename FO>
-__device__ __forceinline__ void for_windows(size_t n, FW&& fw, F&& f, FO&& fo) {
+__device__ __forceinline__ void for_windows_in(size_t n, unsigned bid, unsigned nb, FW&& fw, F&& f, FO&& fo) {
   const int lane = threadIdx.x & 63;
-  const size_t gw = size_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
-  const size_t nw = size_t(gridDim.x) * (kBlock / 64);
+  const size_t gw = size_t(bid) * (kBlock / 64) + (threadIdx.x >> 6);
+  const size_t nw = size_t(nb) * (kBlock / 64);
   const size_t n2 = n >> 1, win = 64 * size_t(U), nwin = n2 / win;
   for (size_t c = gw; c < nwin; c += nw) fw(c * win + lane);
-  for (size_t i = nwin * win + size_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += size_t(gridDim.x) * kBlock)
-    f(i);
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) fo(n - 1);
+  for (size_t i = nwin * win + size_t(bid) * kBlock + threadIdx.x; i < n2; i += size_t(nb) * kBlock) f(i);
+  if ((n & 1) && bid == 0 && threadIdx.x == 0) fo(n - 1);
+}
+// The same over the launch's own grid.
+template <int U, typename FW, typename F, typename FO>
+__device__ __forceinline__ void for_windows(size_t n, FW&& fw, F&& f, FO&& fo) {
+  for_windows_in<U>(n, blockIdx.x, gridDim.x, static_cast<FW&&>(fw), static_cast<F&&>(f), static_cast<FO&&>(fo));
 }
 
 // Workgroups for a window-shaped launch over n doubles: one wave per window of u KiB, at most

@@ -113,10 +113,15 @@ __device__ __forceinline__ void coeff_visit(double (&s)[NV][R], unsigned mm, con
     for (int l = 0; l < R; ++l) s[v][l] += flip(mm, l, xv[v].x) + flip(mm >> 16, l, xv[v].y);
 }
 
+// G > 0: the launch holds gridDim.x / G consecutive vector groups of NV, G workgroups each (one
+// launch for a whole action); workgroup b of group q works as workgroup b of a G-workgroup launch for
+// vectors v0 + q NV .. -- the same visits and partial sums, so the same numbers.  G = 0: one group.
 template <int R, int NV>
-__global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a, int v0) {
+__global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a, int v0, unsigned G) {
   __shared__ double wsum[kBlock / 64];
-  const size_t stride = size_t(gridDim.x) * kBlock, n2 = a.n >> 1;
+  const unsigned nb = G ? G : gridDim.x, bid = G ? blockIdx.x % G : blockIdx.x;
+  if (G) v0 += int(blockIdx.x / G) * NV;
+  const size_t stride = size_t(nb) * kBlock, n2 = a.n >> 1;
   const unsigned* mask2 = reinterpret_cast<const unsigned*>(a.mask);
   const double* xp[NV];
   double xs[NV];
@@ -130,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a, int v
   for (int v = 0; v < NV; ++v)
 #pragma unroll
     for (int l = 0; l < R; ++l) s[v][l] = 0;
-  size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x;
+  size_t i = size_t(bid) * kBlock + threadIdx.x;
   for (; i + stride < n2; i += 2 * stride) {
     const unsigned m0 = mask2[i], m1 = mask2[i + stride];
     double2 x0[NV], x1[NV];
@@ -160,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a, int v
     }
     coeff_visit<R, NV>(s, m0, x0);
   }
-  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+  if ((a.n & 1) && bid == 0 && threadIdx.x == 0) {
     const unsigned mm = a.mask[a.n - 1];
 #pragma unroll
     for (int v = 0; v < NV; ++v)
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_coeff(const SynthArgs a, int v
 #pragma unroll
     for (int l = 0; l < R; ++l) {
       const double t = block_sum(s[v][l], wsum);
-      if (threadIdx.x == 0) a.partial[size_t(blockIdx.x) * a.nvec * R + (v0 + v) * R + l] = t;
+      if (threadIdx.x == 0) a.partial[size_t(bid) * a.nvec * R + (v0 + v) * R + l] = t;
     }
   }
 }
@@ -305,9 +310,12 @@ __device__ __forceinline__ LowrankTab<R, NV, ON> build_tab(const SynthArgs& a, i
 // the visit's masks and operands loaded before its stores).  Element for element the same operations
 // as one pair at a time.
 // EX: the reference's arithmetic (short vectors, kernels_exact.hip): products rounded alone.
+// G > 0: gridDim.x / G vector groups of NV in one launch, G workgroups each (as k_synth_coeff).
 template <int R, bool ADD, int NV, bool EX>
-__global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a, int v0) {
+__global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a, int v0, unsigned G) {
   constexpr int U = kSynthU;
+  const unsigned nb = G ? G : gridDim.x, bid = G ? blockIdx.x % G : blockIdx.x;
+  if (G) v0 += int(blockIdx.x / G) * NV;
   const unsigned* mask2 = reinterpret_cast<const unsigned*>(a.mask);
   const LowrankTab<R, NV, !ADD> tab = build_tab<R, NV, !ADD>(a, v0);
   double c[NV][R];
@@ -342,8 +350,8 @@ __global__ __launch_bounds__(kBlock) void k_synth_apply(const SynthArgs a, int v
       ssp::st2nt(yp[v] + 2 * i, out);
     }
   };
-  ssp::for_windows<U>(
-      a.n,
+  ssp::for_windows_in<U>(
+      a.n, bid, nb,
       [&](size_t p0) {
         unsigned mm[U];
         double2 in[U][NV];
@@ -454,26 +462,32 @@ constexpr int coeff_group() {
   return R > 8 ? 2 : 4;
 }
 
+// merge: the full groups of a.nvec in one launch (grid workgroups per group), when there are several
+// and no partial one.
 template <int R>
-void launch_coeff(unsigned grid, hipStream_t st, const SynthArgs& a) {
+void launch_coeff(unsigned grid, hipStream_t st, const SynthArgs& a, bool merge) {
   constexpr int G = coeff_group<R>();
+  if (merge && a.nvec > G && a.nvec % G == 0) {
+    SSP_LAUNCH((k_synth_coeff<R, G>), dim3(grid * unsigned(a.nvec / G)), dim3(kBlock), 0, st, a, 0, grid);
+    return;
+  }
   for (int v0 = 0; v0 < a.nvec; v0 += G) {
     const int nv = std::min(G, a.nvec - v0);
-    if (nv == 4) SSP_LAUNCH((k_synth_coeff<R, (G >= 4 ? 4 : 1)>), dim3(grid), dim3(kBlock), 0, st, a, v0);
-    else if (nv == 3) SSP_LAUNCH((k_synth_coeff<R, (G >= 4 ? 3 : 1)>), dim3(grid), dim3(kBlock), 0, st, a, v0);
-    else if (nv == 2) SSP_LAUNCH((k_synth_coeff<R, 2>), dim3(grid), dim3(kBlock), 0, st, a, v0);
-    else SSP_LAUNCH((k_synth_coeff<R, 1>), dim3(grid), dim3(kBlock), 0, st, a, v0);
+    if (nv == 4) SSP_LAUNCH((k_synth_coeff<R, (G >= 4 ? 4 : 1)>), dim3(grid), dim3(kBlock), 0, st, a, v0, 0u);
+    else if (nv == 3) SSP_LAUNCH((k_synth_coeff<R, (G >= 4 ? 3 : 1)>), dim3(grid), dim3(kBlock), 0, st, a, v0, 0u);
+    else if (nv == 2) SSP_LAUNCH((k_synth_coeff<R, 2>), dim3(grid), dim3(kBlock), 0, st, a, v0, 0u);
+    else SSP_LAUNCH((k_synth_coeff<R, 1>), dim3(grid), dim3(kBlock), 0, st, a, v0, 0u);
   }
 }
 
 #define SSP_RANK_CASES(F) \
   F(1) F(2) F(3) F(4) F(5) F(6) F(7) F(8) F(9) F(10) F(11) F(12) F(13) F(14) F(15) F(16)
 
-void synth_coeff(unsigned grid, hipStream_t st, const SynthArgs& a) {
+void synth_coeff(unsigned grid, hipStream_t st, const SynthArgs& a, bool merge) {
   switch (a.rank) {
 #define F(r) \
   case r:    \
-    launch_coeff<r>(grid, st, a); \
+    launch_coeff<r>(grid, st, a, merge); \
     break;
     SSP_RANK_CASES(F)
 #undef F
@@ -495,10 +509,14 @@ template <int R, bool ADD, bool EX, bool WIN>
 void launch_apply_ex(const ssp_ctx* ctx, hipStream_t st, const SynthArgs& a) {
   constexpr int G = coeff_group<R>();
   const unsigned grid = WIN ? ssp::win_grid(ctx, a.n, kSynthU, 16) : ssp::stream_grid(ctx, a.n, 1);
+  if (WIN && !EX && ctx->synth_merge && a.nvec > G && a.nvec % G == 0) {  // the full groups in one launch
+    SSP_LAUNCH((k_synth_apply<R, ADD, G, EX>), dim3(grid * unsigned(a.nvec / G)), dim3(kBlock), 0, st, a, 0, grid);
+    return;
+  }
   for (int v0 = 0; v0 < a.nvec; v0 += G) {
     const int nv = std::min(G, a.nvec - v0);
-#define SSP_APPLY(NV)                                                                                   \
-  if (WIN) SSP_LAUNCH((k_synth_apply<R, ADD, NV, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0); \
+#define SSP_APPLY(NV)                                                                                       \
+  if (WIN) SSP_LAUNCH((k_synth_apply<R, ADD, NV, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0, 0u); \
   else SSP_LAUNCH((k_synth_apply_pipe<R, ADD, NV, EX>), dim3(grid), dim3(kBlock), 0, st, a, v0);
     if (nv == 4) { SSP_APPLY((G >= 4 ? 4 : 1)) }
     else if (nv == 3) { SSP_APPLY((G >= 4 ? 3 : 1)) }
@@ -673,7 +691,7 @@ int sspx_synth_action_scaled(ssp_ctx* ctx, const sspx_synth* spec, const double*
       synth_coeff_exact(ctx->stream, a, ctx->result_dev);
       SSP_TRY_HIP(hipGetLastError());
     } else if (n > 0) {
-      synth_coeff(grid, ctx->stream, a);
+      synth_coeff(grid, ctx->stream, a, ctx->synth_merge);
       SSP_TRY_HIP(hipGetLastError());
       SSP_TRY(ssp::launch_reduce_partials(ctx, ctx->partial, int(grid), 1, nc, ctx->result_dev, nc, 0, 0));
     } else {

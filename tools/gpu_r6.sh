@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session steps: the default bench, the C4-shard solve ledger (per-instance rows and the
 # host algebra clock), and a kernel trace of the C4-shard solve.
-#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,benchprof,shapes,smoke,pmcbench,pmcc4,shapetab,selkern,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
+#   tools/gpu_r6.sh STEPS     STEPS: comma-separated of bench,benchprof,mergeab,synthtests,shapes,smoke,pmcbench,pmcc4,shapetab,selkern,c4ledger,c4pipe2,c4prof,c4trace,c4hiptrace,gapprobe,sizeprobe,seltests,selprobe,innertests,csab,outercu,outerab,selsizes,kernargab,kernargab2,fusedab,gputests
 # Outputs under gpurun_out/${SESSION:-r6}/.  Each step has its own time limit; the first failure ends
 # the session.
 set -u -o pipefail
@@ -127,6 +127,18 @@ for s in ${1//,/ }; do
       ;;
     smoke)
       step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $?
+      ;;
+    mergeab)
+      for round in 1 2 3; do
+        for v in 0 1; do
+          SSP_SYNTH_MERGE=$v step "mab_${v}_$round" 120 python -u tools/wall_ab.py --repeat 8 --tag "merge$v" || exit $?
+          grep '^{' "$OUT/mab_${v}_$round.log" >> "$OUT/merge_ab.jsonl" || true
+        done
+      done
+      ;;
+    synthtests)
+      step synthtests 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu -k "synth or trace or solver or sharded" \
+        tests/test_ops_gpu.py tests/test_traces_gpu.py tests/test_solver_gpu.py tests/test_distributed_gpu.py || exit $?
       ;;
     transab)
       step transab 300 python -u tools/transform_ab.py --out "$OUT/transform_ab.json" || exit $?

@@ -32,7 +32,7 @@ def main():
     kw = dict(kw)
     rho, rank, seed = kw.pop("rho"), kw.pop("rank"), kw.pop("seed")
     ctx = sh.Context(0)
-    walls, its = [], None
+    walls, its, ev = [], None, None
     for rep in range(a.repeat + 1):
         t0 = time.perf_counter()
         if solver == "davidson":
@@ -42,10 +42,11 @@ def main():
         ctx.synchronize()
         w = time.perf_counter() - t0
         its = r["iterations"]
+        ev = [float(e).hex() for e in r.get("eigenvalues", [])][:8] if solver == "davidson" else None
         if rep:
             walls.append(w)
     ctx.close()
-    print(json.dumps({"tag": a.tag, "config": a.config, "iterations": its,
+    print(json.dumps({"tag": a.tag, "config": a.config, "iterations": its, "eigenvalues_hex": ev,
                       "env": {k: v for k, v in os.environ.items() if k.startswith("SSP_")},
                       "wall_ms": [round(1e3 * w, 3) for w in walls],
                       "median_ms": round(1e3 * statistics.median(walls), 3),
