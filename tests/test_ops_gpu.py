@@ -600,6 +600,40 @@ def test_synthetic_action(ctx, rank):
     assert np.array_equal(d.numpy(), oracle.synthetic_diagonal(n, rho, rank))
 
 
+@pytest.mark.parametrize("rank,nvec", [(3, 8), (8, 8), (8, 16), (8, 12), (12, 6), (16, 16), (8, 6)])
+def test_synthetic_merged_launches_bit_identical(ctx, rank, nvec, monkeypatch):
+    # SSP_SYNTH_MERGE (read at context creation): one launch for every full vector group of an action /
+    # P-space update (4 vectors per group, 2 from rank 9 on) against one launch per group -- the same
+    # visits and partial sums per workgroup, so the same bits; nvec = 6 at rank 8 has a partial group
+    # and keeps one launch per group.  Odd n: the tail element of the coefficient pass.
+    import ctypes as C
+
+    import itsolv_hbm as ih
+    import subspace_hip as sh
+
+    monkeypatch.setenv("SSP_SYNTH_MERGE", "0")
+    ctx1 = sh.Context(0)
+    try:
+        n, rho, seed = 3_000_001, 0.1, 5
+        spec = ih.Synth(rho=rho, rank=rank, seed=seed, diag_kind=ih.DIAG_LINEAR, alpha=0.0, target=0.0)
+        w = np.random.default_rng(rank).uniform(-1, 1, nvec * rank)
+        outs = []
+        for c in (ctx, ctx1):
+            xx = [c.alloc(n) for _ in range(nvec)]
+            for v, x in enumerate(xx):
+                c.fill_random(x, seed, v)
+            yy = [c.alloc(n) for _ in range(nvec)]
+            c.synth_action(xx, yy, spec)
+            sh._check(c.lib.sspx_synth_add_lowrank(c.handle, C.byref(spec), sh._ptrs(yy), nvec, n, 0, sh._dptr(w)))
+            outs.append([y.numpy() for y in yy])
+            for v in xx + yy:
+                v.free()
+        for a, b in zip(*outs):
+            assert np.array_equal(a, b)
+    finally:
+        ctx1.close()
+
+
 def test_arena_recycles_blocks(ctx):
     used0, _ = ctx.memory_stats()
     vs = [ctx.alloc(1 << 20) for _ in range(4)]
